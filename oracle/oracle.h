@@ -1,0 +1,141 @@
+/*
+ * oracle.h -- CPU restatement of the LTE DL PDSCH receive chain (TEST INFRASTRUCTURE ONLY).
+ *
+ * This directory is the parity oracle for the MI355X-native PHY in srsue_amd/.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the checker
+ * (or the CPU baseline that is timed beside the GPU).  The product path never links it.
+ *
+ * What it restates: the srsLTE-1.0 functions srsUE calls on its DL hot path
+ * (reference: /root/reference/ue/src/phy/phch_worker.cc:74,254,337,347-348; dl_harq.cc:174,232).
+ * srsLTE itself is NOT in the container, so the arithmetic below is
+ * written from 3GPP TS 36.211/36.212/36.213 plus the srsLTE conventions recorded in SURVEY.md
+ * section 8a ([X] tags: LLR>0 => bit 1, MMSE sigma^2 passed in (0.01 from phch_worker.cc:340),
+ * triplet-interleaved turbo input, CRC early stop, N_cb = K_w, MSB-first payload).
+ *
+ * PARITY STATUS: "parity unpinned" against srsLTE's own arithmetic (no reference test or golden
+ * vector exists for this path).  The oracle is pinned instead by 3GPP known-answer
+ * tests (CRC, Gold, QPP permutations, TBS spot values, 36.212 tail layout) and by transmit-chain
+ * ground truth: decoded TB bits must equal the transmitted ones whenever CRC passes.
+ */
+#ifndef LTE_ORACLE_H
+#define LTE_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_NRB_MAX        110
+#define OR_MAX_PORTS      2
+#define OR_NSYMB          14           /* normal CP, symbols per subframe */
+#define OR_TCOD_MAX_K     6144
+#define OR_FILLER_LLR     (-10000.0f)  /* known-zero filler bit, systematic/parity1 (36.212 5.1.2) */
+
+/* ---- cell / grant ---------------------------------------------------------------------- */
+typedef struct {
+  uint32_t id;        /* N_ID^cell 0..503 */
+  uint32_t nof_prb;   /* 6,15,25,50,75,100 */
+  uint32_t nof_ports; /* 1 or 2 */
+} or_cell_t;
+
+typedef struct {
+  uint32_t C, Cp, Cm, Kp, Km, F, B;   /* 36.212 5.1.2 */
+} or_cbsegm_t;
+
+/* ---- tables & small helpers (o_common.c) ------------------------------------------------ */
+int      or_symbol_sz(uint32_t nof_prb);                  /* FFT size N */
+int      or_cp_len(uint32_t N, uint32_t l_in_slot);       /* 160/144 scaled by N/2048 */
+void     or_gold(uint32_t c_init, uint8_t *c, uint32_t len);
+uint32_t or_crc(const uint8_t *bits, uint32_t len, uint32_t poly, int order);
+uint32_t or_crc24a(const uint8_t *bits, uint32_t len);
+uint32_t or_crc24b(const uint8_t *bits, uint32_t len);
+uint32_t or_crc16(const uint8_t *bits, uint32_t len);
+int      or_cb_size_idx(uint32_t K);                      /* index in the 188-entry table or -1 */
+uint32_t or_cb_size(uint32_t idx);
+int      or_qpp(uint32_t K, uint32_t *pi);                /* pi[i] = (f1 i + f2 i^2) mod K */
+int      or_qpp_f(uint32_t K, uint32_t *f1, uint32_t *f2);
+int      or_cbsegm(uint32_t tbs, or_cbsegm_t *s);
+int      or_tbs(uint32_t i_tbs, uint32_t nof_prb);        /* -1 if unknown */
+int      or_mcs(uint32_t mcs, uint32_t *qm, uint32_t *i_tbs);
+void     or_crs_seq(uint32_t id, uint32_t ns, uint32_t l, float *re_im /* 2*220 */);
+int      or_ctrl_symbols(const or_cell_t *c, uint32_t cfi);
+int      or_is_pdsch_re(const or_cell_t *c, uint32_t cfi, uint32_t sf, uint32_t l, uint32_t k);
+/* RE list of the PDSCH in mapping order (36.211 6.3.5): index l*12*nof_prb + k; returns count */
+int      or_pdsch_re_list(const or_cell_t *c, uint32_t cfi, uint32_t sf, const uint8_t *prb_mask,
+                          uint32_t *re_idx);
+int      or_rm_E(uint32_t G, uint32_t C, uint32_t Qm, uint32_t NL, uint32_t r);
+
+/* ---- FFT (o_fft.c), double precision, N = 2^a 3^b ------------------------------------- */
+void     or_dft(const double *in /*2N*/, double *out /*2N*/, int N, int inverse);
+
+/* ---- FEC (o_fec.c) ---------------------------------------------------------------------- */
+/* Turbo encoder, 36.212 5.1.3.2.  in[K] bits (filler positions may hold 0), out = 3(K+4) bits
+ * triplet-interleaved d0_k,d1_k,d2_k; filler d0/d1 positions marked 2 (NULL). */
+int      or_tcod(const uint8_t *in, uint32_t K, uint32_t F, uint8_t *d);
+/* Rate matching (TX), 36.212 5.1.4.1. d: 3(K+4) with 2=NULL. e: E bits */
+int      or_rm_tx(const uint8_t *d, uint32_t K, uint32_t E, uint32_t rv, uint8_t *e);
+/* Rate dematching + HARQ combine (RX): sb[N_cb] softbuffer row (w domain, combined by +=),
+ * new_tb != 0 overwrites (== srsLTE reset_tbs to RX_NULL followed by first write).
+ * out: decoder input 3(K+4) floats, triplet order; filler d0/d1 -> OR_FILLER_LLR. */
+int      or_rm_rx(const float *e, uint32_t E, uint32_t K, uint32_t F, uint32_t rv, int new_tb,
+                  float *sb, float *out);
+uint32_t or_ncb(uint32_t K);
+/* max-log-MAP turbo decoder (float), see o_fec.c header for the exact operation order */
+typedef struct {
+  uint32_t K;
+  uint32_t pi[OR_TCOD_MAX_K], pinv[OR_TCOD_MAX_K];
+  float w[OR_TCOD_MAX_K], llr1[OR_TCOD_MAX_K], llr2[OR_TCOD_MAX_K];
+  float xs[OR_TCOD_MAX_K + 3], xp[OR_TCOD_MAX_K + 3];
+  float beta[(OR_TCOD_MAX_K + 4) * 8];
+} or_tdec_t;
+int      or_tdec_reset(or_tdec_t *h, uint32_t K);
+void     or_tdec_iteration(or_tdec_t *h, const float *in);
+void     or_tdec_decision(const or_tdec_t *h, uint8_t *bits);
+/* decode one codeblock: returns iterations used; *crc_ok set. crc_type 0 = 24B, 1 = 24A */
+int      or_decode_cb(or_tdec_t *h, const float *in, uint32_t K, uint32_t max_its, int early_stop,
+                      int crc_type, uint8_t *bits, int *crc_ok);
+
+/* ---- PHY TX (o_tx.c): synthetic subframe generator (ground truth) ----------------------- */
+typedef struct {
+  or_cell_t cell;
+  uint32_t  sf_idx, cfi, mcs, rv, rnti, tm;  /* tm: 1 = single port, 2 = SFBC (nof_ports = 2) */
+  uint32_t  tbs, qm;                          /* 0 => from the MCS / TBS tables */
+  uint8_t   prb_mask[OR_NRB_MAX];
+  float     snr_db;                           /* per-RE SNR; >= 200 => noiseless */
+  float     h_re[OR_MAX_PORTS], h_im[OR_MAX_PORTS]; /* flat per-port channel */
+  uint64_t  noise_seed;
+  uint32_t  nl_td;                            /* N_L used in rate matching for TM2 (spec: 2) */
+} or_tx_cfg_t;
+/* Builds IQ for one subframe (samples: 2*SF_LEN floats).  tb: TBS/8 bytes (MSB-first).
+ * Also returns the coded/scrambled bits count G and writes iq. Returns 0 ok. */
+int      or_tx_subframe(const or_tx_cfg_t *cfg, const uint8_t *tb, float *iq, uint32_t *G_out);
+int      or_sf_len(uint32_t nof_prb);
+
+/* ---- PHY RX (o_rx.c) ------------------------------------------------------------------- */
+/* OFDM RX: iq -> grid[14][12 nof_prb] complex (interleaved float) */
+int      or_ofdm_rx(const or_cell_t *c, const float *iq, float *grid);
+/* channel estimation: ce[p][14][12 nof_prb]; metrics[5] = {rsrp, rssi, rsrq, noise, snr} */
+int      or_chest(const or_cell_t *c, uint32_t sf, const float *grid, float *ce, float *metrics);
+/* PDSCH soft bits: equalise+demap+descramble; llr[G] */
+int      or_pdsch_llr(const or_cell_t *c, uint32_t cfi, uint32_t sf, const uint8_t *prb_mask,
+                      uint32_t Qm, uint32_t rnti, uint32_t tm, float noise, const float *grid,
+                      const float *ce, float *llr, uint32_t *G_out, float *symbols_out);
+/* PCFICH -> cfi (1..3), 0 on failure */
+int      or_pcfich(const or_cell_t *c, uint32_t sf, const float *grid, const float *ce);
+/* Full TB decode from LLRs: rm_rx per CB (+softbuffer) -> tdec -> TB CRC -> payload.
+ * sb: C rows of or_ncb(K) floats (row stride sb_stride). Returns 0 if TB CRC ok. */
+int      or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL,
+                         uint32_t rv, int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its,
+                         uint8_t *payload, uint32_t *noi_out, uint32_t *cb_crc_ok_out);
+/* End-to-end subframe decode (what srslte_ue_dl_decode_fft_estimate + srslte_pdsch_decode_rnti
+ * do back to back).  Returns 0 if CRC ok. */
+int      or_decode_subframe(const or_cell_t *c, uint32_t sf, uint32_t cfi, const uint8_t *prb_mask,
+                            uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t rnti, uint32_t tm, uint32_t nl_td,
+                            const float *iq, float *sb, uint32_t sb_stride, int new_tb,
+                            uint32_t max_its, uint8_t *payload, uint32_t *noi_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

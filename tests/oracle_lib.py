@@ -1,0 +1,168 @@
+"""ctypes bindings to oracle/liboracle.so -- the CPU restatement used as the parity checker.
+
+Test infrastructure only (imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg).  Builds the library on first use if it is missing (gcc, oracle/Makefile).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+
+NRB_MAX = 110
+NSYMB = 14
+
+
+class Cell(C.Structure):
+    _fields_ = [("id", C.c_uint32), ("nof_prb", C.c_uint32), ("nof_ports", C.c_uint32)]
+
+
+class CbSegm(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("C", "Cp", "Cm", "Kp", "Km", "F", "B")]
+
+
+class TxCfg(C.Structure):
+    _fields_ = [
+        ("cell", Cell),
+        ("sf_idx", C.c_uint32), ("cfi", C.c_uint32), ("mcs", C.c_uint32), ("rv", C.c_uint32),
+        ("rnti", C.c_uint32), ("tm", C.c_uint32),
+        ("tbs", C.c_uint32), ("qm", C.c_uint32),
+        ("prb_mask", C.c_uint8 * NRB_MAX),
+        ("snr_db", C.c_float),
+        ("h_re", C.c_float * 2), ("h_im", C.c_float * 2),
+        ("noise_seed", C.c_uint64),
+        ("nl_td", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = np.ctypeslib.ndpointer
+        f32 = P(np.float32, flags="C_CONTIGUOUS")
+        u8 = P(np.uint8, flags="C_CONTIGUOUS")
+        u32 = P(np.uint32, flags="C_CONTIGUOUS")
+        sig = {
+            "or_symbol_sz": (C.c_int, [C.c_uint32]),
+            "or_sf_len": (C.c_int, [C.c_uint32]),
+            "or_gold": (None, [C.c_uint32, u8, C.c_uint32]),
+            "or_crc": (C.c_uint32, [u8, C.c_uint32, C.c_uint32, C.c_int]),
+            "or_crc24a": (C.c_uint32, [u8, C.c_uint32]),
+            "or_crc24b": (C.c_uint32, [u8, C.c_uint32]),
+            "or_crc16": (C.c_uint32, [u8, C.c_uint32]),
+            "or_cb_size": (C.c_uint32, [C.c_uint32]),
+            "or_cb_size_idx": (C.c_int, [C.c_uint32]),
+            "or_qpp": (C.c_int, [C.c_uint32, u32]),
+            "or_qpp_f": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+            "or_cbsegm": (C.c_int, [C.c_uint32, C.POINTER(CbSegm)]),
+            "or_tbs": (C.c_int, [C.c_uint32, C.c_uint32]),
+            "or_mcs": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+            "or_crs_seq": (None, [C.c_uint32, C.c_uint32, C.c_uint32, f32]),
+            "or_pdsch_re_list": (C.c_int, [C.POINTER(Cell), C.c_uint32, C.c_uint32, u8, u32]),
+            "or_rm_E": (C.c_int, [C.c_uint32] * 5),
+            "or_ncb": (C.c_uint32, [C.c_uint32]),
+            "or_tcod": (C.c_int, [u8, C.c_uint32, C.c_uint32, u8]),
+            "or_rm_tx": (C.c_int, [u8, C.c_uint32, C.c_uint32, C.c_uint32, u8]),
+            "or_rm_rx": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, f32, f32]),
+            "or_decode_cb": (C.c_int, [C.c_void_p, f32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, u8,
+                                       C.POINTER(C.c_int)]),
+            "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
+            "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
+            "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
+            "or_pdsch_llr": (C.c_int, [C.POINTER(Cell), C.c_uint32, C.c_uint32, u8, C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_float, f32, f32, f32, C.POINTER(C.c_uint32), C.c_void_p]),
+            "or_pcfich": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32]),
+            "or_dlsch_decode": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_int, f32, C.c_uint32, C.c_uint32, u8, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint32)]),
+            "or_decode_subframe": (C.c_int, [C.POINTER(Cell), C.c_uint32, C.c_uint32, u8, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, f32, f32, C.c_uint32,
+                                             C.c_int, C.c_uint32, u8, C.POINTER(C.c_uint32)]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+# ------------------------------------------------------------------ convenience wrappers
+TDEC_STATE_BYTES = 4 + 4 * 6144 * 2 + 4 * 6144 * 3 + 4 * 6147 * 2 + 4 * 6148 * 8
+
+
+class Tdec:
+    def __init__(self):
+        self.buf = C.create_string_buffer(TDEC_STATE_BYTES + 64)
+
+    def decode_cb(self, llr, K, max_its=8, early_stop=True, crc24a=False):
+        bits = np.zeros(K, np.uint8)
+        ok = C.c_int(0)
+        its = lib().or_decode_cb(self.buf, np.ascontiguousarray(llr, np.float32), K, max_its,
+                                 int(early_stop), int(crc24a), bits, C.byref(ok))
+        return bits, its, bool(ok.value)
+
+
+def cbsegm(tbs):
+    s = CbSegm()
+    assert lib().or_cbsegm(tbs, C.byref(s)) == 0
+    return s
+
+
+def make_cell(cell_id=1, nof_prb=100, nof_ports=1):
+    return Cell(cell_id, nof_prb, nof_ports)
+
+
+def tx_cfg(cell, sf_idx=1, cfi=1, mcs=28, rv=0, rnti=0x46, tm=1, tbs=0, qm=0, prb=None, snr_db=30.0,
+           h=None, seed=0xA5A5, nl_td=2):
+    cfg = TxCfg()
+    cfg.cell = cell
+    cfg.sf_idx, cfg.cfi, cfg.mcs, cfg.rv, cfg.rnti, cfg.tm = sf_idx, cfi, mcs, rv, rnti, tm
+    cfg.tbs, cfg.qm = tbs, qm
+    for p in range(NRB_MAX):
+        cfg.prb_mask[p] = 1 if (p < cell.nof_prb and (prb is None or prb[p])) else 0
+    cfg.snr_db = snr_db
+    h = h if h is not None else [1.0 + 0j, 0.0 + 0j] if cell.nof_ports == 1 else [0.8 + 0.3j, -0.4 + 0.5j]
+    for p in range(2):
+        cfg.h_re[p] = h[p].real
+        cfg.h_im[p] = h[p].imag
+    cfg.noise_seed = seed
+    cfg.nl_td = nl_td
+    return cfg
+
+
+def tx_subframe(cfg, tb_bytes):
+    n = lib().or_sf_len(cfg.cell.nof_prb)
+    iq = np.zeros(2 * n, np.float32)
+    G = C.c_uint32(0)
+    assert lib().or_tx_subframe(C.byref(cfg), np.ascontiguousarray(tb_bytes, np.uint8), iq, C.byref(G)) == 0
+    return iq, G.value
+
+
+def splitmix_bytes(seed, n):
+    """TB payload generator: splitmix64 stream, little-endian bytes."""
+    out = np.zeros(((n + 7) // 8) * 8, np.uint8)
+    s = seed & 0xFFFFFFFFFFFFFFFF
+    M = 0xFFFFFFFFFFFFFFFF
+    for i in range(0, len(out), 8):
+        s = (s + 0x9E3779B97F4A7C15) & M
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out[i:i + 8] = np.frombuffer(z.to_bytes(8, "little"), np.uint8)
+    return out[:n]
