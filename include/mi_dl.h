@@ -1,0 +1,102 @@
+/*
+ * mi_dl.h -- batched MI355X LTE downlink PDSCH receiver (C ABI, no torch types).
+ *
+ * The batched extension SURVEY.md 8b asks for beside the per-TTI srsLTE API of
+ * include/srslte/srslte.h: N subframes (IQ resident in HBM) are taken through
+ *   OFDM RX -> CRS channel estimation -> equalisation -> soft demap -> descrambling ->
+ *   rate de-matching + HARQ combining -> max-log-MAP turbo decoding -> TB CRC -> payload
+ * by a fixed sequence of gfx950 kernels on one HIP stream.  The per-subframe work is what
+ * srsUE's phch_worker performs per TTI through srslte_ue_dl_decode_fft_estimate and
+ * srslte_pdsch_decode_rnti (/root/reference/ue/src/phy/phch_worker.cc:254, :347-348).
+ *
+ * Multi-GPU: one process per GPU, each with its own batch (subframes are independent; no
+ * collective on the data path).  All functions return 0 on success and a negative value on
+ * error, like the srsLTE API (SRSLTE_SUCCESS / SRSLTE_ERROR).
+ */
+#ifndef MI_DL_H
+#define MI_DL_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_DL_MAX_PRB 110
+
+typedef struct {
+  uint32_t cell_id;      /* N_ID^cell */
+  uint32_t nof_prb;      /* 6, 15, 25, 50, 75, 100 */
+  uint32_t nof_ports;    /* 1 or 2 CRS ports */
+  uint32_t sf_idx;       /* 0..9 */
+  uint32_t cfi;          /* 1..3 (control symbols) */
+  uint32_t tm;           /* 1 = single port, 2 = transmit diversity (SFBC) */
+  uint32_t nl_td;        /* N_L used by rate matching for TM2 (36.212 5.1.4.1.2: 2) */
+  uint32_t rnti;
+  uint32_t rv;           /* redundancy version 0..3 */
+  uint32_t tbs;          /* transport block size, bits */
+  uint32_t Qm;           /* 2, 4, 6 */
+  uint32_t new_tb;       /* 1 = first transmission (softbuffer overwritten), 0 = HARQ combine */
+  uint8_t  prb_mask[MI_DL_MAX_PRB];  /* allocated PRBs (same in both slots) */
+} mi_dl_sf_cfg_t;
+
+/* stages, for mi_dl_batch_stage_ms */
+enum { MI_DL_STAGE_OFDM = 0, MI_DL_STAGE_CHEST, MI_DL_STAGE_DEMAP, MI_DL_STAGE_RM, MI_DL_STAGE_TDEC,
+       MI_DL_STAGE_TB, MI_DL_NSTAGES };
+
+/* buffers that can be downloaded for parity checks */
+enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL_BUF_TB_CRC, MI_DL_BUF_TB_ITS,
+       MI_DL_BUF_METRICS, MI_DL_BUF_CB_ITS, MI_DL_BUF_CB_CRC };
+
+#define MI_DL_FLAG_PROFILE 1u  /* record HIP events around every stage of every run */
+
+typedef struct mi_dl_batch mi_dl_batch_t;
+
+/* Plans a batch (host work + device allocation, once).  max_its: turbo iteration cap
+ * (srslte_sch_set_max_noi), early stop on the code-block CRC as srsLTE does. */
+mi_dl_batch_t *mi_dl_batch_create(const mi_dl_sf_cfg_t *cfgs, uint32_t n_sf, uint32_t max_its, uint32_t flags);
+void   mi_dl_batch_destroy(mi_dl_batch_t *b);
+/* IQ layout: subframe i starts at sample (cf32) mi_dl_batch_iq_offset(b, i) */
+size_t mi_dl_batch_iq_offset(const mi_dl_batch_t *b, uint32_t sf);
+size_t mi_dl_batch_iq_samples(const mi_dl_batch_t *b);
+size_t mi_dl_batch_payload_offset(const mi_dl_batch_t *b, uint32_t sf);
+size_t mi_dl_batch_bytes(const mi_dl_batch_t *b, int which);       /* size of a downloadable buffer */
+size_t mi_dl_batch_offset(const mi_dl_batch_t *b, int which, uint32_t sf);  /* element offset per subframe */
+/* Enqueue the whole receive chain on `stream` (a hipStream_t; NULL = default stream).
+ * d_iq: device pointer to cf32 IQ, mi_dl_batch_iq_samples() samples.  Asynchronous. */
+int    mi_dl_batch_run(mi_dl_batch_t *b, const void *d_iq, void *stream);
+/* Run only the stages in stage_mask (bit i = MI_DL_STAGE_i) -- e.g. RM|TDEC|TB after
+ * mi_dl_batch_upload(MI_DL_BUF_LLR) to decode given soft bits (parity tests). */
+int    mi_dl_batch_run_stages(mi_dl_batch_t *b, const void *d_iq, void *stream, uint32_t stage_mask);
+/* Blocking copy of host data into a batch buffer (grid / ce / LLR injection for parity tests). */
+int    mi_dl_batch_upload(mi_dl_batch_t *b, int which, const void *host, size_t bytes);
+/* Blocking copy of a result buffer to host memory (synchronises the batch's last stream). */
+int    mi_dl_batch_download(mi_dl_batch_t *b, int which, void *host, size_t bytes);
+/* Device pointer of a result buffer (for zero-copy consumers). */
+void  *mi_dl_batch_device_ptr(mi_dl_batch_t *b, int which);
+/* Per-stage device time in ms, averaged over the runs since the last profile reset
+ * (MI_DL_FLAG_PROFILE: HIP events recorded on the run's stream around every stage; synchronises). */
+int    mi_dl_batch_stage_ms(mi_dl_batch_t *b, float *ms /* MI_DL_NSTAGES */, uint32_t *nruns);
+void   mi_dl_batch_profile_reset(mi_dl_batch_t *b);
+/* Algorithmic HBM bytes of one run (SURVEY.md 8d definitions) */
+double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = compulsory total */);
+uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
+uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
+
+/* ---- synthetic transmitter (eNB side, host) used to build benchmark input ------------------
+ * Mirrors srsLTE's PDSCH encode chain: CRC24A, segmentation, turbo code, rate matching,
+ * scrambling, QAM, SFBC, RE mapping + CRS + PCFICH, IFFT (1/sqrt N) + CP, flat per-port
+ * channel h and AWGN at snr_db per RE (>= 200 => noiseless).  iq: 2 * 15 N floats. */
+int    mi_tx_subframe(const mi_dl_sf_cfg_t *cfg, const uint8_t *tb, const float *h_re_im /* 2*ports */,
+                      float snr_db, uint64_t noise_seed, float *iq);
+int    mi_sf_len(uint32_t nof_prb);
+
+/* ---- device / runtime helpers ------------------------------------------------------------ */
+int    mi_device_count(void);
+int    mi_set_device(int dev);
+const char *mi_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,214 @@
+/*
+ * srslte/srslte.h -- srsLTE-1.0-compatible DOWNLINK subset, backed by MI355X (gfx950) kernels.
+ *
+ * srsUE (/root/reference) compiles against "srslte/srslte.h" (e.g. ue/hdr/phy/phch_worker.h:31)
+ * and requires srsLTE >= 1.0.0 (ue/hdr/srslte_version_check.h:30-41, checked at ue/src/ue.cc:39-49).
+ * This header declares the types and entry points srsUE's PHY worker calls on its DL data path
+ * (SURVEY.md 8b).  Each function cites the call site it replaces.  Field names that srsUE
+ * reads directly (ue_dl.sf_symbols, ue_dl.ce, ue_dl.pdsch, ue_dl.pdsch.dl_sch, ue_dl.pdsch_cfg.grant,
+ * ue_dl.chest, ue_dl.pdcch, ue_dl.last_n_cce, ue_dl.last_location) are kept.
+ *
+ * Out of scope here: PDCCH/DCI, PHICH, sync/cell search, uplink,
+ * PRACH, radio -- those still come from srsLTE itself.
+ *
+ * Conventions: 0 = SRSLTE_SUCCESS, -1 = SRSLTE_ERROR; srslte_pdsch_decode_rnti returns 0 iff
+ * the TB CRC passes; payload bits are packed MSB first.
+ */
+#ifndef SRSLTE_MI355X_H
+#define SRSLTE_MI355X_H
+#include <stdbool.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRSLTE_API __attribute__((visibility("default")))
+
+#define SRSLTE_VERSION_MAJOR 1
+#define SRSLTE_VERSION_MINOR 0
+#define SRSLTE_VERSION_PATCH 0
+#define SRSLTE_VERSION_STRING "1.0.0-mi355x"
+#define SRSLTE_VERSION_ENCODE(major, minor, patch) (((major) * 10000) + ((minor) * 100) + (patch))
+#define SRSLTE_VERSION SRSLTE_VERSION_ENCODE(SRSLTE_VERSION_MAJOR, SRSLTE_VERSION_MINOR, SRSLTE_VERSION_PATCH)
+#define SRSLTE_VERSION_CHECK(major, minor, patch) (SRSLTE_VERSION >= SRSLTE_VERSION_ENCODE(major, minor, patch))
+
+#define SRSLTE_SUCCESS 0
+#define SRSLTE_ERROR -1
+#define SRSLTE_ERROR_INVALID_INPUTS -2
+
+#define SRSLTE_MAX_PORTS 4
+#define SRSLTE_MAX_LAYERS 4
+#define SRSLTE_MAX_PRB 110
+#define SRSLTE_NRE 12
+#define SRSLTE_CP_NORM_NSYMB 7
+#define SRSLTE_NSUBFRAMES_X_FRAME 10
+#define SRSLTE_PDSCH_MAX_TDEC_ITERS 4   /* ue.conf.example:83 documents the default 4 */
+
+typedef _Complex float cf_t;
+
+typedef enum { SRSLTE_CP_NORM = 0, SRSLTE_CP_EXT } srslte_cp_t;
+typedef enum { SRSLTE_PHICH_NORM = 0, SRSLTE_PHICH_EXT } srslte_phich_length_t;
+typedef enum { SRSLTE_PHICH_R_1_6 = 0, SRSLTE_PHICH_R_1_2, SRSLTE_PHICH_R_1, SRSLTE_PHICH_R_2 } srslte_phich_resources_t;
+typedef enum { SRSLTE_MOD_BPSK = 0, SRSLTE_MOD_QPSK, SRSLTE_MOD_16QAM, SRSLTE_MOD_64QAM, SRSLTE_MOD_LAST } srslte_mod_t;
+typedef enum { SRSLTE_RNTI_USER = 0, SRSLTE_RNTI_SI, SRSLTE_RNTI_RAR, SRSLTE_RNTI_TEMP, SRSLTE_RNTI_SPS,
+               SRSLTE_RNTI_PCH, SRSLTE_RNTI_NOF_TYPES } srslte_rnti_type_t;
+typedef enum { SRSLTE_MIMO_TYPE_SINGLE_ANTENNA = 0, SRSLTE_MIMO_TYPE_TX_DIVERSITY,
+               SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX } srslte_mimo_type_t;
+
+/* srslte_cell_t, held by value by srsUE (phch_worker.h:101) */
+typedef struct SRSLTE_API {
+  uint32_t nof_prb;
+  uint32_t nof_ports;
+  uint32_t bw_idx;
+  uint32_t id;
+  srslte_cp_t cp;
+  srslte_phich_length_t phich_length;
+  srslte_phich_resources_t phich_resources;
+} srslte_cell_t;
+
+typedef struct SRSLTE_API {
+  srslte_mod_t mod;
+  int tbs;
+  uint32_t idx;
+} srslte_ra_mcs_t;
+
+/* DL grant (srslte_dci_msg_to_dl_grant output, phch_worker.cc:297; read at :355-364) */
+typedef struct SRSLTE_API {
+  bool prb_idx[2][SRSLTE_MAX_PRB];
+  uint32_t nof_prb;
+  uint32_t Qm;
+  srslte_ra_mcs_t mcs;
+} srslte_ra_dl_grant_t;
+
+typedef struct SRSLTE_API {
+  uint32_t nof_re;
+  uint32_t nof_symb;
+  uint32_t nof_bits;
+  uint32_t lstart;
+} srslte_ra_nbits_t;
+
+typedef struct SRSLTE_API {
+  uint32_t F, C, K1, K2, C1, C2, tbs;
+} srslte_cbsegm_t;
+
+typedef struct SRSLTE_API {
+  srslte_cbsegm_t cb_segm;
+  srslte_ra_dl_grant_t grant;
+  srslte_ra_nbits_t nbits;
+  uint32_t rv;
+  uint32_t sf_idx;
+  srslte_mimo_type_t mimo_type;
+  uint32_t nof_layers;
+} srslte_pdsch_cfg_t;
+
+/* HARQ softbuffer: embedded by value in srsUE's dl_harq_process (dl_harq.h:88); the soft bits
+ * live in HBM (group-interleaved layout, see srsue_amd/csrc/rm_body.h), dev is opaque. */
+typedef struct SRSLTE_API {
+  uint32_t max_cb;
+  float **buffer_f;       /* kept for layout compatibility; NULL (soft bits are device resident) */
+  void *dev;              /* device arena: 2 groups x [N_cb][64] floats (K- and K+ code blocks) */
+  uint64_t dev_bytes;
+} srslte_softbuffer_rx_t;
+
+typedef struct SRSLTE_API {
+  uint32_t max_iterations;
+  uint32_t nof_iterations;          /* srslte_pdsch_last_noi (phch_worker.cc:360,848) */
+  float average_nof_iterations;
+} srslte_sch_t;
+
+struct mi_ue_dl_ctx;
+
+typedef struct SRSLTE_API {
+  srslte_cell_t cell;
+  srslte_sch_t dl_sch;              /* srslte_sch_set_max_noi(&ue_dl.pdsch.dl_sch, n) (phch_worker.cc:88) */
+  uint16_t rnti;
+  bool rnti_is_set;
+  struct mi_ue_dl_ctx *ctx;
+} srslte_pdsch_t;
+
+typedef struct SRSLTE_API {
+  srslte_cell_t cell;
+  float rsrp, rssi, rsrq, noise_estimate, snr;
+} srslte_chest_dl_t;
+
+typedef struct SRSLTE_API {
+  uint32_t L;
+  uint32_t ncce;
+} srslte_dci_location_t;
+
+typedef struct SRSLTE_API {
+  srslte_cell_t cell;   /* PDCCH decoding stays on the host in srsLTE */
+  uint32_t nof_cce;
+} srslte_pdcch_t;
+
+/* srslte_ue_dl_t, owned by value per phch_worker (phch_worker.h:111) */
+typedef struct SRSLTE_API {
+  srslte_pdcch_t pdcch;
+  srslte_pdsch_t pdsch;
+  srslte_chest_dl_t chest;
+  srslte_pdsch_cfg_t pdsch_cfg;
+  srslte_cell_t cell;
+  cf_t *sf_symbols;                 /* host mirror of the OFDM grid (read by srslte_pdcch_extract_llr, :260) */
+  cf_t *ce[SRSLTE_MAX_PORTS];       /* host mirror of the channel estimates */
+  uint32_t cfi;
+  uint16_t current_rnti;
+  uint32_t last_n_cce;
+  srslte_dci_location_t last_location;
+  uint64_t pkt_errors, pkts_total;
+  struct mi_ue_dl_ctx *ctx;         /* MI355X device context: HIP stream + HBM workspace */
+} srslte_ue_dl_t;
+
+/* ---- version (ue.cc:39-49) ----------------------------------------------------------------- */
+SRSLTE_API int srslte_get_version_major(void);
+SRSLTE_API int srslte_get_version_minor(void);
+SRSLTE_API int srslte_get_version_patch(void);
+SRSLTE_API char *srslte_get_version(void);
+SRSLTE_API int srslte_check_version(int major, int minor, int patch);
+
+/* ---- UE DL (phch_worker.cc:74,104,127,254,337) ------------------------------------------------ */
+SRSLTE_API int srslte_ue_dl_init(srslte_ue_dl_t *q, srslte_cell_t cell);
+SRSLTE_API void srslte_ue_dl_free(srslte_ue_dl_t *q);
+SRSLTE_API void srslte_ue_dl_set_rnti(srslte_ue_dl_t *q, uint16_t rnti);
+SRSLTE_API int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t *q, cf_t *input, uint32_t sf_idx, uint32_t *cfi);
+SRSLTE_API int srslte_ue_dl_cfg_grant(srslte_ue_dl_t *q, srslte_ra_dl_grant_t *grant, uint32_t cfi, uint32_t sf_idx,
+                                      uint32_t rvidx);
+
+/* ---- PDSCH (phch_worker.cc:347-348, :360, :848; :88) ------------------------------------------ */
+SRSLTE_API int srslte_pdsch_decode_rnti(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
+                                        cf_t *sf_symbols, cf_t *ce[SRSLTE_MAX_PORTS], float noise_estimate,
+                                        uint16_t rnti, uint8_t *data);
+SRSLTE_API uint32_t srslte_pdsch_last_noi(srslte_pdsch_t *q);
+SRSLTE_API void srslte_sch_set_max_noi(srslte_sch_t *q, uint32_t max_iterations);
+
+/* ---- softbuffer (dl_harq.cc:169,174,232; ue_itf_test_sib1.cc:121,136) -------------------------- */
+SRSLTE_API int srslte_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
+SRSLTE_API void srslte_softbuffer_rx_free(srslte_softbuffer_rx_t *q);
+SRSLTE_API void srslte_softbuffer_rx_reset(srslte_softbuffer_rx_t *q);
+SRSLTE_API void srslte_softbuffer_rx_reset_tbs(srslte_softbuffer_rx_t *q, uint32_t tbs);
+
+/* ---- channel-estimation metrics (phch_worker.cc:359,512,519,799,821-823,842,847) --------------- */
+SRSLTE_API float srslte_chest_dl_get_snr(srslte_chest_dl_t *q);
+SRSLTE_API float srslte_chest_dl_get_rssi(srslte_chest_dl_t *q);
+SRSLTE_API float srslte_chest_dl_get_rsrp(srslte_chest_dl_t *q);
+SRSLTE_API float srslte_chest_dl_get_rsrq(srslte_chest_dl_t *q);
+SRSLTE_API float srslte_chest_dl_get_noise_estimate(srslte_chest_dl_t *q);
+
+/* ---- resource allocation helpers (phy.cc:118) ------------------------------------------------ */
+SRSLTE_API int srslte_ra_tbs_from_idx(uint32_t tbs_idx, uint32_t n_prb);
+SRSLTE_API int srslte_ra_tbs_idx_from_mcs(uint32_t mcs);
+SRSLTE_API srslte_mod_t srslte_ra_mod_from_mcs(uint32_t mcs);
+SRSLTE_API uint32_t srslte_mod_bits_x_symbol(srslte_mod_t mod);
+SRSLTE_API int srslte_cbsegm(srslte_cbsegm_t *s, uint32_t tbs);
+
+/* ---- misc (phch_worker.cc:69) ----------------------------------------------------------------- */
+#define SRSLTE_SF_LEN_PRB(nof_prb) (15 * srslte_symbol_sz(nof_prb))
+SRSLTE_API int srslte_symbol_sz(uint32_t nof_prb);
+SRSLTE_API void *srslte_vec_malloc(uint32_t size);   /* 256-B aligned, free()-compatible (phch_worker.cc:102) */
+SRSLTE_API void srslte_vec_free(void *ptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

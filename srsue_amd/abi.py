@@ -1,0 +1,204 @@
+"""ctypes bindings of the C ABI in include/mi_dl.h and include/srslte/srslte.h.
+
+The product is the C-ABI shared library srsue_amd/libsrsue_amd.so (gfx950 kernels + host C++);
+this module only binds it.  Loading fails loudly if the library has not been built -- there is no
+CPU fallback for the receive path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libsrsue_amd.so")
+EMU_PATH = os.path.join(PKG_DIR, "libsrsue_amd_emu.so")
+
+MAX_PRB = 110
+STAGES = ("ofdm", "chest", "demap", "rm", "tdec", "tb")
+BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF_CB_ITS, BUF_CB_CRC = range(9)
+FLAG_PROFILE = 1
+
+
+class SfCfg(C.Structure):
+    """mi_dl_sf_cfg_t (include/mi_dl.h)."""
+    _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "nof_ports", "sf_idx", "cfi", "tm", "nl_td",
+                                          "rnti", "rv", "tbs", "Qm", "new_tb")] + \
+               [("prb_mask", C.c_uint8 * MAX_PRB)]
+
+
+def sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=1, cfi=1, tm=None, rnti=0x46, rv=0, tbs=75376, Qm=6,
+           new_tb=1, prb=None, nl_td=2):
+    c = SfCfg()
+    c.cell_id, c.nof_prb, c.nof_ports, c.sf_idx, c.cfi = cell_id, nof_prb, nof_ports, sf_idx, cfi
+    c.tm = tm if tm is not None else (2 if nof_ports == 2 else 1)
+    c.nl_td, c.rnti, c.rv, c.tbs, c.Qm, c.new_tb = nl_td, rnti, rv, tbs, Qm, new_tb
+    for p in range(MAX_PRB):
+        c.prb_mask[p] = 1 if (p < nof_prb and (prb is None or prb[p])) else 0
+    return c
+
+
+def cfg_array(cfgs):
+    arr = (SfCfg * len(cfgs))()
+    for i, c in enumerate(cfgs):
+        arr[i] = c
+    return arr
+
+
+_lib = None
+_emu = None
+
+
+def lib():
+    """The product library; raises if it is missing (build with __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        vp, u32, sz = C.c_void_p, C.c_uint32, C.c_size_t
+        sig = {
+            "mi_dl_batch_create": (vp, [vp, u32, u32, u32]),
+            "mi_dl_batch_destroy": (None, [vp]),
+            "mi_dl_batch_iq_offset": (sz, [vp, u32]),
+            "mi_dl_batch_iq_samples": (sz, [vp]),
+            "mi_dl_batch_payload_offset": (sz, [vp, u32]),
+            "mi_dl_batch_bytes": (sz, [vp, C.c_int]),
+            "mi_dl_batch_offset": (sz, [vp, C.c_int, u32]),
+            "mi_dl_batch_run": (C.c_int, [vp, vp, vp]),
+            "mi_dl_batch_download": (C.c_int, [vp, C.c_int, vp, sz]),
+            "mi_dl_batch_run_stages": (C.c_int, [vp, vp, vp, u32]),
+            "mi_dl_batch_upload": (C.c_int, [vp, C.c_int, vp, sz]),
+            "mi_dl_batch_device_ptr": (vp, [vp, C.c_int]),
+            "mi_dl_batch_stage_ms": (C.c_int, [vp, vp, vp]),
+            "mi_dl_batch_profile_reset": (None, [vp]),
+            "mi_dl_batch_algo_bytes": (C.c_double, [vp, C.c_int]),
+            "mi_dl_batch_n_codeblocks": (u32, [vp]),
+            "mi_dl_batch_n_groups": (u32, [vp]),
+            "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
+            "mi_sf_len": (C.c_int, [u32]),
+            "mi_device_count": (C.c_int, []),
+            "mi_set_device": (C.c_int, [C.c_int]),
+            "mi_last_error": (C.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def emu():
+    """TEST-ONLY host emulation of the per-lane kernel bodies (never used by the product path)."""
+    global _emu
+    if _emu is None:
+        E = C.CDLL(EMU_PATH)
+        E.emu_decode_llr.restype = C.c_int
+        E.emu_decode_llr.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]
+        E.emu_payload_offset.restype = C.c_size_t
+        E.emu_payload_offset.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        _emu = E
+    return _emu
+
+
+def last_error():
+    return lib().mi_last_error().decode()
+
+
+def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
+    """Synthetic subframe from the product transmitter (mi_tx_subframe)."""
+    n = lib().mi_sf_len(cfg.nof_prb)
+    iq = np.zeros(2 * n, np.float32)
+    hh = None
+    if h is not None:
+        hh = np.zeros(4, np.float32)
+        for p, v in enumerate(h[:2]):
+            hh[2 * p], hh[2 * p + 1] = v.real, v.imag
+    tb = np.ascontiguousarray(tb_bytes, np.uint8)
+    rc = lib().mi_tx_subframe(C.byref(cfg), tb.ctypes.data, None if hh is None else hh.ctypes.data,
+                              float(snr_db), seed, iq.ctypes.data)
+    if rc:
+        raise RuntimeError("mi_tx_subframe failed")
+    return iq
+
+
+class Batch:
+    """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
+
+    def __init__(self, cfgs, max_its=4, profile=False):
+        self.cfgs = list(cfgs)
+        self._arr = cfg_array(self.cfgs)
+        self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its,
+                                          FLAG_PROFILE if profile else 0)
+        if not self.h:
+            raise RuntimeError("mi_dl_batch_create: " + last_error())
+
+    def close(self):
+        if self.h:
+            lib().mi_dl_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def iq_samples(self):
+        return lib().mi_dl_batch_iq_samples(self.h)
+
+    def iq_offset(self, sf):
+        return lib().mi_dl_batch_iq_offset(self.h, sf)
+
+    def run(self, d_iq_ptr, stream_ptr=None):
+        rc = lib().mi_dl_batch_run(self.h, C.c_void_p(d_iq_ptr), C.c_void_p(stream_ptr or 0))
+        if rc:
+            raise RuntimeError("mi_dl_batch_run: " + last_error())
+
+    def run_stages(self, mask, d_iq_ptr=None, stream_ptr=None):
+        rc = lib().mi_dl_batch_run_stages(self.h, C.c_void_p(d_iq_ptr or 0), C.c_void_p(stream_ptr or 0), mask)
+        if rc:
+            raise RuntimeError("mi_dl_batch_run_stages: " + last_error())
+
+    def upload(self, which, host_array):
+        a = np.ascontiguousarray(host_array)
+        if lib().mi_dl_batch_upload(self.h, which, a.ctypes.data, a.nbytes):
+            raise RuntimeError("upload: " + last_error())
+
+    def download(self, which, dtype):
+        n = lib().mi_dl_batch_bytes(self.h, which)
+        out = np.zeros(n // np.dtype(dtype).itemsize, dtype)
+        if lib().mi_dl_batch_download(self.h, which, out.ctypes.data, n):
+            raise RuntimeError("download: " + last_error())
+        return out
+
+    def offset(self, which, sf):
+        return lib().mi_dl_batch_offset(self.h, which, sf)
+
+    def stage_ms(self):
+        """Per-stage device ms averaged over the profiled runs since profile_reset()."""
+        ms = np.zeros(len(STAGES), np.float32)
+        n = C.c_uint32(0)
+        if lib().mi_dl_batch_stage_ms(self.h, ms.ctypes.data, C.byref(n)):
+            raise RuntimeError("stage_ms: " + last_error())
+        return dict(zip(STAGES, ms.tolist())), n.value
+
+    def profile_reset(self):
+        lib().mi_dl_batch_profile_reset(self.h)
+
+    def algo_bytes(self, stage=-1):
+        return lib().mi_dl_batch_algo_bytes(self.h, stage)
+
+    @property
+    def n_codeblocks(self):
+        return lib().mi_dl_batch_n_codeblocks(self.h)
+
+    @property
+    def n_groups(self):
+        return lib().mi_dl_batch_n_groups(self.h)
+
+    def payload(self, sf, all_payload=None):
+        p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)
+        off = lib().mi_dl_batch_payload_offset(self.h, sf)
+        return p[off:off + self.cfgs[sf].tbs // 8]

@@ -1,0 +1,130 @@
+// batch.cpp -- C ABI of the batched receiver (include/mi_dl.h).
+#include <string.h>
+
+#include "engine.h"
+#include "kernels.h"
+
+namespace mi { const char* last_error(); }
+
+struct mi_dl_batch {
+  mi::Engine eng;
+  std::vector<mi_dl_sf_cfg_t> cfgs;
+};
+
+extern "C" {
+
+mi_dl_batch_t* mi_dl_batch_create(const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf, uint32_t max_its, uint32_t flags) {
+  if (!cfgs || !n_sf) { mi::set_error("empty batch"); return nullptr; }
+  auto* b = new mi_dl_batch();
+  b->cfgs.assign(cfgs, cfgs + n_sf);
+  b->eng.max_its = max_its ? max_its : 4;
+  b->eng.flags = flags;
+  (void)hipGetDevice(&b->eng.device);
+  if (b->eng.plan.build(cfgs, n_sf, true) || b->eng.upload(nullptr, true) ||
+      !mi::hip_ok(hipStreamSynchronize(nullptr), "upload sync")) {
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+
+void mi_dl_batch_destroy(mi_dl_batch_t* b) { delete b; }
+
+size_t mi_dl_batch_iq_offset(const mi_dl_batch_t* b, uint32_t sf) {
+  return sf < b->eng.plan.sfs.size() ? b->eng.plan.sfs[sf].iq_off : 0;
+}
+size_t mi_dl_batch_iq_samples(const mi_dl_batch_t* b) { return b->eng.plan.iq_samples; }
+size_t mi_dl_batch_payload_offset(const mi_dl_batch_t* b, uint32_t sf) {
+  return sf < b->eng.plan.tbs.size() ? b->eng.plan.tbs[sf].pay_off : 0;
+}
+
+static mi::DevBuf* buf_of(mi_dl_batch_t* b, int which, size_t* bytes) {
+  const mi::Plan& P = b->eng.plan;
+  const size_t nsf = P.sfs.size();
+  switch (which) {
+    case MI_DL_BUF_GRID: *bytes = P.grid_elems * 8; return &b->eng.d_grid;
+    case MI_DL_BUF_CE: *bytes = P.ce_elems * 8; return &b->eng.d_ce;
+    case MI_DL_BUF_LLR: *bytes = P.e_floats * 4; return &b->eng.d_e;
+    case MI_DL_BUF_PAYLOAD: *bytes = P.payload_bytes; return &b->eng.d_payload;
+    case MI_DL_BUF_TB_CRC: *bytes = nsf * 4; return &b->eng.d_tbok;
+    case MI_DL_BUF_TB_ITS: *bytes = nsf * 4; return &b->eng.d_tbits;
+    case MI_DL_BUF_METRICS: *bytes = nsf * 5 * 4; return &b->eng.d_metrics;
+    case MI_DL_BUF_CB_ITS: *bytes = P.lanes.size() * 4; return &b->eng.d_cbits;
+    case MI_DL_BUF_CB_CRC: *bytes = P.lanes.size() * 4; return &b->eng.d_cbcrc;
+  }
+  *bytes = 0;
+  return nullptr;
+}
+
+size_t mi_dl_batch_bytes(const mi_dl_batch_t* b, int which) {
+  size_t n = 0;
+  buf_of(const_cast<mi_dl_batch_t*>(b), which, &n);
+  return n;
+}
+
+size_t mi_dl_batch_offset(const mi_dl_batch_t* b, int which, uint32_t sf) {
+  const mi::Plan& P = b->eng.plan;
+  if (sf >= P.sfs.size()) return 0;
+  switch (which) {
+    case MI_DL_BUF_GRID: return P.sfs[sf].grid_off;
+    case MI_DL_BUF_CE: return P.sfs[sf].ce_off;
+    case MI_DL_BUF_LLR: return P.sfs[sf].e_off;
+    case MI_DL_BUF_PAYLOAD: return P.tbs[sf].pay_off;
+    default: return sf;
+  }
+}
+
+int mi_dl_batch_run(mi_dl_batch_t* b, const void* d_iq, void* stream) {
+  if (!b || !d_iq) { mi::set_error("null argument"); return -1; }
+  return b->eng.run(d_iq, reinterpret_cast<hipStream_t>(stream), 0xFFFFFFFFu, nullptr);
+}
+
+int mi_dl_batch_run_stages(mi_dl_batch_t* b, const void* d_iq, void* stream, uint32_t mask) {
+  if (!b) { mi::set_error("null argument"); return -1; }
+  if ((mask & 1u) && !d_iq) { mi::set_error("OFDM stage needs IQ"); return -1; }
+  return b->eng.run(d_iq, reinterpret_cast<hipStream_t>(stream), mask, nullptr);
+}
+
+int mi_dl_batch_upload(mi_dl_batch_t* b, int which, const void* host, size_t bytes) {
+  size_t n = 0;
+  mi::DevBuf* d = buf_of(b, which, &n);
+  if (!d || bytes > n) { mi::set_error("bad buffer or size"); return -1; }
+  if (!mi::hip_ok(hipStreamSynchronize(b->eng.last_stream), "sync")) return -1;
+  return mi::hip_ok(hipMemcpy(d->p, host, bytes, hipMemcpyHostToDevice), "upload") ? 0 : -1;
+}
+
+int mi_dl_batch_download(mi_dl_batch_t* b, int which, void* host, size_t bytes) {
+  size_t n = 0;
+  mi::DevBuf* d = buf_of(b, which, &n);
+  if (!d || bytes > n) { mi::set_error("bad buffer or size"); return -1; }
+  if (!mi::hip_ok(hipStreamSynchronize(b->eng.last_stream), "sync")) return -1;
+  return mi::hip_ok(hipMemcpy(host, d->p, bytes, hipMemcpyDeviceToHost), "download") ? 0 : -1;
+}
+
+void* mi_dl_batch_device_ptr(mi_dl_batch_t* b, int which) {
+  size_t n = 0;
+  mi::DevBuf* d = buf_of(b, which, &n);
+  return d ? d->p : nullptr;
+}
+
+int mi_dl_batch_stage_ms(mi_dl_batch_t* b, float* ms, uint32_t* nruns) { return b->eng.stage_ms(ms, nruns); }
+void mi_dl_batch_profile_reset(mi_dl_batch_t* b) { b->eng.profile_reset(); }
+
+double mi_dl_batch_algo_bytes(const mi_dl_batch_t* b, int which_stage) {
+  if (which_stage < 0) return b->eng.plan.bytes_compulsory;
+  if (which_stage >= MI_DL_NSTAGES) return 0;
+  return b->eng.plan.stage_bytes[which_stage];
+}
+
+uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t* b) { return b->eng.plan.n_cb; }
+uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
+
+int mi_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+int mi_set_device(int dev) { return mi::hip_ok(hipSetDevice(dev), "hipSetDevice") ? 0 : -1; }
+const char* mi_last_error(void) { return mi::last_error(); }
+
+}  // extern "C"

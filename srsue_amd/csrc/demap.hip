@@ -1,0 +1,126 @@
+// demap.hip -- PDSCH RE gather + equalisation + max-log soft demapping + descrambling.
+//
+// Replaces, inside srslte_pdsch_decode_rnti (/root/reference/ue/src/phy/phch_worker.cc:347-348,
+// noise_estimate = 0.01 from :340): srslte_pdsch_get (RE gather), srslte_predecoding_single /
+// srslte_predecoding_diversity + layerdemap (TM1 / TM2 SFBC), srslte_demod_soft_demodulate
+// (max-log, sigma^2 = 0.5, LLR > 0 => bit 1) and srslte_scrambling_f (c(i) = 1 flips the sign).
+//
+// One lane per RE (TM1) or per SFBC RE pair (TM2).  The RE list (36.211 6.3.5 mapping order) is
+// a per-configuration device table, so grid/ce reads walk consecutive subcarriers and every lane
+// writes its Qm LLRs contiguously (float2 stores): the LLR stream leaves fully coalesced.
+#include "kernels.h"
+
+namespace mi {
+
+template <int QM>
+__device__ __forceinline__ float pam_level(int lab) {
+  // lab: this dimension's bits, MSB first (36.211 7.1 Gray mapping, separable I/Q)
+  if constexpr (QM == 2) {
+    return (1 - 2 * (lab & 1)) * 0.70710678118654752440f;
+  } else if constexpr (QM == 4) {
+    const int b0 = (lab >> 1) & 1, b1 = lab & 1;
+    return (float)((1 - 2 * b0) * (1 + 2 * b1)) * 0.31622776601683793320f;
+  } else {
+    const int b0 = (lab >> 2) & 1, b1 = (lab >> 1) & 1, b2 = lab & 1;
+    return (float)((1 - 2 * b0) * (4 - (1 - 2 * b1) * (2 - (1 - 2 * b2)))) * 0.15430334996209191026f;
+  }
+}
+
+// writes the QM/2 LLRs of one dimension at llr[0], llr[2], llr[4] (I at even, Q at odd slots)
+template <int QM>
+__device__ __forceinline__ void demap_dim(float x, float* llr) {
+  constexpr int NB = QM / 2, NL = 1 << NB;
+  float d2[NL];
+#pragma unroll
+  for (int lab = 0; lab < NL; lab++) {
+    const float d = x - pam_level<QM>(lab);
+    d2[lab] = d * d;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    float m0 = 3.0e38f, m1 = 3.0e38f;
+#pragma unroll
+    for (int lab = 0; lab < NL; lab++) {
+      if ((lab >> (NB - 1 - j)) & 1) m1 = fminf(m1, d2[lab]); else m0 = fminf(m0, d2[lab]);
+    }
+    llr[2 * j] = (m0 - m1) * 2.0f;   // / sigma^2, sigma^2 = 0.5
+  }
+}
+
+template <int QM>
+__device__ __forceinline__ void demap_store(float2 x, const uint32_t* __restrict__ scr, uint32_t bit0,
+                                            float* __restrict__ out) {
+  float l[QM];
+  demap_dim<QM>(x.x, l);
+  demap_dim<QM>(x.y, l + 1);
+#pragma unroll
+  for (int b = 0; b < QM; b++) {
+    const uint32_t i = bit0 + b;
+    if ((scr[i >> 5] >> (i & 31)) & 1u) l[b] = -l[b];
+  }
+  float2* o = reinterpret_cast<float2*>(out + bit0);
+#pragma unroll
+  for (int b = 0; b < QM; b += 2) o[b / 2] = make_float2(l[b], l[b + 1]);
+}
+
+template <int QM>
+__device__ __forceinline__ void demap_unit(const MiPdschDesc& pd, uint32_t u, const float2* __restrict__ g,
+                                           const float2* __restrict__ c0, const float2* __restrict__ c1,
+                                           const uint32_t* __restrict__ re, const uint32_t* __restrict__ scr,
+                                           float* __restrict__ e, float noise) {
+  if (pd.tm != 2) {
+    const uint32_t r = re[u];
+    const float2 y = g[r], h = c0[r];
+    const float den = h.x * h.x + h.y * h.y + noise;
+    const float2 x = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
+    demap_store<QM>(x, scr, u * QM, e);
+  } else {
+    const uint32_t ra = re[2 * u], rb = re[2 * u + 1];
+    const float2 r0 = g[ra], r1 = g[rb];
+    const float2 h00 = c0[ra], h01 = c0[rb], h10 = c1[ra], h11 = c1[rb];
+    float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
+    if (hh <= 0.f) hh = 1e-9f;
+    const float s = 1.41421356237309504880f / hh;
+    const float2 x0 = make_float2(s * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
+                                  s * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
+    const float2 x1 = make_float2(s * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
+                                  s * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
+    demap_store<QM>(x0, scr, 2 * u * QM, e);
+    demap_store<QM>(x1, scr, (2 * u + 1) * QM, e);
+  }
+}
+
+__global__ __launch_bounds__(256) void demap_kernel(const float2* __restrict__ grid, const float2* __restrict__ ce,
+                                                   float* __restrict__ e, const MiSfDesc* __restrict__ sfs,
+                                                   const MiPdschDesc* __restrict__ pds,
+                                                   const MiCellDesc* __restrict__ cells,
+                                                   const uint32_t* __restrict__ re_tab,
+                                                   const uint32_t* __restrict__ scr_tab, float noise) {
+  const MiSfDesc d = sfs[blockIdx.y];
+  const MiPdschDesc pd = pds[d.pdsch];
+  const uint32_t units = pd.tm == 2 ? pd.nre / 2 : pd.nre;
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= units) return;
+  const MiCellDesc c = cells[d.cell];
+  const float2* g = grid + d.grid_off;
+  const float2* c0 = ce + d.ce_off;
+  const float2* c1 = c0 + (size_t)NSYMB * c.W;
+  const uint32_t* re = re_tab + pd.re_off;
+  const uint32_t* scr = scr_tab + pd.scr_off;
+  float* out = e + d.e_off;
+  switch (pd.Qm) {
+    case 2: demap_unit<2>(pd, u, g, c0, c1, re, scr, out, noise); break;
+    case 4: demap_unit<4>(pd, u, g, c0, c1, re, scr, out, noise); break;
+    default: demap_unit<6>(pd, u, g, c0, c1, re, scr, out, noise); break;
+  }
+}
+
+void launch_demap(const float2* grid, const float2* ce, float* e, const MiSfDesc* sfs, const MiPdschDesc* pd,
+                  const MiCellDesc* cells, const uint32_t* re_tab, const uint32_t* scr, uint32_t n_sf,
+                  uint32_t max_units, float noise, hipStream_t st) {
+  if (!n_sf || !max_units) return;
+  dim3 g((max_units + 255) / 256, n_sf);
+  hipLaunchKernelGGL(demap_kernel, g, dim3(256), 0, st, grid, ce, e, sfs, pd, cells, re_tab, scr, noise);
+}
+
+}  // namespace mi

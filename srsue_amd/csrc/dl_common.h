@@ -1,0 +1,113 @@
+// dl_common.h -- shared host/device definitions for the MI355X LTE DL PDSCH path.
+//
+// The path replaces what srsUE reaches through srslte_ue_dl_decode_fft_estimate and
+// srslte_pdsch_decode_rnti (/root/reference/ue/src/phy/phch_worker.cc:254, :347-348).
+// Everything here is spec arithmetic (3GPP TS 36.211 / 36.212 / 36.213) shared by the host
+// planner and the gfx950 kernels.
+#pragma once
+#include <stdint.h>
+#if defined(MI_EMU)
+// host-only emulation build (tests): plain C++ stand-ins for the HIP vector type / qualifiers
+#include <math.h>
+#define __host__
+#define __device__
+struct float2 { float x, y; };
+inline float2 make_float2(float a, float b) { return float2{a, b}; }
+#else
+#include <hip/hip_runtime.h>
+#endif
+
+namespace mi {
+
+constexpr int NRB_MAX = 110;
+constexpr int NSYMB = 14;            // normal CP, symbols per subframe
+constexpr int KMAX = 6144;           // largest turbo code block
+constexpr int NCB_MAX = 3 * 32 * ((KMAX + 4 + 31) / 32);   // 18528
+constexpr int LANES = 64;            // code blocks per wavefront group (one CB per lane)
+constexpr int BETA_W = 8;            // beta checkpoint spacing in the turbo kernel
+constexpr float FILLER_LLR = -10000.0f;
+
+__host__ __device__ inline int symbol_sz(uint32_t nof_prb) {
+  return nof_prb <= 6 ? 128 : nof_prb <= 15 ? 256 : nof_prb <= 25 ? 512 : nof_prb <= 50 ? 1024
+       : nof_prb <= 75 ? 1536 : nof_prb <= 110 ? 2048 : -1;
+}
+__host__ __device__ inline int cp_len(int N, int l_in_slot) { return (l_in_slot == 0 ? 160 : 144) * N / 2048; }
+__host__ __device__ inline int sf_len(int N) { return 15 * N; }
+// sample offset of the useful part of OFDM symbol l (0..13) inside the subframe
+__host__ __device__ inline int symbol_offset(int N, int l) {
+  int slot = l / 7, lp = l % 7;
+  int off = slot * (15 * N / 2);
+  for (int q = 0; q < lp; q++) off += cp_len(N, q) + N;
+  return off + cp_len(N, lp);
+}
+// FFT bin of grid subcarrier k (DC skipped), 36.211 6.12
+__host__ __device__ inline int sc_bin(int k, int W, int N) { return k < W / 2 ? N - W / 2 + k : k - W / 2 + 1; }
+
+// 36.212 5.1.4.1.1 inter-column permutation
+__host__ __device__ inline uint32_t subblock_perm(uint32_t c) {
+  // bit-reversal of the 5-bit column index
+  return ((c & 1) << 4) | ((c & 2) << 2) | (c & 4) | ((c & 8) >> 2) | ((c & 16) >> 4);
+}
+
+}  // namespace mi
+
+// --------------------------------------------------------------------------------------------
+// Device-side descriptors built by the host planner (plan.cpp) and read by the kernels.
+// --------------------------------------------------------------------------------------------
+struct MiCellDesc {          // one per distinct (cell id, nof_prb, nof_ports)
+  uint32_t id, nof_prb, nof_ports, N, W;
+  uint32_t crs_off;          // float2 offset of CRS table [20 ns][2 l'][220]
+};
+
+struct MiPdschDesc {         // one per distinct PDSCH mapping (cell, cfi, sf, prb mask, Qm, tm, rnti)
+  uint32_t cell;             // index into MiCellDesc
+  uint32_t sf_idx, nre, Qm, tm, G;
+  uint32_t re_off;           // offset into the RE index table (uint32 grid indices)
+  uint32_t scr_off;          // offset into scrambling word table (uint32 words, bit i = word[i/32] >> (i%32))
+};
+
+struct MiSfDesc {            // one per subframe of the batch
+  uint64_t iq_off;           // float2 offset into the IQ batch buffer
+  uint64_t grid_off;         // float2 offset into grid buffer (ce uses nof_ports * same stride)
+  uint64_t ce_off;
+  uint64_t e_off;            // float offset into the LLR buffer
+  uint32_t pdsch;            // MiPdschDesc index
+  uint32_t cell;             // MiCellDesc index
+  uint32_t sf_idx;
+  uint32_t tb;               // TB index
+};
+
+struct MiLaneDesc {          // one per code block (lane of a group)
+  uint64_t e_off;            // float offset of this CB's E LLRs
+  uint32_t E;
+  uint32_t r0;               // number of non-null circular-buffer positions before k0(rv)
+  uint32_t Nv;               // non-null circular-buffer positions (depends on K and F)
+  uint32_t F;                // filler bits (only CB 0 of a TB may have F > 0)
+  uint32_t rank_off;         // int32 offset of this (K, F)'s rank table [Ncb] (-1 = <NULL>)
+  uint32_t new_tb;           // 1 = first transmission (overwrite softbuffer), 0 = combine
+  uint32_t crc24a;           // 1 when C == 1 (code-block CRC is the TB CRC24A)
+  uint32_t tb;               // owning TB
+  uint32_t valid;            // 0 for padding lanes of a partial group
+  uint32_t pad;
+};
+
+struct MiGroupDesc {         // one per wavefront group of <= 64 code blocks of equal K
+  uint32_t K, Ncb;
+  uint32_t lane0;            // first MiLaneDesc index (64 consecutive entries)
+  uint32_t ktab;             // K-table index (pos / pi tables)
+  uint64_t sb_off;           // float offset of the group's softbuffer region [Ncb][64]
+  uint64_t scratch_off;      // float offset of the group's turbo scratch (w, llr1, beta ckpt)
+  uint64_t dec_off;          // byte offset of decision bytes [K][64]
+};
+
+struct MiKTab {              // per K, device resident
+  uint32_t K, Ncb;
+  uint32_t pos_off;          // uint32 offset: pos[3*(K+4)] circular-buffer position of d_i(k)
+  uint32_t pi_off;           // uint32 offset: pi[K]
+};
+
+struct MiTbDesc {            // one per transport block
+  uint32_t tbs, C, Kp, Km, Cm, F;
+  uint32_t cb_list;          // offset into the lane-index list: C entries, CB r -> MiLaneDesc index
+  uint32_t pay_off;          // byte offset into payload buffer
+};

@@ -1,0 +1,89 @@
+// emu.cpp -- TEST-ONLY host emulation of the per-lane kernel bodies (rm_body.h, tdec_body.h,
+// tb_body.h) driven by the real planner.  Built into libsrsue_amd_emu.so with g++ -DMI_EMU; it is
+// never linked into the product library.  Lanes of those kernels never communicate, so running
+// each lane's code to completion in turn reproduces the GPU result operation for operation; the
+// CPU test suite uses it to check planner + rate de-matching + turbo + TB assembly bit-exactly
+// against the oracle without a GPU.
+#include <string.h>
+
+#include <vector>
+
+#include "kernels_consts.h"
+#include "plan.h"
+#include "rm_body.h"
+#include "tb_body.h"
+#include "tdec_body.h"
+
+extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
+                              uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
+  mi::Plan P;
+  if (P.build(cfgs, n, true)) return -1;
+  std::vector<float> e(P.e_floats, 0.f), sb(P.sb_floats, 0.f), scr(P.scratch_floats, 0.f);
+  std::vector<uint8_t> dec(P.dec_bytes, 0), cbb(P.lanes.size() * mi::CB_BYTES_STRIDE, 0);
+  std::vector<uint32_t> cits(P.lanes.size(), 0), ccrc(P.lanes.size(), 0);
+  size_t src = 0;
+  for (uint32_t s = 0; s < n; s++) {
+    const uint32_t G = P.pds[P.sfs[s].pdsch].G;
+    memcpy(&e[P.sfs[s].e_off], llr_concat + src, G * sizeof(float));
+    src += G;
+  }
+  for (const MiGroupDesc& g : P.groups) {
+    for (int lane = 0; lane < mi::LANES; lane++) {
+      const MiLaneDesc& ld = P.lanes[g.lane0 + lane];
+      if (!ld.valid) continue;
+      const int32_t* rank = reinterpret_cast<const int32_t*>(&P.kdata[ld.rank_off]);
+      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_one(ld, rank, e.data(), &sb[g.sb_off], p, lane);
+    }
+    const MiKTab& kt = P.ktabs[g.ktab];
+    for (int lane = 0; lane < mi::LANES; lane++) {
+      const uint32_t li = g.lane0 + lane;
+      const MiLaneDesc& ld = P.lanes[li];
+      if (!ld.valid) continue;
+      mi::TdecArgs a;
+      a.sb = &sb[g.sb_off];
+      a.pos = &P.kdata[kt.pos_off];
+      a.pi = &P.kdata[kt.pi_off];
+      a.scr = &scr[g.scratch_off];
+      a.dec = &dec[g.dec_off];
+      a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
+      a.K = g.K; a.F = ld.F; a.max_its = max_its; a.early_stop = 1; a.crc24a = ld.crc24a;
+      mi::TdecLaneResult r = mi::tdec_lane(a, lane);
+      cits[li] = r.its;
+      ccrc[li] = r.crc_ok;
+    }
+  }
+  for (uint32_t t = 0; t < n; t++) {
+    const MiTbDesc& tb = P.tbs[t];
+    const uint32_t* lanes = &P.cb_list[tb.cb_list];
+    const uint32_t nbytes = (tb.tbs + 24) / 8;
+    std::vector<uint8_t> buf(nbytes);
+    for (uint32_t j = 0; j < nbytes; j++) {
+      uint32_t r, off;
+      mi::tb_byte_src(tb, j, r, off);
+      buf[j] = cbb[(size_t)lanes[r] * mi::CB_BYTES_STRIDE + off];
+    }
+    memcpy(payload + tb.pay_off, buf.data(), tb.tbs / 8);
+    // parallel-CRC formulation of the GPU kernel with 256 segments
+    const uint32_t seg = (nbytes + 255) / 256;
+    uint32_t crc = 0;
+    for (uint32_t th = 0; th < 256; th++) {
+      const uint32_t b0 = th * seg;
+      if (b0 >= nbytes) continue;
+      const uint32_t m = (b0 + seg <= nbytes) ? seg : nbytes - b0;
+      uint32_t c = mi::crc24_bytes(buf.data() + b0, m, mi::CRC24A_POLY);
+      crc ^= mi::gf24_mulmod(c, mi::gf24_xpow8(nbytes - b0 - m, mi::CRC24A_POLY), mi::CRC24A_POLY);
+    }
+    tb_ok[t] = crc == 0;
+    uint32_t its = 0;
+    for (uint32_t r = 0; r < tb.C; r++) its = cits[lanes[r]] > its ? cits[lanes[r]] : its;
+    tb_its[t] = its;
+  }
+  if (cb_its) memcpy(cb_its, cits.data(), cits.size() * 4);
+  return 0;
+}
+
+extern "C" size_t emu_payload_offset(const mi_dl_sf_cfg_t* cfgs, uint32_t n, uint32_t sf) {
+  mi::Plan P;
+  if (P.build(cfgs, n, true)) return 0;
+  return P.tbs[sf].pay_off;
+}

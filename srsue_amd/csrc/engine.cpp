@@ -1,0 +1,165 @@
+// engine.cpp -- batch planner, HBM workspace and kernel launch sequence (see engine.h).
+//
+// Planning happens once per batch (or once per TTI with cached tables for the per-TTI srsLTE
+// API): resource-element lists, scrambling words, CRS tables, code-block segmentation, rate
+// matching splits and the grouping of code blocks into 64-lane wavefront groups of equal K.
+// run() only enqueues kernels on the caller's stream, so it can be captured in a HIP graph.
+#include "engine.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "kernels.h"
+
+namespace mi {
+
+bool hip_ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return false;
+}
+
+bool DevBuf::ensure(size_t n) {
+  if (n <= bytes && p) return true;
+  release();
+  size_t a = (n + 255) & ~(size_t)255;
+  if (a == 0) a = 256;
+  if (!hip_ok(hipMalloc(&p, a), "hipMalloc")) { p = nullptr; bytes = 0; return false; }
+  bytes = a;
+  return true;
+}
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+Engine::~Engine() {
+  for (auto& set : ev_sets)
+    for (auto& e : set) (void)hipEventDestroy(e);
+}
+
+template <class T>
+static bool up(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
+  if (!b.ensure(sizeof(T) * std::max<size_t>(v.size(), 1))) return false;
+  if (v.empty()) return true;
+  return hip_ok(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st), "upload");
+}
+
+int Engine::upload(hipStream_t st, bool alloc_sb) {
+  const Plan& P = plan;
+  bool ok = up(d_cells, P.cells, st) && up(d_crs, P.crs, st) && up(d_pds, P.pds, st) && up(d_re, P.re_tab, st) &&
+            up(d_scr, P.scr_tab, st) && up(d_sfs, P.sfs, st) && up(d_lanes, P.lanes, st) &&
+            up(d_groups, P.groups, st) && up(d_ktabs, P.ktabs, st) && up(d_kdata, P.kdata, st) &&
+            up(d_tbs, P.tbs, st) && up(d_cblist, P.cb_list, st) && up(d_fftlist, P.fft_list_flat, st);
+  if (!ok) return -1;
+  // twiddles per FFT size (double precision on the host)
+  bool need_tw = false;
+  for (auto& fl : P.fft_lists) need_tw |= !tw_off.count(fl.first);
+  if (need_tw) {
+    std::vector<float> tw;
+    tw_off.clear();
+    for (int N : {128, 256, 512, 1024, 1536, 2048}) {
+      tw_off[N] = tw.size() / 2;
+      for (int t = 0; t < N; t++) {
+        tw.push_back((float)cos(-2.0 * M_PI * t / N));
+        tw.push_back((float)sin(-2.0 * M_PI * t / N));
+      }
+    }
+    if (!up(d_tw, tw, st)) return -1;
+  }
+  const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
+  ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
+  if (P.has_pdsch) {
+    ok = ok && d_e.ensure(P.e_floats * 4) && d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
+         d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
+         d_cbcrc.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
+         d_tbits.ensure(nsf * 4);
+    if (alloc_sb) {
+      size_t before = d_sb.bytes;
+      ok = ok && d_sb.ensure(P.sb_floats * 4);
+      if (ok && d_sb.bytes != before) ok = hip_ok(hipMemsetAsync(d_sb.p, 0, d_sb.bytes, st), "memset sb");
+    }
+  }
+  return ok ? 0 : -1;
+}
+
+int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_override) {
+  const Plan& P = plan;
+  last_stream = st;
+  const bool prof = flags & MI_DL_FLAG_PROFILE;
+  hipEvent_t* ev = nullptr;
+  if (prof) {
+    if (ev_used == ev_sets.size()) {
+      std::vector<hipEvent_t> set(MI_DL_NSTAGES + 1);
+      for (auto& e : set)
+        if (!hip_ok(hipEventCreate(&e), "event")) return -1;
+      ev_sets.push_back(set);
+    }
+    ev = ev_sets[ev_used++].data();
+  }
+  auto mark = [&](int i) {
+    if (prof) (void)hipEventRecord(ev[i], st);
+  };
+  const uint32_t nsf = (uint32_t)P.sfs.size();
+  mark(0);
+  if (mask & (1u << MI_DL_STAGE_OFDM)) {
+    for (size_t i = 0; i < P.fft_lists.size(); i++) {
+      const int N = P.fft_lists[i].first;
+      launch_ofdm_rx(N, reinterpret_cast<const float2*>(d_iq), d_grid.as<float2>(), d_sfs.as<MiSfDesc>(),
+                     d_fftlist.as<uint32_t>() + P.fft_list_off[i], (uint32_t)P.fft_lists[i].second.size(),
+                     d_tw.as<float2>() + tw_off[N], P.fft_W[i], st);
+    }
+  }
+  mark(1);
+  if (mask & (1u << MI_DL_STAGE_CHEST))
+    launch_chest(d_grid.as<float2>(), d_ce.as<float2>(), d_sfs.as<MiSfDesc>(), d_cells.as<MiCellDesc>(),
+                 d_crs.as<float2>(), d_metrics.as<float>(), nsf, st);
+  mark(2);
+  if (P.has_pdsch) {
+    float* sb = sb_override ? sb_override : d_sb.as<float>();
+    if (mask & (1u << MI_DL_STAGE_DEMAP))
+      launch_demap(d_grid.as<float2>(), d_ce.as<float2>(), d_e.as<float>(), d_sfs.as<MiSfDesc>(),
+                   d_pds.as<MiPdschDesc>(), d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), nsf,
+                   P.max_units, noise, st);
+    mark(3);
+    if (mask & (1u << MI_DL_STAGE_RM))
+      launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+                        d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
+    mark(4);
+    if (mask & (1u << MI_DL_STAGE_TDEC))
+      launch_tdec(sb, d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
+                  d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(),
+                  d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop, st);
+    mark(5);
+    if (mask & (1u << MI_DL_STAGE_TB))
+      launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
+                d_cbits.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(), d_cblist.as<uint32_t>(), st);
+    mark(6);
+  } else {
+    for (int i = 3; i <= 6; i++) mark(i);
+  }
+  return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
+}
+
+int Engine::stage_ms(float* ms, uint32_t* nruns) {
+  if (!ev_used) { set_error("no profiled run (MI_DL_FLAG_PROFILE)"); return -1; }
+  for (int i = 0; i < MI_DL_NSTAGES; i++) ms[i] = 0.f;
+  for (size_t r = 0; r < ev_used; r++) {
+    hipEvent_t* ev = ev_sets[r].data();
+    if (!hip_ok(hipEventSynchronize(ev[MI_DL_NSTAGES]), "event sync")) return -1;
+    for (int i = 0; i < MI_DL_NSTAGES; i++) {
+      float t = 0.f;
+      if (!hip_ok(hipEventElapsedTime(&t, ev[i], ev[i + 1]), "elapsed")) return -1;
+      ms[i] += t / (float)ev_used;
+    }
+  }
+  if (nruns) *nruns = (uint32_t)ev_used;
+  return 0;
+}
+
+}  // namespace mi

@@ -1,0 +1,51 @@
+// engine.h -- batch planner + device workspace + launch sequence of the DL PDSCH receive chain.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "plan.h"
+
+namespace mi {
+
+bool hip_ok(hipError_t e, const char* what);
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  bool ensure(size_t n);   // grow-only
+  void release();
+  ~DevBuf() { release(); }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Device workspace + launcher.  One per batch or per srslte_ue_dl_t instance.
+struct Engine {
+  Plan plan;
+  uint32_t max_its = 4, early_stop = 1, flags = 0;
+  float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
+  // descriptor tables
+  DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,
+      d_fftlist, d_tw;
+  // data buffers
+  DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_payload, d_tbok,
+      d_tbits;
+  std::map<int, size_t> tw_off;   // FFT size -> float2 offset in d_tw
+  hipStream_t last_stream = nullptr;
+  // profiling: one event set per run since the last reset (MI_DL_FLAG_PROFILE)
+  std::vector<std::vector<hipEvent_t>> ev_sets;
+  size_t ev_used = 0;
+  int device = 0;
+
+  ~Engine();
+  int upload(hipStream_t st, bool alloc_sb);
+  // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.
+  int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override);
+  int stage_ms(float* ms, uint32_t* nruns);   // average over the runs since profile_reset()
+  void profile_reset() { ev_used = 0; }
+};
+
+}  // namespace mi

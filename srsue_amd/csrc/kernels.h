@@ -1,0 +1,33 @@
+// kernels.h -- host launchers of the gfx950 kernels of the DL PDSCH path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "dl_common.h"
+#include "kernels_consts.h"
+
+namespace mi {
+
+// OFDM RX (srslte_ofdm_rx_sf): one workgroup per subframe, 14 FFTs of size N
+void launch_ofdm_rx(int N, const float2* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
+                    uint32_t n, const float2* tw, uint32_t W, hipStream_t st);
+// channel estimation (srslte_chest_dl_estimate): one workgroup per subframe, all ports
+void launch_chest(const float2* grid, float2* ce, const MiSfDesc* sfs, const MiCellDesc* cells,
+                  const float2* crs, float* metrics, uint32_t n_sf, hipStream_t st);
+// equalise + soft demap + descramble (srslte_predecoding_* / demod_soft / scrambling_f)
+void launch_demap(const float2* grid, const float2* ce, float* e, const MiSfDesc* sfs,
+                  const MiPdschDesc* pd, const MiCellDesc* cells, const uint32_t* re_tab,
+                  const uint32_t* scr, uint32_t n_sf, uint32_t max_units, float noise, hipStream_t st);
+// rate de-matching + HARQ combining into the group-interleaved softbuffer (srslte_rm_turbo_rx)
+void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
+                       const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups,
+                       uint32_t max_ncb, hipStream_t st);
+// turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
+void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
+                 uint32_t* cb_crc, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
+                 const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop,
+                 hipStream_t st);
+// TB assembly + CRC24A + payload packing
+void launch_tb(const uint8_t* cb_bytes, uint8_t* payload, uint32_t* tb_crc_ok, uint32_t* tb_its,
+               const uint32_t* cb_its, const MiTbDesc* tbs, uint32_t n_tb, const uint32_t* cb_list,
+               hipStream_t st);
+
+}  // namespace mi

@@ -1,0 +1,152 @@
+// ofdm.hip -- OFDM demodulation (replaces srslte_ofdm_rx_sf inside srslte_ue_dl_decode_fft_estimate,
+// /root/reference/ue/src/phy/phch_worker.cc:254).
+//
+// One 256-thread workgroup per subframe runs the 14 symbol FFTs back to back: the first Stockham
+// stage reads the IQ straight from HBM with consecutive lanes on consecutive samples (coalesced),
+// the remaining radix-8/4/3 stages exchange through one LDS buffer, and the twiddles
+// exp(-2 pi i t / N) are staged into LDS once per workgroup and reused by all 14 symbols.  The
+// last pass writes the 12 N_RB used subcarriers (DC skipped) row-major [symbol][subcarrier].
+// Unnormalised forward DFT (oracle/o_rx.c convention).
+#include "kernels.h"
+
+namespace mi {
+
+__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 c_mul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 c_mul_nj(float2 a) { return make_float2(a.y, -a.x); }   // * (-j)
+
+__device__ __forceinline__ void dft2(float2& a, float2& b) { float2 t = a; a = c_add(t, b); b = c_sub(t, b); }
+
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
+  float2 t0 = c_add(a, c), t1 = c_sub(a, c), t2 = c_add(b, d), t3 = c_sub(b, d);
+  a = c_add(t0, t2);
+  c = c_sub(t0, t2);
+  b = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - j t3
+  d = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + j t3
+}
+
+template <int R> __device__ __forceinline__ void dft(float2 (&v)[R]);
+
+template <> __device__ __forceinline__ void dft<2>(float2 (&v)[2]) { dft2(v[0], v[1]); }
+template <> __device__ __forceinline__ void dft<4>(float2 (&v)[4]) { dft4(v[0], v[1], v[2], v[3]); }
+template <> __device__ __forceinline__ void dft<3>(float2 (&v)[3]) {
+  const float s = 0.86602540378443864676f;
+  float2 a = v[0], t = c_add(v[1], v[2]), u = c_sub(v[1], v[2]);
+  float2 m = make_float2(a.x - 0.5f * t.x, a.y - 0.5f * t.y);
+  v[0] = c_add(a, t);
+  v[1] = make_float2(m.x + s * u.y, m.y - s * u.x);
+  v[2] = make_float2(m.x - s * u.y, m.y + s * u.x);
+}
+template <> __device__ __forceinline__ void dft<8>(float2 (&v)[8]) {
+  float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+  dft4(e0, e1, e2, e3);
+  dft4(o0, o1, o2, o3);
+  const float r = 0.70710678118654752440f;
+  o1 = make_float2((o1.x + o1.y) * r, (o1.y - o1.x) * r);     // * (1-j)/sqrt2
+  o2 = c_mul_nj(o2);                                          // * -j
+  o3 = make_float2((o3.y - o3.x) * r, (-o3.x - o3.y) * r);    // * (-1-j)/sqrt2
+  v[0] = c_add(e0, o0); v[4] = c_sub(e0, o0);
+  v[1] = c_add(e1, o1); v[5] = c_sub(e1, o1);
+  v[2] = c_add(e2, o2); v[6] = c_sub(e2, o2);
+  v[3] = c_add(e3, o3); v[7] = c_sub(e3, o3);
+}
+
+// One Stockham stage (decimation in time): butterfly j reads x[j + r N/R], twiddles by
+// W_{Ns R}^{(j mod Ns) r}, writes y[(j / Ns) Ns R + j mod Ns + r Ns].
+template <int N, int R, bool FIRST>
+__device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict__ gsrc, const float2* tw, int Ns) {
+  constexpr int NB = N / R;
+  constexpr int PER = (NB + 255) / 256;
+  const int tid = threadIdx.x;
+  float2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; p++) {
+    const int j = tid + p * 256;
+    if (j < NB) {
+#pragma unroll
+      for (int r = 0; r < R; r++) v[p][r] = FIRST ? gsrc[j + r * NB] : buf[j + r * NB];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < PER; p++) {
+    const int j = tid + p * 256;
+    if (j < NB) {
+      const int k = j % Ns;
+      if (!FIRST) {
+        const int step = k * (N / (Ns * R));
+#pragma unroll
+        for (int r = 1; r < R; r++) v[p][r] = c_mul(v[p][r], tw[step * r]);
+      }
+      dft<R>(v[p]);
+      const int base = (j / Ns) * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; r++) buf[base + r * Ns] = v[p][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int N>
+__device__ __forceinline__ void fft_symbol(float2* buf, const float2* __restrict__ src, const float2* tw) {
+  if constexpr (N == 2048) {
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
+    fft_stage<N, 8, false>(buf, src, tw, 64); fft_stage<N, 4, false>(buf, src, tw, 512);
+  } else if constexpr (N == 1536) {
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
+    fft_stage<N, 8, false>(buf, src, tw, 64); fft_stage<N, 3, false>(buf, src, tw, 512);
+  } else if constexpr (N == 1024) {
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
+    fft_stage<N, 4, false>(buf, src, tw, 64); fft_stage<N, 4, false>(buf, src, tw, 256);
+  } else if constexpr (N == 512) {
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
+    fft_stage<N, 8, false>(buf, src, tw, 64);
+  } else if constexpr (N == 256) {
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
+    fft_stage<N, 4, false>(buf, src, tw, 64);
+  } else {
+    static_assert(N == 128, "unsupported FFT size");
+    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 4, false>(buf, src, tw, 8);
+    fft_stage<N, 4, false>(buf, src, tw, 32);
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void ofdm_rx_kernel(const float2* __restrict__ iq, float2* __restrict__ grid,
+                                                      const MiSfDesc* __restrict__ sfs,
+                                                      const uint32_t* __restrict__ list,
+                                                      const float2* __restrict__ twg, uint32_t W) {
+  __shared__ float2 buf[N];
+  __shared__ float2 tw[N];
+  const MiSfDesc d = sfs[list[blockIdx.x]];
+  for (int t = threadIdx.x; t < N; t += 256) tw[t] = twg[t];
+  __syncthreads();
+  const float2* src_sf = iq + d.iq_off;
+  float2* dst = grid + d.grid_off;
+  for (int l = 0; l < NSYMB; l++) {
+    fft_symbol<N>(buf, src_sf + symbol_offset(N, l), tw);
+    for (int k = threadIdx.x; k < (int)W; k += 256) dst[l * W + k] = buf[sc_bin(k, (int)W, N)];
+    __syncthreads();
+  }
+}
+
+void launch_ofdm_rx(int N, const float2* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
+                    uint32_t n, const float2* tw, uint32_t W, hipStream_t st) {
+  if (n == 0) return;
+  dim3 g(n), b(256);
+  switch (N) {
+    case 2048: hipLaunchKernelGGL(ofdm_rx_kernel<2048>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 1536: hipLaunchKernelGGL(ofdm_rx_kernel<1536>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 1024: hipLaunchKernelGGL(ofdm_rx_kernel<1024>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 512: hipLaunchKernelGGL(ofdm_rx_kernel<512>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 256: hipLaunchKernelGGL(ofdm_rx_kernel<256>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 128: hipLaunchKernelGGL(ofdm_rx_kernel<128>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    default: break;
+  }
+}
+
+}  // namespace mi

@@ -1,0 +1,244 @@
+// plan.cpp -- batch planner (see engine.cpp header): RE lists, scrambling words, CRS tables,
+// code-block segmentation, rate-matching splits and 64-lane grouping of equal-K code blocks.
+#include "plan.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace mi {
+
+static thread_local std::string g_err;
+void set_error(const std::string& s) { g_err = s; }
+const char* last_error() { return g_err.c_str(); }
+
+static size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
+
+int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
+  has_pdsch = with_pdsch;
+  cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
+  fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
+  iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
+  max_units = max_ncb = n_cb = 0;
+  bytes_compulsory = 0;
+  for (double& b : stage_bytes) b = 0;
+
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cell_idx;
+  std::map<std::vector<uint32_t>, uint32_t> pd_idx;
+  std::map<int, std::vector<uint32_t>> fft_map;
+  std::vector<uint32_t> re;
+
+  struct CbRef { uint32_t K, tb, r; };
+  std::vector<CbRef> cbs;
+  std::vector<CbSegm> segs(n);
+
+  for (uint32_t s = 0; s < n; s++) {
+    const mi_dl_sf_cfg_t& c = cfgs[s];
+    const int N = symbol_sz(c.nof_prb);
+    if (N < 0 || c.nof_prb == 0 || c.nof_ports < 1 || c.nof_ports > 2 || c.sf_idx > 9) {
+      set_error("invalid cell configuration");
+      return -1;
+    }
+    const uint32_t W = 12 * c.nof_prb;
+    auto ck = std::make_tuple(c.cell_id, c.nof_prb, c.nof_ports);
+    uint32_t ci;
+    auto it = cell_idx.find(ck);
+    if (it == cell_idx.end()) {
+      ci = (uint32_t)cells.size();
+      cell_idx[ck] = ci;
+      MiCellDesc cd{c.cell_id, c.nof_prb, c.nof_ports, (uint32_t)N, W, (uint32_t)(crs.size() / 2)};
+      cells.push_back(cd);
+      auto& tab = crs_cache[ck];
+      if (tab.empty()) {
+        tab.resize(20 * 2 * 2 * NRB_MAX * 2);
+        for (uint32_t ns = 0; ns < 20; ns++)
+          for (uint32_t li = 0; li < 2; li++) crs_seq(c.cell_id, ns, li ? 4 : 0, &tab[((ns * 2 + li) * 2 * NRB_MAX) * 2]);
+      }
+      crs.insert(crs.end(), tab.begin(), tab.end());
+    } else {
+      ci = it->second;
+    }
+    MiSfDesc sd{};
+    sd.iq_off = iq_samples;
+    sd.grid_off = grid_elems;
+    sd.ce_off = ce_elems;
+    sd.cell = ci;
+    sd.sf_idx = c.sf_idx;
+    sd.tb = s;
+    iq_samples += (size_t)sf_len(N);
+    grid_elems += (size_t)NSYMB * W;
+    ce_elems += (size_t)NSYMB * W * c.nof_ports;
+    fft_map[N].push_back(s);
+    stage_bytes[MI_DL_STAGE_OFDM] += (double)sf_len(N) * 8 + (double)NSYMB * W * 8;
+    stage_bytes[MI_DL_STAGE_CHEST] += (double)NSYMB * W * 8 * c.nof_ports + 4.0 * W * 8;
+    bytes_compulsory += (double)sf_len(N) * 8;
+
+    if (with_pdsch) {
+      if (c.tm == 2 && c.nof_ports != 2) { set_error("TM2 needs 2 ports"); return -1; }
+      if (c.Qm != 2 && c.Qm != 4 && c.Qm != 6) { set_error("Qm must be 2, 4 or 6"); return -1; }
+      if (c.tbs == 0 || c.tbs % 8) { set_error("TBS must be a positive multiple of 8"); return -1; }
+      std::vector<uint32_t> pk = {ci, c.cfi, c.sf_idx, c.Qm, c.tm, c.rnti};
+      for (uint32_t p = 0; p < c.nof_prb; p++) pk.push_back(c.prb_mask[p] ? 1u : 0u);
+      uint32_t pi_;
+      auto pit = pd_idx.find(pk);
+      if (pit == pd_idx.end()) {
+        pi_ = (uint32_t)pds.size();
+        pd_idx[pk] = pi_;
+        const uint32_t nre = pdsch_re_list(c.cell_id, c.nof_prb, c.nof_ports, c.cfi, c.sf_idx, c.prb_mask, re);
+        if (c.tm == 2 && (nre & 1)) { set_error("odd RE count for SFBC"); return -1; }
+        MiPdschDesc pd{ci, c.sf_idx, nre, c.Qm, c.tm, nre * c.Qm, (uint32_t)re_tab.size(), (uint32_t)scr_tab.size()};
+        re_tab.insert(re_tab.end(), re.begin(), re.end());
+        const uint32_t G = pd.G, nw = (G + 31) / 32 + 1;
+        auto sk = std::make_tuple(c.cell_id, c.rnti, c.sf_idx, G);
+        auto& words = scr_cache[sk];
+        if (words.empty()) {
+          words.resize(nw);
+          gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, G, words.data());
+        }
+        scr_tab.insert(scr_tab.end(), words.begin(), words.end());
+        pds.push_back(pd);
+      } else {
+        pi_ = pit->second;
+      }
+      const MiPdschDesc& pd = pds[pi_];
+      sd.pdsch = pi_;
+      sd.e_off = e_floats;
+      e_floats += align4(pd.G);
+      const uint32_t units = pd.tm == 2 ? pd.nre / 2 : pd.nre;
+      max_units = std::max(max_units, units);
+      // ---- transport block
+      CbSegm sg;
+      if (cbsegm(c.tbs, &sg)) { set_error("segmentation failed"); return -1; }
+      segs[s] = sg;
+      MiTbDesc tb{};
+      tb.tbs = c.tbs; tb.C = sg.C; tb.Kp = sg.Kp; tb.Km = sg.Km; tb.Cm = sg.Cm; tb.F = sg.F;
+      tb.pay_off = (uint32_t)payload_bytes;
+      payload_bytes += c.tbs / 8;
+      tbs.push_back(tb);
+      for (uint32_t r = 0; r < sg.C; r++) cbs.push_back({r < sg.Cm ? sg.Km : sg.Kp, s, r});
+      stage_bytes[MI_DL_STAGE_DEMAP] += (double)pd.nre * 8 * (1 + c.nof_ports) + (double)pd.G * 4;
+      bytes_compulsory += (double)c.tbs / 8;
+    }
+    sfs.push_back(sd);
+  }
+  for (auto& kv : fft_map) {
+    fft_lists.push_back(kv);
+    fft_list_off.push_back(fft_list_flat.size());
+    fft_list_flat.insert(fft_list_flat.end(), kv.second.begin(), kv.second.end());
+    fft_W.push_back(12 * cfgs[kv.second[0]].nof_prb);
+  }
+  if (!with_pdsch) return 0;
+
+  // ---- group code blocks of equal K into 64-lane wavefront groups
+  std::stable_sort(cbs.begin(), cbs.end(), [](const CbRef& a, const CbRef& b) { return a.K < b.K; });
+  std::map<uint32_t, uint32_t> ktab_idx;
+  for (size_t i = 0; i < cbs.size();) {
+    const uint32_t K = cbs[i].K;
+    size_t j = i;
+    while (j < cbs.size() && cbs[j].K == K) j++;
+    uint32_t kt;
+    auto kit = ktab_idx.find(K);
+    if (kit == ktab_idx.end()) {
+      kt = (uint32_t)ktabs.size();
+      ktab_idx[K] = kt;
+      auto& kp = kpos_cache[K];
+      if (kp.first.empty()) { cb_pos_table(K, kp.first); qpp_table(K, kp.second); }
+      MiKTab t{K, ncb_of(K), (uint32_t)kdata.size(), 0};
+      kdata.insert(kdata.end(), kp.first.begin(), kp.first.end());
+      t.pi_off = (uint32_t)kdata.size();
+      kdata.insert(kdata.end(), kp.second.begin(), kp.second.end());
+      ktabs.push_back(t);
+    } else {
+      kt = kit->second;
+    }
+    const uint32_t Ncb = ncb_of(K);
+    max_ncb = std::max(max_ncb, Ncb);
+    for (size_t g0 = i; g0 < j; g0 += LANES) {
+      MiGroupDesc g{};
+      g.K = K; g.Ncb = Ncb; g.ktab = kt;
+      g.lane0 = (uint32_t)lanes.size();
+      g.sb_off = sb_floats;
+      g.scratch_off = scratch_floats;
+      g.dec_off = dec_bytes;
+      sb_floats += (size_t)Ncb * LANES;
+      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / BETA_W + 1));
+      dec_bytes += (size_t)K * LANES;
+      groups.push_back(g);
+      for (size_t q = 0; q < (size_t)LANES; q++) {
+        MiLaneDesc ld{};
+        if (g0 + q < j) {
+          const CbRef& cr = cbs[g0 + q];
+          const mi_dl_sf_cfg_t& c = cfgs[cr.tb];
+          const CbSegm& sg = segs[cr.tb];
+          const MiPdschDesc& pd = pds[sfs[cr.tb].pdsch];
+          const uint32_t F = cr.r == 0 ? sg.F : 0;
+          const uint32_t NL = c.tm == 2 ? (c.nl_td ? c.nl_td : 2) : 1;
+          uint64_t eo = sfs[cr.tb].e_off;
+          for (uint32_t rr = 0; rr < cr.r; rr++) eo += rm_E(pd.G, sg.C, c.Qm, NL, rr);
+          ld.e_off = eo;
+          ld.E = rm_E(pd.G, sg.C, c.Qm, NL, cr.r);
+          auto& rk = rank_cache[{K, F}];
+          if (rk.first.empty()) cb_rank_table(K, F, rk.first, &rk.second);
+          ld.Nv = rk.second;
+          const uint32_t k0 = k0_of(K, c.rv);
+          uint32_t r0 = 0;
+          for (uint32_t p = 0; p < k0 && p < Ncb; p++) r0 += rk.first[p] >= 0 ? 1 : 0;
+          ld.r0 = r0 % ld.Nv;
+          ld.F = F;
+          ld.new_tb = c.new_tb ? 1 : 0;
+          ld.crc24a = sg.C == 1 ? 1 : 0;
+          ld.tb = cr.tb;
+          ld.valid = 1;
+          // rank table offset: one copy per (K, F) in kdata
+          ld.rank_off = 0xFFFFFFFFu;
+          lanes.push_back(ld);
+          stage_bytes[MI_DL_STAGE_RM] += (double)ld.E * 4 + (double)Ncb * 4 * (ld.new_tb ? 1 : 2);
+          stage_bytes[MI_DL_STAGE_TDEC] += (double)(3 * K + 12) * 4 + (double)K / 8;
+          bytes_compulsory += (double)ncb_of(K) * 4 * (ld.new_tb ? 1 : 2);
+          n_cb++;
+        } else {
+          lanes.push_back(ld);
+        }
+      }
+    }
+    i = j;
+  }
+  // rank tables into kdata, patch lane offsets
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> rank_off;
+  for (size_t gi = 0; gi < groups.size(); gi++) {
+    for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+      MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
+      if (!ld.valid) continue;
+      auto key = std::make_pair(groups[gi].K, ld.F);
+      auto ro = rank_off.find(key);
+      if (ro == rank_off.end()) {
+        const auto& rk = rank_cache[key].first;
+        uint32_t off = (uint32_t)kdata.size();
+        for (int32_t v : rk) kdata.push_back((uint32_t)v);
+        rank_off[key] = off;
+        ld.rank_off = off;
+      } else {
+        ld.rank_off = ro->second;
+      }
+    }
+  }
+  // TB -> lane lists
+  std::vector<std::vector<uint32_t>> tb_lanes(n);
+  for (size_t gi = 0; gi < groups.size(); gi++)
+    for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+      const MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
+      if (ld.valid) tb_lanes[ld.tb].push_back(groups[gi].lane0 + q);
+    }
+  // lanes of a TB were appended in CB order within each K run; K- blocks (r < Cm) come first
+  for (uint32_t s = 0; s < n; s++) {
+    auto& v = tb_lanes[s];
+    // order by CB index r: CBs with K- precede K+ ones (36.212 5.1.2), K runs are sorted ascending
+    tbs[s].cb_list = (uint32_t)cb_list.size();
+    cb_list.insert(cb_list.end(), v.begin(), v.end());
+  }
+  return 0;
+}
+
+}  // namespace mi

@@ -1,0 +1,52 @@
+// plan.h -- host planner of the DL PDSCH receive chain (no HIP runtime dependency, so the
+// test-only emulation build can link it too).
+#pragma once
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "dl_common.h"
+#include "mi_dl.h"
+#include "tables.h"
+
+namespace mi {
+
+void set_error(const std::string& s);
+const char* last_error();
+
+struct Plan {
+  std::vector<MiCellDesc> cells;
+  std::vector<float> crs;                 // float2 pairs
+  std::vector<MiPdschDesc> pds;
+  std::vector<uint32_t> re_tab, scr_tab;
+  std::vector<MiSfDesc> sfs;
+  std::vector<MiLaneDesc> lanes;
+  std::vector<MiGroupDesc> groups;
+  std::vector<MiKTab> ktabs;
+  std::vector<uint32_t> kdata;
+  std::vector<MiTbDesc> tbs;
+  std::vector<uint32_t> cb_list;
+  std::vector<std::pair<int, std::vector<uint32_t>>> fft_lists;   // FFT size -> subframe indices
+  std::vector<uint32_t> fft_list_flat;
+  std::vector<size_t> fft_list_off;
+  std::vector<uint32_t> fft_W;
+  size_t iq_samples = 0, grid_elems = 0, ce_elems = 0, e_floats = 0, sb_floats = 0, scratch_floats = 0;
+  size_t dec_bytes = 0, payload_bytes = 0;
+  uint32_t max_units = 0, max_ncb = 0, n_cb = 0;
+  bool has_pdsch = true;
+  // algorithmic byte counts
+  double bytes_compulsory = 0;
+  double stage_bytes[MI_DL_NSTAGES] = {0};
+
+  // cached per-key tables (kept across rebuilds)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<float>> crs_cache;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::vector<uint32_t>> scr_cache;
+  std::map<uint32_t, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> kpos_cache;
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<std::vector<int32_t>, uint32_t>> rank_cache;
+
+  // has_pdsch = false plans only OFDM + channel estimation (per-TTI front half)
+  int build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool has_pdsch);
+};
+
+}  // namespace mi

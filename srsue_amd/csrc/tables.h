@@ -1,0 +1,38 @@
+// tables.h -- host-side spec tables and index maps (36.211 / 36.212 / 36.213) for the planner.
+#pragma once
+#include <stdint.h>
+#include <vector>
+
+namespace mi {
+
+struct CbSegm { uint32_t C, Cp, Cm, Kp, Km, F, B; };
+
+int qpp_params(uint32_t K, uint32_t* f1, uint32_t* f2);           // 36.212 Table 5.1.3-3
+bool cb_size_valid(uint32_t K);
+int cbsegm(uint32_t tbs, CbSegm* s);                                // 36.212 5.1.2
+int tbs_from_idx(uint32_t i_tbs, uint32_t nof_prb);                 // 36.213 7.1.7.2.1 (spot columns)
+int mcs_to_itbs(uint32_t mcs, uint32_t* qm);                        // 36.213 Table 7.1.7.1-1
+uint32_t rm_E(uint32_t G, uint32_t C, uint32_t Qm, uint32_t NL, uint32_t r);   // 36.212 5.1.4.1.2
+uint32_t ncb_of(uint32_t K);
+uint32_t k0_of(uint32_t K, uint32_t rv);
+// circular-buffer maps of one code block size: pos[t] for decoder input t = 3k + i, and the rank
+// table (number of non-null positions before p, -1 for <NULL>) for F filler bits.
+void cb_pos_table(uint32_t K, std::vector<uint32_t>& pos);
+void cb_rank_table(uint32_t K, uint32_t F, std::vector<int32_t>& rank, uint32_t* Nv);
+void qpp_table(uint32_t K, std::vector<uint32_t>& pi);
+// 36.211 7.2 Gold sequence, packed 32 bits per word (bit i at word[i/32] bit i%32)
+void gold_words(uint32_t c_init, uint32_t nbits, uint32_t* words);
+void gold_bits(uint32_t c_init, uint32_t nbits, uint8_t* bits);
+// 36.211 6.10.1.1 CRS r_{l,ns}(m), m < 220 (interleaved re, im)
+void crs_seq(uint32_t id, uint32_t ns, uint32_t l, float* re_im);
+// PDSCH RE membership / list (36.211 6.3.5 mapping order), grid index l * 12 N_RB + k
+int ctrl_symbols(uint32_t nof_prb, uint32_t cfi);
+bool is_pdsch_re(uint32_t id, uint32_t nof_prb, uint32_t nof_ports, uint32_t cfi, uint32_t sf, uint32_t l, uint32_t k);
+uint32_t pdsch_re_list(uint32_t id, uint32_t nof_prb, uint32_t nof_ports, uint32_t cfi, uint32_t sf,
+                       const uint8_t* prb_mask, std::vector<uint32_t>& re);
+// PCFICH REs (36.211 6.7.4) in symbol 0, and scrambling init (36.211 6.7.1)
+void pcfich_k(uint32_t id, uint32_t nof_prb, uint32_t* k16);
+uint32_t pcfich_cinit(uint32_t id, uint32_t sf);
+void cfi_codeword(uint32_t cfi, uint8_t* b32);                       // 36.212 Table 5.3.4-1
+
+}  // namespace mi

@@ -1,0 +1,69 @@
+// tb_body.h -- transport-block assembly and CRC24A (36.212 5.1.1 / 5.1.2), the tail of
+// srslte_pdsch_decode_rnti (/root/reference/ue/src/phy/phch_worker.cc:347-348): code-block bits
+// without filler and CB CRC are concatenated, the TB CRC24A is checked (return 0 <=> CRC ok) and
+// the payload is packed MSB-first into bytes (srsUE treats it as bytes: ue/src/mac/demux.cc:180).
+//
+// The CRC is computed in parallel: each lane takes a byte segment, computes its zero-initialised
+// CRC register, and shifts it to the end of the message by multiplying with x^(8 n) mod g in
+// GF(2)[x] (CRC(A||B) = CRC(A) x^|B| + CRC(B)); XOR of all shifted registers is the message CRC.
+#pragma once
+#include "dl_common.h"
+#ifndef MI_HD
+#define MI_HD __host__ __device__
+#endif
+
+namespace mi {
+
+constexpr uint32_t CRC24A_POLY = 0x864CFBu;
+constexpr uint32_t CRC24B_POLY = 0x800063u;
+
+MI_HD inline uint32_t crc24_bytes(const uint8_t* p, uint32_t n, uint32_t poly) {
+  uint32_t crc = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t byte = p[i];
+    for (int b = 7; b >= 0; b--) {
+      const uint32_t fb = ((crc >> 23) ^ (byte >> b)) & 1u;
+      crc = ((crc << 1) & 0xFFFFFFu) ^ (fb ? poly : 0u);
+    }
+  }
+  return crc;
+}
+
+// a * b mod (x^24 + poly) over GF(2)
+MI_HD inline uint32_t gf24_mulmod(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= 0x1000000u | poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+
+// x^(8 n) mod (x^24 + poly)
+MI_HD inline uint32_t gf24_xpow8(uint32_t n, uint32_t poly) {
+  uint32_t res = 1, base = 0x100u;
+  while (n) {
+    if (n & 1u) res = gf24_mulmod(res, base, poly);
+    base = gf24_mulmod(base, base, poly);
+    n >>= 1;
+  }
+  return res;
+}
+
+// which code block / byte of that block holds TB byte j (CB payload bytes are byte aligned:
+// K, F and the 24-bit CB CRC are multiples of 8)
+MI_HD inline void tb_byte_src(const MiTbDesc& t, uint32_t j, uint32_t& r, uint32_t& off) {
+  const uint32_t L = t.C > 1 ? 3 : 0;
+  uint32_t start = 0;
+  for (r = 0; r < t.C; r++) {
+    const uint32_t Kr = r < t.Cm ? t.Km : t.Kp;
+    const uint32_t Fr = r == 0 ? t.F : 0;
+    const uint32_t nr = Kr / 8 - Fr / 8 - L;
+    if (j < start + nr) { off = Fr / 8 + (j - start); return; }
+    start += nr;
+  }
+  r = t.C - 1; off = 0;
+}
+
+}  // namespace mi

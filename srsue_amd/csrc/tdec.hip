@@ -1,0 +1,47 @@
+// tdec.hip -- turbo decoder launch: one 64-lane wavefront per group of code blocks of equal K
+// (tdec_body.h holds the per-lane algorithm and its bit-exactness contract with the oracle).
+#include "kernels.h"
+#include "tdec_body.h"
+
+namespace mi {
+
+__global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, float* __restrict__ scratch,
+                                                 uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
+                                                 uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
+                                                 const MiGroupDesc* __restrict__ groups,
+                                                 const MiLaneDesc* __restrict__ lanes,
+                                                 const MiKTab* __restrict__ ktabs,
+                                                 const uint32_t* __restrict__ kdata, uint32_t max_its,
+                                                 uint32_t early_stop) {
+  const MiGroupDesc g = groups[blockIdx.x];
+  const int lane = threadIdx.x;
+  const uint32_t li = g.lane0 + lane;
+  const MiLaneDesc ld = lanes[li];
+  if (!ld.valid) return;
+  const MiKTab kt = ktabs[g.ktab];
+  TdecArgs a;
+  a.sb = sb + g.sb_off;
+  a.pos = kdata + kt.pos_off;
+  a.pi = kdata + kt.pi_off;
+  a.scr = scratch + g.scratch_off;
+  a.dec = dec + g.dec_off;
+  a.cb_bytes = cb_bytes + (size_t)li * CB_BYTES_STRIDE;
+  a.K = g.K;
+  a.F = ld.F;
+  a.max_its = max_its;
+  a.early_stop = early_stop;
+  a.crc24a = ld.crc24a;
+  const TdecLaneResult r = tdec_lane(a, lane);
+  cb_its[li] = r.its;
+  cb_crc[li] = r.crc_ok;
+}
+
+void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
+                 const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data,
+                 uint32_t n_groups, uint32_t max_its, uint32_t early_stop, hipStream_t st) {
+  if (!n_groups) return;
+  hipLaunchKernelGGL(tdec_kernel, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups,
+                     lanes, ktabs, ktab_data, max_its, early_stop);
+}
+
+}  // namespace mi

@@ -1,0 +1,208 @@
+// tdec_body.h -- max-log-MAP turbo decoder, one code block per lane (gfx950 wavefront = 64 CBs).
+//
+// Replaces srslte_tdec_reset / srslte_tdec_iteration / srslte_tdec_decision + the CRC early stop
+// of srsLTE's decode_tb, reached from srslte_pdsch_decode_rnti (/root/reference/ue/src/phy/
+// phch_worker.cc:347-348) with the iteration cap of srslte_sch_set_max_noi (phch_worker.cc:88).
+//
+// Layout (MI355X-first): the 64 code blocks of a group share K, so every memory index is
+// wave-uniform -- the QPP interleaver Pi(k) and the circular-buffer position of each d-stream bit
+// come from scalar tables, and a wave-instruction touches 64 consecutive floats [index][lane]:
+// fully coalesced 256-B accesses even for the interleaved decoder.  The lane reads its systematic
+// and parity LLRs straight out of the HARQ softbuffer (rate de-matching fused into the loads).
+// The full-length backward recursion is kept exact by storing beta every BETA_W steps and
+// recomputing the window in registers during the forward pass, so decisions and extrinsics are
+// bit-identical to the oracle (oracle/o_fec.c documents the operation order reproduced here).
+#pragma once
+#include "dl_common.h"
+
+#ifndef MI_HD
+#define MI_HD __host__ __device__
+#endif
+
+namespace mi {
+
+// trellis of the 36.212 PCCC constituent encoder: s = 4 s1 + 2 s2 + s3
+MI_HD constexpr int tr_next(int s, int u) { return (((u ^ (s >> 1) ^ s) & 1) << 2) | (s >> 1); }
+MI_HD constexpr int tr_par(int s, int u) { return ((u ^ (s >> 1) ^ s) ^ (s >> 2) ^ s) & 1; }
+// predecessor (state, input) pairs of state sp: prev states have s>>1 == sp & 3
+MI_HD constexpr int tr_prev_s(int sp, int j) { return ((sp & 3) << 1) | j; }
+MI_HD constexpr int tr_prev_u(int sp, int j) {
+  // input u such that tr_next(prev, u) == sp
+  return ((sp >> 2) ^ (tr_prev_s(sp, j) >> 1) ^ tr_prev_s(sp, j)) & 1;
+}
+
+struct TdecArgs {
+  const float* sb;        // group softbuffer [Ncb][64]
+  const uint32_t* pos;    // [3(K+4)] circular-buffer position of decoder input t = 3k+i
+  const uint32_t* pi;     // [K]
+  float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/W+1)*8][64]
+  uint8_t* dec;           // [K][64] decision bytes
+  uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
+  uint32_t K, F, max_its, early_stop, crc24a;
+};
+
+struct TdecLaneResult { uint32_t its; uint32_t crc_ok; };
+
+MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
+  return u ? (z ? luz : lu) : (z ? lp : 0.0f);
+}
+
+template <bool DEC2>
+MI_HD inline void tdec_inputs(const TdecArgs& a, int lane, bool first, uint32_t k, float& xs, float& xp,
+                              float& l1, float& wv) {
+  const uint32_t K = a.K;
+  if (k < K) {
+    if (!DEC2) {
+      uint32_t t = 3 * k;
+      float sys = (k < a.F) ? FILLER_LLR : a.sb[(size_t)a.pos[t] * LANES + lane];
+      float p1 = (k < a.F) ? FILLER_LLR : a.sb[(size_t)a.pos[t + 1] * LANES + lane];
+      wv = first ? 0.0f : a.scr[(size_t)k * LANES + lane];
+      xs = sys + wv;
+      xp = p1;
+    } else {
+      uint32_t i = a.pi[k];
+      l1 = a.scr[(size_t)(K + i) * LANES + lane];
+      wv = first ? 0.0f : a.scr[(size_t)i * LANES + lane];
+      xs = l1 - wv;
+      xp = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
+    }
+  } else {
+    uint32_t j = k - K;
+    uint32_t t = 3 * K + (DEC2 ? 6 : 0) + 2 * j;
+    xs = a.sb[(size_t)a.pos[t] * LANES + lane];
+    xp = a.sb[(size_t)a.pos[t + 1] * LANES + lane];
+  }
+}
+
+// one backward step: beta_k from beta_{k+1}
+MI_HD inline void beta_step(const float (&bn)[8], float xs, float xp, float (&bk)[8]) {
+  const float luz = xs + xp;
+  float m[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    float b0 = bn[tr_next(s, 0)] + gam(0, tr_par(s, 0), xs, xp, luz);
+    float b1 = bn[tr_next(s, 1)] + gam(1, tr_par(s, 1), xs, xp, luz);
+    m[s] = fmaxf(b0, b1);
+  }
+#pragma unroll
+  for (int s = 0; s < 8; s++) bk[s] = m[s] - m[0];
+}
+
+// one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1}
+MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, float xp) {
+  const float luz = xs + xp;
+  const float NINF = -INFINITY;
+  float c[8][2], m0 = NINF, m1 = NINF;
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      c[s][u] = al[s] + gam(u, tr_par(s, u), xs, xp, luz);
+      float t = c[s][u] + bn[tr_next(s, u)];
+      if (u) m1 = fmaxf(m1, t); else m0 = fmaxf(m0, t);
+    }
+  }
+  float llr = m1 - m0;
+  float na[8];
+#pragma unroll
+  for (int sp = 0; sp < 8; sp++)
+    na[sp] = fmaxf(c[tr_prev_s(sp, 0)][tr_prev_u(sp, 0)], c[tr_prev_s(sp, 1)][tr_prev_u(sp, 1)]);
+#pragma unroll
+  for (int s = 0; s < 8; s++) al[s] = na[s] - na[0];
+  return llr;
+}
+
+template <bool DEC2>
+MI_HD inline void tdec_half(const TdecArgs& a, int lane, bool first) {
+  const uint32_t K = a.K;
+  float* ck = a.scr + (size_t)2 * K * LANES;  // beta checkpoints
+  const float NINF = -INFINITY;
+  float b[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) b[s] = s ? NINF : 0.0f;
+  float l1d, wvd;
+  // ---- backward pass: tail steps K+2..K, then windows; checkpoint every BETA_W steps
+  for (int k = (int)K + 2; k >= (int)K; k--) {
+    float xs, xp;
+    tdec_inputs<DEC2>(a, lane, first, (uint32_t)k, xs, xp, l1d, wvd);
+    float nb[8];
+    beta_step(b, xs, xp, nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+#pragma unroll
+  for (int s = 0; s < 8; s++) ck[((size_t)(K / BETA_W) * 8 + s) * LANES + lane] = b[s];
+  for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
+    float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) tdec_inputs<DEC2>(a, lane, first, (uint32_t)(base + i), xs[i], xp[i], l1d, wvd);
+#pragma unroll
+    for (int i = BETA_W - 1; i >= 0; i--) {
+      if (base + i == 0) break;
+      float nb[8];
+      beta_step(b, xs[i], xp[i], nb);
+#pragma unroll
+      for (int s = 0; s < 8; s++) b[s] = nb[s];
+    }
+    if (base > 0) {
+#pragma unroll
+      for (int s = 0; s < 8; s++) ck[((size_t)(base / BETA_W) * 8 + s) * LANES + lane] = b[s];
+    }
+  }
+  // ---- forward pass over windows, recomputing beta_{base+1..base+W} from the checkpoint
+  float al[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
+  for (uint32_t base = 0; base < K; base += BETA_W) {
+    float xs[BETA_W], xp[BETA_W], l1[BETA_W], wv[BETA_W];
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) tdec_inputs<DEC2>(a, lane, first, base + i, xs[i], xp[i], l1[i], wv[i]);
+    float bw[BETA_W][8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ck[((size_t)(base / BETA_W + 1) * 8 + s) * LANES + lane];
+#pragma unroll
+    for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) {
+      const uint32_t k = base + i;
+      float llr = alpha_step(al, bw[i], xs[i], xp[i]);
+      if (!DEC2) {
+        a.scr[(size_t)(K + k) * LANES + lane] = llr;                 // llr1
+      } else {
+        const uint32_t pk = a.pi[k];
+        a.scr[(size_t)pk * LANES + lane] = wv[i] + (llr - l1[i]);    // w update
+        a.dec[(size_t)pk * LANES + lane] = llr > 0.0f ? 1 : 0;       // decision
+      }
+    }
+  }
+}
+
+MI_HD inline uint32_t tdec_crc(const TdecArgs& a, int lane) {
+  const uint32_t poly = a.crc24a ? 0x864CFBu : 0x800063u;
+  uint32_t crc = 0;
+  for (uint32_t k = 0; k < a.K; k++) {
+    uint32_t fb = ((crc >> 23) ^ a.dec[(size_t)k * LANES + lane]) & 1u;
+    crc = ((crc << 1) & 0xFFFFFFu) ^ (fb ? poly : 0u);
+  }
+  return crc;
+}
+
+MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
+  TdecLaneResult r{0, 0};
+  for (uint32_t it = 0; it < a.max_its; it++) {
+    tdec_half<false>(a, lane, it == 0);
+    tdec_half<true>(a, lane, it == 0);
+    r.its = it + 1;
+    r.crc_ok = tdec_crc(a, lane) == 0;
+    if (a.early_stop && r.crc_ok) break;
+  }
+  for (uint32_t j = 0; j < a.K / 8; j++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) v |= (uint32_t)a.dec[(size_t)(8 * j + q) * LANES + lane] << (7 - q);
+    a.cb_bytes[j] = (uint8_t)v;
+  }
+  return r;
+}
+
+}  // namespace mi

@@ -1,0 +1,97 @@
+"""GPU parity tests: the HIP chain (through the C ABI) against the CPU oracle on identical inputs.
+
+Tolerances (BASELINE.json north_star): grid / channel estimates / LLRs within 1e-4 relative (max abs
+error over the RMS of the oracle array); decoded TB bits, TB CRC and turbo iteration counts
+bit-exact.  The turbo decoder itself is compared on identical LLRs (uploaded into the batch), where
+even CRC-failing decodes must match the oracle bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_subframes, oracle_dlsch, oracle_front, rel_err, tb_bytes
+from srsue_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
+
+
+def run_batch(cfgs, iqs, max_its=4, profile=False):
+    b = abi.Batch(cfgs, max_its=max_its, profile=profile)
+    flat = np.zeros(2 * b.iq_samples, np.float32)
+    for i, iq in enumerate(iqs):
+        o = 2 * b.iq_offset(i)
+        flat[o:o + len(iq)] = iq
+    d = torch.from_numpy(flat).cuda()
+    b.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return b
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built):
+    assert torch.cuda.is_available()
+
+
+CASES = [
+    dict(nof_prb=100, nof_ports=1, sf_idx=1, tbs=75376, Qm=6),                 # configs[1]: 20 MHz TM1 MCS-28
+    dict(nof_prb=100, nof_ports=2, sf_idx=2, tbs=75376, Qm=6),                 # configs[2]: TM2 64QAM
+    dict(nof_prb=100, nof_ports=1, sf_idx=0, tbs=75376, Qm=6),                 # PBCH / sync holes
+    dict(nof_prb=100, nof_ports=2, sf_idx=5, tbs=40000, Qm=4, cfi=2),
+    dict(nof_prb=6, nof_ports=1, sf_idx=1, tbs=4392, Qm=6, cell_id=301),       # 1.4 MHz
+    dict(nof_prb=15, nof_ports=2, sf_idx=3, tbs=2856, Qm=4, cell_id=7),        # 3 MHz, N = 256
+    dict(nof_prb=25, nof_ports=1, sf_idx=4, tbs=7000, Qm=4, cell_id=11, rv=2), # filler bits, K-/K+
+    dict(nof_prb=50, nof_ports=1, sf_idx=6, tbs=36696, Qm=6, cell_id=2),
+    dict(nof_prb=75, nof_ports=1, sf_idx=9, tbs=40000, Qm=6, cell_id=5, cfi=3),  # N = 1536
+]
+
+
+def test_mixed_batch_front_end_and_decode():
+    cfgs = [abi.sf_cfg(**c) for c in CASES]
+    iqs, tbs = make_subframes(cfgs, snr_db=30.0)
+    b = run_batch(cfgs, iqs)
+    grid = b.download(abi.BUF_GRID, np.float32)
+    ce = b.download(abi.BUF_CE, np.float32)
+    llr = b.download(abi.BUF_LLR, np.float32)
+    pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+    crc = b.download(abi.BUF_TB_CRC, np.uint32)
+    its = b.download(abi.BUF_TB_ITS, np.uint32)
+    for i, c in enumerate(cfgs):
+        og, oce, _, ollr = oracle_front(c, iqs[i])
+        go = 2 * b.offset(abi.BUF_GRID, i)
+        co = 2 * b.offset(abi.BUF_CE, i)
+        lo = b.offset(abi.BUF_LLR, i)
+        assert rel_err(grid[go:go + len(og)], og) < TOL, f"grid case {i}"
+        assert rel_err(ce[co:co + len(oce)], oce) < TOL, f"ce case {i}"
+        assert rel_err(llr[lo:lo + len(ollr)], ollr) < TOL, f"llr case {i}"
+        ok, opay, onoi, _ = oracle_dlsch(c, ollr)
+        p = b.payload(i, pay)
+        assert crc[i] == 1 and ok, f"CRC case {i}"
+        assert np.array_equal(p, tbs[i]), f"payload vs transmitted TB, case {i}"
+        assert np.array_equal(p, opay), f"payload vs oracle, case {i}"
+        assert its[i] == onoi
+
+
+@pytest.mark.parametrize("snr", [15.0, 17.5, 18.5, 19.5])
+def test_turbo_bit_exact_on_identical_llrs(snr):
+    """Waterfall region: CRC passes and fails; GPU == oracle bit for bit either way."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + (i % 4), tbs=75376, Qm=6) for i in range(4)]
+    iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=int(snr * 10))
+    b = abi.Batch(cfgs, max_its=4)
+    llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
+    flat = np.zeros(b.download(abi.BUF_LLR, np.float32).shape, np.float32)
+    for i, l in enumerate(llrs):
+        o = b.offset(abi.BUF_LLR, i)
+        flat[o:o + len(l)] = l
+    b.upload(abi.BUF_LLR, flat)
+    b.run_stages(S_RM_TDEC_TB)
+    pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+    crc = b.download(abi.BUF_TB_CRC, np.uint32)
+    its = b.download(abi.BUF_TB_ITS, np.uint32)
+    for i, c in enumerate(cfgs):
+        ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
+        assert bool(crc[i]) == ok
+        assert its[i] == onoi
+        assert np.array_equal(b.payload(i, pay), opay)
