@@ -24,8 +24,9 @@ constexpr int NSYMB = 14;            // normal CP, symbols per subframe
 constexpr int KMAX = 6144;           // largest turbo code block
 constexpr int NCB_MAX = 3 * 32 * ((KMAX + 4 + 31) / 32);   // 18528
 constexpr int LANES = 64;            // code blocks per wavefront group (one CB per lane)
-constexpr int BETA_W = 8;            // beta checkpoint spacing in the turbo kernel
+constexpr int BETA_W = 4;            // beta checkpoint spacing in the turbo kernel (161 VGPRs: 3 waves/SIMD)
 constexpr float FILLER_LLR = -10000.0f;
+constexpr int RM_CHUNK = 128;        // circular-buffer positions per rate-dematch workgroup
 
 __host__ __device__ inline int symbol_sz(uint32_t nof_prb) {
   return nof_prb <= 6 ? 128 : nof_prb <= 15 ? 256 : nof_prb <= 25 ? 512 : nof_prb <= 50 ? 1024
@@ -83,7 +84,8 @@ struct MiLaneDesc {          // one per code block (lane of a group)
   uint32_t r0;               // number of non-null circular-buffer positions before k0(rv)
   uint32_t Nv;               // non-null circular-buffer positions (depends on K and F)
   uint32_t F;                // filler bits (only CB 0 of a TB may have F > 0)
-  uint32_t rank_off;         // int32 offset of this (K, F)'s rank table [Ncb] (-1 = <NULL>)
+  uint32_t rank_off;         // int32 offset of this (K, F)'s rank table [Ncb] (-1 = <NULL>), followed
+                             // by the rank at every RM_CHUNK-th position [Ncb / RM_CHUNK + 2]
   uint32_t new_tb;           // 1 = first transmission (overwrite softbuffer), 0 = combine
   uint32_t crc24a;           // 1 when C == 1 (code-block CRC is the TB CRC24A)
   uint32_t tb;               // owning TB
@@ -104,6 +106,8 @@ struct MiKTab {              // per K, device resident
   uint32_t K, Ncb;
   uint32_t pos_off;          // uint32 offset: pos[3*(K+4)] circular-buffer position of d_i(k)
   uint32_t pi_off;           // uint32 offset: pi[K]
+  uint32_t crca_off;         // uint32 offset: CRC24A contribution of a single 1 at bit i, [K]
+  uint32_t crcb_off;         // uint32 offset: same for CRC24B
 };
 
 struct MiTbDesc {            // one per transport block

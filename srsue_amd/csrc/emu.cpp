@@ -43,6 +43,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.sb = &sb[g.sb_off];
       a.pos = &P.kdata[kt.pos_off];
       a.pi = &P.kdata[kt.pi_off];
+      a.crc_a = &P.kdata[kt.crca_off];
+      a.crc_b = &P.kdata[kt.crcb_off];
       a.scr = &scr[g.scratch_off];
       a.dec = &dec[g.dec_off];
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];

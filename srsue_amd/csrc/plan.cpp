@@ -144,11 +144,19 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       kt = (uint32_t)ktabs.size();
       ktab_idx[K] = kt;
       auto& kp = kpos_cache[K];
-      if (kp.first.empty()) { cb_pos_table(K, kp.first); qpp_table(K, kp.second); }
-      MiKTab t{K, ncb_of(K), (uint32_t)kdata.size(), 0};
-      kdata.insert(kdata.end(), kp.first.begin(), kp.first.end());
-      t.pi_off = (uint32_t)kdata.size();
-      kdata.insert(kdata.end(), kp.second.begin(), kp.second.end());
+      if (kp.empty()) {
+        kp.resize(4);
+        cb_pos_table(K, kp[0]);
+        qpp_table(K, kp[1]);
+        crc_bit_table(K, 0x864CFBu, kp[2]);
+        crc_bit_table(K, 0x800063u, kp[3]);
+      }
+      MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
+      uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
+      for (int q = 0; q < 4; q++) {
+        *offs[q] = (uint32_t)kdata.size();
+        kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
+      }
       ktabs.push_back(t);
     } else {
       kt = kit->second;
@@ -217,6 +225,14 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         const auto& rk = rank_cache[key].first;
         uint32_t off = (uint32_t)kdata.size();
         for (int32_t v : rk) kdata.push_back((uint32_t)v);
+        // chunk table: non-null positions before c * RM_CHUNK, c = 0 .. ceil(Ncb / RM_CHUNK)
+        const uint32_t nch = (uint32_t)((rk.size() + RM_CHUNK - 1) / RM_CHUNK);
+        uint32_t cnt = 0;
+        for (uint32_t c = 0, p = 0; c <= nch; c++) {
+          const uint32_t end = std::min<uint32_t>(c * RM_CHUNK, (uint32_t)rk.size());
+          for (; p < end; p++) cnt += rk[p] >= 0 ? 1 : 0;
+          kdata.push_back(cnt);
+        }
         rank_off[key] = off;
         ld.rank_off = off;
       } else {

@@ -1,29 +1,67 @@
 // rm.hip -- rate de-matching + HARQ combine into the group-interleaved softbuffer [Ncb][64 lanes].
-// See rm_body.h.  Each wavefront owns a run of circular-buffer positions for the 64 code blocks of
-// a group, so softbuffer reads and writes are 256-B coalesced rows; each lane streams its own
-// code block's LLRs in order (cache-line reuse across consecutive positions).
+//
+// Semantics: rm_body.h (bit-identical to the serial srslte_rm_turbo_rx loop).  MI355X layout: one
+// 256-thread workgroup owns RM_CHUNK circular-buffer positions of one 64-code-block group.  The
+// positions of a chunk receive a contiguous run of each code block's LLRs (the non-null ranks of
+// the chunk, modulo N_v), so the workgroup first stages, per lane, that run of e into an LDS tile
+// with coalesced 256-B loads (one wavefront per code-block row), then every wavefront combines one
+// position for all 64 lanes: softbuffer rows are read and written as 256-B coalesced rows and the
+// LLRs come from LDS (row stride RM_CHUNK + 1 floats: conflict-free column reads).  Repetition
+// beyond N_v (E > N_v, low code rates) adds the further copies straight from HBM in order.
 #include "kernels.h"
 #include "rm_body.h"
 
 namespace mi {
 
-constexpr int RM_PPW = 32;   // positions per wavefront
-
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata) {
+  __shared__ float tile[LANES][RM_CHUNK + 1];
+  __shared__ uint32_t ra_s[LANES], nr_s[LANES];
   const MiGroupDesc g = groups[blockIdx.y];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t pa = blockIdx.x * RM_CHUNK;
+  if (pa >= g.Ncb) return;
+  const uint32_t tid = threadIdx.x;
+  if (tid < LANES) {
+    const MiLaneDesc ld = lanes[g.lane0 + tid];
+    uint32_t ra = 0, nr = 0;
+    if (ld.valid) {
+      const uint32_t* ch = kdata + ld.rank_off + g.Ncb;
+      ra = ch[pa / RM_CHUNK];
+      nr = ch[pa / RM_CHUNK + 1] - ra;
+    }
+    ra_s[tid] = ra;
+    nr_s[tid] = nr;
+  }
+  __syncthreads();
+  // stage: tile[lane][t] = e_lane[(ra - r0 + t) mod Nv], t < nr
+  for (uint32_t idx = tid; idx < (uint32_t)LANES * RM_CHUNK; idx += 256) {
+    const uint32_t l = idx / RM_CHUNK, t = idx % RM_CHUNK;
+    if (t < nr_s[l]) {
+      const MiLaneDesc& ld = lanes[g.lane0 + l];
+      const uint32_t j = (ra_s[l] + ld.Nv - ld.r0 + t) % ld.Nv;
+      tile[l][t] = j < ld.E ? e[ld.e_off + j] : 0.0f;
+    }
+  }
+  __syncthreads();
+  const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
   const MiLaneDesc ld = lanes[g.lane0 + lane];
   if (!ld.valid) return;
   const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + ld.rank_off);
   float* sbg = sb + g.sb_off;
-  const uint32_t p0 = (blockIdx.x * 4 + wave) * RM_PPW;
-  for (int i = 0; i < RM_PPW; i++) {
-    const uint32_t p = p0 + i;
+  const uint32_t ra = ra_s[lane];
+  for (uint32_t i = (uint32_t)wave; i < (uint32_t)RM_CHUNK; i += 4) {
+    const uint32_t p = pa + i;
     if (p >= g.Ncb) break;
-    rm_combine_one(ld, rank, e, sbg, p, lane);
+    const int32_t rk = rank[p];
+    float v = ld.new_tb ? 0.0f : sbg[(size_t)p * LANES + lane];
+    if (rk >= 0) {
+      uint32_t j = ((uint32_t)rk + ld.Nv - ld.r0) % ld.Nv;
+      if (j < ld.E) v = v + tile[lane][(uint32_t)rk - ra];
+      for (j += ld.Nv; j < ld.E; j += ld.Nv) v = v + e[ld.e_off + j];
+    }
+    sbg[(size_t)p * LANES + lane] = v;
   }
 }
 
@@ -31,7 +69,7 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
                        const MiKTab* /*ktabs*/, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
                        hipStream_t st) {
   if (!n_groups) return;
-  dim3 g((max_ncb + 4 * RM_PPW - 1) / (4 * RM_PPW), n_groups);
+  dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
   hipLaunchKernelGGL(rm_combine_kernel, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data);
 }
 

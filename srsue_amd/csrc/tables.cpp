@@ -77,6 +77,16 @@ void qpp_table(uint32_t K, std::vector<uint32_t>& pi) {
   }
 }
 
+void crc_bit_table(uint32_t K, uint32_t poly, std::vector<uint32_t>& t) {
+  t.resize(K);
+  uint32_t c = poly;   // message "1": register = g mod x^24
+  for (int i = (int)K - 1; i >= 0; i--) {
+    t[i] = c;
+    const uint32_t fb = (c >> 23) & 1u;   // append one zero bit
+    c = ((c << 1) & 0xFFFFFFu) ^ (fb ? poly : 0u);
+  }
+}
+
 int cbsegm(uint32_t tbs, CbSegm* s) {
   const uint32_t Z = 6144;
   memset(s, 0, sizeof(*s));

@@ -20,6 +20,8 @@ uint32_t k0_of(uint32_t K, uint32_t rv);
 void cb_pos_table(uint32_t K, std::vector<uint32_t>& pos);
 void cb_rank_table(uint32_t K, uint32_t F, std::vector<int32_t>& rank, uint32_t* Nv);
 void qpp_table(uint32_t K, std::vector<uint32_t>& pi);
+// CRC register of a K-bit message holding a single 1 at bit i (zero init): x^(K-1-i+24) mod g
+void crc_bit_table(uint32_t K, uint32_t poly, std::vector<uint32_t>& t);
 // 36.211 7.2 Gold sequence, packed 32 bits per word (bit i at word[i/32] bit i%32)
 void gold_words(uint32_t c_init, uint32_t nbits, uint32_t* words);
 void gold_bits(uint32_t c_init, uint32_t nbits, uint8_t* bits);

@@ -23,6 +23,8 @@ __global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, 
   a.sb = sb + g.sb_off;
   a.pos = kdata + kt.pos_off;
   a.pi = kdata + kt.pi_off;
+  a.crc_a = kdata + kt.crca_off;
+  a.crc_b = kdata + kt.crcb_off;
   a.scr = scratch + g.scratch_off;
   a.dec = dec + g.dec_off;
   a.cb_bytes = cb_bytes + (size_t)li * CB_BYTES_STRIDE;

@@ -12,6 +12,12 @@
 // The full-length backward recursion is kept exact by storing beta every BETA_W steps and
 // recomputing the window in registers during the forward pass, so decisions and extrinsics are
 // bit-identical to the oracle (oracle/o_fec.c documents the operation order reproduced here).
+//
+// Latency hiding: each pass walks windows of BETA_W steps; the loads of window j+1 (and its beta
+// checkpoint) are issued before window j is computed (software pipelining, no data-dependent
+// branches around loads), and the code-block CRC is accumulated during the last half-iteration
+// from a per-K table of single-bit CRC contributions (CRC is linear over GF(2)), so no separate
+// CRC pass re-reads the decisions.
 #pragma once
 #include "dl_common.h"
 
@@ -27,7 +33,6 @@ MI_HD constexpr int tr_par(int s, int u) { return ((u ^ (s >> 1) ^ s) ^ (s >> 2)
 // predecessor (state, input) pairs of state sp: prev states have s>>1 == sp & 3
 MI_HD constexpr int tr_prev_s(int sp, int j) { return ((sp & 3) << 1) | j; }
 MI_HD constexpr int tr_prev_u(int sp, int j) {
-  // input u such that tr_next(prev, u) == sp
   return ((sp >> 2) ^ (tr_prev_s(sp, j) >> 1) ^ tr_prev_s(sp, j)) & 1;
 }
 
@@ -35,6 +40,8 @@ struct TdecArgs {
   const float* sb;        // group softbuffer [Ncb][64]
   const uint32_t* pos;    // [3(K+4)] circular-buffer position of decoder input t = 3k+i
   const uint32_t* pi;     // [K]
+  const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
+  const uint32_t* crc_b;  // [K] same for CRC24B
   float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/W+1)*8][64]
   uint8_t* dec;           // [K][64] decision bytes
   uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
@@ -45,33 +52,6 @@ struct TdecLaneResult { uint32_t its; uint32_t crc_ok; };
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
-}
-
-template <bool DEC2>
-MI_HD inline void tdec_inputs(const TdecArgs& a, int lane, bool first, uint32_t k, float& xs, float& xp,
-                              float& l1, float& wv) {
-  const uint32_t K = a.K;
-  if (k < K) {
-    if (!DEC2) {
-      uint32_t t = 3 * k;
-      float sys = (k < a.F) ? FILLER_LLR : a.sb[(size_t)a.pos[t] * LANES + lane];
-      float p1 = (k < a.F) ? FILLER_LLR : a.sb[(size_t)a.pos[t + 1] * LANES + lane];
-      wv = first ? 0.0f : a.scr[(size_t)k * LANES + lane];
-      xs = sys + wv;
-      xp = p1;
-    } else {
-      uint32_t i = a.pi[k];
-      l1 = a.scr[(size_t)(K + i) * LANES + lane];
-      wv = first ? 0.0f : a.scr[(size_t)i * LANES + lane];
-      xs = l1 - wv;
-      xp = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
-    }
-  } else {
-    uint32_t j = k - K;
-    uint32_t t = 3 * K + (DEC2 ? 6 : 0) + 2 * j;
-    xs = a.sb[(size_t)a.pos[t] * LANES + lane];
-    xp = a.sb[(size_t)a.pos[t + 1] * LANES + lane];
-  }
 }
 
 // one backward step: beta_k from beta_{k+1}
@@ -112,35 +92,78 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
   return llr;
 }
 
-template <bool DEC2>
-MI_HD inline void tdec_half(const TdecArgs& a, int lane, bool first) {
+// raw per-step inputs of one window: DEC1 {sys, p1, w}, DEC2 {llr1[pi], w[pi], p2}
+struct TdecWin { float a[BETA_W], b[BETA_W], c[BETA_W]; };
+
+template <bool DEC2, bool FIRST>
+MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin& r) {
   const uint32_t K = a.K;
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    const uint32_t k = base + i;
+    if (!DEC2) {
+      r.a[i] = a.sb[(size_t)a.pos[3 * k] * LANES + lane];
+      r.b[i] = a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane];
+      r.c[i] = FIRST ? 0.0f : a.scr[(size_t)k * LANES + lane];
+    } else {
+      const uint32_t pk = a.pi[k];
+      r.a[i] = a.scr[(size_t)(K + pk) * LANES + lane];
+      r.b[i] = FIRST ? 0.0f : a.scr[(size_t)pk * LANES + lane];
+      r.c[i] = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
+    }
+  }
+}
+
+// decoder inputs (xs, xp) of step base+i from the raw window values (filler: known-zero bits)
+template <bool DEC2>
+MI_HD inline void tdec_xs_xp(const TdecWin& r, int i, uint32_t k, uint32_t F, float& xs, float& xp) {
+  if (!DEC2) {
+    const bool fill = k < F;
+    xs = (fill ? FILLER_LLR : r.a[i]) + r.c[i];
+    xp = fill ? FILLER_LLR : r.b[i];
+  } else {
+    xs = r.a[i] - r.b[i];
+    xp = r.c[i];
+  }
+}
+
+template <bool DEC2, bool FIRST>
+MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
+  const uint32_t K = a.K, F = a.F;
   float* ck = a.scr + (size_t)2 * K * LANES;  // beta checkpoints
   const float NINF = -INFINITY;
   float b[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) b[s] = s ? NINF : 0.0f;
-  float l1d, wvd;
-  // ---- backward pass: tail steps K+2..K, then windows; checkpoint every BETA_W steps
-  for (int k = (int)K + 2; k >= (int)K; k--) {
-    float xs, xp;
-    tdec_inputs<DEC2>(a, lane, first, (uint32_t)k, xs, xp, l1d, wvd);
-    float nb[8];
-    beta_step(b, xs, xp, nb);
+  // ---- backward pass: 3 tail steps (regular trellis), then windows from the end
+  {
+    const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
+    float tx[3], tp[3];
 #pragma unroll
-    for (int s = 0; s < 8; s++) b[s] = nb[s];
+    for (int j = 0; j < 3; j++) {
+      tx[j] = a.sb[(size_t)a.pos[t0 + 2 * j] * LANES + lane];
+      tp[j] = a.sb[(size_t)a.pos[t0 + 2 * j + 1] * LANES + lane];
+    }
+#pragma unroll
+    for (int j = 2; j >= 0; j--) {
+      float nb[8];
+      beta_step(b, tx[j], tp[j], nb);
+#pragma unroll
+      for (int s = 0; s < 8; s++) b[s] = nb[s];
+    }
   }
 #pragma unroll
   for (int s = 0; s < 8; s++) ck[((size_t)(K / BETA_W) * 8 + s) * LANES + lane] = b[s];
+  TdecWin cur, nxt;
+  tdec_load_window<DEC2, FIRST>(a, lane, K - BETA_W, cur);
   for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
-    float xs[BETA_W], xp[BETA_W];
-#pragma unroll
-    for (int i = 0; i < BETA_W; i++) tdec_inputs<DEC2>(a, lane, first, (uint32_t)(base + i), xs[i], xp[i], l1d, wvd);
+    if (base >= BETA_W) tdec_load_window<DEC2, FIRST>(a, lane, (uint32_t)(base - BETA_W), nxt);
 #pragma unroll
     for (int i = BETA_W - 1; i >= 0; i--) {
-      if (base + i == 0) break;
-      float nb[8];
-      beta_step(b, xs[i], xp[i], nb);
+      if (base + i == 0) break;   // beta_0 is never used
+      float xs, xp, nb[8];
+      tdec_xs_xp<DEC2>(cur, i, (uint32_t)(base + i), F, xs, xp);
+      beta_step(b, xs, xp, nb);
 #pragma unroll
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
@@ -148,52 +171,64 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, bool first) {
 #pragma unroll
       for (int s = 0; s < 8; s++) ck[((size_t)(base / BETA_W) * 8 + s) * LANES + lane] = b[s];
     }
+    cur = nxt;
   }
   // ---- forward pass over windows, recomputing beta_{base+1..base+W} from the checkpoint
   float al[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
-  for (uint32_t base = 0; base < K; base += BETA_W) {
-    float xs[BETA_W], xp[BETA_W], l1[BETA_W], wv[BETA_W];
+  float ckc[8], ckn[8];
+  tdec_load_window<DEC2, FIRST>(a, lane, 0, cur);
 #pragma unroll
-    for (int i = 0; i < BETA_W; i++) tdec_inputs<DEC2>(a, lane, first, base + i, xs[i], xp[i], l1[i], wv[i]);
+  for (int s = 0; s < 8; s++) ckc[s] = ck[((size_t)1 * 8 + s) * LANES + lane];
+  for (uint32_t base = 0; base < K; base += BETA_W) {
+    if (base + BETA_W < K) {
+      tdec_load_window<DEC2, FIRST>(a, lane, base + BETA_W, nxt);
+#pragma unroll
+      for (int s = 0; s < 8; s++) ckn[s] = ck[((size_t)(base / BETA_W + 2) * 8 + s) * LANES + lane];
+    }
+    float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(cur, i, base + i, F, xs[i], xp[i]);
     float bw[BETA_W][8];
 #pragma unroll
-    for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ck[((size_t)(base / BETA_W + 1) * 8 + s) * LANES + lane];
+    for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
 #pragma unroll
     for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
     for (int i = 0; i < BETA_W; i++) {
       const uint32_t k = base + i;
-      float llr = alpha_step(al, bw[i], xs[i], xp[i]);
+      const float llr = alpha_step(al, bw[i], xs[i], xp[i]);
       if (!DEC2) {
-        a.scr[(size_t)(K + k) * LANES + lane] = llr;                 // llr1
+        a.scr[(size_t)(K + k) * LANES + lane] = llr;                         // llr1
       } else {
         const uint32_t pk = a.pi[k];
-        a.scr[(size_t)pk * LANES + lane] = wv[i] + (llr - l1[i]);    // w update
-        a.dec[(size_t)pk * LANES + lane] = llr > 0.0f ? 1 : 0;       // decision
+        a.scr[(size_t)pk * LANES + lane] = cur.b[i] + (llr - cur.a[i]);      // w update
+        const bool bit = llr > 0.0f;
+        a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                       // decision
+        const uint32_t t = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
+        crc ^= bit ? t : 0u;                                                  // CRC by linearity
       }
     }
+    cur = nxt;
+#pragma unroll
+    for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
   }
-}
-
-MI_HD inline uint32_t tdec_crc(const TdecArgs& a, int lane) {
-  const uint32_t poly = a.crc24a ? 0x864CFBu : 0x800063u;
-  uint32_t crc = 0;
-  for (uint32_t k = 0; k < a.K; k++) {
-    uint32_t fb = ((crc >> 23) ^ a.dec[(size_t)k * LANES + lane]) & 1u;
-    crc = ((crc << 1) & 0xFFFFFFu) ^ (fb ? poly : 0u);
-  }
-  return crc;
 }
 
 MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
-    tdec_half<false>(a, lane, it == 0);
-    tdec_half<true>(a, lane, it == 0);
+    uint32_t crc = 0;
+    if (it == 0) {
+      tdec_half<false, true>(a, lane, crc);
+      tdec_half<true, true>(a, lane, crc);
+    } else {
+      tdec_half<false, false>(a, lane, crc);
+      tdec_half<true, false>(a, lane, crc);
+    }
     r.its = it + 1;
-    r.crc_ok = tdec_crc(a, lane) == 0;
+    r.crc_ok = crc == 0;
     if (a.early_stop && r.crc_ok) break;
   }
   for (uint32_t j = 0; j < a.K / 8; j++) {
