@@ -37,17 +37,29 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
     s_j0[tid] = j0; s_nr[tid] = nr; s_nv[tid] = ld.Nv; s_E[tid] = ld.E; s_eoff[tid] = ld.e_off;
   }
   __syncthreads();
-  // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; 64 threads per code-block row
-  for (uint32_t l = tid >> 6; l < (uint32_t)LANES; l += 4) {
-    const uint32_t nr = s_nr[l], nv = s_nv[l], E = s_E[l];
-    const float* el = e + s_eoff[l];
-    uint32_t j = s_j0[l] + (tid & 63);
-    if (j >= nv) j -= nv;
-    for (uint32_t t = tid & 63; t < nr; t += 64) {
-      tile[l][t] = j < E ? el[j] : 0.0f;
-      j += 64;
-      if (j >= nv) j -= nv;
+  // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
+  // all of a wavefront's loads issued before its LDS writes
+  constexpr int ROWS = LANES / 4, PER = RM_CHUNK / 64;
+  {
+    float v[ROWS][PER];
+    const uint32_t w = tid >> 6, q = tid & 63;
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+      const uint32_t l = w + 4 * r;
+      const uint32_t nr = s_nr[l], nv = s_nv[l], E = s_E[l];
+      const float* el = e + s_eoff[l];
+#pragma unroll
+      for (int c = 0; c < PER; c++) {
+        const uint32_t t = q + 64 * c;
+        uint32_t j = s_j0[l] + t;
+        if (j >= nv) j -= nv;
+        v[r][c] = (t < nr && j < E) ? el[j] : 0.0f;
+      }
     }
+#pragma unroll
+    for (int r = 0; r < ROWS; r++)
+#pragma unroll
+      for (int c = 0; c < PER; c++) tile[w + 4 * r][q + 64 * c] = v[r][c];
   }
   __syncthreads();
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
@@ -59,13 +71,22 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   const uint32_t ra = ch[pa / RM_CHUNK];
   const uint32_t j0 = s_j0[lane], nv = ld.Nv, E = ld.E;
   const bool rep = E > nv;
-  for (uint32_t i = (uint32_t)wave; i < (uint32_t)RM_CHUNK; i += 4) {
-    const uint32_t p = pa + i;
-    if (p >= g.Ncb) break;
-    const int32_t rk = rank[p];
-    float v = ld.new_tb ? 0.0f : sbg[(size_t)p * LANES + lane];
-    if (rk >= 0) {
-      const uint32_t t = (uint32_t)rk - ra;
+  constexpr int NP = RM_CHUNK / 4;
+  int32_t rk[NP];
+  float old[NP];
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    const uint32_t p = pa + (uint32_t)wave + 4u * i;
+    rk[i] = p < g.Ncb ? rank[p] : -2;
+    old[i] = (!ld.new_tb && p < g.Ncb) ? sbg[(size_t)p * LANES + lane] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    const uint32_t p = pa + (uint32_t)wave + 4u * i;
+    if (rk[i] == -2) continue;
+    float v = old[i];
+    if (rk[i] >= 0) {
+      const uint32_t t = (uint32_t)rk[i] - ra;
       uint32_t j = j0 + t;
       if (j >= nv) j -= nv;
       if (j < E) v = v + tile[lane][t];
