@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU measurement recipe, run through gpurun:  ./tools/profile.sh <tag>
+#  1. the default bench line (python3 bench.py)
+#  2. rocprofv3 --kernel-trace --stats of the SAME command (per-kernel average durations)
+#  3. separate PMC passes FETCH_SIZE and WRITE_SIZE (MI355X_MICROARCH.md: TCC slots do not fit both)
+#  4. tools/summarize_profile.py -> summary.json / summary.md (traffic per launch, agreement check)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1
+shift
+ARGS="$@"
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 python3 $R/bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err || exit 11
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/prof_trace.log 2>&1 || exit 12
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py $ARGS --no-cpu-baseline > $OUT/prof_fetch.log 2>&1 || exit 13
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS --no-cpu-baseline > $OUT/prof_write.log 2>&1 || exit 14
+python3 $R/tools/summarize_profile.py $OUT || exit 15
+echo done

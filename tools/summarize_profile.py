@@ -1,0 +1,70 @@
+"""Summarise a tools/profile.sh output directory into summary.json + summary.md.
+
+Per kernel: rocprofv3 kernel-trace average duration, HBM traffic per launch from the PMC passes
+(FETCH_SIZE x 2 + WRITE_SIZE, in KiB units -> bytes; the x2 is the gfx950 FETCH_SIZE correction of
+MI355X_MICROARCH.md section HBM, which we checked against the OFDM kernel's known byte count), and
+for the dominant kernel the algorithmic bytes / agreement with the bench line's live HIP-event time.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def short(name):
+    n = name.split("(")[0]
+    return n.replace("void ", "").replace("mi::", "")
+
+
+def main(d):
+    bench = json.load(open(os.path.join(d, "bench.json")))
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))):
+        stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                                   "pct": float(r["Percentage"])}
+    pmc = collections.defaultdict(dict)
+    for sub, cname in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(os.path.join(d, sub, "run_counter_collection.csv"))):
+            if r["Counter_Name"] == cname:
+                acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            pmc[k][cname] = sum(v) / len(v)
+    kernels = {}
+    for k, s in stats.items():
+        if not k.startswith(("tdec", "rm_", "demap", "ofdm", "chest", "tb_")):
+            continue
+        f = pmc.get(k, {}).get("FETCH_SIZE")
+        w = pmc.get(k, {}).get("WRITE_SIZE")
+        traffic = None if f is None or w is None else (2 * f + w) * 1024
+        kernels[k] = dict(s, traffic_bytes_per_launch=traffic,
+                          traffic_GBs=None if traffic is None else traffic / (s["avg_ms"] * 1e-3) / 1e9)
+    rl = bench["roofline"]
+    td = kernels.get("tdec_kernel", {})
+    summary = {
+        "bench": {k: bench[k] for k in ("value", "unit", "ms_per_step", "stage_ms_per_step", "config")},
+        "roofline_bench": rl,
+        "kernels": kernels,
+        "tdec_agreement": {"bench_hip_event_avg_ms": rl["avg_launch_ms"], "rocprof_avg_ms": td.get("avg_ms"),
+                           "ratio": None if not td else round(td["avg_ms"] / rl["avg_launch_ms"], 4)},
+        "tdec_traffic_over_algorithmic": None if not td.get("traffic_bytes_per_launch") else
+        round(td["traffic_bytes_per_launch"] / rl["algorithmic_bytes_per_launch"], 3),
+    }
+    json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
+    with open(os.path.join(d, "summary.md"), "w") as f:
+        f.write(f"# Profile summary ({os.path.basename(d)})\n\n")
+        f.write(f"bench: {bench['value']} {bench['unit']}, {bench['ms_per_step']} ms/step, {bench['config']['workload']}\n\n")
+        f.write("| kernel | calls | avg ms (rocprof) | % time | HBM traffic / launch (MB) | GB/s |\n|---|---|---|---|---|---|\n")
+        for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["pct"]):
+            t = v["traffic_bytes_per_launch"]
+            tmb = "-" if t is None else "%.1f" % (t / 1e6)
+            gbs = "-" if t is None else "%.0f" % v["traffic_GBs"]
+            f.write("| %s | %d | %.4f | %.2f | %s | %s |\n" % (k, v["calls"], v["avg_ms"], v["pct"], tmb, gbs))
+        f.write(f"\ntdec agreement (rocprof / bench HIP events): {summary['tdec_agreement']}\n")
+        f.write(f"\ntdec traffic / algorithmic bytes: {summary['tdec_traffic_over_algorithmic']}\n")
+    print(json.dumps(summary["tdec_agreement"]), summary["tdec_traffic_over_algorithmic"])
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
