@@ -50,6 +50,30 @@ def tb_payload(seed, nbytes):
     return out[:nbytes]
 
 
+def kernel_src_hash():
+    """Content hash of the HIP/C++ sources: a committed PMC traffic figure is only reported when it
+    was measured on exactly these kernels (profiles/traffic.json, written by tools/profile.sh)."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "srsue_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".h", ".hip", ".cpp")) and f != "emu.cpp":
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(sf_per_gpu):
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        t = json.load(open(p))
+    except (OSError, ValueError):
+        return None, None
+    if t.get("src_hash") != kernel_src_hash() or t.get("sf_per_gpu") != sf_per_gpu:
+        return None, None
+    return t["tdec_traffic_bytes_per_launch"], "profiles/traffic.json: " + t["source"]
+
+
 def make_cfg(i, new_tb=1):
     return abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=SF_CYCLE[i % len(SF_CYCLE)], cfi=1, tm=1,
                       rnti=0x46, rv=0, tbs=TBS_MCS28_100PRB, Qm=6, new_tb=new_tb)
@@ -172,6 +196,7 @@ def main():
         tdec_ms = stage["tdec"]
         tdec_bytes = batch.algo_bytes(4)
         achieved = tdec_bytes / (tdec_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(B)
         out = {
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
@@ -186,7 +211,7 @@ def main():
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": "tdec_kernel (max-log-MAP turbo)", "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": tdec_bytes,
                          "avg_launch_ms": round(tdec_ms, 4), "launches_averaged": nprof},
         }

@@ -11,6 +11,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_src_hash  # noqa: E402
+
 
 def short(name):
     n = name.split("(")[0]
@@ -52,6 +55,12 @@ def main(d):
         round(td["traffic_bytes_per_launch"] / rl["algorithmic_bytes_per_launch"], 3),
     }
     json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
+    if td.get("traffic_bytes_per_launch"):
+        json.dump({"src_hash": kernel_src_hash(), "sf_per_gpu": bench["config"]["subframes_per_gpu"],
+                   "tdec_traffic_bytes_per_launch": td["traffic_bytes_per_launch"],
+                   "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench command "
+                             f"({os.path.basename(d)}); bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024"},
+                  open(os.path.join(d, "traffic.json"), "w"), indent=1)
     with open(os.path.join(d, "summary.md"), "w") as f:
         f.write(f"# Profile summary ({os.path.basename(d)})\n\n")
         f.write(f"bench: {bench['value']} {bench['unit']}, {bench['ms_per_step']} ms/step, {bench['config']['workload']}\n\n")
