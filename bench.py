@@ -79,12 +79,32 @@ def make_cfg(i, new_tb=1):
                       rnti=0x46, rv=0, tbs=TBS_MCS28_100PRB, Qm=6, new_tb=new_tb)
 
 
-def make_pool(pool, snr_db, threads):
-    """Distinct synthetic subframes from the product's transmitter (mi_tx_subframe), CPU threads."""
+def shard_range(total, rank, world):
+    """Contiguous subframe range of one rank (no exchange step, contiguous shards)."""
+    per, rem = divmod(total, world)
+    start = rank * per + min(rank, rem)
+    return start, per + (1 if rank < rem else 0)
+
+
+def reduce_over_ranks(elapsed, n_ok, n_cb, world, device="cpu"):
+    """The only cross-rank traffic: max of the elapsed time, sums of CRC-OK TBs and code blocks."""
+    if world == 1:
+        return elapsed, float(n_ok), float(n_cb)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([float(n_ok), float(n_cb)], dtype=torch.float64, device=device)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return float(t[0]), float(s[0]), float(s[1])
+
+
+def make_pool(pool, snr_db, threads, first=0):
+    """Distinct synthetic subframes from the product's transmitter (mi_tx_subframe), CPU threads.
+    Subframe g (global index) carries TB splitmix64(0x5EED0000 + g) and noise seed 0xA5A5 + g."""
     def one(i):
-        c = make_cfg(i)
-        tb = tb_payload(i, c.tbs // 8)
-        return abi.tx_subframe(c, tb, snr_db=snr_db, seed=0xA5A5 + i), tb
+        g = first + i
+        c = make_cfg(g)
+        tb = tb_payload(g, c.tbs // 8)
+        return abi.tx_subframe(c, tb, snr_db=snr_db, seed=0xA5A5 + g), tb
     with cf.ThreadPoolExecutor(max_workers=threads) as ex:
         res = list(ex.map(one, range(pool)))
     return [r[0] for r in res], [r[1] for r in res]
@@ -143,8 +163,9 @@ def main():
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
 
     B = args.sf_per_gpu
-    pool_iq, pool_tb = make_pool(min(args.pool, B), args.snr, threads)
-    cfgs = [make_cfg(i) for i in range(B)]
+    first, _ = shard_range(B * world, rank, world)          # this rank's global subframe indices
+    pool_iq, pool_tb = make_pool(min(args.pool, B), args.snr, threads, first)
+    cfgs = [make_cfg(first + i) for i in range(B)]
     batch = abi.Batch(cfgs, max_its=args.max_its, profile=True)
     # stage the pool in HBM once, replicate on device into the batch IQ layout
     sfl = len(pool_iq[0])   # floats per subframe
@@ -179,15 +200,7 @@ def main():
     n_ok = int(crc.sum())
     bad = sum(int(not np.array_equal(batch.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(0, B, max(1, B // 64)))
     ncb = batch.n_codeblocks
-    tot = torch.tensor([elapsed, float(n_ok), float(ncb), float(its.mean())], dtype=torch.float64, device=dev)
-    if world > 1:
-        t_max = tot[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        s = tot[1:3].clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        elapsed, n_ok_all, ncb_all = float(t_max[0]), float(s[0]), float(s[1])
-    else:
-        n_ok_all, ncb_all = float(n_ok), float(ncb)
+    elapsed, n_ok_all, ncb_all = reduce_over_ranks(elapsed, n_ok, ncb, world, dev)
 
     if rank == 0:
         K = args.steps

@@ -1,0 +1,92 @@
+"""Generates the committed golden fixtures under tests/golden/ (run from the repo root:
+`python tests/golden/make_golden.py`).  Parity is unpinned against srsLTE itself (not in the
+container), so the fixtures pin (a) 3GPP-derived known answers and transmit-chain
+ground truth and (b) the oracle's own outputs, so any later change to the oracle is caught.
+
+Fixtures
+  tdec_K40.npz            info bits, noiseless LLRs (+-4), decoded bits           
+  tdec_K6144_ebno.npz     config 1 (turbodecoder_test): K=6144, BPSK/AWGN at Eb/N0 {0.5,1,1.5,2,3} dB,
+                          8 fixed iterations, early stop off: LLRs, decisions, bit errors
+  rm_K5824.npz            rate-match -> de-match round trip, rv 0..3, E = 6924   
+  sf_1p4mhz.npz           1.4 MHz TM1 subframe: IQ (product TX, 20 dB), TB, oracle grid/ce/LLR/payload
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.dirname(HERE)]
+import oracle_lib as O  # noqa: E402
+from helpers import oracle_dlsch, oracle_front  # noqa: E402
+from srsue_amd import abi  # noqa: E402
+
+
+def turbo_llr(bits, K, ebno_db, rng, amp=None):
+    d = np.zeros(3 * (K + 4), np.uint8)
+    assert O.lib().or_tcod(np.ascontiguousarray(bits, np.uint8), K, 0, d) == 0
+    x = 1.0 - 2.0 * d                       # BPSK: 0 -> +1
+    if amp is not None:
+        return (-amp * x).astype(np.float32)
+    rate = K / (3.0 * K + 12)
+    sigma2 = 1.0 / (2 * rate * 10 ** (ebno_db / 10))
+    y = x + rng.normal(0, np.sqrt(sigma2), x.shape)
+    return (-2.0 * y / sigma2).astype(np.float32)   # LLR > 0 => bit 1
+
+
+def main():
+    L = O.lib()
+    rng = np.random.default_rng(1)
+    # --- K = 40 noiseless
+    b40 = rng.integers(0, 2, 40).astype(np.uint8)
+    l40 = turbo_llr(b40, 40, None, rng, amp=4.0)
+    dec40, its, ok = O.Tdec().decode_cb(l40, 40, max_its=8, early_stop=False)
+    np.savez_compressed(os.path.join(HERE, "tdec_K40.npz"), bits=b40, llr=l40, dec=dec40)
+    # --- K = 6144, config 1 sweep
+    K = 6144
+    ebnos = np.array([0.5, 1.0, 1.5, 2.0, 3.0])
+    bits = rng.integers(0, 2, K).astype(np.uint8)
+    llrs, decs, errs = [], [], []
+    td = O.Tdec()
+    for e in ebnos:
+        llr = turbo_llr(bits, K, e, np.random.default_rng(int(e * 10) + 1))
+        dec, its, ok = td.decode_cb(llr, K, max_its=8, early_stop=False)
+        llrs.append(llr); decs.append(dec); errs.append(int(np.sum(dec != bits)))
+    np.savez_compressed(os.path.join(HERE, "tdec_K6144_ebno.npz"), ebno=ebnos, bits=bits, llr=np.stack(llrs),
+                        dec=np.stack(decs), errors=np.array(errs))
+    print("K=6144 bit errors per Eb/N0", dict(zip(ebnos.tolist(), errs)))
+    # --- rate matching round trip
+    K, E = 5824, 6924
+    bk = rng.integers(0, 2, K).astype(np.uint8)
+    d = np.zeros(3 * (K + 4), np.uint8)
+    L.or_tcod(bk, K, 0, d)
+    ncb = L.or_ncb(K)
+    es, outs = [], []
+    for rv in range(4):
+        e = np.zeros(E, np.uint8)
+        L.or_rm_tx(d, K, E, rv, e)
+        llr = (2.0 * e - 1.0).astype(np.float32)
+        sb = np.zeros(ncb, np.float32)
+        out = np.zeros(3 * (K + 4), np.float32)
+        L.or_rm_rx(llr, E, K, 0, rv, 1, sb, out)
+        es.append(e); outs.append(out)
+    np.savez_compressed(os.path.join(HERE, "rm_K5824.npz"), d=d, e=np.stack(es), out=np.stack(outs))
+    # --- 1.4 MHz subframe
+    cfg = abi.sf_cfg(cell_id=301, nof_prb=6, nof_ports=1, sf_idx=1, cfi=2, tbs=2344, Qm=4)
+    tb = O.splitmix_bytes(0x5EED0000 + 7, cfg.tbs // 8)
+    iq = abi.tx_subframe(cfg, tb, snr_db=20.0, seed=0xA5A5 + 7)
+    grid, ce, met, llr = oracle_front(cfg, iq)
+    ok, pay, noi, _ = oracle_dlsch(cfg, llr)
+    assert ok and np.array_equal(pay, tb)
+    np.savez_compressed(os.path.join(HERE, "sf_1p4mhz.npz"), iq=iq, tb=tb, grid=grid, ce=ce, metrics=met, llr=llr,
+                        payload=pay, noi=np.array([noi]),
+                        cfg=np.array([cfg.cell_id, cfg.nof_prb, cfg.nof_ports, cfg.sf_idx, cfg.cfi, cfg.tbs, cfg.Qm]))
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,69 @@
+"""CPU, world_size 2 over gloo: the multi-GPU structure of bench.py (one process per GPU, contiguous
+subframe shards, no collective on the data path, max-over-ranks timing + sums) exercised with the
+test-only host emulation of the decoder kernels standing in for the GPU."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from helpers import oracle_front
+    from srsue_amd import abi
+    total = 6
+    first, n = bench.shard_range(total, rank, world)
+    cfgs, llrs, tbs = [], [], []
+    for g in range(first, first + n):
+        c = abi.sf_cfg(cell_id=1, nof_prb=6, nof_ports=1, sf_idx=bench.SF_CYCLE[g % 8], tbs=4392, Qm=6)
+        tb = bench.tb_payload(g, c.tbs // 8)
+        iq = abi.tx_subframe(c, tb, snr_db=30.0, seed=0xA5A5 + g)
+        cfgs.append(c); llrs.append(oracle_front(c, iq)[3]); tbs.append(tb)
+    arr = abi.cfg_array(cfgs)
+    flat = np.concatenate(llrs).astype(np.float32)
+    pe = np.zeros(sum(c.tbs // 8 for c in cfgs), np.uint8)
+    ok = np.zeros(n, np.uint32)
+    its = np.zeros(n, np.uint32)
+    abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data, ok.ctypes.data,
+                             its.ctypes.data, None)
+    good = all(np.array_equal(pe[i * 549:(i + 1) * 549], tbs[i]) for i in range(n))
+    elapsed = 0.5 + rank       # stand-in timings: the max must win
+    t, n_ok, n_cb = bench.reduce_over_ranks(elapsed, int(ok.sum()), n, world)
+    q.put((rank, first, n, good, t, n_ok, n_cb))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_without_data_path_collective(built):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 3), (3, 3)]          # contiguous shards cover 0..5
+    assert all(r[3] for r in res)                                     # each rank decoded its own TBs
+    assert all(r[4] == 1.5 for r in res)                              # max over ranks
+    assert all(r[5] == 6 and r[6] == 6 for r in res)                  # sums over ranks
+
+
+def test_shard_range_covers_everything():
+    import bench
+    for total in (1, 7, 100000):
+        for world in (1, 2, 4, 8):
+            spans = [bench.shard_range(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and sum(n for _, n in spans) == total
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
