@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libsrsue_amd.so")
+LIB_PATH = os.environ.get("SRSUE_AMD_LIB") or os.path.join(PKG_DIR, "libsrsue_amd.so")
 EMU_PATH = os.path.join(PKG_DIR, "libsrsue_amd_emu.so")
 
 MAX_PRB = 110

@@ -24,7 +24,11 @@ constexpr int NSYMB = 14;            // normal CP, symbols per subframe
 constexpr int KMAX = 6144;           // largest turbo code block
 constexpr int NCB_MAX = 3 * 32 * ((KMAX + 4 + 31) / 32);   // 18528
 constexpr int LANES = 64;            // code blocks per wavefront group (one CB per lane)
-constexpr int BETA_W = 4;            // beta checkpoint spacing in the turbo kernel (161 VGPRs: 3 waves/SIMD)
+constexpr int BETA_W = 4;            // beta register window of the turbo kernel
+#ifndef MI_TDEC_CK
+#define MI_TDEC_CK 4
+#endif
+constexpr int TDEC_CK = MI_TDEC_CK;  // beta checkpoint spacing: BETA_W (one window) or 2 BETA_W
 constexpr float FILLER_LLR = -10000.0f;
 constexpr int RM_CHUNK = 128;        // circular-buffer positions per rate-dematch workgroup
 

@@ -171,7 +171,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       g.scratch_off = scratch_floats;
       g.dec_off = dec_bytes;
       sb_floats += (size_t)Ncb * LANES;
-      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / BETA_W + 1));
+      scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK + 1));
       dec_bytes += (size_t)K * LANES;
       groups.push_back(g);
       for (size_t q = 0; q < (size_t)LANES; q++) {

@@ -42,7 +42,7 @@ struct TdecArgs {
   const uint32_t* pi;     // [K]
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
   const uint32_t* crc_b;  // [K] same for CRC24B
-  float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/W+1)*8][64]
+  float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/(2W)+1)*7][64]
   uint8_t* dec;           // [K][64] decision bytes
   uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
   uint32_t K, F, max_its, early_stop, crc24a;
@@ -127,15 +127,47 @@ MI_HD inline void tdec_xs_xp(const TdecWin& r, int i, uint32_t k, uint32_t F, fl
   }
 }
 
+// beta checkpoint c (= beta at step c * CK) holds states 1..7 (state 0 is 0 after normalisation)
+MI_HD inline void ck_store(float* ck, uint32_t c, int lane, const float (&b)[8]) {
+#pragma unroll
+  for (int s = 1; s < 8; s++) ck[((size_t)c * 7 + (s - 1)) * LANES + lane] = b[s];
+}
+MI_HD inline void ck_load(const float* ck, uint32_t c, int lane, float (&b)[8]) {
+  b[0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; s++) b[s] = ck[((size_t)c * 7 + (s - 1)) * LANES + lane];
+}
+
+// per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
+template <bool DEC2>
+MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, const TdecWin& w, int i, uint32_t& crc) {
+  const uint32_t K = a.K;
+  if (!DEC2) {
+    a.scr[(size_t)(K + k) * LANES + lane] = llr;                       // llr1
+  } else {
+    const uint32_t pk = a.pi[k];
+    a.scr[(size_t)pk * LANES + lane] = w.b[i] + (llr - w.a[i]);        // w update
+    const bool bit = llr > 0.0f;
+    a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                     // decision
+    const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
+    crc ^= bit ? tt : 0u;                                               // CRC by linearity
+  }
+}
+
+// One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then
+// the K info steps, checkpointed every CK = 2 BETA_W steps.  Forward pass: per checkpoint interval
+// [a, a + CK) the beta values are recomputed from the checkpoint at a + CK as two register windows
+// of BETA_W steps (first half, then second half), alpha and the LLRs follow.
 template <bool DEC2, bool FIRST>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
+  constexpr int CK = TDEC_CK;
+  static_assert(CK == BETA_W || CK == 2 * BETA_W, "checkpoint spacing");
   const uint32_t K = a.K, F = a.F;
   float* ck = a.scr + (size_t)2 * K * LANES;  // beta checkpoints
   const float NINF = -INFINITY;
   float b[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) b[s] = s ? NINF : 0.0f;
-  // ---- backward pass: 3 tail steps (regular trellis), then windows from the end
   {
     const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
     float tx[3], tp[3];
@@ -152,8 +184,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
   }
-#pragma unroll
-  for (int s = 0; s < 8; s++) ck[((size_t)(K / BETA_W) * 8 + s) * LANES + lane] = b[s];
+  ck_store(ck, K / CK, lane, b);
   TdecWin cur, nxt;
   tdec_load_window<DEC2, FIRST>(a, lane, K - BETA_W, cur);
   for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
@@ -167,52 +198,93 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
 #pragma unroll
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
-    if (base > 0) {
-#pragma unroll
-      for (int s = 0; s < 8; s++) ck[((size_t)(base / BETA_W) * 8 + s) * LANES + lane] = b[s];
-    }
+    if (base > 0 && base % CK == 0) ck_store(ck, (uint32_t)base / CK, lane, b);
     cur = nxt;
   }
-  // ---- forward pass over windows, recomputing beta_{base+1..base+W} from the checkpoint
+  // ---- forward pass
   float al[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
-  float ckc[8], ckn[8];
-  tdec_load_window<DEC2, FIRST>(a, lane, 0, cur);
-#pragma unroll
-  for (int s = 0; s < 8; s++) ckc[s] = ck[((size_t)1 * 8 + s) * LANES + lane];
-  for (uint32_t base = 0; base < K; base += BETA_W) {
-    if (base + BETA_W < K) {
-      tdec_load_window<DEC2, FIRST>(a, lane, base + BETA_W, nxt);
-#pragma unroll
-      for (int s = 0; s < 8; s++) ckn[s] = ck[((size_t)(base / BETA_W + 2) * 8 + s) * LANES + lane];
-    }
-    float xs[BETA_W], xp[BETA_W];
-#pragma unroll
-    for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(cur, i, base + i, F, xs[i], xp[i]);
-    float bw[BETA_W][8];
-#pragma unroll
-    for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
-#pragma unroll
-    for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
-#pragma unroll
-    for (int i = 0; i < BETA_W; i++) {
-      const uint32_t k = base + i;
-      const float llr = alpha_step(al, bw[i], xs[i], xp[i]);
-      if (!DEC2) {
-        a.scr[(size_t)(K + k) * LANES + lane] = llr;                         // llr1
-      } else {
-        const uint32_t pk = a.pi[k];
-        a.scr[(size_t)pk * LANES + lane] = cur.b[i] + (llr - cur.a[i]);      // w update
-        const bool bit = llr > 0.0f;
-        a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                       // decision
-        const uint32_t t = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
-        crc ^= bit ? t : 0u;                                                  // CRC by linearity
+  if constexpr (CK == BETA_W) {
+    float ckc[8], ckn[8];
+    tdec_load_window<DEC2, FIRST>(a, lane, 0, cur);
+    ck_load(ck, 1, lane, ckc);
+    for (uint32_t base = 0; base < K; base += BETA_W) {
+      if (base + BETA_W < K) {
+        tdec_load_window<DEC2, FIRST>(a, lane, base + BETA_W, nxt);
+        ck_load(ck, base / BETA_W + 2, lane, ckn);
       }
+      float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(cur, i, base + i, F, xs[i], xp[i]);
+      float bw[BETA_W][8];
+#pragma unroll
+      for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
+#pragma unroll
+      for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+#pragma unroll
+      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), cur, i, crc);
+      cur = nxt;
+#pragma unroll
+      for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
     }
-    cur = nxt;
+    return;
+  } else {
+  TdecWin c0, c1, n0, n1;   // inputs of the current interval (two halves) and of the next one
+  float ckc[8], ckn[8];
+  tdec_load_window<DEC2, FIRST>(a, lane, 0, c0);
+  tdec_load_window<DEC2, FIRST>(a, lane, BETA_W, c1);
+  ck_load(ck, 1, lane, ckc);
+  n0 = c0;
+  n1 = c1;
+  for (uint32_t base = 0; base < K; base += CK) {
+    const bool more = base + CK < K;
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      // staggered prefetch: next interval's first half during this first half, its second half
+      // (and checkpoint) during this second half -- at most three windows live at once
+      if (more) {
+        if (half == 0) tdec_load_window<DEC2, FIRST>(a, lane, base + CK, n0);
+        else {
+          tdec_load_window<DEC2, FIRST>(a, lane, base + CK + BETA_W, n1);
+          ck_load(ck, base / CK + 2, lane, ckn);
+        }
+      }
+      const TdecWin& w = half ? c1 : c0;
+      const uint32_t hb = base + (uint32_t)half * BETA_W;
+      float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(w, i, hb + i, F, xs[i], xp[i]);
+      float bw[BETA_W][8];
+      if (half == 0) {
+        // beta_{a+8} -> beta_{a+4} (discarded path), then the window beta_{a+1..a+4}
+        float t[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) t[s] = ckc[s];
+#pragma unroll
+        for (int i = BETA_W - 1; i >= 0; i--) {
+          float xs2, xp2, nb[8];
+          tdec_xs_xp<DEC2>(c1, i, base + BETA_W + i, F, xs2, xp2);
+          beta_step(t, xs2, xp2, nb);
+#pragma unroll
+          for (int s = 0; s < 8; s++) t[s] = nb[s];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = t[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
+      }
+#pragma unroll
+      for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+#pragma unroll
+      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2>(a, lane, hb + i, alpha_step(al, bw[i], xs[i], xp[i]), w, i, crc);
+    }
+    c0 = n0;
+    c1 = n1;
 #pragma unroll
     for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
+  }
   }
 }
 
