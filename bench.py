@@ -33,6 +33,15 @@ METRIC = "PDSCH decoded Mbps + turbo codeblocks/s, 20 MHz MCS-28, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 TBS_MCS28_100PRB = 75376
 SF_CYCLE = (1, 2, 3, 4, 6, 7, 8, 9)   # headline runs avoid PSS/SSS/PBCH subframes
+# 36.213 Table 7.1.7.2.1-1 columns (I_TBS 0..26) used by the mixed-bandwidth config
+TBS_6 = (152, 208, 256, 328, 408, 504, 600, 712, 808, 936, 1032, 1192, 1352, 1544, 1736, 1800, 1928, 2152, 2344,
+         2600, 2792, 2984, 3240, 3496, 3624, 3752, 4392)
+TBS_25 = (680, 904, 1096, 1416, 1800, 2216, 2600, 3112, 3496, 4008, 4392, 4968, 5736, 6456, 7224, 7736, 7992, 9144,
+          9912, 10680, 11448, 12576, 13536, 14112, 15264, 15840, 18336)
+TBS_50 = (1384, 1800, 2216, 2856, 3624, 4392, 5160, 6200, 6968, 7992, 8760, 9912, 11448, 12960, 14112, 15264, 16416,
+          18336, 19848, 21384, 22920, 25456, 27376, 28336, 30576, 31704, 36696)
+TBS_100 = (2792, 3624, 4584, 5736, 7224, 8760, 10296, 12216, 14112, 15840, 17568, 19848, 22920, 25456, 28336, 30576,
+           32856, 36696, 39232, 43816, 46888, 51024, 55056, 57336, 61664, 63776, 75376)
 
 
 def tb_payload(seed, nbytes):
@@ -97,45 +106,139 @@ def reduce_over_ranks(elapsed, n_ok, n_cb, world, device="cpu"):
     return float(t[0]), float(s[0]), float(s[1])
 
 
-def make_pool(pool, snr_db, threads, first=0):
+def make_pool(cfgs, snr_db, threads, first=0, h=None):
     """Distinct synthetic subframes from the product's transmitter (mi_tx_subframe), CPU threads.
     Subframe g (global index) carries TB splitmix64(0x5EED0000 + g) and noise seed 0xA5A5 + g."""
     def one(i):
         g = first + i
-        c = make_cfg(g)
+        c = cfgs[i]
         tb = tb_payload(g, c.tbs // 8)
-        return abi.tx_subframe(c, tb, snr_db=snr_db, seed=0xA5A5 + g), tb
+        return abi.tx_subframe(c, tb, h=h, snr_db=snr_db, seed=0xA5A5 + g), tb
     with cf.ThreadPoolExecutor(max_workers=threads) as ex:
-        res = list(ex.map(one, range(pool)))
+        res = list(ex.map(one, range(len(cfgs))))
     return [r[0] for r in res], [r[1] for r in res]
 
 
-def cpu_baseline(seconds, pool_iq, pool_tb):
+def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what):
     """Oracle (CPU restatement, 1 thread) end-to-end on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     import oracle_lib as O
     L = O.lib()
-    cell = O.make_cell(1, 100, 1)
-    s = O.cbsegm(TBS_MCS28_100PRB)
-    ncb = L.or_ncb(s.Kp)
-    sb = np.zeros(s.C * ncb, np.float32)
-    pay = np.zeros(TBS_MCS28_100PRB // 8, np.uint8)
     noi = C.c_uint32()
-    mask = np.ones(110, np.uint8)
-    n = ok = 0
+    n = ok = bits = ncbs = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         i = n % len(pool_iq)
-        rc = L.or_decode_subframe(C.byref(cell), SF_CYCLE[i % len(SF_CYCLE)], 1, mask, TBS_MCS28_100PRB, 6, 0, 0x46, 1,
-                                  2, pool_iq[i], sb, ncb, 1, 4, pay, C.byref(noi))
-        ok += int(rc == 0 and np.array_equal(pay, pool_tb[i]))
+        c = pool_cfgs[i]
+        s = O.cbsegm(c.tbs)
+        ncb = L.or_ncb(s.Kp)
+        sb = np.zeros(s.C * ncb, np.float32)
+        pay = np.zeros(c.tbs // 8, np.uint8)
+        cell = O.make_cell(c.cell_id, c.nof_prb, c.nof_ports)
+        rc = L.or_decode_subframe(C.byref(cell), c.sf_idx, c.cfi, np.array(list(c.prb_mask), np.uint8), c.tbs, c.Qm,
+                                  c.rv, c.rnti, c.tm, 2, pool_iq[i], sb, ncb, 1, 4, pay, C.byref(noi))
+        good = rc == 0 and np.array_equal(pay, pool_tb[i])
+        ok += int(good)
+        bits += c.tbs if good else 0
+        ncbs += s.C
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(ok * TBS_MCS28_100PRB / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "port",
-            "sample": f"{n} subframes (20 MHz TM1 MCS-28, 30 dB) through the oracle's full chain "
-                      f"(oracle/ C restatement, single thread) in {dt:.1f} s; {ok} CRC-OK",
-            "codeblocks_per_s": round(n * s.C / dt, 1)}
+    return {"value": round(bits / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "port",
+            "sample": f"{n} subframes ({what}) through the oracle's full chain (oracle/ C restatement, "
+                      f"single thread) in {dt:.1f} s; {ok} CRC-OK",
+            "codeblocks_per_s": round(ncbs / dt, 1)}
+
+
+def config_cfgs(config, B, first):
+    """Subframe configurations of BASELINE configs[1..4] (2/4: TM1 MCS-28; 3: TM2 64QAM MCS-28;
+    5: mixed 1.4/5/10/20 MHz cells with variable allocation and MCS, seeded)."""
+    if config in (2, 4):
+        return [make_cfg(first + i) for i in range(B)]
+    if config == 3:
+        return [abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=2, sf_idx=SF_CYCLE[(first + i) % 8], cfi=1, tm=2,
+                           rnti=0x46, rv=0, tbs=TBS_MCS28_100PRB, Qm=6) for i in range(B)]
+    rng = np.random.default_rng(0x5EED + first)
+    cols = {6: TBS_6, 25: TBS_25, 50: TBS_50, 100: TBS_100}
+    cfgs = []
+    for i in range(B):
+        nprb = (6, 25, 50, 100)[(first + i) % 4]
+        lprb = int(rng.choice([x for x in (6, 25, 50, 100) if x <= nprb]))
+        start = int(rng.integers(0, nprb - lprb + 1))
+        mcs = int(rng.integers(0, 29))
+        prb = [start <= p < start + lprb for p in range(nprb)]
+        while True:   # an eNB never schedules a code rate above ~0.93: step the MCS down until it fits
+            qm, itbs = (2, mcs) if mcs <= 9 else (4, mcs - 1) if mcs <= 16 else (6, mcs - 2)
+            c = abi.sf_cfg(cell_id=1 + (first + i) % 4, nof_prb=nprb, nof_ports=1, sf_idx=SF_CYCLE[(first + i) % 8],
+                           cfi=1 if nprb > 10 else 2, tm=1, rnti=0x46, rv=0, tbs=cols[lprb][itbs], Qm=qm, prb=prb)
+            ncb = -(-(c.tbs + 24) // 6120)
+            if (c.tbs + 24 * (ncb + 1)) <= 0.93 * abi.pdsch_G(c) or mcs == 0:
+                break
+            mcs -= 1
+        cfgs.append(c)
+    return cfgs
+
+
+def bench_codeblocks(args, world, rank, dev):
+    """configs[0]: turbodecoder_test -- K = 6144, 8 fixed iterations, BPSK/AWGN LLRs."""
+    K, n = 6144, args.cb_per_gpu
+    rng = np.random.default_rng(1 + rank)
+    pool = min(args.pool, n)
+    bits = rng.integers(0, 2, (pool, K)).astype(np.uint8)
+    sigma2 = 1.0 / (2 * (K / (3.0 * K + 12)) * 10 ** (args.ebno / 10))
+    llr = np.stack([(-2.0 * ((1.0 - 2.0 * abi.turbo_encode(b, K)) + rng.normal(0, np.sqrt(sigma2), 3 * K + 12))
+                     / sigma2).astype(np.float32) for b in bits])
+    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True)
+    d = torch.from_numpy(llr).to(dev)[torch.arange(n, device=dev) % pool].contiguous()
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(args.warmup):
+        tb.run(d.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    tb.profile_reset()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tb.run(d.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stage, nprof = tb.stage_ms()
+    dec, its, _ = tb.results()
+    ber = float(np.mean(dec[:pool] != bits))
+    elapsed, _, n_all = reduce_over_ranks(elapsed, 0, n, world, dev)
+    if rank:
+        return None
+    cbps = n_all * args.steps / elapsed
+    ab = tb.algo_bytes()
+    ach = ab / (stage["tdec"] * 1e-3) / 1e9
+    out = {"metric": METRIC, "value": round(cbps * K / 1e6, 2), "unit": "Mbps", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
+                                  f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
+                      "codeblocks_per_gpu": n},
+           "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
+           "roofline": {"kernel": "tdec_kernel (max-log-MAP turbo)", "bound": "hbm", "achieved": round(ach, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                        "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(stage["tdec"], 4),
+                        "launches_averaged": nprof}}
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        td = O.Tdec()
+        m = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            td.decode_cb(llr[m % pool], K, max_its=8, early_stop=False)
+            m += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(m * K / dt / 1e6, 4), "unit": "Mbps", "cores": 1, "kind": "port",
+                               "sample": f"{m} code blocks K=6144 x 8 iterations through the oracle's max-log-MAP "
+                                         f"(single thread) in {dt:.1f} s", "codeblocks_per_s": round(m / dt, 2)}
+    tb.close()
+    return out
 
 
 def main():
@@ -149,7 +252,15 @@ def main():
     ap.add_argument("--max-its", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
+                    help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
+    ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
+    ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
     args = ap.parse_args()
+    if args.config == 2:
+        args.sf_per_gpu = 1
+    elif args.config == 3 and args.sf_per_gpu == 12500:
+        args.sf_per_gpu = 1000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -161,19 +272,39 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    if args.config == 1:
+        out = bench_codeblocks(args, world, rank, dev)
+        if out:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     B = args.sf_per_gpu
     first, _ = shard_range(B * world, rank, world)          # this rank's global subframe indices
-    pool_iq, pool_tb = make_pool(min(args.pool, B), args.snr, threads, first)
-    cfgs = [make_cfg(first + i) for i in range(B)]
+    P = min(args.pool, B)
+    P -= P % 8 if P >= 8 else 0                             # keep the sf_idx cycle aligned
+    cfgs = config_cfgs(args.config, B, first)
+    # the pool: subframes 0..P-1 of this shard; subframe i of the batch reuses pool entry i % P
+    if args.config == 5:
+        P = B                                               # every mixed subframe is distinct
+    h = [0.8 + 0.3j, -0.4 + 0.5j] if args.config == 3 else None
+    pool_iq, pool_tb = make_pool(cfgs[:P], args.snr, threads, first, h)
     batch = abi.Batch(cfgs, max_its=args.max_its, profile=True)
     # stage the pool in HBM once, replicate on device into the batch IQ layout
-    sfl = len(pool_iq[0])   # floats per subframe
-    d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
-    idx = torch.arange(B, device=dev) % len(pool_iq)
-    d_iq.view(B, sfl).copy_(d_pool[idx])       # all 20 MHz: offsets are i * sfl
-    del d_pool
+    if args.config == 5:
+        flat = np.zeros(2 * batch.iq_samples, np.float32)
+        for i, iq in enumerate(pool_iq):
+            o = 2 * batch.iq_offset(i)
+            flat[o:o + len(iq)] = iq
+        d_iq.copy_(torch.from_numpy(flat))
+    else:
+        sfl = len(pool_iq[0])   # floats per subframe (one bandwidth)
+        d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
+        idx = torch.arange(B, device=dev) % len(pool_iq)
+        d_iq.view(B, sfl).copy_(d_pool[idx])
+        del d_pool
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -199,12 +330,17 @@ def main():
     pay = batch.download(abi.BUF_PAYLOAD, np.uint8)
     n_ok = int(crc.sum())
     bad = sum(int(not np.array_equal(batch.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(0, B, max(1, B // 64)))
+    bits_ok = float(sum(c.tbs for c, o in zip(cfgs, crc) if o))
     ncb = batch.n_codeblocks
-    elapsed, n_ok_all, ncb_all = reduce_over_ranks(elapsed, n_ok, ncb, world, dev)
+    elapsed, bits_all, ncb_all = reduce_over_ranks(elapsed, bits_ok, ncb, world, dev)
 
+    what = {2: "configs[1] 20 MHz TM1 SISO PDSCH MCS-28 (TBS 75376, 13 x K=5824), single subframe",
+            3: "configs[2] 20 MHz TM2 (2-port SFBC) 64QAM MCS-28 (TBS 75376)",
+            4: "configs[3] shard: 20 MHz TM1 SISO PDSCH MCS-28 (TBS 75376, 13 x K=5824) subframes of configs[1]",
+            5: "configs[4] mixed 1.4/5/10/20 MHz cells, random allocation 6-100 PRB and MCS 0-28"}[args.config]
     if rank == 0:
         K = args.steps
-        mbps = n_ok_all * K * TBS_MCS28_100PRB / elapsed / 1e6
+        mbps = bits_all * K / elapsed / 1e6
         cbps = ncb_all * K / elapsed
         tdec_ms = stage["tdec"]
         tdec_bytes = batch.algo_bytes(4)
@@ -214,9 +350,8 @@ def main():
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"20 MHz TM1 SISO PDSCH MCS-28 (TBS 75376, 13 x K=5824), {B} subframes per GPU "
-                                   f"per step (configs[3] shard of configs[1] subframes), CFI 1, {args.snr:g} dB AWGN",
-                       "subframes_per_gpu": B, "tbs": TBS_MCS28_100PRB, "mcs": 28, "nof_prb": 100, "tm": 1,
+            "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
+                       "baseline_config": args.config, "subframes_per_gpu": B,
                        "max_its": args.max_its, "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
@@ -229,7 +364,7 @@ def main():
                          "avg_launch_ms": round(tdec_ms, 4), "launches_averaged": nprof},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, pool_iq, pool_tb)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what)
         print(json.dumps(out), flush=True)
     batch.close()
     if world > 1:

@@ -83,6 +83,23 @@ double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = co
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 
+/* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =
+ * srsLTE turbodecoder_test).  n_cb code blocks of size K; decoder input per block = 3(K+4) fp32
+ * LLRs in triplet order d0_k d1_k d2_k with the 36.212 tail layout, LLR > 0 => bit 1 (device
+ * memory, [n_cb][3(K+4)]).  max_its iterations; early_stop on the block CRC (24A if crc24a, else
+ * 24B) or a fixed iteration count.  Decisions: K/8 bytes per block, MSB first. */
+typedef struct mi_tdec_batch mi_tdec_batch_t;
+mi_tdec_batch_t *mi_tdec_create(uint32_t K, uint32_t n_cb, uint32_t max_its, int early_stop, int crc24a,
+                                uint32_t flags);
+void   mi_tdec_destroy(mi_tdec_batch_t *b);
+int    mi_tdec_run(mi_tdec_batch_t *b, const float *d_in, void *stream);
+int    mi_tdec_download(mi_tdec_batch_t *b, uint8_t *bits /* n_cb*K/8 */, uint32_t *its, uint32_t *crc_ok);
+int    mi_tdec_stage_ms(mi_tdec_batch_t *b, float *ms /* MI_DL_NSTAGES */, uint32_t *nruns);
+void   mi_tdec_profile_reset(mi_tdec_batch_t *b);
+double mi_tdec_algo_bytes(const mi_tdec_batch_t *b);
+/* 36.212 5.1.3 turbo encoder (host): bits[K] -> d[3(K+4)] triplet order, 2 = <NULL> filler */
+int    mi_turbo_encode(const uint8_t *bits, uint32_t K, uint32_t F, uint8_t *d);
+
 /* ---- synthetic transmitter (eNB side, host) used to build benchmark input ------------------
  * Mirrors srsLTE's PDSCH encode chain: CRC24A, segmentation, turbo code, rate matching,
  * scrambling, QAM, SFBC, RE mapping + CRS + PCFICH, IFFT (1/sqrt N) + CP, flat per-port
@@ -90,6 +107,8 @@ uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 int    mi_tx_subframe(const mi_dl_sf_cfg_t *cfg, const uint8_t *tb, const float *h_re_im /* 2*ports */,
                       float snr_db, uint64_t noise_seed, float *iq);
 int    mi_sf_len(uint32_t nof_prb);
+/* number of PDSCH bits G of a configuration (RE count x Qm, 36.211 6.3.5 / 6.4) */
+int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
 
 /* ---- device / runtime helpers ------------------------------------------------------------ */
 int    mi_device_count(void);

@@ -75,7 +75,16 @@ def lib():
             "mi_dl_batch_n_codeblocks": (u32, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
+            "mi_turbo_encode": (C.c_int, [vp, u32, u32, vp]),
+            "mi_tdec_create": (vp, [u32, u32, u32, C.c_int, C.c_int, u32]),
+            "mi_tdec_destroy": (None, [vp]),
+            "mi_tdec_run": (C.c_int, [vp, vp, vp]),
+            "mi_tdec_download": (C.c_int, [vp, vp, vp, vp]),
+            "mi_tdec_stage_ms": (C.c_int, [vp, vp, vp]),
+            "mi_tdec_profile_reset": (None, [vp]),
+            "mi_tdec_algo_bytes": (C.c_double, [vp]),
             "mi_sf_len": (C.c_int, [u32]),
+            "mi_pdsch_G": (C.c_int, [vp]),
             "mi_device_count": (C.c_int, []),
             "mi_set_device": (C.c_int, [C.c_int]),
             "mi_last_error": (C.c_char_p, []),
@@ -202,3 +211,62 @@ class Batch:
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)
         off = lib().mi_dl_batch_payload_offset(self.h, sf)
         return p[off:off + self.cfgs[sf].tbs // 8]
+
+
+def turbo_encode(bits, K, F=0):
+    """36.212 turbo encoder of the product (host): 3(K+4) values in triplet order, 2 = <NULL>."""
+    d = np.zeros(3 * (K + 4), np.uint8)
+    b = np.ascontiguousarray(bits, np.uint8)
+    if lib().mi_turbo_encode(b.ctypes.data, K, F, d.ctypes.data):
+        raise RuntimeError("mi_turbo_encode failed")
+    return d
+
+
+class TdecBatch:
+    """Raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* / turbodecoder_test contract)."""
+
+    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False):
+        self.K, self.n_cb = K, n_cb
+        self.h = lib().mi_tdec_create(K, n_cb, max_its, int(early_stop), int(crc24a), FLAG_PROFILE if profile else 0)
+        if not self.h:
+            raise RuntimeError("mi_tdec_create: " + last_error())
+
+    def run(self, d_in_ptr, stream_ptr=None):
+        if lib().mi_tdec_run(self.h, C.c_void_p(d_in_ptr), C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_tdec_run: " + last_error())
+
+    def results(self):
+        bits = np.zeros(self.n_cb * self.K // 8, np.uint8)
+        its = np.zeros(self.n_cb, np.uint32)
+        ok = np.zeros(self.n_cb, np.uint32)
+        if lib().mi_tdec_download(self.h, bits.ctypes.data, its.ctypes.data, ok.ctypes.data):
+            raise RuntimeError("mi_tdec_download: " + last_error())
+        return np.unpackbits(bits).reshape(self.n_cb, self.K), its, ok
+
+    def stage_ms(self):
+        ms = np.zeros(len(STAGES), np.float32)
+        n = C.c_uint32(0)
+        if lib().mi_tdec_stage_ms(self.h, ms.ctypes.data, C.byref(n)):
+            raise RuntimeError("stage_ms: " + last_error())
+        return dict(zip(STAGES, ms.tolist())), n.value
+
+    def profile_reset(self):
+        lib().mi_tdec_profile_reset(self.h)
+
+    def algo_bytes(self):
+        return lib().mi_tdec_algo_bytes(self.h)
+
+    def close(self):
+        if self.h:
+            lib().mi_tdec_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pdsch_G(cfg):
+    return lib().mi_pdsch_G(C.byref(cfg))

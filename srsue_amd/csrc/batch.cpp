@@ -119,6 +119,49 @@ double mi_dl_batch_algo_bytes(const mi_dl_batch_t* b, int which_stage) {
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t* b) { return b->eng.plan.n_cb; }
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
 
+/* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */
+struct mi_tdec_batch {
+  mi::Engine eng;
+};
+
+mi_tdec_batch_t* mi_tdec_create(uint32_t K, uint32_t n_cb, uint32_t max_its, int early_stop, int crc24a,
+                                uint32_t flags) {
+  auto* b = new mi_tdec_batch();
+  b->eng.max_its = max_its ? max_its : 8;
+  b->eng.early_stop = early_stop ? 1 : 0;
+  b->eng.flags = flags;
+  if (b->eng.plan.build_codeblocks(K, n_cb, crc24a != 0) || b->eng.upload(nullptr, true) ||
+      !mi::hip_ok(hipStreamSynchronize(nullptr), "upload sync")) {
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+void mi_tdec_destroy(mi_tdec_batch_t* b) { delete b; }
+int mi_tdec_run(mi_tdec_batch_t* b, const float* d_in, void* stream) {
+  if (!b || !d_in) { mi::set_error("null argument"); return -1; }
+  return b->eng.run_codeblocks(d_in, reinterpret_cast<hipStream_t>(stream));
+}
+int mi_tdec_download(mi_tdec_batch_t* b, uint8_t* bits, uint32_t* its, uint32_t* crc_ok) {
+  const mi::Plan& P = b->eng.plan;
+  if (!mi::hip_ok(hipStreamSynchronize(b->eng.last_stream), "sync")) return -1;
+  std::vector<uint32_t> li(P.lanes.size()), lc(P.lanes.size());
+  std::vector<uint8_t> rows((size_t)P.lanes.size() * mi::CB_BYTES_STRIDE);
+  bool ok = mi::hip_ok(hipMemcpy(rows.data(), b->eng.d_cbbytes.p, rows.size(), hipMemcpyDeviceToHost), "D2H") &&
+            mi::hip_ok(hipMemcpy(li.data(), b->eng.d_cbits.p, li.size() * 4, hipMemcpyDeviceToHost), "D2H") &&
+            mi::hip_ok(hipMemcpy(lc.data(), b->eng.d_cbcrc.p, lc.size() * 4, hipMemcpyDeviceToHost), "D2H");
+  if (!ok) return -1;
+  for (uint32_t c = 0; c < P.cb_n; c++) {   // lanes are in code-block order
+    if (bits) memcpy(bits + (size_t)c * (P.cb_K / 8), &rows[(size_t)c * mi::CB_BYTES_STRIDE], P.cb_K / 8);
+    if (its) its[c] = li[c];
+    if (crc_ok) crc_ok[c] = lc[c];
+  }
+  return 0;
+}
+int mi_tdec_stage_ms(mi_tdec_batch_t* b, float* ms, uint32_t* nruns) { return b->eng.stage_ms(ms, nruns); }
+void mi_tdec_profile_reset(mi_tdec_batch_t* b) { b->eng.profile_reset(); }
+double mi_tdec_algo_bytes(const mi_tdec_batch_t* b) { return b->eng.plan.stage_bytes[MI_DL_STAGE_TDEC]; }
+
 int mi_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -74,7 +74,7 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   }
   const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
   ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
-  if (P.has_pdsch) {
+  if (P.has_pdsch || P.cb_n) {
     ok = ok && d_e.ensure(P.e_floats * 4) && d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
          d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
          d_cbcrc.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
@@ -143,6 +143,35 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   } else {
     for (int i = 3; i <= 6; i++) mark(i);
   }
+  return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
+}
+
+int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
+  const Plan& P = plan;
+  last_stream = st;
+  const bool prof = flags & MI_DL_FLAG_PROFILE;
+  hipEvent_t* ev = nullptr;
+  if (prof) {
+    if (ev_used == ev_sets.size()) {
+      std::vector<hipEvent_t> set(MI_DL_NSTAGES + 1);
+      for (auto& e : set)
+        if (!hip_ok(hipEventCreate(&e), "event")) return -1;
+      ev_sets.push_back(set);
+    }
+    ev = ev_sets[ev_used++].data();
+  }
+  auto mark = [&](int i) {
+    if (prof) (void)hipEventRecord(ev[i], st);
+  };
+  for (int i = 0; i <= MI_DL_STAGE_RM; i++) mark(i);
+  launch_cb_scatter(d_in, d_sb.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
+                    (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
+  mark(MI_DL_STAGE_TDEC);
+  launch_tdec(d_sb.as<float>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
+              d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+              d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop, st);
+  mark(MI_DL_STAGE_TB);
+  mark(MI_DL_NSTAGES);
   return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
 }
 

@@ -44,6 +44,8 @@ struct Engine {
   int upload(hipStream_t st, bool alloc_sb);
   // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.
   int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override);
+  // raw code-block decoding: scatter d into the softbuffer layout, then the turbo kernel
+  int run_codeblocks(const float* d_in, hipStream_t st);
   int stage_ms(float* ms, uint32_t* nruns);   // average over the runs since profile_reset()
   void profile_reset() { ev_used = 0; }
 };

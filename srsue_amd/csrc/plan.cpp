@@ -17,6 +17,7 @@ static size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 
 int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   has_pdsch = with_pdsch;
+  cb_K = cb_n = 0;
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
@@ -254,6 +255,62 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     tbs[s].cb_list = (uint32_t)cb_list.size();
     cb_list.insert(cb_list.end(), v.begin(), v.end());
   }
+  return 0;
+}
+
+int Plan::build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a) {
+  if (!cb_size_valid(K) || n_cb == 0) { set_error("invalid code block size"); return -1; }
+  cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
+  fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
+  iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
+  max_units = max_ncb = n_cb = 0;
+  bytes_compulsory = 0;
+  for (double& b : stage_bytes) b = 0;
+
+  has_pdsch = false;
+  cb_K = K;
+  cb_n = n_cb;
+  auto& kp = kpos_cache[K];
+  if (kp.empty()) {
+    kp.resize(4);
+    cb_pos_table(K, kp[0]);
+    qpp_table(K, kp[1]);
+    crc_bit_table(K, 0x864CFBu, kp[2]);
+    crc_bit_table(K, 0x800063u, kp[3]);
+  }
+  MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
+  uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
+  for (int q = 0; q < 4; q++) {
+    *offs[q] = (uint32_t)kdata.size();
+    kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
+  }
+  ktabs.push_back(t);
+  const uint32_t Ncb = ncb_of(K);
+  max_ncb = Ncb;
+  for (uint32_t g0 = 0; g0 < n_cb; g0 += LANES) {
+    MiGroupDesc g{};
+    g.K = K; g.Ncb = Ncb; g.ktab = 0;
+    g.lane0 = (uint32_t)lanes.size();
+    g.sb_off = sb_floats;
+    g.scratch_off = scratch_floats;
+    g.dec_off = dec_bytes;
+    sb_floats += (size_t)Ncb * LANES;
+    scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK + 1));
+    dec_bytes += (size_t)K * LANES;
+    groups.push_back(g);
+    for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+      MiLaneDesc ld{};
+      if (g0 + q < n_cb) {
+        ld.valid = 1; ld.crc24a = crc24a ? 1 : 0; ld.tb = g0 + q; ld.F = 0;
+      }
+      lanes.push_back(ld);
+    }
+  }
+  this->n_cb = n_cb;
+  stage_bytes[MI_DL_STAGE_RM] = (double)n_cb * (3 * K + 12) * 4 * 2;        // scatter: read + write
+  stage_bytes[MI_DL_STAGE_TDEC] = (double)n_cb * ((3 * K + 12) * 4 + K / 8);  // SURVEY 8d per CB
+  bytes_compulsory = stage_bytes[MI_DL_STAGE_TDEC];
   return 0;
 }
 

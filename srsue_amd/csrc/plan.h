@@ -47,6 +47,9 @@ struct Plan {
 
   // has_pdsch = false plans only OFDM + channel estimation (per-TTI front half)
   int build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool has_pdsch);
+  // raw code-block mode (srslte_tdec_* contract): n_cb blocks of size K, no PHY front end
+  int build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a);
+  uint32_t cb_K = 0, cb_n = 0;
 };
 
 }  // namespace mi

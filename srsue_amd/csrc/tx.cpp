@@ -32,7 +32,7 @@ static inline int rsc(int& s, int u) {
 }
 
 // d: 3(K+4) entries, 0/1 or 2 = <NULL>
-static void turbo_encode(const uint8_t* c, uint32_t K, uint32_t F, uint8_t* d) {
+void turbo_encode(const uint8_t* c, uint32_t K, uint32_t F, uint8_t* d) {
   std::vector<uint32_t> pi;
   qpp_table(K, pi);
   int s1 = 0, s2 = 0;
@@ -253,6 +253,16 @@ int tx_subframe(const mi_dl_sf_cfg_t* c, const uint8_t* tb, const float* h, floa
 extern "C" int mi_tx_subframe(const mi_dl_sf_cfg_t* cfg, const uint8_t* tb, const float* h_re_im, float snr_db,
                               uint64_t noise_seed, float* iq) {
   return mi::tx_subframe(cfg, tb, h_re_im, snr_db, noise_seed, iq);
+}
+extern "C" int mi_turbo_encode(const uint8_t* bits, uint32_t K, uint32_t F, uint8_t* d) {
+  if (!mi::cb_size_valid(K) || F >= K) return -1;
+  mi::turbo_encode(bits, K, F, d);
+  return 0;
+}
+extern "C" int mi_pdsch_G(const mi_dl_sf_cfg_t* c) {
+  if (!c || mi::symbol_sz(c->nof_prb) < 0) return -1;
+  std::vector<uint32_t> re;
+  return (int)(mi::pdsch_re_list(c->cell_id, c->nof_prb, c->nof_ports, c->cfi, c->sf_idx, c->prb_mask, re) * c->Qm);
 }
 extern "C" int mi_sf_len(uint32_t nof_prb) {
   const int N = mi::symbol_sz(nof_prb);
