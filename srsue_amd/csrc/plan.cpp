@@ -258,8 +258,8 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   return 0;
 }
 
-int Plan::build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a) {
-  if (!cb_size_valid(K) || n_cb == 0) { set_error("invalid code block size"); return -1; }
+int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
+  if (!cb_size_valid(K) || ncb_req == 0) { set_error("invalid code block size"); return -1; }
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
@@ -270,7 +270,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a) {
 
   has_pdsch = false;
   cb_K = K;
-  cb_n = n_cb;
+  cb_n = ncb_req;
   auto& kp = kpos_cache[K];
   if (kp.empty()) {
     kp.resize(4);
@@ -288,7 +288,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a) {
   ktabs.push_back(t);
   const uint32_t Ncb = ncb_of(K);
   max_ncb = Ncb;
-  for (uint32_t g0 = 0; g0 < n_cb; g0 += LANES) {
+  for (uint32_t g0 = 0; g0 < ncb_req; g0 += LANES) {
     MiGroupDesc g{};
     g.K = K; g.Ncb = Ncb; g.ktab = 0;
     g.lane0 = (uint32_t)lanes.size();
@@ -301,15 +301,15 @@ int Plan::build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a) {
     groups.push_back(g);
     for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
       MiLaneDesc ld{};
-      if (g0 + q < n_cb) {
+      if (g0 + q < ncb_req) {
         ld.valid = 1; ld.crc24a = crc24a ? 1 : 0; ld.tb = g0 + q; ld.F = 0;
       }
       lanes.push_back(ld);
     }
   }
-  this->n_cb = n_cb;
-  stage_bytes[MI_DL_STAGE_RM] = (double)n_cb * (3 * K + 12) * 4 * 2;        // scatter: read + write
-  stage_bytes[MI_DL_STAGE_TDEC] = (double)n_cb * ((3 * K + 12) * 4 + K / 8);  // SURVEY 8d per CB
+  n_cb = ncb_req;
+  stage_bytes[MI_DL_STAGE_RM] = (double)ncb_req * (3 * K + 12) * 4 * 2;        // scatter: read + write
+  stage_bytes[MI_DL_STAGE_TDEC] = (double)ncb_req * ((3 * K + 12) * 4 + K / 8);  // SURVEY 8d per CB
   bytes_compulsory = stage_bytes[MI_DL_STAGE_TDEC];
   return 0;
 }
