@@ -72,13 +72,13 @@ def kernel_src_hash():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(sf_per_gpu):
+def pmc_traffic(sf_per_gpu, tdec):
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         t = json.load(open(p))
     except (OSError, ValueError):
         return None, None
-    if t.get("src_hash") != kernel_src_hash() or t.get("sf_per_gpu") != sf_per_gpu:
+    if t.get("src_hash") != kernel_src_hash() or t.get("sf_per_gpu") != sf_per_gpu or t.get("tdec", "gen") != tdec:
         return None, None
     return t["tdec_traffic_bytes_per_launch"], "profiles/traffic.json: " + t["source"]
 
@@ -119,35 +119,66 @@ def make_pool(cfgs, snr_db, threads, first=0, h=None):
     return [r[0] for r in res], [r[1] for r in res]
 
 
-def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what):
-    """Oracle (CPU restatement, 1 thread) end-to-end on a bounded sample of the same workload."""
+def host_threads():
+    """CPU threads the baseline may use: this process's affinity, capped at the one-GPU box share (16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def run_for(seconds, nthreads, work):
+    """Calls work(thread_id, i) in nthreads threads until the deadline (ctypes releases the GIL, so the
+    oracle's C code runs in parallel); returns (sum of work() results, elapsed s)."""
+    deadline = time.perf_counter() + seconds
+
+    def loop(t):
+        acc, i = [0, 0, 0], 0
+        while time.perf_counter() < deadline:
+            r = work(t, i)
+            acc = [a + b for a, b in zip(acc, r)]
+            i += nthreads
+        return acc
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=nthreads) as ex:
+        res = list(ex.map(loop, range(nthreads)))
+    return [sum(r[j] for r in res) for j in range(3)], time.perf_counter() - t0
+
+
+def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what, i16):
+    """The oracle chain (this repo's C restatement) on a bounded sample of the same workload, on one
+    thread and on all host threads; the turbo decoder is the SSE4.1 int16 one (oracle/o_simd.c, the
+    srsLTE SSE design) in int16 mode, the float srsLTE-gen restatement otherwise."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     import oracle_lib as O
     L = O.lib()
-    noi = C.c_uint32()
-    n = ok = bits = ncbs = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        i = n % len(pool_iq)
+    L.or_set_tdec_mode(O.TDEC_SIMD if i16 else O.TDEC_GEN)
+
+    def one(t, i):
+        i %= len(pool_iq)
         c = pool_cfgs[i]
         s = O.cbsegm(c.tbs)
         ncb = L.or_ncb(s.Kp)
         sb = np.zeros(s.C * ncb, np.float32)
         pay = np.zeros(c.tbs // 8, np.uint8)
+        noi = C.c_uint32()
         cell = O.make_cell(c.cell_id, c.nof_prb, c.nof_ports)
         rc = L.or_decode_subframe(C.byref(cell), c.sf_idx, c.cfi, np.array(list(c.prb_mask), np.uint8), c.tbs, c.Qm,
                                   c.rv, c.rnti, c.tm, 2, pool_iq[i], sb, ncb, 1, 4, pay, C.byref(noi))
         good = rc == 0 and np.array_equal(pay, pool_tb[i])
-        ok += int(good)
-        bits += c.tbs if good else 0
-        ncbs += s.C
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(bits / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "port",
-            "sample": f"{n} subframes ({what}) through the oracle's full chain (oracle/ C restatement, "
-                      f"single thread) in {dt:.1f} s; {ok} CRC-OK",
-            "codeblocks_per_s": round(ncbs / dt, 1)}
+        return (c.tbs if good else 0, s.C, 1)
+    T = host_threads()
+    (b1, c1, n1), dt1 = run_for(seconds / 3, 1, one)
+    (bT, cT, nT), dtT = run_for(2 * seconds / 3, T, one)
+    L.or_set_tdec_mode(O.TDEC_GEN)
+    dec = "SSE4.1 int16 turbo (oracle/o_simd.c)" if i16 else "float srsLTE-gen turbo restatement"
+    return {"value": round(bT / dtT / 1e6, 3), "unit": "Mbps", "cores": T, "kind": "port",
+            "value_1core": round(b1 / dt1 / 1e6, 3),
+            "sample": f"{nT} subframes ({what}) through the oracle's full chain with the {dec}, {T} threads in "
+                      f"{dtT:.1f} s; 1 thread: {n1} subframes in {dt1:.1f} s",
+            "codeblocks_per_s": round(cT / dtT, 1)}
 
 
 def config_cfgs(config, B, first):
@@ -179,6 +210,11 @@ def config_cfgs(config, B, first):
     return cfgs
 
 
+def dtype_of(args):
+    """f32 everywhere (front end, softbuffer); in i16 mode the turbo metrics are int16-exact integers."""
+    return "f32+i16" if args.tdec == "i16" else "f32"
+
+
 def bench_codeblocks(args, world, rank, dev):
     """configs[0]: turbodecoder_test -- K = 6144, 8 fixed iterations, BPSK/AWGN LLRs."""
     K, n = 6144, args.cb_per_gpu
@@ -188,7 +224,7 @@ def bench_codeblocks(args, world, rank, dev):
     sigma2 = 1.0 / (2 * (K / (3.0 * K + 12)) * 10 ** (args.ebno / 10))
     llr = np.stack([(-2.0 * ((1.0 - 2.0 * abi.turbo_encode(b, K)) + rng.normal(0, np.sqrt(sigma2), 3 * K + 12))
                      / sigma2).astype(np.float32) for b in bits])
-    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True)
+    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True, tdec_i16=args.tdec == "i16")
     d = torch.from_numpy(llr).to(dev)[torch.arange(n, device=dev) % pool].contiguous()
     sptr = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(args.warmup):
@@ -215,10 +251,10 @@ def bench_codeblocks(args, world, rank, dev):
     ach = ab / (stage["tdec"] * 1e-3) / 1e9
     out = {"metric": METRIC, "value": round(cbps * K / 1e6, 2), "unit": "Mbps", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
            "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
                                   f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
-                      "codeblocks_per_gpu": n},
+                      "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec},
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
            "roofline": {"kernel": "tdec_kernel (max-log-MAP turbo)", "bound": "hbm", "achieved": round(ach, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
@@ -227,16 +263,31 @@ def bench_codeblocks(args, world, rank, dev):
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
-        td = O.Tdec()
-        m = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds:
-            td.decode_cb(llr[m % pool], K, max_its=8, early_stop=False)
-            m += 1
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(m * K / dt / 1e6, 4), "unit": "Mbps", "cores": 1, "kind": "port",
-                               "sample": f"{m} code blocks K=6144 x 8 iterations through the oracle's max-log-MAP "
-                                         f"(single thread) in {dt:.1f} s", "codeblocks_per_s": round(m / dt, 2)}
+        L, T, i16 = O.lib(), host_threads(), args.tdec == "i16"
+        if i16:
+            # SSE4.1 int16 decoder, one code block per thread, all threads on the same batch call
+            def work(t, i):
+                m = 4
+                out_b = np.zeros((m, K), np.uint8)
+                its_ = np.zeros(m, np.uint32)
+                ok_ = np.zeros(m, np.uint8)
+                j = (i * m) % (pool - m + 1)
+                L.or_simd_decode_batch(llr[j:j + m], llr.shape[1], m, K, 8, 0, 0, out_b, its_, ok_, 1)
+                return (m, 0, 0)
+        else:
+            tds = [O.Tdec() for _ in range(T)]
+
+            def work(t, i):
+                tds[t].decode_cb(llr[i % pool], K, max_its=8, early_stop=False)
+                return (1, 0, 0)
+        (m1, _, _), dt1 = run_for(args.cpu_seconds / 3, 1, work)
+        (mT, _, _), dtT = run_for(2 * args.cpu_seconds / 3, T, work)
+        dec = "SSE4.1 int16 max-log-MAP (oracle/o_simd.c)" if i16 else "float max-log-MAP restatement (oracle/o_fec.c)"
+        out["cpu_baseline"] = {"value": round(mT * K / dtT / 1e6, 4), "unit": "Mbps", "cores": T, "kind": "port",
+                               "value_1core": round(m1 * K / dt1 / 1e6, 4),
+                               "sample": f"{mT} code blocks K=6144 x 8 iterations through the {dec}, {T} threads "
+                                         f"in {dtT:.1f} s; 1 thread: {m1} in {dt1:.1f} s",
+                               "codeblocks_per_s": round(mT / dtT, 2)}
     tb.close()
     return out
 
@@ -256,6 +307,8 @@ def main():
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
     ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
     ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
+    ap.add_argument("--tdec", choices=("gen", "i16"), default="gen",
+                    help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
     args = ap.parse_args()
     if args.config == 2:
         args.sf_per_gpu = 1
@@ -290,7 +343,7 @@ def main():
         P = B                                               # every mixed subframe is distinct
     h = [0.8 + 0.3j, -0.4 + 0.5j] if args.config == 3 else None
     pool_iq, pool_tb = make_pool(cfgs[:P], args.snr, threads, first, h)
-    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True)
+    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16")
     # stage the pool in HBM once, replicate on device into the batch IQ layout
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
     if args.config == 5:
@@ -345,13 +398,13 @@ def main():
         tdec_ms = stage["tdec"]
         tdec_bytes = batch.algo_bytes(4)
         achieved = tdec_bytes / (tdec_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(B)
+        traffic, traffic_src = pmc_traffic(B, args.tdec)
         out = {
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
-                       "baseline_config": args.config, "subframes_per_gpu": B,
+                       "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
@@ -364,7 +417,8 @@ def main():
                          "avg_launch_ms": round(tdec_ms, 4), "launches_averaged": nprof},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
+                                               args.tdec == "i16")
         print(json.dumps(out), flush=True)
     batch.close()
     if world > 1:

@@ -29,7 +29,7 @@
 static const uint8_t P_COL[32] = {0,16,8,24,4,20,12,28,2,18,10,26,6,22,14,30,
                                   1,17,9,25,5,21,13,29,3,19,11,27,7,23,15,31};
 
-static void trellis(int s, int u, int *next, int *z) {
+void or_trellis(int s, int u, int *next, int *z) {
   int s1 = (s >> 2) & 1, s2 = (s >> 1) & 1, s3 = s & 1;
   int a = u ^ s2 ^ s3;
   *z = a ^ s1 ^ s3;
@@ -43,7 +43,7 @@ int or_tcod(const uint8_t *in, uint32_t K, uint32_t F, uint8_t *d) {
   uint8_t tail[12];
   for (uint32_t k = 0; k < K; k++) {
     int u = (k < F) ? 0 : (in[k] & 1);
-    trellis(s, u, &n, &z);
+    or_trellis(s, u, &n, &z);
     d[3 * k] = (uint8_t)u; d[3 * k + 1] = (uint8_t)z; s = n;
   }
   for (int j = 0; j < 3; j++) {
@@ -55,7 +55,7 @@ int or_tcod(const uint8_t *in, uint32_t K, uint32_t F, uint8_t *d) {
   for (uint32_t k = 0; k < K; k++) {
     uint32_t src = pi[k];
     int u = (src < F) ? 0 : (in[src] & 1);
-    trellis(s, u, &n, &z);
+    or_trellis(s, u, &n, &z);
     d[3 * k + 2] = (uint8_t)z; s = n;
   }
   for (int j = 0; j < 3; j++) {
@@ -121,13 +121,13 @@ int or_rm_rx(const float *e, uint32_t E, uint32_t K, uint32_t F, uint32_t rv, in
 /* ------------------------------- max-log-MAP ------------------------------------------- */
 static int NEXT[8][2], PAR[8][2], PREV_S[8][2], PREV_U[8][2];
 static int tables_ready = 0;
-static void init_tables(void) {
+static void __attribute__((constructor)) init_tables(void) {
   if (tables_ready) return;
   int cnt[8] = {0};
   for (int s = 0; s < 8; s++)
     for (int u = 0; u < 2; u++) {
       int n, z;
-      trellis(s, u, &n, &z);
+      or_trellis(s, u, &n, &z);
       NEXT[s][u] = n; PAR[s][u] = z;
       PREV_S[n][cnt[n]] = s; PREV_U[n][cnt[n]] = u; cnt[n]++;
     }
@@ -209,3 +209,115 @@ int or_decode_cb(or_tdec_t *h, const float *in, uint32_t K, uint32_t max_its, in
   *crc_ok = ok;
   return (int)its;
 }
+
+/* ------------------------- int16 ("SSE") max-log-MAP ----------------------------------------
+ * Restates the design of srsLTE's SSE turbo decoder (srslte_tdec_sse, built when CMake finds
+ * SSE4.1: reference CMakeLists.txt:58-68 -> -DLV_HAVE_SSE; SURVEY.md 8a a5.6: 8 int16 state
+ * metrics per __m128i, float LLRs converted to int16 on entry).  The srsLTE source is not in the
+ * container, so the fixed-point constants are this build's, chosen so that NO int16 operation
+ * can overflow: every value below is an exact integer and the three implementations (this int32
+ * code, the SSE4.1 CPU baseline in oracle/o_simd.c with saturating int16 ops, and the GPU kernel
+ * computing on integer-valued fp32) produce identical extrinsics, decisions and iteration counts.
+ *   input    q(x) = clamp(rint(32 x), +-511)                 (filler -10000 -> -511)
+ *   DEC1     xs1 = q(Ls) + w                 (|w| <= 1023, so |xs1| <= 1534: no clamp), xp = q(Lp1)
+ *   DEC2     xs2 = clamp(llr1[pi] - w[pi], +-1535),  xp = q(Lp2); tails use q() directly
+ *   extr.    w[pi(k)] = clamp(llr2_k - xs2_k, +-1023)   (DEC2's extrinsic; equals the gen
+ *            schedule's w + llr2 - llr1 whenever no clamp engages)
+ *   decision bit_i = llr2[pi^-1(i)] > 0
+ *   trellis  exactly the float recursion above (normalised to state 0; -inf = any value below
+ *            -2^15, it can never win a max).  Bounds: R = 1535 + 511 = 2046 bounds the spread of
+ *            one step's branch metrics, any state reaches any other in 3 steps, so normalised
+ *            alpha/beta lie in +-3R = +-6138, pre-normalisation candidates in +-4R and LLRs in
+ *            +-13R = +-26598; llr1 - w and llr2 - xs2 stay inside +-28133: all inside int16.
+ */
+static int32_t clampi(int32_t x, int32_t c) { return x < -c ? -c : (x > c ? c : x); }
+
+int32_t or_q16(float x) {
+  float y = rintf(x * OR_I16_SCALE);
+  y = fminf(fmaxf(y, (float)-OR_I16_CI), (float)OR_I16_CI);
+  return (int32_t)y;
+}
+
+#define NEG16 (-(1 << 28))
+static void map_dec16(const int32_t *xs, const int32_t *xp, int32_t *out, uint32_t K, int32_t *beta) {
+  for (int s = 0; s < 8; s++) beta[(K + 3) * 8 + s] = s ? NEG16 : 0;
+  for (int k = (int)K + 2; k >= 1; k--) {
+    int32_t g[2][2] = {{0, xp[k]}, {xs[k], xs[k] + xp[k]}};
+    const int32_t *bn = beta + (k + 1) * 8;
+    int32_t m[8];
+    for (int s = 0; s < 8; s++) {
+      int32_t b0 = bn[NEXT[s][0]] + g[0][PAR[s][0]], b1 = bn[NEXT[s][1]] + g[1][PAR[s][1]];
+      m[s] = b0 > b1 ? b0 : b1;
+    }
+    for (int s = 0; s < 8; s++) beta[k * 8 + s] = m[s] - m[0];
+  }
+  int32_t alpha[8];
+  for (int s = 0; s < 8; s++) alpha[s] = s ? NEG16 : 0;
+  for (uint32_t k = 0; k < K; k++) {
+    int32_t g[2][2] = {{0, xp[k]}, {xs[k], xs[k] + xp[k]}};
+    const int32_t *bn = beta + (k + 1) * 8;
+    int32_t c[8][2], m0 = INT32_MIN, m1 = INT32_MIN;
+    for (int s = 0; s < 8; s++)
+      for (int u = 0; u < 2; u++) {
+        c[s][u] = alpha[s] + g[u][PAR[s][u]];
+        int32_t t = c[s][u] + bn[NEXT[s][u]];
+        if (u) { if (t > m1) m1 = t; } else { if (t > m0) m0 = t; }
+      }
+    out[k] = m1 - m0;
+    int32_t a[8];
+    for (int s = 0; s < 8; s++) {
+      int32_t x0 = c[PREV_S[s][0]][PREV_U[s][0]], x1 = c[PREV_S[s][1]][PREV_U[s][1]];
+      a[s] = x0 > x1 ? x0 : x1;
+    }
+    for (int s = 0; s < 8; s++) alpha[s] = a[s] - a[0];
+  }
+}
+
+int or_tdec16_reset(or_tdec16_t *h, uint32_t K) {
+  init_tables();
+  if (K > OR_TCOD_MAX_K || or_qpp(K, h->pi)) return -1;
+  h->K = K;
+  for (uint32_t i = 0; i < K; i++) h->pinv[h->pi[i]] = i;
+  memset(h->w, 0, sizeof(int32_t) * K);
+  return 0;
+}
+
+void or_tdec16_iteration(or_tdec16_t *h, const float *in) {
+  uint32_t K = h->K;
+  for (uint32_t k = 0; k < 3 * K + 12; k++) h->q[k] = or_q16(in[k]);
+  const int32_t *q = h->q;
+  for (uint32_t k = 0; k < K; k++) { h->xs[k] = q[3 * k] + h->w[k]; h->xp[k] = q[3 * k + 1]; }
+  for (uint32_t j = 0; j < 3; j++) { h->xs[K + j] = q[3 * K + 2 * j]; h->xp[K + j] = q[3 * K + 2 * j + 1]; }
+  map_dec16(h->xs, h->xp, h->llr1, K, h->beta);
+  for (uint32_t k = 0; k < K; k++) {
+    h->xs[k] = clampi(h->llr1[h->pi[k]] - h->w[h->pi[k]], OR_I16_CX);
+    h->xp[k] = q[3 * k + 2];
+  }
+  for (uint32_t j = 0; j < 3; j++) { h->xs[K + j] = q[3 * K + 6 + 2 * j]; h->xp[K + j] = q[3 * K + 7 + 2 * j]; }
+  map_dec16(h->xs, h->xp, h->llr2, K, h->beta);
+  for (uint32_t k = 0; k < K; k++) h->w[h->pi[k]] = clampi(h->llr2[k] - h->xs[k], OR_I16_CW);
+}
+
+void or_tdec16_decision(const or_tdec16_t *h, uint8_t *bits) {
+  for (uint32_t i = 0; i < h->K; i++) bits[i] = h->llr2[h->pinv[i]] > 0 ? 1 : 0;
+}
+
+int or_decode_cb16(or_tdec16_t *h, const float *in, uint32_t K, uint32_t max_its, int early_stop,
+                   int crc_type, uint8_t *bits, int *crc_ok) {
+  if (or_tdec16_reset(h, K)) return -1;
+  uint32_t its = 0;
+  int ok = 0;
+  do {
+    or_tdec16_iteration(h, in);
+    its++;
+    or_tdec16_decision(h, bits);
+    ok = ((crc_type ? or_crc24a(bits, K) : or_crc24b(bits, K)) == 0);
+    if (early_stop && ok) break;
+  } while (its < max_its);
+  *crc_ok = ok;
+  return (int)its;
+}
+
+static int g_tdec_mode = OR_TDEC_GEN;
+void or_set_tdec_mode(int mode) { g_tdec_mode = mode; }
+int or_get_tdec_mode(void) { return g_tdec_mode; }

@@ -232,7 +232,11 @@ int or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uin
                     uint32_t *noi_out, uint32_t *cb_crc_ok_out) {
   or_cbsegm_t sg;
   if (or_cbsegm(tbs, &sg)) return -1;
-  static or_tdec_t h;
+  /* per-call decoder state: or_dlsch_decode / or_decode_subframe are called from several threads
+     by the CPU baseline */
+  int mode = or_get_tdec_mode();
+  void *h = malloc(mode == OR_TDEC_GEN ? sizeof(or_tdec_t)
+                   : mode == OR_TDEC_I16 ? sizeof(or_tdec16_t) : or_simd_tdec_size());
   float *din = (float *)malloc(sizeof(float) * 3 * (OR_TCOD_MAX_K + 4));
   uint8_t *bits = (uint8_t *)malloc(OR_TCOD_MAX_K), *b = (uint8_t *)malloc(sg.B + 8);
   uint32_t pos = 0, pb = 0, noi = 0, ncb_ok = 0;
@@ -242,7 +246,9 @@ int or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uin
     or_rm_rx(llr + pos, E, K, F, rv, new_tb, sb + (size_t)r * sb_stride, din);
     pos += E;
     int ok;
-    int its = or_decode_cb(&h, din, K, max_its, 1, sg.C == 1, bits, &ok);
+    int its = mode == OR_TDEC_I16    ? or_decode_cb16((or_tdec16_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok)
+              : mode == OR_TDEC_SIMD ? or_simd_decode_cb(h, din, K, max_its, 1, sg.C == 1, bits, &ok)
+                                     : or_decode_cb((or_tdec_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok);
     if ((uint32_t)its > noi) noi = (uint32_t)its;
     ncb_ok += ok ? 1 : 0;
     uint32_t L = sg.C > 1 ? 24 : 0;
@@ -253,7 +259,7 @@ int or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uin
   for (uint32_t i = 0; i < tbs; i++) payload[i / 8] |= (uint8_t)(b[i] << (7 - i % 8));
   if (noi_out) *noi_out = noi;
   if (cb_crc_ok_out) *cb_crc_ok_out = ncb_ok;
-  free(din); free(bits); free(b);
+  free(din); free(bits); free(b); free(h);
   return tb_ok ? 0 : -1;
 }
 

@@ -95,6 +95,40 @@ void     or_tdec_decision(const or_tdec_t *h, uint8_t *bits);
 /* decode one codeblock: returns iterations used; *crc_ok set. crc_type 0 = 24B, 1 = 24A */
 int      or_decode_cb(or_tdec_t *h, const float *in, uint32_t K, uint32_t max_its, int early_stop,
                       int crc_type, uint8_t *bits, int *crc_ok);
+/* int16 ("SSE") max-log-MAP: exact-integer restatement of srsLTE's SSE decoder design, see the
+ * o_fec.c section header for the quantisation and clamps.  Same call contract as the float one. */
+#define OR_I16_SCALE 32.0f
+#define OR_I16_CI    511
+#define OR_I16_CX    1535
+#define OR_I16_CW    1023
+typedef struct {
+  uint32_t K;
+  uint32_t pi[OR_TCOD_MAX_K], pinv[OR_TCOD_MAX_K];
+  int32_t  w[OR_TCOD_MAX_K], llr1[OR_TCOD_MAX_K], llr2[OR_TCOD_MAX_K];
+  int32_t  xs[OR_TCOD_MAX_K + 3], xp[OR_TCOD_MAX_K + 3];
+  int32_t  q[3 * OR_TCOD_MAX_K + 12];
+  int32_t  beta[(OR_TCOD_MAX_K + 4) * 8];
+} or_tdec16_t;
+int32_t  or_q16(float x);
+int      or_tdec16_reset(or_tdec16_t *h, uint32_t K);
+void     or_tdec16_iteration(or_tdec16_t *h, const float *in);
+void     or_tdec16_decision(const or_tdec16_t *h, uint8_t *bits);
+int      or_decode_cb16(or_tdec16_t *h, const float *in, uint32_t K, uint32_t max_its, int early_stop,
+                        int crc_type, uint8_t *bits, int *crc_ok);
+/* decoder used by or_dlsch_decode / or_decode_subframe (test infrastructure switch) */
+#define OR_TDEC_GEN 0
+#define OR_TDEC_I16 1
+#define OR_TDEC_SIMD 2   /* the SSE4.1 implementation of the int16 decoder (o_simd.c) */
+void     or_set_tdec_mode(int mode);
+int      or_get_tdec_mode(void);
+/* SSE4.1 int16 decoder (CPU baseline), bit-identical to or_decode_cb16.  state: or_simd_tdec_size()
+ * bytes (any alignment).  Batch: n code blocks of equal K, input i at in + i*stride floats. */
+size_t   or_simd_tdec_size(void);
+int      or_simd_decode_cb(void *state, const float *in, uint32_t K, uint32_t max_its, int early_stop,
+                           int crc_type, uint8_t *bits, int *crc_ok);
+int      or_simd_decode_batch(const float *in, uint32_t stride, uint32_t n, uint32_t K, uint32_t max_its,
+                              int early_stop, int crc_type, uint8_t *bits, uint32_t *its, uint8_t *ok,
+                              uint32_t nthreads);
 
 /* ---- PHY TX (o_tx.c): synthetic subframe generator (ground truth) ----------------------- */
 typedef struct {

@@ -17,6 +17,7 @@ MAX_PRB = 110
 STAGES = ("ofdm", "chest", "demap", "rm", "tdec", "tb")
 BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF_CB_ITS, BUF_CB_CRC = range(9)
 FLAG_PROFILE = 1
+FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic, see include/mi_dl.h
 
 
 class SfCfg(C.Structure):
@@ -104,6 +105,8 @@ def emu():
         E.emu_decode_llr.restype = C.c_int
         E.emu_decode_llr.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]
+        E.emu_set_tdec_i16.restype = None
+        E.emu_set_tdec_i16.argtypes = [C.c_int]
         E.emu_payload_offset.restype = C.c_size_t
         E.emu_payload_offset.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _emu = E
@@ -134,11 +137,11 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
-        self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its,
-                                          FLAG_PROFILE if profile else 0)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else 0)
+        self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())
 
@@ -225,9 +228,10 @@ def turbo_encode(bits, K, F=0):
 class TdecBatch:
     """Raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* / turbodecoder_test contract)."""
 
-    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False):
+    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False, tdec_i16=False):
         self.K, self.n_cb = K, n_cb
-        self.h = lib().mi_tdec_create(K, n_cb, max_its, int(early_stop), int(crc24a), FLAG_PROFILE if profile else 0)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else 0)
+        self.h = lib().mi_tdec_create(K, n_cb, max_its, int(early_stop), int(crc24a), flags)
         if not self.h:
             raise RuntimeError("mi_tdec_create: " + last_error())
 

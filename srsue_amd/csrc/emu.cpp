@@ -14,6 +14,9 @@
 #include "tb_body.h"
 #include "tdec_body.h"
 
+static int g_q16 = 0;   // turbo arithmetic of the emulated decoder (MI_DL_FLAG_TDEC_I16)
+extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
+
 extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
                               uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
   mi::Plan P;
@@ -49,7 +52,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.dec = &dec[g.dec_off];
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
       a.K = g.K; a.F = ld.F; a.max_its = max_its; a.early_stop = 1; a.crc24a = ld.crc24a;
-      mi::TdecLaneResult r = mi::tdec_lane(a, lane);
+      mi::TdecLaneResult r = g_q16 ? mi::tdec_lane<true>(a, lane) : mi::tdec_lane<false>(a, lane);
       cits[li] = r.its;
       ccrc[li] = r.crc_ok;
     }

@@ -24,7 +24,7 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
 void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
                  uint32_t* cb_crc, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop,
-                 hipStream_t st);
+                 bool q16, hipStream_t st);
 // raw code-block decoder input [cb][3(K+4)] -> group-interleaved softbuffer layout
 void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, const MiKTab* ktabs,
                        const uint32_t* kdata, uint32_t n_groups, uint32_t K, uint32_t n_cb, hipStream_t st);

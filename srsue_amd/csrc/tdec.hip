@@ -5,6 +5,7 @@
 
 namespace mi {
 
+template <bool Q16>
 __global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, float* __restrict__ scratch,
                                                  uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
                                                  uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
@@ -33,17 +34,21 @@ __global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, 
   a.max_its = max_its;
   a.early_stop = early_stop;
   a.crc24a = ld.crc24a;
-  const TdecLaneResult r = tdec_lane(a, lane);
+  const TdecLaneResult r = tdec_lane<Q16>(a, lane);
   cb_its[li] = r.its;
   cb_crc[li] = r.crc_ok;
 }
 
 void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data,
-                 uint32_t n_groups, uint32_t max_its, uint32_t early_stop, hipStream_t st) {
+                 uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16, hipStream_t st) {
   if (!n_groups) return;
-  hipLaunchKernelGGL(tdec_kernel, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups,
-                     lanes, ktabs, ktab_data, max_its, early_stop);
+  if (q16)
+    hipLaunchKernelGGL(tdec_kernel<true>, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
+                       groups, lanes, ktabs, ktab_data, max_its, early_stop);
+  else
+    hipLaunchKernelGGL(tdec_kernel<false>, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
+                       groups, lanes, ktabs, ktab_data, max_its, early_stop);
 }
 
 }  // namespace mi

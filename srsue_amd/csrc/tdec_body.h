@@ -18,6 +18,13 @@
 // branches around loads), and the code-block CRC is accumulated during the last half-iteration
 // from a per-K table of single-bit CRC contributions (CRC is linear over GF(2)), so no separate
 // CRC pass re-reads the decisions.
+//
+// Two arithmetic modes (template parameter Q16), both bit-exact against their oracle:
+//  * Q16 = false: srsLTE-gen float decoder (oracle or_decode_cb);
+//  * Q16 = true : the int16 "SSE" decoder (oracle or_decode_cb16, CPU baseline or_simd_decode_cb):
+//    inputs quantised q(x) = clamp(rint(32 x), +-511), DEC2 systematic clamped to +-1535, extrinsic
+//    w = clamp(llr2 - xs2, +-1023).  Every metric is then an integer of magnitude < 2^15, which
+//    fp32 adds/subs/max represent exactly, so the same register code reproduces the int16 decoder.
 #pragma once
 #include "dl_common.h"
 
@@ -49,6 +56,13 @@ struct TdecArgs {
 };
 
 struct TdecLaneResult { uint32_t its; uint32_t crc_ok; };
+
+// int16-mode constants (oracle/oracle.h OR_I16_*)
+constexpr float I16_SCALE = 32.0f, I16_CI = 511.0f, I16_CX = 1535.0f, I16_CW = 1023.0f;
+MI_HD inline float clampf(float x, float c) { return fminf(fmaxf(x, -c), c); }
+// decoder input as read from the softbuffer: raw float, or quantised in int16 mode
+template <bool Q16>
+MI_HD inline float qin(float x) { return Q16 ? clampf(rintf(x * I16_SCALE), I16_CI) : x; }
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
@@ -95,34 +109,35 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
 // raw per-step inputs of one window: DEC1 {sys, p1, w}, DEC2 {llr1[pi], w[pi], p2}
 struct TdecWin { float a[BETA_W], b[BETA_W], c[BETA_W]; };
 
-template <bool DEC2, bool FIRST>
+template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin& r) {
   const uint32_t K = a.K;
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
-      r.a[i] = a.sb[(size_t)a.pos[3 * k] * LANES + lane];
-      r.b[i] = a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane];
+      r.a[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k] * LANES + lane]);
+      r.b[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane]);
       r.c[i] = FIRST ? 0.0f : a.scr[(size_t)k * LANES + lane];
     } else {
       const uint32_t pk = a.pi[k];
       r.a[i] = a.scr[(size_t)(K + pk) * LANES + lane];
       r.b[i] = FIRST ? 0.0f : a.scr[(size_t)pk * LANES + lane];
-      r.c[i] = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
+      r.c[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane]);
     }
   }
 }
 
 // decoder inputs (xs, xp) of step base+i from the raw window values (filler: known-zero bits)
-template <bool DEC2>
+template <bool DEC2, bool Q16>
 MI_HD inline void tdec_xs_xp(const TdecWin& r, int i, uint32_t k, uint32_t F, float& xs, float& xp) {
+  constexpr float FILL = Q16 ? -I16_CI : FILLER_LLR;   // q(FILLER_LLR) = -511
   if (!DEC2) {
     const bool fill = k < F;
-    xs = (fill ? FILLER_LLR : r.a[i]) + r.c[i];
-    xp = fill ? FILLER_LLR : r.b[i];
+    xs = (fill ? FILL : r.a[i]) + r.c[i];
+    xp = fill ? FILL : r.b[i];
   } else {
-    xs = r.a[i] - r.b[i];
+    xs = Q16 ? clampf(r.a[i] - r.b[i], I16_CX) : r.a[i] - r.b[i];
     xp = r.c[i];
   }
 }
@@ -139,14 +154,16 @@ MI_HD inline void ck_load(const float* ck, uint32_t c, int lane, float (&b)[8]) 
 }
 
 // per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
-template <bool DEC2>
-MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, const TdecWin& w, int i, uint32_t& crc) {
+template <bool DEC2, bool Q16>
+MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, float xs, const TdecWin& w, int i,
+                            uint32_t& crc) {
   const uint32_t K = a.K;
   if (!DEC2) {
     a.scr[(size_t)(K + k) * LANES + lane] = llr;                       // llr1
   } else {
     const uint32_t pk = a.pi[k];
-    a.scr[(size_t)pk * LANES + lane] = w.b[i] + (llr - w.a[i]);        // w update
+    a.scr[(size_t)pk * LANES + lane] = Q16 ? clampf(llr - xs, I16_CW)   // w update
+                                           : w.b[i] + (llr - w.a[i]);
     const bool bit = llr > 0.0f;
     a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                     // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
@@ -158,7 +175,7 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, 
 // the K info steps, checkpointed every CK = 2 BETA_W steps.  Forward pass: per checkpoint interval
 // [a, a + CK) the beta values are recomputed from the checkpoint at a + CK as two register windows
 // of BETA_W steps (first half, then second half), alpha and the LLRs follow.
-template <bool DEC2, bool FIRST>
+template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   constexpr int CK = TDEC_CK;
   static_assert(CK == BETA_W || CK == 2 * BETA_W, "checkpoint spacing");
@@ -173,8 +190,8 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
     float tx[3], tp[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      tx[j] = a.sb[(size_t)a.pos[t0 + 2 * j] * LANES + lane];
-      tp[j] = a.sb[(size_t)a.pos[t0 + 2 * j + 1] * LANES + lane];
+      tx[j] = qin<Q16>(a.sb[(size_t)a.pos[t0 + 2 * j] * LANES + lane]);
+      tp[j] = qin<Q16>(a.sb[(size_t)a.pos[t0 + 2 * j + 1] * LANES + lane]);
     }
 #pragma unroll
     for (int j = 2; j >= 0; j--) {
@@ -186,14 +203,14 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   }
   ck_store(ck, K / CK, lane, b);
   TdecWin cur, nxt;
-  tdec_load_window<DEC2, FIRST>(a, lane, K - BETA_W, cur);
+  tdec_load_window<DEC2, FIRST, Q16>(a, lane, K - BETA_W, cur);
   for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
-    if (base >= BETA_W) tdec_load_window<DEC2, FIRST>(a, lane, (uint32_t)(base - BETA_W), nxt);
+    if (base >= BETA_W) tdec_load_window<DEC2, FIRST, Q16>(a, lane, (uint32_t)(base - BETA_W), nxt);
 #pragma unroll
     for (int i = BETA_W - 1; i >= 0; i--) {
       if (base + i == 0) break;   // beta_0 is never used
       float xs, xp, nb[8];
-      tdec_xs_xp<DEC2>(cur, i, (uint32_t)(base + i), F, xs, xp);
+      tdec_xs_xp<DEC2, Q16>(cur, i, (uint32_t)(base + i), F, xs, xp);
       beta_step(b, xs, xp, nb);
 #pragma unroll
       for (int s = 0; s < 8; s++) b[s] = nb[s];
@@ -207,23 +224,23 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
   if constexpr (CK == BETA_W) {
     float ckc[8], ckn[8];
-    tdec_load_window<DEC2, FIRST>(a, lane, 0, cur);
+    tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, cur);
     ck_load(ck, 1, lane, ckc);
     for (uint32_t base = 0; base < K; base += BETA_W) {
       if (base + BETA_W < K) {
-        tdec_load_window<DEC2, FIRST>(a, lane, base + BETA_W, nxt);
+        tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + BETA_W, nxt);
         ck_load(ck, base / BETA_W + 2, lane, ckn);
       }
       float xs[BETA_W], xp[BETA_W];
 #pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(cur, i, base + i, F, xs[i], xp[i]);
+      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(cur, i, base + i, F, xs[i], xp[i]);
       float bw[BETA_W][8];
 #pragma unroll
       for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
 #pragma unroll
       for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), cur, i, crc);
+      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2, Q16>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], cur, i, crc);
       cur = nxt;
 #pragma unroll
       for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
@@ -232,8 +249,8 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   } else {
   TdecWin c0, c1, n0, n1;   // inputs of the current interval (two halves) and of the next one
   float ckc[8], ckn[8];
-  tdec_load_window<DEC2, FIRST>(a, lane, 0, c0);
-  tdec_load_window<DEC2, FIRST>(a, lane, BETA_W, c1);
+  tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, c0);
+  tdec_load_window<DEC2, FIRST, Q16>(a, lane, BETA_W, c1);
   ck_load(ck, 1, lane, ckc);
   n0 = c0;
   n1 = c1;
@@ -244,9 +261,9 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       // staggered prefetch: next interval's first half during this first half, its second half
       // (and checkpoint) during this second half -- at most three windows live at once
       if (more) {
-        if (half == 0) tdec_load_window<DEC2, FIRST>(a, lane, base + CK, n0);
+        if (half == 0) tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK, n0);
         else {
-          tdec_load_window<DEC2, FIRST>(a, lane, base + CK + BETA_W, n1);
+          tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK + BETA_W, n1);
           ck_load(ck, base / CK + 2, lane, ckn);
         }
       }
@@ -254,7 +271,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       const uint32_t hb = base + (uint32_t)half * BETA_W;
       float xs[BETA_W], xp[BETA_W];
 #pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2>(w, i, hb + i, F, xs[i], xp[i]);
+      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(w, i, hb + i, F, xs[i], xp[i]);
       float bw[BETA_W][8];
       if (half == 0) {
         // beta_{a+8} -> beta_{a+4} (discarded path), then the window beta_{a+1..a+4}
@@ -264,7 +281,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
 #pragma unroll
         for (int i = BETA_W - 1; i >= 0; i--) {
           float xs2, xp2, nb[8];
-          tdec_xs_xp<DEC2>(c1, i, base + BETA_W + i, F, xs2, xp2);
+          tdec_xs_xp<DEC2, Q16>(c1, i, base + BETA_W + i, F, xs2, xp2);
           beta_step(t, xs2, xp2, nb);
 #pragma unroll
           for (int s = 0; s < 8; s++) t[s] = nb[s];
@@ -278,7 +295,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
 #pragma unroll
       for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2>(a, lane, hb + i, alpha_step(al, bw[i], xs[i], xp[i]), w, i, crc);
+      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2, Q16>(a, lane, hb + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, i, crc);
     }
     c0 = n0;
     c1 = n1;
@@ -288,16 +305,17 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   }
 }
 
+template <bool Q16>
 MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
     uint32_t crc = 0;
     if (it == 0) {
-      tdec_half<false, true>(a, lane, crc);
-      tdec_half<true, true>(a, lane, crc);
+      tdec_half<false, true, Q16>(a, lane, crc);
+      tdec_half<true, true, Q16>(a, lane, crc);
     } else {
-      tdec_half<false, false>(a, lane, crc);
-      tdec_half<true, false>(a, lane, crc);
+      tdec_half<false, false, Q16>(a, lane, crc);
+      tdec_half<true, false, Q16>(a, lane, crc);
     }
     r.its = it + 1;
     r.crc_ok = crc == 0;

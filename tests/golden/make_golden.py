@@ -9,6 +9,10 @@ Fixtures
                           8 fixed iterations, early stop off: LLRs, decisions, bit errors
   rm_K5824.npz            rate-match -> de-match round trip, rv 0..3, E = 6924   
   sf_1p4mhz.npz           1.4 MHz TM1 subframe: IQ (product TX, 20 dB), TB, oracle grid/ce/LLR/payload
+  tdec16_K6144.npz        the config-1 LLRs of tdec_K6144_ebno.npz through the int16 ("SSE") decoder:
+                          decisions, bit errors, and the decisions after 1 and 2 iterations
+
+`python tests/golden/make_golden.py tdec16` regenerates only the int16 fixture.
 """
 import ctypes as C
 import os
@@ -36,7 +40,26 @@ def turbo_llr(bits, K, ebno_db, rng, amp=None):
     return (-2.0 * y / sigma2).astype(np.float32)   # LLR > 0 => bit 1
 
 
+def make_tdec16():
+    """int16 decoder on the committed config-1 LLRs (so the fixture is tied to tdec_K6144_ebno.npz)."""
+    g = np.load(os.path.join(HERE, "tdec_K6144_ebno.npz"))
+    td = O.Tdec(O.TDEC_I16)
+    decs, d1, d2, errs = [], [], [], []
+    for llr in g["llr"]:
+        dec, its, ok = td.decode_cb(llr, 6144, max_its=8, early_stop=False)
+        decs.append(dec); errs.append(int(np.sum(dec != g["bits"])))
+        d1.append(td.decode_cb(llr, 6144, max_its=1, early_stop=False)[0])
+        d2.append(td.decode_cb(llr, 6144, max_its=2, early_stop=False)[0])
+    np.savez_compressed(os.path.join(HERE, "tdec16_K6144.npz"), ebno=g["ebno"], dec=np.stack(decs),
+                        dec_it1=np.packbits(np.stack(d1), axis=1), dec_it2=np.packbits(np.stack(d2), axis=1),
+                        errors=np.array(errs))
+    print("int16 K=6144 bit errors per Eb/N0", dict(zip(g["ebno"].tolist(), errs)))
+
+
 def main():
+    if sys.argv[1:] == ["tdec16"]:
+        make_tdec16()
+        return
     L = O.lib()
     rng = np.random.default_rng(1)
     # --- K = 40 noiseless
@@ -83,6 +106,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "sf_1p4mhz.npz"), iq=iq, tb=tb, grid=grid, ce=ce, metrics=met, llr=llr,
                         payload=pay, noi=np.array([noi]),
                         cfg=np.array([cfg.cell_id, cfg.nof_prb, cfg.nof_ports, cfg.sf_idx, cfg.cfi, cfg.tbs, cfg.Qm]))
+    make_tdec16()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

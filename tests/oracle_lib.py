@@ -80,6 +80,16 @@ def lib():
             "or_rm_rx": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, f32, f32]),
             "or_decode_cb": (C.c_int, [C.c_void_p, f32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, u8,
                                        C.POINTER(C.c_int)]),
+            "or_decode_cb16": (C.c_int, [C.c_void_p, f32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, u8,
+                                         C.POINTER(C.c_int)]),
+            "or_q16": (C.c_int32, [C.c_float]),
+            "or_simd_tdec_size": (C.c_size_t, []),
+            "or_simd_decode_cb": (C.c_int, [C.c_void_p, f32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, u8,
+                                            C.POINTER(C.c_int)]),
+            "or_simd_decode_batch": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                               C.c_int, u8, u32, u8, C.c_uint32]),
+            "or_set_tdec_mode": (None, [C.c_int]),
+            "or_get_tdec_mode": (C.c_int, []),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -103,18 +113,38 @@ def lib():
 
 # ------------------------------------------------------------------ convenience wrappers
 TDEC_STATE_BYTES = 4 + 4 * 6144 * 2 + 4 * 6144 * 3 + 4 * 6147 * 2 + 4 * 6148 * 8
+TDEC16_STATE_BYTES = TDEC_STATE_BYTES + 4 * (3 * 6144 + 12)
+TDEC_GEN, TDEC_I16, TDEC_SIMD = 0, 1, 2
 
 
 class Tdec:
-    def __init__(self):
-        self.buf = C.create_string_buffer(TDEC_STATE_BYTES + 64)
+    """One oracle turbo decoder; mode TDEC_GEN (float, srsLTE gen) or TDEC_I16 (int16, SSE design)."""
+    def __init__(self, mode=TDEC_GEN):
+        self.mode = mode
+        size = {TDEC_GEN: TDEC_STATE_BYTES, TDEC_I16: TDEC16_STATE_BYTES}.get(mode) or lib().or_simd_tdec_size()
+        self.buf = C.create_string_buffer(size + 64)
 
     def decode_cb(self, llr, K, max_its=8, early_stop=True, crc24a=False):
         bits = np.zeros(K, np.uint8)
         ok = C.c_int(0)
-        its = lib().or_decode_cb(self.buf, np.ascontiguousarray(llr, np.float32), K, max_its,
+        fn = {TDEC_GEN: lib().or_decode_cb, TDEC_I16: lib().or_decode_cb16,
+              TDEC_SIMD: lib().or_simd_decode_cb}[self.mode]
+        its = fn(self.buf, np.ascontiguousarray(llr, np.float32), K, max_its,
                                  int(early_stop), int(crc24a), bits, C.byref(ok))
         return bits, its, bool(ok.value)
+
+
+class tdec_mode:
+    """Context manager selecting the decoder or_dlsch_decode / or_decode_subframe use."""
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = lib().or_get_tdec_mode()
+        lib().or_set_tdec_mode(self.mode)
+
+    def __exit__(self, *a):
+        lib().or_set_tdec_mode(self.prev)
 
 
 def cbsegm(tbs):

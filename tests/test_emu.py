@@ -25,19 +25,28 @@ CASES = [  # nof_prb, ports, tbs, Qm, snr, sf, rv, cell
 ]
 
 
+@pytest.mark.parametrize("mode", ["gen", "i16"])
 @pytest.mark.parametrize("nprb,ports,tbs,qm,snr,sf,rv,cid", CASES)
-def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, sf, rv, cid):
+def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, sf, rv, cid, mode):
+    """Planner + rate de-matching + turbo (float gen or int16 SSE arithmetic) + TB assembly, emulated
+    lane by lane on the host, against the oracle decoder of the same arithmetic."""
     cfg = abi.sf_cfg(cell_id=cid, nof_prb=nprb, nof_ports=ports, sf_idx=sf, tbs=tbs, Qm=qm, rv=rv)
     tb = tb_bytes(sf, tbs)
     iq = abi.tx_subframe(cfg, tb, snr_db=snr, seed=sf + 7)
     llr = oracle_front(cfg, iq)[3]
-    ok, opay, onoi, _ = oracle_dlsch(cfg, llr)
+    q16 = mode == "i16"
+    with O.tdec_mode(O.TDEC_I16 if q16 else O.TDEC_GEN):
+        ok, opay, onoi, _ = oracle_dlsch(cfg, llr)
     arr = abi.cfg_array([cfg])
     pe = np.zeros(tbs // 8, np.uint8)
     eok = np.zeros(1, np.uint32)
     eits = np.zeros(1, np.uint32)
-    rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), 1, np.ascontiguousarray(llr).ctypes.data, 4,
-                                  pe.ctypes.data, eok.ctypes.data, eits.ctypes.data, None)
+    abi.emu().emu_set_tdec_i16(int(q16))
+    try:
+        rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), 1, np.ascontiguousarray(llr).ctypes.data, 4,
+                                      pe.ctypes.data, eok.ctypes.data, eits.ctypes.data, None)
+    finally:
+        abi.emu().emu_set_tdec_i16(0)
     assert rc == 0
     assert bool(eok[0]) == ok
     assert eits[0] == onoi

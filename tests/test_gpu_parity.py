@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch
 
+import oracle_lib as O
 from helpers import make_subframes, oracle_dlsch, oracle_front, rel_err, tb_bytes
 from srsue_amd import abi
 
@@ -18,8 +19,8 @@ TOL = 1e-4
 S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
 
 
-def run_batch(cfgs, iqs, max_its=4, profile=False):
-    b = abi.Batch(cfgs, max_its=max_its, profile=profile)
+def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False):
+    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16)
     flat = np.zeros(2 * b.iq_samples, np.float32)
     for i, iq in enumerate(iqs):
         o = 2 * b.iq_offset(i)
@@ -48,10 +49,11 @@ CASES = [
 ]
 
 
-def test_mixed_batch_front_end_and_decode():
+@pytest.mark.parametrize("i16", [False, True])
+def test_mixed_batch_front_end_and_decode(i16):
     cfgs = [abi.sf_cfg(**c) for c in CASES]
     iqs, tbs = make_subframes(cfgs, snr_db=30.0)
-    b = run_batch(cfgs, iqs)
+    b = run_batch(cfgs, iqs, tdec_i16=i16)
     grid = b.download(abi.BUF_GRID, np.float32)
     ce = b.download(abi.BUF_CE, np.float32)
     llr = b.download(abi.BUF_LLR, np.float32)
@@ -66,7 +68,8 @@ def test_mixed_batch_front_end_and_decode():
         assert rel_err(grid[go:go + len(og)], og) < TOL, f"grid case {i}"
         assert rel_err(ce[co:co + len(oce)], oce) < TOL, f"ce case {i}"
         assert rel_err(llr[lo:lo + len(ollr)], ollr) < TOL, f"llr case {i}"
-        ok, opay, onoi, _ = oracle_dlsch(c, ollr)
+        with O.tdec_mode(O.TDEC_I16 if i16 else O.TDEC_GEN):
+            ok, opay, onoi, _ = oracle_dlsch(c, ollr)
         p = b.payload(i, pay)
         assert crc[i] == 1 and ok, f"CRC case {i}"
         assert np.array_equal(p, tbs[i]), f"payload vs transmitted TB, case {i}"
@@ -74,12 +77,13 @@ def test_mixed_batch_front_end_and_decode():
         assert its[i] == onoi
 
 
-@pytest.mark.parametrize("snr", [15.0, 17.5, 18.5, 19.5])
-def test_turbo_bit_exact_on_identical_llrs(snr):
+@pytest.mark.parametrize("i16", [False, True])
+@pytest.mark.parametrize("snr", [15.0, 17.5, 18.5, 19.5, 21.0])
+def test_turbo_bit_exact_on_identical_llrs(snr, i16):
     """Waterfall region: CRC passes and fails; GPU == oracle bit for bit either way."""
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + (i % 4), tbs=75376, Qm=6) for i in range(4)]
     iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=int(snr * 10))
-    b = abi.Batch(cfgs, max_its=4)
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16)
     llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
     flat = np.zeros(b.download(abi.BUF_LLR, np.float32).shape, np.float32)
     for i, l in enumerate(llrs):
@@ -91,7 +95,8 @@ def test_turbo_bit_exact_on_identical_llrs(snr):
     crc = b.download(abi.BUF_TB_CRC, np.uint32)
     its = b.download(abi.BUF_TB_ITS, np.uint32)
     for i, c in enumerate(cfgs):
-        ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
+        with O.tdec_mode(O.TDEC_I16 if i16 else O.TDEC_GEN):
+            ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
         assert bool(crc[i]) == ok
         assert its[i] == onoi
         assert np.array_equal(b.payload(i, pay), opay)

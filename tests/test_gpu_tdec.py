@@ -1,6 +1,7 @@
 """GPU: raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* contract of BASELINE configs[0],
 srsLTE's turbodecoder_test): K = 6144, 8 fixed iterations, no early stop, BPSK/AWGN LLRs across the
-waterfall -- decisions bit-identical to the oracle and to the committed golden fixture."""
+waterfall -- decisions bit-identical to the oracle and to the committed golden fixture, for both the
+float (srsLTE-gen) and the int16 (srsLTE SSE design) arithmetic."""
 import os
 
 import numpy as np
@@ -21,28 +22,33 @@ def llr_bpsk(d, K, ebno_db, rng):
     return (-2.0 * y / sigma2).astype(np.float32)
 
 
-def test_golden_config1_on_gpu(built):
+@pytest.mark.parametrize("i16", [False, True])
+def test_golden_config1_on_gpu(built, i16):
     g = np.load(os.path.join(GOLDEN, "tdec_K6144_ebno.npz"))
+    ref = np.load(os.path.join(GOLDEN, "tdec16_K6144.npz"))["dec"] if i16 else g["dec"]
     n = len(g["ebno"])
-    tb = abi.TdecBatch(6144, n, max_its=8, early_stop=False)
+    tb = abi.TdecBatch(6144, n, max_its=8, early_stop=False, tdec_i16=i16)
     d = torch.from_numpy(np.ascontiguousarray(g["llr"])).cuda()
     tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
     bits, its, _ = tb.results()
     assert np.all(its == 8)
-    assert np.array_equal(bits, g["dec"])
+    assert np.array_equal(bits, ref)
 
 
+@pytest.mark.parametrize("i16", [False, True])
 @pytest.mark.parametrize("K,ebno", [(6144, 0.6), (6144, 0.8), (5824, 1.0), (40, 2.0), (512, 1.5)])
-def test_codeblocks_bit_exact_vs_oracle(built, K, ebno):
+def test_codeblocks_bit_exact_vs_oracle(built, K, ebno, i16):
     rng = np.random.default_rng(K + int(ebno * 10))
     n = 70                                      # two 64-lane groups, the second partial
     bits = rng.integers(0, 2, (n, K)).astype(np.uint8)
     llr = np.stack([llr_bpsk(abi.turbo_encode(b, K), K, ebno, rng) for b in bits])
-    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False)
+    if i16:
+        llr *= np.float32(rng.uniform(0.5, 8.0))   # exercise the quantiser range too
+    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, tdec_i16=i16)
     d = torch.from_numpy(llr).cuda()
     tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
     got, its, _ = tb.results()
-    td = O.Tdec()
+    td = O.Tdec(O.TDEC_I16 if i16 else O.TDEC_GEN)
     for i in range(n):
         dec, oits, _ = td.decode_cb(llr[i], K, max_its=8, early_stop=False)
         assert np.array_equal(got[i], dec), f"cb {i}"

@@ -57,6 +57,7 @@ def main(d):
     json.dump(summary, open(os.path.join(d, "summary.json"), "w"), indent=1)
     if td.get("traffic_bytes_per_launch"):
         json.dump({"src_hash": kernel_src_hash(), "sf_per_gpu": bench["config"]["subframes_per_gpu"],
+                   "tdec": bench["config"].get("turbo_arithmetic", "gen"),
                    "tdec_traffic_bytes_per_launch": td["traffic_bytes_per_launch"],
                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench command "
                              f"({os.path.basename(d)}); bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024"},
