@@ -63,6 +63,18 @@ MI_HD inline float clampf(float x, float c) { return fminf(fmaxf(x, -c), c); }
 // decoder input as read from the softbuffer: raw float, or quantised in int16 mode
 template <bool Q16>
 MI_HD inline float qin(float x) { return Q16 ? clampf(rintf(x * I16_SCALE), I16_CI) : x; }
+// scratch streams (w, llr1, beta checkpoints): fp32, or int16 in int16 mode (every stored value is
+// an integer inside +-26598, see above), addressed by element index so both share the layout
+template <bool Q16>
+MI_HD inline float scr_ld(const float* scr, size_t i) {
+  if constexpr (Q16) return (float)reinterpret_cast<const int16_t*>(scr)[i];
+  else return scr[i];
+}
+template <bool Q16>
+MI_HD inline void scr_st(float* scr, size_t i, float v) {
+  if constexpr (Q16) reinterpret_cast<int16_t*>(scr)[i] = (int16_t)(int32_t)v;
+  else scr[i] = v;
+}
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
@@ -118,11 +130,11 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
     if (!DEC2) {
       r.a[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k] * LANES + lane]);
       r.b[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane]);
-      r.c[i] = FIRST ? 0.0f : a.scr[(size_t)k * LANES + lane];
+      r.c[i] = FIRST ? 0.0f : scr_ld<Q16>(a.scr, (size_t)k * LANES + lane);
     } else {
       const uint32_t pk = a.pi[k];
-      r.a[i] = a.scr[(size_t)(K + pk) * LANES + lane];
-      r.b[i] = FIRST ? 0.0f : a.scr[(size_t)pk * LANES + lane];
+      r.a[i] = scr_ld<Q16>(a.scr, (size_t)(K + pk) * LANES + lane);
+      r.b[i] = FIRST ? 0.0f : scr_ld<Q16>(a.scr, (size_t)pk * LANES + lane);
       r.c[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane]);
     }
   }
@@ -142,15 +154,19 @@ MI_HD inline void tdec_xs_xp(const TdecWin& r, int i, uint32_t k, uint32_t F, fl
   }
 }
 
-// beta checkpoint c (= beta at step c * CK) holds states 1..7 (state 0 is 0 after normalisation)
-MI_HD inline void ck_store(float* ck, uint32_t c, int lane, const float (&b)[8]) {
+// beta checkpoint c (= beta at step c * CK) holds states 1..7 (state 0 is 0 after normalisation);
+// ck0 = element index of checkpoint 0 in the scratch stream.  Checkpoints are taken at k <= K, where
+// every state is reachable, so no -inf is ever stored.
+template <bool Q16>
+MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) ck[((size_t)c * 7 + (s - 1)) * LANES + lane] = b[s];
+  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane, b[s]);
 }
-MI_HD inline void ck_load(const float* ck, uint32_t c, int lane, float (&b)[8]) {
+template <bool Q16>
+MI_HD inline void ck_load(const float* scr, size_t ck0, uint32_t c, int lane, float (&b)[8]) {
   b[0] = 0.0f;
 #pragma unroll
-  for (int s = 1; s < 8; s++) b[s] = ck[((size_t)c * 7 + (s - 1)) * LANES + lane];
+  for (int s = 1; s < 8; s++) b[s] = scr_ld<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane);
 }
 
 // per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
@@ -159,11 +175,11 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, 
                             uint32_t& crc) {
   const uint32_t K = a.K;
   if (!DEC2) {
-    a.scr[(size_t)(K + k) * LANES + lane] = llr;                       // llr1
+    scr_st<Q16>(a.scr, (size_t)(K + k) * LANES + lane, llr);            // llr1
   } else {
     const uint32_t pk = a.pi[k];
-    a.scr[(size_t)pk * LANES + lane] = Q16 ? clampf(llr - xs, I16_CW)   // w update
-                                           : w.b[i] + (llr - w.a[i]);
+    scr_st<Q16>(a.scr, (size_t)pk * LANES + lane,                       // w update
+                Q16 ? clampf(llr - xs, I16_CW) : w.b[i] + (llr - w.a[i]));
     const bool bit = llr > 0.0f;
     a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                     // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
@@ -180,7 +196,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   constexpr int CK = TDEC_CK;
   static_assert(CK == BETA_W || CK == 2 * BETA_W, "checkpoint spacing");
   const uint32_t K = a.K, F = a.F;
-  float* ck = a.scr + (size_t)2 * K * LANES;  // beta checkpoints
+  const size_t ck = (size_t)2 * K * LANES;  // beta checkpoints (element index)
   const float NINF = -INFINITY;
   float b[8];
 #pragma unroll
@@ -201,7 +217,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
   }
-  ck_store(ck, K / CK, lane, b);
+  ck_store<Q16>(a.scr, ck, K / CK, lane, b);
   TdecWin cur, nxt;
   tdec_load_window<DEC2, FIRST, Q16>(a, lane, K - BETA_W, cur);
   for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
@@ -215,7 +231,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
 #pragma unroll
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
-    if (base > 0 && base % CK == 0) ck_store(ck, (uint32_t)base / CK, lane, b);
+    if (base > 0 && base % CK == 0) ck_store<Q16>(a.scr, ck, (uint32_t)base / CK, lane, b);
     cur = nxt;
   }
   // ---- forward pass
@@ -225,11 +241,11 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   if constexpr (CK == BETA_W) {
     float ckc[8], ckn[8];
     tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, cur);
-    ck_load(ck, 1, lane, ckc);
+    ck_load<Q16>(a.scr, ck, 1, lane, ckc);
     for (uint32_t base = 0; base < K; base += BETA_W) {
       if (base + BETA_W < K) {
         tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + BETA_W, nxt);
-        ck_load(ck, base / BETA_W + 2, lane, ckn);
+        ck_load<Q16>(a.scr, ck, base / BETA_W + 2, lane, ckn);
       }
       float xs[BETA_W], xp[BETA_W];
 #pragma unroll
@@ -251,7 +267,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   float ckc[8], ckn[8];
   tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, c0);
   tdec_load_window<DEC2, FIRST, Q16>(a, lane, BETA_W, c1);
-  ck_load(ck, 1, lane, ckc);
+  ck_load<Q16>(a.scr, ck, 1, lane, ckc);
   n0 = c0;
   n1 = c1;
   for (uint32_t base = 0; base < K; base += CK) {
@@ -264,7 +280,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
         if (half == 0) tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK, n0);
         else {
           tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK + BETA_W, n1);
-          ck_load(ck, base / CK + 2, lane, ckn);
+          ck_load<Q16>(a.scr, ck, base / CK + 2, lane, ckn);
         }
       }
       const TdecWin& w = half ? c1 : c0;
