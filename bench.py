@@ -307,7 +307,7 @@ def main():
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
     ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
     ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
-    ap.add_argument("--tdec", choices=("gen", "i16"), default="gen",
+    ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
     args = ap.parse_args()
     if args.config == 2:

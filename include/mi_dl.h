@@ -49,10 +49,12 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
        MI_DL_BUF_METRICS, MI_DL_BUF_CB_ITS, MI_DL_BUF_CB_CRC };
 
 #define MI_DL_FLAG_PROFILE 1u  /* record HIP events around every stage of every run */
-/* turbo decoder arithmetic: default = srsLTE-gen float decoder (srslte_tdec_gen); TDEC_I16 = the
- * int16 decoder of srsLTE's SSE design (srslte_tdec_sse, what srsUE runs on SSE4.1 hosts:
- * reference CMakeLists.txt:58-68), fixed-point contract in DESIGN.md 4.5. */
+/* turbo decoder arithmetic.  Default (and MI_DL_FLAG_TDEC_I16): the int16 decoder of srsLTE's SSE
+ * design (srslte_tdec_sse, what srsUE runs on SSE4.1 hosts: reference CMakeLists.txt:58-68 adds
+ * -DLV_HAVE_SSE), fixed-point contract in DESIGN.md 4.5.  MI_DL_FLAG_TDEC_GEN: the float
+ * srsLTE-gen decoder (srslte_tdec_gen, the non-SSE build).  Both are bit-exact to their oracle. */
 #define MI_DL_FLAG_TDEC_I16 2u
+#define MI_DL_FLAG_TDEC_GEN 4u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 

@@ -17,7 +17,8 @@ MAX_PRB = 110
 STAGES = ("ofdm", "chest", "demap", "rm", "tdec", "tb")
 BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF_CB_ITS, BUF_CB_CRC = range(9)
 FLAG_PROFILE = 1
-FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic, see include/mi_dl.h
+FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic (the default), see include/mi_dl.h
+FLAG_TDEC_GEN = 4   # float srsLTE-gen turbo arithmetic
 
 
 class SfCfg(C.Structure):
@@ -137,10 +138,10 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=False):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
-        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else 0)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())
@@ -228,9 +229,9 @@ def turbo_encode(bits, K, F=0):
 class TdecBatch:
     """Raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* / turbodecoder_test contract)."""
 
-    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False, tdec_i16=False):
+    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False, tdec_i16=True):
         self.K, self.n_cb = K, n_cb
-        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else 0)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
         self.h = lib().mi_tdec_create(K, n_cb, max_its, int(early_stop), int(crc24a), flags)
         if not self.h:
             raise RuntimeError("mi_tdec_create: " + last_error())

@@ -135,7 +135,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
       launch_tdec(sb, d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
                   d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(),
                   d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
-                  (flags & MI_DL_FLAG_TDEC_I16) != 0, st);
+                  (flags & MI_DL_FLAG_TDEC_GEN) == 0, st);
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
@@ -171,7 +171,7 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
   launch_tdec(d_sb.as<float>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
               d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
-              (flags & MI_DL_FLAG_TDEC_I16) != 0, st);
+              (flags & MI_DL_FLAG_TDEC_GEN) == 0, st);
   mark(MI_DL_STAGE_TB);
   mark(MI_DL_NSTAGES);
   return hip_ok(hipGetLastError(), "launch") ? 0 : -1;

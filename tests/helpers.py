@@ -26,8 +26,12 @@ def oracle_front(cfg, iq):
     return grid, ce, met, llr[:G.value]
 
 
-def oracle_dlsch(cfg, llr, max_its=4, sb=None, new_tb=True):
-    """Oracle rate de-matching + turbo decoding + TB CRC of one TB."""
+def oracle_dlsch(cfg, llr, max_its=4, sb=None, new_tb=True, i16=None):
+    """Oracle rate de-matching + turbo decoding + TB CRC of one TB.  i16: True = int16 (SSE-design)
+    decoder, False = float gen decoder, None = whatever O.tdec_mode currently selects."""
+    if i16 is not None:
+        with O.tdec_mode(O.TDEC_I16 if i16 else O.TDEC_GEN):
+            return oracle_dlsch(cfg, llr, max_its, sb, new_tb)
     L = O.lib()
     s = O.cbsegm(cfg.tbs)
     ncb = L.or_ncb(s.Kp)

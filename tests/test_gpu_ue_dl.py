@@ -51,7 +51,7 @@ def test_ue_dl_tti_matches_oracle(ports, cfi, own):
     res = run_harness(1, 100, ports, [(c, iq, True, 0, own) for c, iq in zip(cfgs, iqs)])
     for i, (c, (ret, cf, noi, met, pay)) in enumerate(zip(cfgs, res)):
         _, _, omet, ollr = oracle_front(c, iqs[i])
-        ok, opay, onoi, _ = oracle_dlsch(c, ollr)
+        ok, opay, onoi, _ = oracle_dlsch(c, ollr, i16=True)   # the library default arithmetic
         assert cf == cfi
         assert ret == 0 and ok
         assert np.array_equal(pay, tb_bytes(i, c.tbs)) and np.array_equal(pay, opay)
@@ -67,8 +67,8 @@ def test_ue_dl_harq_soft_combining():
     iq1 = abi.tx_subframe(c1, tb, snr_db=16.0, seed=12)
     res = run_harness(1, 100, 1, [(c0, iq0, True, 4, True), (c1, iq1, False, 4, True)])
     l0, l1 = oracle_front(c0, iq0)[3], oracle_front(c1, iq1)[3]
-    ok0, pay0, noi0, sb = oracle_dlsch(c0, l0)
-    ok1, pay1, noi1, _ = oracle_dlsch(c1, l1, sb=sb, new_tb=False)
+    ok0, pay0, noi0, sb = oracle_dlsch(c0, l0, i16=True)
+    ok1, pay1, noi1, _ = oracle_dlsch(c1, l1, sb=sb, new_tb=False, i16=True)
     assert (res[0][0] == 0) == ok0 and not ok0, "rv0 alone is expected to fail at 16 dB"
     assert np.array_equal(res[0][4], pay0) and res[0][2] == noi0
     assert res[1][0] == 0 and ok1
