@@ -29,6 +29,11 @@ constexpr int BETA_W = 4;            // beta register window of the turbo kernel
 #define MI_TDEC_CK 4
 #endif
 constexpr int TDEC_CK = MI_TDEC_CK;  // beta checkpoint spacing: BETA_W (one window) or 2 BETA_W
+#ifndef MI_TDEC_CK_Q16
+#define MI_TDEC_CK_Q16 4
+#endif
+constexpr int TDEC_CK_Q16 = MI_TDEC_CK_Q16;   // same for the int16 decoder (fewer VGPRs per value)
+constexpr int TDEC_CK_MIN = TDEC_CK < TDEC_CK_Q16 ? TDEC_CK : TDEC_CK_Q16;   // scratch sizing
 constexpr float FILLER_LLR = -10000.0f;
 constexpr int RM_CHUNK = 128;        // circular-buffer positions per rate-dematch workgroup
 

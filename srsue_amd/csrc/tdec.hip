@@ -6,7 +6,7 @@
 namespace mi {
 
 template <bool Q16>
-__global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, float* __restrict__ scratch,
+__device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* __restrict__ scratch,
                                                  uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
                                                  uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
                                                  const MiGroupDesc* __restrict__ groups,
@@ -39,15 +39,39 @@ __global__ __launch_bounds__(64) void tdec_kernel(const float* __restrict__ sb, 
   cb_crc[li] = r.crc_ok;
 }
 
+// float decoder: 163 VGPRs -> 3 waves per SIMD by itself
+__global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ sb, float* __restrict__ scratch,
+                                                     uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
+                                                     uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
+                                                     const MiGroupDesc* __restrict__ groups,
+                                                     const MiLaneDesc* __restrict__ lanes,
+                                                     const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata,
+                                                     uint32_t max_its, uint32_t early_stop) {
+  tdec_group<false>(sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
+// int16 decoder: held to MI_TDEC_I16_WAVES waves per SIMD (3: <= 168 VGPRs), enough to keep every
+// group of a 12,500-subframe batch resident (2,540 waves on 1,024 SIMDs)
+#ifndef MI_TDEC_I16_WAVES
+#define MI_TDEC_I16_WAVES 3
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_TDEC_I16_WAVES)))
+void tdec_kernel_i16(const float* __restrict__ sb, float* __restrict__ scratch, uint8_t* __restrict__ dec,
+                     uint8_t* __restrict__ cb_bytes, uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
+                     const MiGroupDesc* __restrict__ groups, const MiLaneDesc* __restrict__ lanes,
+                     const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata, uint32_t max_its,
+                     uint32_t early_stop) {
+  tdec_group<true>(sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
+
 void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data,
                  uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16, hipStream_t st) {
   if (!n_groups) return;
   if (q16)
-    hipLaunchKernelGGL(tdec_kernel<true>, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
+    hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
                        groups, lanes, ktabs, ktab_data, max_its, early_stop);
   else
-    hipLaunchKernelGGL(tdec_kernel<false>, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
+    hipLaunchKernelGGL(tdec_kernel_gen, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
                        groups, lanes, ktabs, ktab_data, max_its, early_stop);
 }
 

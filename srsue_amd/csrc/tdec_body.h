@@ -26,6 +26,8 @@
 //    w = clamp(llr2 - xs2, +-1023).  Every metric is then an integer of magnitude < 2^15, which
 //    fp32 adds/subs/max represent exactly, so the same register code reproduces the int16 decoder.
 #pragma once
+#include <type_traits>
+
 #include "dl_common.h"
 
 #ifndef MI_HD
@@ -63,18 +65,6 @@ MI_HD inline float clampf(float x, float c) { return fminf(fmaxf(x, -c), c); }
 // decoder input as read from the softbuffer: raw float, or quantised in int16 mode
 template <bool Q16>
 MI_HD inline float qin(float x) { return Q16 ? clampf(rintf(x * I16_SCALE), I16_CI) : x; }
-// scratch streams (w, llr1, beta checkpoints): fp32, or int16 in int16 mode (every stored value is
-// an integer inside +-26598, see above), addressed by element index so both share the layout
-template <bool Q16>
-MI_HD inline float scr_ld(const float* scr, size_t i) {
-  if constexpr (Q16) return (float)reinterpret_cast<const int16_t*>(scr)[i];
-  else return scr[i];
-}
-template <bool Q16>
-MI_HD inline void scr_st(float* scr, size_t i, float v) {
-  if constexpr (Q16) reinterpret_cast<int16_t*>(scr)[i] = (int16_t)(int32_t)v;
-  else scr[i] = v;
-}
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
@@ -118,60 +108,86 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
   return llr;
 }
 
-// raw per-step inputs of one window: DEC1 {sys, p1, w}, DEC2 {llr1[pi], w[pi], p2}
-struct TdecWin { float a[BETA_W], b[BETA_W], c[BETA_W]; };
+// Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats, int16
+// scratch words as int) and converted only when the window is computed, so that the loads of the
+// next window stay in flight while the current one is computed.
+//   DEC1: s0 = systematic, s1 = parity 1, r0 = w            (FIRST: w = 0, not loaded)
+//   DEC2: s0 = parity 2,   r0 = llr1[pi], r1 = w[pi]         (FIRST: w = 0, not loaded)
+//   ck  : states 1..7 of the beta checkpoint closing the window (forward pass only)
+template <bool Q16>
+struct TdecWin {
+  using R = typename std::conditional<Q16, int32_t, float>::type;
+  float s0[BETA_W], s1[BETA_W];
+  R r0[BETA_W], r1[BETA_W];
+  R ck[7];
+};
+
+// scratch streams (w, llr1, beta checkpoints): fp32, or int16 in int16 mode (every stored value is
+// an integer inside +-26598, see above), addressed by element index so both share the layout
+template <bool Q16>
+MI_HD inline typename TdecWin<Q16>::R scr_raw(const float* scr, size_t i) {
+  if constexpr (Q16) return (int32_t)reinterpret_cast<const int16_t*>(scr)[i];
+  else return scr[i];
+}
+template <bool Q16>
+MI_HD inline float scr_cvt(typename TdecWin<Q16>::R x) { return (float)x; }
+template <bool Q16>
+MI_HD inline void scr_st(float* scr, size_t i, float v) {
+  if constexpr (Q16) reinterpret_cast<int16_t*>(scr)[i] = (int16_t)(int32_t)v;
+  else scr[i] = v;
+}
 
 template <bool DEC2, bool FIRST, bool Q16>
-MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin& r) {
+MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
   const uint32_t K = a.K;
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
-      r.a[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k] * LANES + lane]);
-      r.b[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane]);
-      r.c[i] = FIRST ? 0.0f : scr_ld<Q16>(a.scr, (size_t)k * LANES + lane);
+      r.s0[i] = a.sb[(size_t)a.pos[3 * k] * LANES + lane];
+      r.s1[i] = a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane];
+      r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, (size_t)k * LANES + lane);
     } else {
       const uint32_t pk = a.pi[k];
-      r.a[i] = scr_ld<Q16>(a.scr, (size_t)(K + pk) * LANES + lane);
-      r.b[i] = FIRST ? 0.0f : scr_ld<Q16>(a.scr, (size_t)pk * LANES + lane);
-      r.c[i] = qin<Q16>(a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane]);
+      r.s0[i] = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
+      r.r0[i] = scr_raw<Q16>(a.scr, (size_t)(K + pk) * LANES + lane);
+      r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, (size_t)pk * LANES + lane);
     }
   }
 }
 
-// decoder inputs (xs, xp) of step base+i from the raw window values (filler: known-zero bits)
-template <bool DEC2, bool Q16>
-MI_HD inline void tdec_xs_xp(const TdecWin& r, int i, uint32_t k, uint32_t F, float& xs, float& xp) {
-  constexpr float FILL = Q16 ? -I16_CI : FILLER_LLR;   // q(FILLER_LLR) = -511
-  if (!DEC2) {
-    const bool fill = k < F;
-    xs = (fill ? FILL : r.a[i]) + r.c[i];
-    xp = fill ? FILL : r.b[i];
-  } else {
-    xs = Q16 ? clampf(r.a[i] - r.b[i], I16_CX) : r.a[i] - r.b[i];
-    xp = r.c[i];
-  }
-}
-
-// beta checkpoint c (= beta at step c * CK) holds states 1..7 (state 0 is 0 after normalisation);
-// ck0 = element index of checkpoint 0 in the scratch stream.  Checkpoints are taken at k <= K, where
-// every state is reachable, so no -inf is ever stored.
+// beta checkpoint c (= beta at step c * BETA_W) holds states 1..7 (state 0 is 0 after
+// normalisation); ck0 = element index of checkpoint 0 in the scratch stream.  Checkpoints are
+// taken at k <= K, where every state is reachable, so no -inf is ever stored.
 template <bool Q16>
 MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
 #pragma unroll
   for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane, b[s]);
 }
 template <bool Q16>
-MI_HD inline void ck_load(const float* scr, size_t ck0, uint32_t c, int lane, float (&b)[8]) {
-  b[0] = 0.0f;
+MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane, TdecWin<Q16>& r) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) b[s] = scr_ld<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane);
+  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane);
+}
+
+// decoder inputs (xs, xp) of step base+i from the raw window (filler: known-zero bits)
+template <bool DEC2, bool Q16>
+MI_HD inline void tdec_xs_xp(const TdecWin<Q16>& r, int i, uint32_t k, uint32_t F, float& xs, float& xp) {
+  constexpr float FILL = Q16 ? -I16_CI : FILLER_LLR;   // q(FILLER_LLR) = -511
+  if (!DEC2) {
+    const bool fill = k < F;
+    xs = (fill ? FILL : qin<Q16>(r.s0[i])) + scr_cvt<Q16>(r.r0[i]);
+    xp = fill ? FILL : qin<Q16>(r.s1[i]);
+  } else {
+    const float d = scr_cvt<Q16>(r.r0[i]) - scr_cvt<Q16>(r.r1[i]);
+    xs = Q16 ? clampf(d, I16_CX) : d;
+    xp = qin<Q16>(r.s0[i]);
+  }
 }
 
 // per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
 template <bool DEC2, bool Q16>
-MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, float xs, const TdecWin& w, int i,
+MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, float xs, const TdecWin<Q16>& w, int i,
                             uint32_t& crc) {
   const uint32_t K = a.K;
   if (!DEC2) {
@@ -179,7 +195,8 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, 
   } else {
     const uint32_t pk = a.pi[k];
     scr_st<Q16>(a.scr, (size_t)pk * LANES + lane,                       // w update
-                Q16 ? clampf(llr - xs, I16_CW) : w.b[i] + (llr - w.a[i]));
+                Q16 ? clampf(llr - xs, I16_CW)
+                    : scr_cvt<Q16>(w.r1[i]) + (llr - scr_cvt<Q16>(w.r0[i])));
     const bool bit = llr > 0.0f;
     a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                     // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
@@ -187,15 +204,47 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, 
   }
 }
 
-// One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then
-// the K info steps, checkpointed every CK = 2 BETA_W steps.  Forward pass: per checkpoint interval
-// [a, a + CK) the beta values are recomputed from the checkpoint at a + CK as two register windows
-// of BETA_W steps (first half, then second half), alpha and the LLRs follow.
+// backward steps of one window (steps base+W-1 .. base); beta_0 is computed but never used
+template <bool DEC2, bool Q16>
+MI_HD inline void tdec_beta_window(const TdecWin<Q16>& w, uint32_t base, uint32_t F, float (&b)[8]) {
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    float xs, xp, nb[8];
+    tdec_xs_xp<DEC2, Q16>(w, i, base + i, F, xs, xp);
+    beta_step(b, xs, xp, nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+}
+
+// forward steps of one window: beta_{base+1..base+W} recomputed in registers from the window's
+// closing checkpoint, then alpha and the LLRs
+template <bool DEC2, bool Q16>
+MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base, float (&al)[8],
+                                    uint32_t& crc) {
+  float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(w, i, base + i, a.F, xs[i], xp[i]);
+  float bw[BETA_W][8];
+  bw[BETA_W - 1][0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = scr_cvt<Q16>(w.ck[s - 1]);
+#pragma unroll
+  for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++)
+    tdec_emit<DEC2, Q16>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, i, crc);
+}
+
+// One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then the
+// K info steps, checkpointed every BETA_W steps.  Forward pass: per window the beta values are
+// recomputed from the window's closing checkpoint, alpha and the LLRs follow.  Both passes are
+// unrolled by two windows with ping-pong buffers A/B: the loads of window j+1 are issued before
+// window j is computed and are first used one window later (K is a multiple of 8 for every LTE
+// code block size, so the window count K/4 is even and the loops have no remainder).
 template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
-  constexpr int CK = TDEC_CK;
-  static_assert(CK == BETA_W || CK == 2 * BETA_W, "checkpoint spacing");
-  const uint32_t K = a.K, F = a.F;
+  const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
   const size_t ck = (size_t)2 * K * LANES;  // beta checkpoints (element index)
   const float NINF = -INFINITY;
   float b[8];
@@ -217,107 +266,34 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
   }
-  ck_store<Q16>(a.scr, ck, K / CK, lane, b);
-  TdecWin cur, nxt;
-  tdec_load_window<DEC2, FIRST, Q16>(a, lane, K - BETA_W, cur);
-  for (int base = (int)K - BETA_W; base >= 0; base -= BETA_W) {
-    if (base >= BETA_W) tdec_load_window<DEC2, FIRST, Q16>(a, lane, (uint32_t)(base - BETA_W), nxt);
-#pragma unroll
-    for (int i = BETA_W - 1; i >= 0; i--) {
-      if (base + i == 0) break;   // beta_0 is never used
-      float xs, xp, nb[8];
-      tdec_xs_xp<DEC2, Q16>(cur, i, (uint32_t)(base + i), F, xs, xp);
-      beta_step(b, xs, xp, nb);
-#pragma unroll
-      for (int s = 0; s < 8; s++) b[s] = nb[s];
-    }
-    if (base > 0 && base % CK == 0) ck_store<Q16>(a.scr, ck, (uint32_t)base / CK, lane, b);
-    cur = nxt;
+  ck_store<Q16>(a.scr, ck, nw, lane, b);
+  TdecWin<Q16> A, B;
+  // ---- backward pass: windows nw-1 (A), nw-2 (B), ...
+  tdec_load_window<DEC2, FIRST, Q16>(a, lane, (nw - 1) * BETA_W, A);
+  for (uint32_t j = nw - 1;; j -= 2) {
+    tdec_load_window<DEC2, FIRST, Q16>(a, lane, (j - 1) * BETA_W, B);
+    tdec_beta_window<DEC2, Q16>(A, j * BETA_W, F, b);
+    ck_store<Q16>(a.scr, ck, j, lane, b);
+    const uint32_t jn = j >= 3 ? j - 2 : 1;   // last round: a harmless reload
+    tdec_load_window<DEC2, FIRST, Q16>(a, lane, jn * BETA_W, A);
+    tdec_beta_window<DEC2, Q16>(B, (j - 1) * BETA_W, F, b);
+    if (j == 1) break;
+    ck_store<Q16>(a.scr, ck, j - 1, lane, b);
   }
-  // ---- forward pass
+  // ---- forward pass: windows 0 (A), 1 (B), ...; window j closes with checkpoint j + 1
   float al[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
-  if constexpr (CK == BETA_W) {
-    float ckc[8], ckn[8];
-    tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, cur);
-    ck_load<Q16>(a.scr, ck, 1, lane, ckc);
-    for (uint32_t base = 0; base < K; base += BETA_W) {
-      if (base + BETA_W < K) {
-        tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + BETA_W, nxt);
-        ck_load<Q16>(a.scr, ck, base / BETA_W + 2, lane, ckn);
-      }
-      float xs[BETA_W], xp[BETA_W];
-#pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(cur, i, base + i, F, xs[i], xp[i]);
-      float bw[BETA_W][8];
-#pragma unroll
-      for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
-#pragma unroll
-      for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
-#pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2, Q16>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], cur, i, crc);
-      cur = nxt;
-#pragma unroll
-      for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
-    }
-    return;
-  } else {
-  TdecWin c0, c1, n0, n1;   // inputs of the current interval (two halves) and of the next one
-  float ckc[8], ckn[8];
-  tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, c0);
-  tdec_load_window<DEC2, FIRST, Q16>(a, lane, BETA_W, c1);
-  ck_load<Q16>(a.scr, ck, 1, lane, ckc);
-  n0 = c0;
-  n1 = c1;
-  for (uint32_t base = 0; base < K; base += CK) {
-    const bool more = base + CK < K;
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      // staggered prefetch: next interval's first half during this first half, its second half
-      // (and checkpoint) during this second half -- at most three windows live at once
-      if (more) {
-        if (half == 0) tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK, n0);
-        else {
-          tdec_load_window<DEC2, FIRST, Q16>(a, lane, base + CK + BETA_W, n1);
-          ck_load<Q16>(a.scr, ck, base / CK + 2, lane, ckn);
-        }
-      }
-      const TdecWin& w = half ? c1 : c0;
-      const uint32_t hb = base + (uint32_t)half * BETA_W;
-      float xs[BETA_W], xp[BETA_W];
-#pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(w, i, hb + i, F, xs[i], xp[i]);
-      float bw[BETA_W][8];
-      if (half == 0) {
-        // beta_{a+8} -> beta_{a+4} (discarded path), then the window beta_{a+1..a+4}
-        float t[8];
-#pragma unroll
-        for (int s = 0; s < 8; s++) t[s] = ckc[s];
-#pragma unroll
-        for (int i = BETA_W - 1; i >= 0; i--) {
-          float xs2, xp2, nb[8];
-          tdec_xs_xp<DEC2, Q16>(c1, i, base + BETA_W + i, F, xs2, xp2);
-          beta_step(t, xs2, xp2, nb);
-#pragma unroll
-          for (int s = 0; s < 8; s++) t[s] = nb[s];
-        }
-#pragma unroll
-        for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = t[s];
-      } else {
-#pragma unroll
-        for (int s = 0; s < 8; s++) bw[BETA_W - 1][s] = ckc[s];
-      }
-#pragma unroll
-      for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
-#pragma unroll
-      for (int i = 0; i < BETA_W; i++) tdec_emit<DEC2, Q16>(a, lane, hb + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, i, crc);
-    }
-    c0 = n0;
-    c1 = n1;
-#pragma unroll
-    for (int s = 0; s < 8; s++) ckc[s] = ckn[s];
-  }
+  tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, A);
+  ck_load_raw<Q16>(a.scr, ck, 1, lane, A);
+  for (uint32_t j = 0; j < nw; j += 2) {
+    tdec_load_window<DEC2, FIRST, Q16>(a, lane, (j + 1) * BETA_W, B);
+    ck_load_raw<Q16>(a.scr, ck, j + 2, lane, B);
+    tdec_alpha_window<DEC2, Q16>(a, lane, A, j * BETA_W, al, crc);
+    const uint32_t jn = j + 2 < nw ? j + 2 : nw - 1;   // last round: a harmless reload
+    tdec_load_window<DEC2, FIRST, Q16>(a, lane, jn * BETA_W, A);
+    ck_load_raw<Q16>(a.scr, ck, jn + 1, lane, A);
+    tdec_alpha_window<DEC2, Q16>(a, lane, B, (j + 1) * BETA_W, al, crc);
   }
 }
 

@@ -70,6 +70,10 @@ def test_ue_dl_harq_soft_combining():
     ok0, pay0, noi0, sb = oracle_dlsch(c0, l0, i16=True)
     ok1, pay1, noi1, _ = oracle_dlsch(c1, l1, sb=sb, new_tb=False, i16=True)
     assert (res[0][0] == 0) == ok0 and not ok0, "rv0 alone is expected to fail at 16 dB"
-    assert np.array_equal(res[0][4], pay0) and res[0][2] == noi0
+    # a failing decode is compared on CRC verdict and iterations only: the per-TTI path computes its own
+    # LLRs (within 1e-4 of the oracle's, not bit-identical) and the int16 quantiser turns a few of those
+    # last-bit differences into one-step input differences, which a non-converging decode does not hide.
+    # Decoder bit-exactness on identical LLRs, failing decodes included: test_gpu_parity.py.
+    assert res[0][2] == noi0
     assert res[1][0] == 0 and ok1
     assert np.array_equal(res[1][4], tb) and np.array_equal(res[1][4], pay1) and res[1][2] == noi1

@@ -16,7 +16,7 @@ from bench import kernel_src_hash  # noqa: E402
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.split("(")[0].split("<")[0]      # template arguments dropped: tdec_kernel<true> -> tdec_kernel
     return n.replace("void ", "").replace("mi::", "")
 
 
