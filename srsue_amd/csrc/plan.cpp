@@ -15,6 +15,25 @@ const char* last_error() { return g_err.c_str(); }
 
 static size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 
+void Plan::add_ktab(uint32_t K) {
+  auto& kp = kpos_cache[K];
+  if (kp.empty()) {
+    kp.resize(5);
+    cb_pos_table(K, kp[0]);
+    qpp_table(K, kp[1]);
+    crc_bit_table(K, 0x864CFBu, kp[2]);
+    crc_bit_table(K, 0x800063u, kp[3]);
+    cb_tix_table(K, kp[0], kp[4]);
+  }
+  MiKTab t{K, ncb_of(K), 0, 0, 0, 0, 0};
+  uint32_t* offs[5] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off, &t.tix_off};
+  for (int q = 0; q < 5; q++) {
+    *offs[q] = (uint32_t)kdata.size();
+    kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
+  }
+  ktabs.push_back(t);
+}
+
 int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   has_pdsch = with_pdsch;
   cb_K = cb_n = 0;
@@ -144,21 +163,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     if (kit == ktab_idx.end()) {
       kt = (uint32_t)ktabs.size();
       ktab_idx[K] = kt;
-      auto& kp = kpos_cache[K];
-      if (kp.empty()) {
-        kp.resize(4);
-        cb_pos_table(K, kp[0]);
-        qpp_table(K, kp[1]);
-        crc_bit_table(K, 0x864CFBu, kp[2]);
-        crc_bit_table(K, 0x800063u, kp[3]);
-      }
-      MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
-      uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
-      for (int q = 0; q < 4; q++) {
-        *offs[q] = (uint32_t)kdata.size();
-        kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
-      }
-      ktabs.push_back(t);
+      add_ktab(K);
     } else {
       kt = kit->second;
     }
@@ -271,21 +276,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   has_pdsch = false;
   cb_K = K;
   cb_n = ncb_req;
-  auto& kp = kpos_cache[K];
-  if (kp.empty()) {
-    kp.resize(4);
-    cb_pos_table(K, kp[0]);
-    qpp_table(K, kp[1]);
-    crc_bit_table(K, 0x864CFBu, kp[2]);
-    crc_bit_table(K, 0x800063u, kp[3]);
-  }
-  MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
-  uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
-  for (int q = 0; q < 4; q++) {
-    *offs[q] = (uint32_t)kdata.size();
-    kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
-  }
-  ktabs.push_back(t);
+  add_ktab(K);
   const uint32_t Ncb = ncb_of(K);
   max_ncb = Ncb;
   for (uint32_t g0 = 0; g0 < ncb_req; g0 += LANES) {

@@ -46,7 +46,8 @@ MI_HD constexpr int tr_prev_u(int sp, int j) {
 }
 
 struct TdecArgs {
-  const float* sb;        // group softbuffer [Ncb][64]
+  const float* sb;        // group softbuffer [Ncb][64]                         (float decoder)
+  const int16_t* q16;     // group quantised decoder inputs [3(K+4)][64], natural order (int16 decoder)
   const uint32_t* pos;    // [3(K+4)] circular-buffer position of decoder input t = 3k+i
   const uint32_t* pi;     // [K]
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
@@ -59,12 +60,6 @@ struct TdecArgs {
 
 struct TdecLaneResult { uint32_t its; uint32_t crc_ok; };
 
-// int16-mode constants (oracle/oracle.h OR_I16_*)
-constexpr float I16_SCALE = 32.0f, I16_CI = 511.0f, I16_CX = 1535.0f, I16_CW = 1023.0f;
-MI_HD inline float clampf(float x, float c) { return fminf(fmaxf(x, -c), c); }
-// decoder input as read from the softbuffer: raw float, or quantised in int16 mode
-template <bool Q16>
-MI_HD inline float qin(float x) { return Q16 ? clampf(rintf(x * I16_SCALE), I16_CI) : x; }
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
@@ -108,33 +103,78 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
   return llr;
 }
 
-// Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats, int16
-// scratch words as int) and converted only when the window is computed, so that the loads of the
-// next window stay in flight while the current one is computed.
+// Row access [row][64 lanes].  On the GPU every row stream is read/written with buffer instructions:
+// a scalar resource descriptor on the stream base, the row offset (wave-uniform) in soffset and the
+// lane's byte offset in one VGPR shared by all accesses -- no per-access 64-bit address arithmetic
+// and no address registers held across the pipelined windows (plain global pointers compile to
+// one v_lshl_add_u64 + a VGPR pair per load on gfx950).  The host emulation indexes directly.
+// Offsets are 32-bit: every stream is addressed from its group's base (< 6 MB).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+template <class T>
+__device__ inline T row_ld(const T* base, size_t row, int lane) {
+  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T)), vo = (uint32_t)lane * (uint32_t)sizeof(T);
+  if constexpr (sizeof(T) == 4)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), vo, so, 0));
+  else if constexpr (sizeof(T) == 2)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(row_rsrc(base), vo, so, 0));
+  else
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b8(row_rsrc(base), vo, so, 0));
+}
+template <class T>
+__device__ inline void row_st(T* base, size_t row, int lane, T v) {
+  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T)), vo = (uint32_t)lane * (uint32_t)sizeof(T);
+  if constexpr (sizeof(T) == 4)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), row_rsrc(base), vo, so, 0);
+  else if constexpr (sizeof(T) == 2)
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), row_rsrc(base), vo, so, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), row_rsrc(base), vo, so, 0);
+}
+#else
+template <class T>
+inline T row_ld(const T* base, size_t row, int lane) { return base[row * LANES + (uint32_t)lane]; }
+template <class T>
+inline void row_st(T* base, size_t row, int lane, T v) { base[row * LANES + (uint32_t)lane] = v; }
+#endif
+
+// Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats or
+// int16 words as int) and converted only when the window is computed, so that the loads of the next
+// window stay in flight while the current one is computed.
 //   DEC1: s0 = systematic, s1 = parity 1, r0 = w            (FIRST: w = 0, not loaded)
 //   DEC2: s0 = parity 2,   r0 = llr1[pi], r1 = w[pi]         (FIRST: w = 0, not loaded)
+//   (s0/s1: softbuffer floats via the position table, or int16 q[3k+i] rows in int16 mode)
 //   ck  : states 1..7 of the beta checkpoint closing the window (forward pass only)
 template <bool Q16>
 struct TdecWin {
   using R = typename std::conditional<Q16, int32_t, float>::type;
-  float s0[BETA_W], s1[BETA_W];
+  R s0[BETA_W], s1[BETA_W];
   R r0[BETA_W], r1[BETA_W];
   R ck[7];
 };
 
-// scratch streams (w, llr1, beta checkpoints): fp32, or int16 in int16 mode (every stored value is
-// an integer inside +-26598, see above), addressed by element index so both share the layout
+// scratch streams (w, llr1, beta checkpoints): fp32 rows, or int16 rows in int16 mode (every stored
+// value is an integer inside +-26598, see above); both views share the row layout
 template <bool Q16>
-MI_HD inline typename TdecWin<Q16>::R scr_raw(const float* scr, size_t i) {
-  if constexpr (Q16) return (int32_t)reinterpret_cast<const int16_t*>(scr)[i];
-  else return scr[i];
+MI_HD inline typename TdecWin<Q16>::R scr_raw(const float* scr, size_t row, int lane) {
+  if constexpr (Q16) return (int32_t)row_ld(reinterpret_cast<const int16_t*>(scr), row, lane);
+  else return row_ld(scr, row, lane);
 }
 template <bool Q16>
 MI_HD inline float scr_cvt(typename TdecWin<Q16>::R x) { return (float)x; }
 template <bool Q16>
-MI_HD inline void scr_st(float* scr, size_t i, float v) {
-  if constexpr (Q16) reinterpret_cast<int16_t*>(scr)[i] = (int16_t)(int32_t)v;
-  else scr[i] = v;
+MI_HD inline void scr_st(float* scr, size_t row, int lane, float v) {
+  if constexpr (Q16) row_st(reinterpret_cast<int16_t*>(scr), row, lane, (int16_t)(int32_t)v);
+  else row_st(scr, row, lane, v);
+}
+
+// raw decoder input t (= 3k + i): softbuffer float at position pos[t], or the int16 q row t
+template <bool Q16>
+MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t t, int lane) {
+  if constexpr (Q16) return (int32_t)row_ld(a.q16, t, lane);
+  else return row_ld(a.sb, a.pos[t], lane);
 }
 
 template <bool DEC2, bool FIRST, bool Q16>
@@ -144,30 +184,30 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
-      r.s0[i] = a.sb[(size_t)a.pos[3 * k] * LANES + lane];
-      r.s1[i] = a.sb[(size_t)a.pos[3 * k + 1] * LANES + lane];
-      r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, (size_t)k * LANES + lane);
+      r.s0[i] = dec_in<Q16>(a, 3 * k, lane);
+      r.s1[i] = dec_in<Q16>(a, 3 * k + 1, lane);
+      r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, k, lane);
     } else {
       const uint32_t pk = a.pi[k];
-      r.s0[i] = a.sb[(size_t)a.pos[3 * k + 2] * LANES + lane];
-      r.r0[i] = scr_raw<Q16>(a.scr, (size_t)(K + pk) * LANES + lane);
-      r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, (size_t)pk * LANES + lane);
+      r.s0[i] = dec_in<Q16>(a, 3 * k + 2, lane);
+      r.r0[i] = scr_raw<Q16>(a.scr, (size_t)K + pk, lane);
+      r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, pk, lane);
     }
   }
 }
 
 // beta checkpoint c (= beta at step c * BETA_W) holds states 1..7 (state 0 is 0 after
-// normalisation); ck0 = element index of checkpoint 0 in the scratch stream.  Checkpoints are
+// normalisation); ck0 = row of checkpoint 0 in the scratch stream.  Checkpoints are
 // taken at k <= K, where every state is reachable, so no -inf is ever stored.
 template <bool Q16>
 MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane, b[s]);
+  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + (size_t)c * 7 + (s - 1), lane, b[s]);
 }
 template <bool Q16>
 MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane, TdecWin<Q16>& r) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + ((size_t)c * 7 + (s - 1)) * LANES + lane);
+  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + (size_t)c * 7 + (s - 1), lane);
 }
 
 // decoder inputs (xs, xp) of step base+i from the raw window (filler: known-zero bits)
@@ -176,12 +216,12 @@ MI_HD inline void tdec_xs_xp(const TdecWin<Q16>& r, int i, uint32_t k, uint32_t 
   constexpr float FILL = Q16 ? -I16_CI : FILLER_LLR;   // q(FILLER_LLR) = -511
   if (!DEC2) {
     const bool fill = k < F;
-    xs = (fill ? FILL : qin<Q16>(r.s0[i])) + scr_cvt<Q16>(r.r0[i]);
-    xp = fill ? FILL : qin<Q16>(r.s1[i]);
+    xs = (fill ? FILL : scr_cvt<Q16>(r.s0[i])) + scr_cvt<Q16>(r.r0[i]);
+    xp = fill ? FILL : scr_cvt<Q16>(r.s1[i]);
   } else {
     const float d = scr_cvt<Q16>(r.r0[i]) - scr_cvt<Q16>(r.r1[i]);
     xs = Q16 ? clampf(d, I16_CX) : d;
-    xp = qin<Q16>(r.s0[i]);
+    xp = scr_cvt<Q16>(r.s0[i]);
   }
 }
 
@@ -191,14 +231,14 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, 
                             uint32_t& crc) {
   const uint32_t K = a.K;
   if (!DEC2) {
-    scr_st<Q16>(a.scr, (size_t)(K + k) * LANES + lane, llr);            // llr1
+    scr_st<Q16>(a.scr, (size_t)K + k, lane, llr);                       // llr1
   } else {
     const uint32_t pk = a.pi[k];
-    scr_st<Q16>(a.scr, (size_t)pk * LANES + lane,                       // w update
+    scr_st<Q16>(a.scr, pk, lane,                                         // w update
                 Q16 ? clampf(llr - xs, I16_CW)
                     : scr_cvt<Q16>(w.r1[i]) + (llr - scr_cvt<Q16>(w.r0[i])));
     const bool bit = llr > 0.0f;
-    a.dec[(size_t)pk * LANES + lane] = bit ? 1 : 0;                     // decision
+    row_st(a.dec, pk, lane, (uint8_t)(bit ? 1 : 0));                    // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
     crc ^= bit ? tt : 0u;                                               // CRC by linearity
   }
@@ -245,7 +285,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
-  const size_t ck = (size_t)2 * K * LANES;  // beta checkpoints (element index)
+  const size_t ck = (size_t)2 * K;  // beta checkpoints (row)
   const float NINF = -INFINITY;
   float b[8];
 #pragma unroll
@@ -255,8 +295,8 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
     float tx[3], tp[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      tx[j] = qin<Q16>(a.sb[(size_t)a.pos[t0 + 2 * j] * LANES + lane]);
-      tp[j] = qin<Q16>(a.sb[(size_t)a.pos[t0 + 2 * j + 1] * LANES + lane]);
+      tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0 + 2 * j, lane));
+      tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0 + 2 * j + 1, lane));
     }
 #pragma unroll
     for (int j = 2; j >= 0; j--) {
@@ -316,7 +356,7 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   for (uint32_t j = 0; j < a.K / 8; j++) {
     uint32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) v |= (uint32_t)a.dec[(size_t)(8 * j + q) * LANES + lane] << (7 - q);
+    for (int q = 0; q < 8; q++) v |= (uint32_t)row_ld(a.dec, 8 * j + q, lane) << (7 - q);
     a.cb_bytes[j] = (uint8_t)v;
   }
   return r;
