@@ -2,17 +2,14 @@
 // contract, BASELINE configs[0] = srsLTE turbodecoder_test): decoder inputs d[cb][3(K+4)] in
 // triplet order are written into the group-interleaved layout [N_cb][64] the turbo kernel reads,
 // through the same per-K position table (LDS transpose: coalesced reads of each code block's row,
-// 256-B coalesced row writes).  Int16 turbo mode also writes the quantised decoder-input stream
-// q[t][lane] (natural order) that the int16 decoder reads, as the rate de-matcher does.
+// 256-B coalesced row writes).
 #include "kernels.h"
 
 namespace mi {
 
 constexpr int SC_T = 64;   // decoder-input elements per workgroup
 
-template <bool Q16>
 __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict__ d, float* __restrict__ sb,
-                                                        float* __restrict__ scratch,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiKTab* __restrict__ ktabs,
                                                         const uint32_t* __restrict__ kdata, uint32_t n_cb) {
@@ -32,23 +29,13 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict
     const uint32_t t = t0 + i;
     if (t < T) sbg[(size_t)pos[t] * LANES + q] = tile[q][i];
   }
-  if (Q16) {
-    int16_t* q16 = reinterpret_cast<int16_t*>(scratch + g.scratch_off) + q16_elem_off(g.K);
-    for (uint32_t i = w; i < (uint32_t)SC_T; i += 4) {
-      const uint32_t t = t0 + i;
-      if (t < T) q16[(size_t)t * LANES + q] = (int16_t)q16f(tile[q][i]);
-    }
-  }
 }
 
-void launch_cb_scatter(const float* d, float* sb, float* scratch, const MiGroupDesc* groups, const MiKTab* ktabs,
-                       const uint32_t* kdata, uint32_t n_groups, uint32_t K, uint32_t n_cb, bool q16, hipStream_t st) {
+void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, const MiKTab* ktabs,
+                       const uint32_t* kdata, uint32_t n_groups, uint32_t K, uint32_t n_cb, hipStream_t st) {
   if (!n_groups) return;
   dim3 g((3 * (K + 4) + SC_T - 1) / SC_T, n_groups);
-  if (q16)
-    hipLaunchKernelGGL(cb_scatter_kernel<true>, g, dim3(256), 0, st, d, sb, scratch, groups, ktabs, kdata, n_cb);
-  else
-    hipLaunchKernelGGL(cb_scatter_kernel<false>, g, dim3(256), 0, st, d, sb, scratch, groups, ktabs, kdata, n_cb);
+  hipLaunchKernelGGL(cb_scatter_kernel, g, dim3(256), 0, st, d, sb, groups, ktabs, kdata, n_cb);
 }
 
 }  // namespace mi

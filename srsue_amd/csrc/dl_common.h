@@ -117,7 +117,6 @@ struct MiKTab {              // per K, device resident
   uint32_t pi_off;           // uint32 offset: pi[K]
   uint32_t crca_off;         // uint32 offset: CRC24A contribution of a single 1 at bit i, [K]
   uint32_t crcb_off;         // uint32 offset: same for CRC24B
-  uint32_t tix_off;          // uint32 offset: tix[Ncb] = t with pos[t] == p, or 0xffffffff (dummy bit)
 };
 
 namespace mi {
@@ -128,8 +127,8 @@ __host__ __device__ inline float clampf(float x, float c) { return fminf(fmaxf(x
 __host__ __device__ inline float q16f(float x) { return clampf(rintf(x * I16_SCALE), I16_CI); }
 // In int16 mode a group's scratch (sized in floats for the float decoder) holds int16 streams: w [K],
 // llr1 [K], beta checkpoints [7 (K/4 + 1)], each [..][64 lanes], then from this int16 element index
-// the quantised decoder inputs q [3 (K + 4)][64] in natural (triplet) order, written by the rate
-// de-matcher (or cb_scatter) and read by the decoder.  Fits: 3K + 12 <= 2K + 7 (K/4 + 1) for K >= 7.
+// the quantised decoder inputs q [3 (K + 4)][64] in natural (triplet) order, written by the decoder's
+// first pass from the softbuffer and read by every later pass.  Fits: 3K + 12 <= 2K + 7 (K/4 + 1) for K >= 7.
 __host__ __device__ inline size_t q16_elem_off(uint32_t K) {
   return (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
 }

@@ -39,10 +39,6 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
     }
     const MiKTab& kt = P.ktabs[g.ktab];
     int16_t* q16 = reinterpret_cast<int16_t*>(&scr[g.scratch_off]) + mi::q16_elem_off(g.K);
-    if (g_q16)
-      for (int lane = 0; lane < mi::LANES; lane++)
-        if (P.lanes[g.lane0 + lane].valid)
-          for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_q16_one(&P.kdata[kt.tix_off], &sb[g.sb_off], q16, p, lane);
     for (int lane = 0; lane < mi::LANES; lane++) {
       const uint32_t li = g.lane0 + lane;
       const MiLaneDesc& ld = P.lanes[li];

@@ -128,9 +128,8 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                    P.max_units, noise, st);
     mark(3);
     if (mask & (1u << MI_DL_STAGE_RM))
-      launch_rm_combine(d_e.as<float>(), sb, d_scratch.as<float>(), d_groups.as<MiGroupDesc>(),
-                        d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
-                        (uint32_t)P.groups.size(), P.max_ncb, q16(), st);
+      launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+                        d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC))
       launch_tdec(sb, d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
@@ -166,8 +165,8 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
     if (prof) (void)hipEventRecord(ev[i], st);
   };
   for (int i = 0; i <= MI_DL_STAGE_RM; i++) mark(i);
-  launch_cb_scatter(d_in, d_sb.as<float>(), d_scratch.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(),
-                    d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.cb_K, P.cb_n, q16(), st);
+  launch_cb_scatter(d_in, d_sb.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
+                    (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
   mark(MI_DL_STAGE_TDEC);
   launch_tdec(d_sb.as<float>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),

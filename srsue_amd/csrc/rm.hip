@@ -9,20 +9,14 @@
 // coalesced rows and the LLRs come from LDS (row stride RM_CHUNK + 1 floats: conflict-free column
 // reads).  No integer division in the loops: ranks are rebased with one conditional add.
 // Repetition beyond N_v (E > N_v, low code rates) adds the further copies from HBM in order.
-// Int16 turbo mode (Q16): each combined position is also quantised into the decoder-input stream
-// q[t][lane] (t = the decoder index of position p, per-K table tix) in the group's scratch, so the
-// decoder reads 2-byte rows in natural order instead of gathering fp32 softbuffer rows.
 #include "kernels.h"
 #include "rm_body.h"
 
 namespace mi {
 
-template <bool Q16>
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
-                                                        float* __restrict__ scratch,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
-                                                        const MiKTab* __restrict__ ktabs,
                                                         const uint32_t* __restrict__ kdata) {
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
@@ -77,8 +71,6 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   const uint32_t ra = ch[pa / RM_CHUNK];
   const uint32_t j0 = s_j0[lane], nv = ld.Nv, E = ld.E;
   const bool rep = E > nv;
-  const uint32_t* tix = kdata + ktabs[g.ktab].tix_off;
-  int16_t* q16 = reinterpret_cast<int16_t*>(scratch + g.scratch_off) + q16_elem_off(g.K);
   constexpr int NP = RM_CHUNK / 4;
   int32_t rk[NP];
   float old[NP];
@@ -102,22 +94,15 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
         for (j += nv; j < E; j += nv) v = v + e[ld.e_off + j];
     }
     sbg[(size_t)p * LANES + lane] = v;
-    if (Q16) {
-      const uint32_t t = tix[p];
-      if (t != 0xffffffffu) q16[(size_t)t * LANES + lane] = (int16_t)q16f(v);
-    }
   }
 }
 
-void launch_rm_combine(const float* e, float* sb, float* scratch, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                       const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, bool q16,
+void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
+                       const MiKTab* /*ktabs*/, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
                        hipStream_t st) {
   if (!n_groups) return;
   dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
-  if (q16)
-    hipLaunchKernelGGL(rm_combine_kernel<true>, g, dim3(256), 0, st, e, sb, scratch, groups, lanes, ktabs, ktab_data);
-  else
-    hipLaunchKernelGGL(rm_combine_kernel<false>, g, dim3(256), 0, st, e, sb, scratch, groups, lanes, ktabs, ktab_data);
+  hipLaunchKernelGGL(rm_combine_kernel, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data);
 }
 
 }  // namespace mi

@@ -27,11 +27,4 @@ MI_HD inline void rm_combine_one(const MiLaneDesc& ld, const int32_t* rank, cons
   sbg[(size_t)p * LANES + lane] = v;
 }
 
-// int16 turbo mode: the combined value of position p also lands quantised in the decoder-input
-// stream q[t][lane], t = tix[p] (rm.hip does this right after the combine)
-MI_HD inline void rm_q16_one(const uint32_t* tix, const float* sbg, int16_t* q16, uint32_t p, int lane) {
-  const uint32_t t = tix[p];
-  if (t != 0xffffffffu) q16[(size_t)t * LANES + lane] = (int16_t)q16f(sbg[(size_t)p * LANES + lane]);
-}
-
 }  // namespace mi

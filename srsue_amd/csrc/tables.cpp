@@ -166,11 +166,6 @@ void cb_pos_table(uint32_t K, std::vector<uint32_t>& pos) {
   }
 }
 
-void cb_tix_table(uint32_t K, const std::vector<uint32_t>& pos, std::vector<uint32_t>& tix) {
-  tix.assign(ncb_of(K), 0xffffffffu);
-  for (uint32_t t = 0; t < pos.size(); t++) tix[pos[t]] = t;
-}
-
 void cb_rank_table(uint32_t K, uint32_t F, std::vector<int32_t>& rank, uint32_t* Nv) {
   const uint32_t D = K + 4, R = (D + 31) / 32, KP = 32 * R, ND = KP - D, Ncb = 3 * KP;
   std::vector<uint8_t> null(Ncb, 0);

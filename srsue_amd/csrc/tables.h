@@ -18,8 +18,6 @@ uint32_t k0_of(uint32_t K, uint32_t rv);
 // circular-buffer maps of one code block size: pos[t] for decoder input t = 3k + i, and the rank
 // table (number of non-null positions before p, -1 for <NULL>) for F filler bits.
 void cb_pos_table(uint32_t K, std::vector<uint32_t>& pos);
-// inverse of cb_pos_table over the circular buffer: tix[p] = t with pos[t] == p, 0xffffffff otherwise
-void cb_tix_table(uint32_t K, const std::vector<uint32_t>& pos, std::vector<uint32_t>& tix);
 void cb_rank_table(uint32_t K, uint32_t F, std::vector<int32_t>& rank, uint32_t* Nv);
 void qpp_table(uint32_t K, std::vector<uint32_t>& pi);
 // CRC register of a K-bit message holding a single 1 at bit i (zero init): x^(K-1-i+24) mod g

@@ -22,7 +22,7 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
   const MiKTab kt = ktabs[g.ktab];
   TdecArgs a;
   a.sb = sb + g.sb_off;
-  a.q16 = reinterpret_cast<const int16_t*>(scratch + g.scratch_off) + q16_elem_off(g.K);
+  a.q16 = reinterpret_cast<int16_t*>(scratch + g.scratch_off) + q16_elem_off(g.K);
   a.pos = kdata + kt.pos_off;
   a.pi = kdata + kt.pi_off;
   a.crc_a = kdata + kt.crca_off;

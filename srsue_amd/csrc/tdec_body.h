@@ -47,7 +47,8 @@ MI_HD constexpr int tr_prev_u(int sp, int j) {
 
 struct TdecArgs {
   const float* sb;        // group softbuffer [Ncb][64]                         (float decoder)
-  const int16_t* q16;     // group quantised decoder inputs [3(K+4)][64], natural order (int16 decoder)
+  int16_t* q16;           // group quantised decoder inputs [3(K+4)][64], natural order (int16 decoder;
+                          // written by the first pass of the first iteration, read by all others)
   const uint32_t* pos;    // [3(K+4)] circular-buffer position of decoder input t = 3k+i
   const uint32_t* pi;     // [K]
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
@@ -113,9 +114,12 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
 __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
+// row = wave-uniform row (soffset), crow = compile-time row delta (folded into the instruction's
+// immediate offset): consecutive rows of one window share a single soffset SGPR
 template <class T>
-__device__ inline T row_ld(const T* base, size_t row, int lane) {
-  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T)), vo = (uint32_t)lane * (uint32_t)sizeof(T);
+__device__ inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
+  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
+  const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
   if constexpr (sizeof(T) == 4)
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), vo, so, 0));
   else if constexpr (sizeof(T) == 2)
@@ -124,8 +128,9 @@ __device__ inline T row_ld(const T* base, size_t row, int lane) {
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b8(row_rsrc(base), vo, so, 0));
 }
 template <class T>
-__device__ inline void row_st(T* base, size_t row, int lane, T v) {
-  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T)), vo = (uint32_t)lane * (uint32_t)sizeof(T);
+__device__ inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
+  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
+  const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
   if constexpr (sizeof(T) == 4)
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), row_rsrc(base), vo, so, 0);
   else if constexpr (sizeof(T) == 2)
@@ -135,9 +140,13 @@ __device__ inline void row_st(T* base, size_t row, int lane, T v) {
 }
 #else
 template <class T>
-inline T row_ld(const T* base, size_t row, int lane) { return base[row * LANES + (uint32_t)lane]; }
+inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
+  return base[(row + crow) * LANES + (uint32_t)lane];
+}
 template <class T>
-inline void row_st(T* base, size_t row, int lane, T v) { base[row * LANES + (uint32_t)lane] = v; }
+inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
+  base[(row + crow) * LANES + (uint32_t)lane] = v;
+}
 #endif
 
 // Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats or
@@ -147,52 +156,75 @@ inline void row_st(T* base, size_t row, int lane, T v) { base[row * LANES + (uin
 //   DEC2: s0 = parity 2,   r0 = llr1[pi], r1 = w[pi]         (FIRST: w = 0, not loaded)
 //   (s0/s1: softbuffer floats via the position table, or int16 q[3k+i] rows in int16 mode)
 //   ck  : states 1..7 of the beta checkpoint closing the window (forward pass only)
+//   f0..f2: the three softbuffer inputs of a step, in the int16 decoder's first pass only
 template <bool Q16>
 struct TdecWin {
   using R = typename std::conditional<Q16, int32_t, float>::type;
   R s0[BETA_W], s1[BETA_W];
   R r0[BETA_W], r1[BETA_W];
   R ck[7];
+  float f0[BETA_W], f1[BETA_W], f2[BETA_W];
 };
 
 // scratch streams (w, llr1, beta checkpoints): fp32 rows, or int16 rows in int16 mode (every stored
 // value is an integer inside +-26598, see above); both views share the row layout
+// element view of scratch row 0 of a stream starting `row0` rows into the scratch
 template <bool Q16>
-MI_HD inline typename TdecWin<Q16>::R scr_raw(const float* scr, size_t row, int lane) {
-  if constexpr (Q16) return (int32_t)row_ld(reinterpret_cast<const int16_t*>(scr), row, lane);
-  else return row_ld(scr, row, lane);
+MI_HD inline const float* scr_at(const float* scr, size_t row0) {
+  if constexpr (Q16) return reinterpret_cast<const float*>(reinterpret_cast<const int16_t*>(scr) + row0 * LANES);
+  else return scr + row0 * LANES;
+}
+template <bool Q16>
+MI_HD inline float* scr_at(float* scr, size_t row0) { return const_cast<float*>(scr_at<Q16>((const float*)scr, row0)); }
+template <bool Q16>
+MI_HD inline typename TdecWin<Q16>::R scr_raw(const float* scr, size_t row, int lane, uint32_t crow = 0) {
+  if constexpr (Q16) return (int32_t)row_ld(reinterpret_cast<const int16_t*>(scr), row, lane, crow);
+  else return row_ld(scr, row, lane, crow);
 }
 template <bool Q16>
 MI_HD inline float scr_cvt(typename TdecWin<Q16>::R x) { return (float)x; }
 template <bool Q16>
-MI_HD inline void scr_st(float* scr, size_t row, int lane, float v) {
-  if constexpr (Q16) row_st(reinterpret_cast<int16_t*>(scr), row, lane, (int16_t)(int32_t)v);
-  else row_st(scr, row, lane, v);
+MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t crow = 0) {
+  if constexpr (Q16) row_st(reinterpret_cast<int16_t*>(scr), row, lane, (int16_t)(int32_t)v, crow);
+  else row_st(scr, row, lane, v, crow);
 }
 
 // raw decoder input t (= 3k + i): softbuffer float at position pos[t], or the int16 q row t
 template <bool Q16>
-MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t t, int lane) {
-  if constexpr (Q16) return (int32_t)row_ld(a.q16, t, lane);
-  else return row_ld(a.sb, a.pos[t], lane);
+MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t t0, uint32_t dt, int lane) {
+  if constexpr (Q16) return (int32_t)row_ld(a.q16, t0, lane, dt);
+  else return row_ld(a.sb, a.pos[t0 + dt], lane);
 }
 
 template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
-  const uint32_t K = a.K;
+  const float* llr1 = scr_at<Q16>(a.scr, a.K);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
-      r.s0[i] = dec_in<Q16>(a, 3 * k, lane);
-      r.s1[i] = dec_in<Q16>(a, 3 * k + 1, lane);
-      r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, k, lane);
+      r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i, lane);
+      r.s1[i] = dec_in<Q16>(a, 3 * base, 3 * i + 1, lane);
+      r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
     } else {
       const uint32_t pk = a.pi[k];
-      r.s0[i] = dec_in<Q16>(a, 3 * k + 2, lane);
-      r.r0[i] = scr_raw<Q16>(a.scr, (size_t)K + pk, lane);
+      r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i + 2, lane);
+      r.r0[i] = scr_raw<Q16>(llr1, pk, lane);
       r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, pk, lane);
     }
+  }
+}
+
+// int16 decoder, first pass (DEC1 backward, iteration 0): the three softbuffer inputs of each step
+// through the position table; the window computation quantises them and writes the q rows
+template <bool Q16>
+MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    const uint32_t t = 3 * (base + i);
+    r.f0[i] = row_ld(a.sb, a.pos[t], lane);
+    r.f1[i] = row_ld(a.sb, a.pos[t + 1], lane);
+    r.f2[i] = row_ld(a.sb, a.pos[t + 2], lane);
   }
 }
 
@@ -202,12 +234,12 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
 template <bool Q16>
 MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + (size_t)c * 7 + (s - 1), lane, b[s]);
+  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + (size_t)c * 7, lane, b[s], s - 1);
 }
 template <bool Q16>
 MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane, TdecWin<Q16>& r) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + (size_t)c * 7 + (s - 1), lane);
+  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + (size_t)c * 7, lane, s - 1);
 }
 
 // decoder inputs (xs, xp) of step base+i from the raw window (filler: known-zero bits)
@@ -227,11 +259,11 @@ MI_HD inline void tdec_xs_xp(const TdecWin<Q16>& r, int i, uint32_t k, uint32_t 
 
 // per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
 template <bool DEC2, bool Q16>
-MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t k, float llr, float xs, const TdecWin<Q16>& w, int i,
-                            uint32_t& crc) {
-  const uint32_t K = a.K;
+MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, float llr, float xs,
+                            const TdecWin<Q16>& w, uint32_t& crc) {
+  const uint32_t k = base + i;
   if (!DEC2) {
-    scr_st<Q16>(a.scr, (size_t)K + k, lane, llr);                       // llr1
+    scr_st<Q16>(scr_at<Q16>(a.scr, a.K), base, lane, llr, i);           // llr1
   } else {
     const uint32_t pk = a.pi[k];
     scr_st<Q16>(a.scr, pk, lane,                                         // w update
@@ -257,6 +289,26 @@ MI_HD inline void tdec_beta_window(const TdecWin<Q16>& w, uint32_t base, uint32_
   }
 }
 
+// the same for the int16 decoder's first pass: quantise the window's softbuffer inputs, store them as
+// q rows 3k..3k+2 (read by every later pass), then the backward steps (w = 0 in iteration 0)
+template <bool Q16>
+MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+                                       float (&b)[8]) {
+  constexpr float FILL = -I16_CI;
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    const float q0 = q16f(w.f0[i]), q1 = q16f(w.f1[i]), q2 = q16f(w.f2[i]);
+    row_st(a.q16, 3 * base, lane, (int16_t)q0, 3 * i);
+    row_st(a.q16, 3 * base, lane, (int16_t)q1, 3 * i + 1);
+    row_st(a.q16, 3 * base, lane, (int16_t)q2, 3 * i + 2);
+    const bool fill = base + i < a.F;
+    float nb[8];
+    beta_step(b, fill ? FILL : q0, fill ? FILL : q1, nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+}
+
 // forward steps of one window: beta_{base+1..base+W} recomputed in registers from the window's
 // closing checkpoint, then alpha and the LLRs
 template <bool DEC2, bool Q16>
@@ -273,7 +325,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
   for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++)
-    tdec_emit<DEC2, Q16>(a, lane, base + i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, i, crc);
+    tdec_emit<DEC2, Q16>(a, lane, base, i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, crc);
 }
 
 // One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then the
@@ -284,6 +336,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 // code block size, so the window count K/4 is even and the loops have no remainder).
 template <bool DEC2, bool FIRST, bool Q16>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
+  constexpr bool MKQ = Q16 && FIRST && !DEC2;   // int16 decoder's first pass: softbuffer -> q rows
   const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
   const size_t ck = (size_t)2 * K;  // beta checkpoints (row)
   const float NINF = -INFINITY;
@@ -293,10 +346,21 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   {
     const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
     float tx[3], tp[3];
+    if constexpr (MKQ) {
+      // all 12 tail inputs (both constituent codes) quantised into their q rows
+      float tq[12];
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-      tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0 + 2 * j, lane));
-      tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0 + 2 * j + 1, lane));
+      for (int j = 0; j < 12; j++) tq[j] = q16f(row_ld(a.sb, a.pos[3 * K + j], lane));
+#pragma unroll
+      for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
+#pragma unroll
+      for (int j = 0; j < 3; j++) { tx[j] = tq[2 * j]; tp[j] = tq[2 * j + 1]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0, 2 * j, lane));
+        tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0, 2 * j + 1, lane));
+      }
     }
 #pragma unroll
     for (int j = 2; j >= 0; j--) {
@@ -309,14 +373,21 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   ck_store<Q16>(a.scr, ck, nw, lane, b);
   TdecWin<Q16> A, B;
   // ---- backward pass: windows nw-1 (A), nw-2 (B), ...
-  tdec_load_window<DEC2, FIRST, Q16>(a, lane, (nw - 1) * BETA_W, A);
+  auto load = [&](uint32_t w, TdecWin<Q16>& r) {
+    if constexpr (MKQ) tdec_load_window_sb<Q16>(a, lane, w * BETA_W, r);
+    else tdec_load_window<DEC2, FIRST, Q16>(a, lane, w * BETA_W, r);
+  };
+  auto beta = [&](const TdecWin<Q16>& r, uint32_t w) {
+    if constexpr (MKQ) tdec_beta_window_mkq<Q16>(a, lane, r, w * BETA_W, b);
+    else tdec_beta_window<DEC2, Q16>(r, w * BETA_W, F, b);
+  };
+  load(nw - 1, A);
   for (uint32_t j = nw - 1;; j -= 2) {
-    tdec_load_window<DEC2, FIRST, Q16>(a, lane, (j - 1) * BETA_W, B);
-    tdec_beta_window<DEC2, Q16>(A, j * BETA_W, F, b);
+    load(j - 1, B);
+    beta(A, j);
     ck_store<Q16>(a.scr, ck, j, lane, b);
-    const uint32_t jn = j >= 3 ? j - 2 : 1;   // last round: a harmless reload
-    tdec_load_window<DEC2, FIRST, Q16>(a, lane, jn * BETA_W, A);
-    tdec_beta_window<DEC2, Q16>(B, (j - 1) * BETA_W, F, b);
+    load(j >= 3 ? j - 2 : 1, A);   // last round: a harmless reload
+    beta(B, j - 1);
     if (j == 1) break;
     ck_store<Q16>(a.scr, ck, j - 1, lane, b);
   }
