@@ -110,7 +110,10 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
 // and no address registers held across the pipelined windows (plain global pointers compile to
 // one v_lshl_add_u64 + a VGPR pair per load on gfx950).  The host emulation indexes directly.
 // Offsets are 32-bit: every stream is addressed from its group's base (< 6 MB).
-#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef MI_ROW_BUFFER
+#define MI_ROW_BUFFER 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
 __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
@@ -140,13 +143,25 @@ __device__ inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow 
 }
 #else
 template <class T>
-inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
+MI_HD inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
   return base[(row + crow) * LANES + (uint32_t)lane];
 }
 template <class T>
-inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
+MI_HD inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
   base[(row + crow) * LANES + (uint32_t)lane] = v;
 }
+#endif
+
+// Where the int16 decoder reads its channel inputs from (the float decoder always uses SRC_SB):
+//   SRC_SB  the fp32 softbuffer through the position table, quantised at use
+//   SRC_MKQ (DEC1 only) the backward pass reads the softbuffer, quantises all three streams and
+//           writes the q rows; the forward pass reads the q rows
+//   SRC_Q   the int16 q rows [3(K+4)][64] (2-byte rows, natural order, no position table)
+// The q rows are created in iteration MI_TDEC_MKQ_IT (1 = only once a second iteration is needed:
+// a one-iteration decode never pays for them).
+enum { SRC_SB = 0, SRC_MKQ = 1, SRC_Q = 2 };
+#ifndef MI_TDEC_MKQ_IT
+#define MI_TDEC_MKQ_IT 1
 #endif
 
 // Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats or
@@ -196,28 +211,35 @@ MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t t0, uin
   else return row_ld(a.sb, a.pos[t0 + dt], lane);
 }
 
-template <bool DEC2, bool FIRST, bool Q16>
+template <bool DEC2, bool FIRST, bool Q16, bool SQ>
 MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
   const float* llr1 = scr_at<Q16>(a.scr, a.K);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
-      r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i, lane);
-      r.s1[i] = dec_in<Q16>(a, 3 * base, 3 * i + 1, lane);
+      if constexpr (Q16 && !SQ) {
+        r.f0[i] = row_ld(a.sb, a.pos[3 * k], lane);
+        r.f1[i] = row_ld(a.sb, a.pos[3 * k + 1], lane);
+      } else {
+        r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i, lane);
+        r.s1[i] = dec_in<Q16>(a, 3 * base, 3 * i + 1, lane);
+      }
       r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
     } else {
       const uint32_t pk = a.pi[k];
-      r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i + 2, lane);
+      if constexpr (Q16 && !SQ) r.f0[i] = row_ld(a.sb, a.pos[3 * k + 2], lane);
+      else r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i + 2, lane);
       r.r0[i] = scr_raw<Q16>(llr1, pk, lane);
       r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, pk, lane);
     }
   }
 }
 
-// int16 decoder, first pass (DEC1 backward, iteration 0): the three softbuffer inputs of each step
-// through the position table; the window computation quantises them and writes the q rows
-template <bool Q16>
+// int16 decoder, q-creating pass (DEC1 backward of iteration MI_TDEC_MKQ_IT): the three softbuffer
+// inputs of each step through the position table (+ w); the window computation quantises them and
+// writes the q rows
+template <bool FIRST, bool Q16>
 MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
@@ -225,6 +247,7 @@ MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base
     r.f0[i] = row_ld(a.sb, a.pos[t], lane);
     r.f1[i] = row_ld(a.sb, a.pos[t + 1], lane);
     r.f2[i] = row_ld(a.sb, a.pos[t + 2], lane);
+    r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
   }
 }
 
@@ -243,17 +266,27 @@ MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane
 }
 
 // decoder inputs (xs, xp) of step base+i from the raw window (filler: known-zero bits)
-template <bool DEC2, bool Q16>
+template <bool Q16, bool SQ>
+MI_HD inline float chan0(const TdecWin<Q16>& r, int i) {
+  if constexpr (Q16 && !SQ) return q16f(r.f0[i]);
+  else return scr_cvt<Q16>(r.s0[i]);
+}
+template <bool Q16, bool SQ>
+MI_HD inline float chan1(const TdecWin<Q16>& r, int i) {
+  if constexpr (Q16 && !SQ) return q16f(r.f1[i]);
+  else return scr_cvt<Q16>(r.s1[i]);
+}
+template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_xs_xp(const TdecWin<Q16>& r, int i, uint32_t k, uint32_t F, float& xs, float& xp) {
   constexpr float FILL = Q16 ? -I16_CI : FILLER_LLR;   // q(FILLER_LLR) = -511
   if (!DEC2) {
     const bool fill = k < F;
-    xs = (fill ? FILL : scr_cvt<Q16>(r.s0[i])) + scr_cvt<Q16>(r.r0[i]);
-    xp = fill ? FILL : scr_cvt<Q16>(r.s1[i]);
+    xs = (fill ? FILL : chan0<Q16, SQ>(r, i)) + scr_cvt<Q16>(r.r0[i]);
+    xp = fill ? FILL : chan1<Q16, SQ>(r, i);
   } else {
     const float d = scr_cvt<Q16>(r.r0[i]) - scr_cvt<Q16>(r.r1[i]);
     xs = Q16 ? clampf(d, I16_CX) : d;
-    xp = scr_cvt<Q16>(r.s0[i]);
+    xp = chan0<Q16, SQ>(r, i);
   }
 }
 
@@ -277,12 +310,12 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, f
 }
 
 // backward steps of one window (steps base+W-1 .. base); beta_0 is computed but never used
-template <bool DEC2, bool Q16>
+template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_beta_window(const TdecWin<Q16>& w, uint32_t base, uint32_t F, float (&b)[8]) {
 #pragma unroll
   for (int i = BETA_W - 1; i >= 0; i--) {
     float xs, xp, nb[8];
-    tdec_xs_xp<DEC2, Q16>(w, i, base + i, F, xs, xp);
+    tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, F, xs, xp);
     beta_step(b, xs, xp, nb);
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
@@ -290,7 +323,7 @@ MI_HD inline void tdec_beta_window(const TdecWin<Q16>& w, uint32_t base, uint32_
 }
 
 // the same for the int16 decoder's first pass: quantise the window's softbuffer inputs, store them as
-// q rows 3k..3k+2 (read by every later pass), then the backward steps (w = 0 in iteration 0)
+// q rows 3k..3k+2 (read by every later pass), then the backward steps
 template <bool Q16>
 MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                        float (&b)[8]) {
@@ -303,7 +336,7 @@ MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWi
     row_st(a.q16, 3 * base, lane, (int16_t)q2, 3 * i + 2);
     const bool fill = base + i < a.F;
     float nb[8];
-    beta_step(b, fill ? FILL : q0, fill ? FILL : q1, nb);
+    beta_step(b, (fill ? FILL : q0) + scr_cvt<Q16>(w.r0[i]), fill ? FILL : q1, nb);
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
   }
@@ -311,12 +344,12 @@ MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWi
 
 // forward steps of one window: beta_{base+1..base+W} recomputed in registers from the window's
 // closing checkpoint, then alpha and the LLRs
-template <bool DEC2, bool Q16>
+template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base, float (&al)[8],
                                     uint32_t& crc) {
   float xs[BETA_W], xp[BETA_W];
 #pragma unroll
-  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16>(w, i, base + i, a.F, xs[i], xp[i]);
+  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
   float bw[BETA_W][8];
   bw[BETA_W - 1][0] = 0.0f;
 #pragma unroll
@@ -334,9 +367,11 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 // unrolled by two windows with ping-pong buffers A/B: the loads of window j+1 are issued before
 // window j is computed and are first used one window later (K is a multiple of 8 for every LTE
 // code block size, so the window count K/4 is even and the loops have no remainder).
-template <bool DEC2, bool FIRST, bool Q16>
+template <bool DEC2, bool FIRST, bool Q16, int SRC>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
-  constexpr bool MKQ = Q16 && FIRST && !DEC2;   // int16 decoder's first pass: softbuffer -> q rows
+  constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;   // backward pass: softbuffer -> q rows
+  constexpr bool SQB = Q16 && SRC == SRC_Q;              // backward pass reads q rows
+  constexpr bool SQF = Q16 && SRC != SRC_SB;             // forward pass reads q rows
   const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
   const size_t ck = (size_t)2 * K;  // beta checkpoints (row)
   const float NINF = -INFINITY;
@@ -355,6 +390,12 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
       for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
 #pragma unroll
       for (int j = 0; j < 3; j++) { tx[j] = tq[2 * j]; tp[j] = tq[2 * j + 1]; }
+    } else if constexpr (Q16 && !SQB) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        tx[j] = q16f(row_ld(a.sb, a.pos[t0 + 2 * j], lane));
+        tp[j] = q16f(row_ld(a.sb, a.pos[t0 + 2 * j + 1], lane));
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 3; j++) {
@@ -374,12 +415,12 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   TdecWin<Q16> A, B;
   // ---- backward pass: windows nw-1 (A), nw-2 (B), ...
   auto load = [&](uint32_t w, TdecWin<Q16>& r) {
-    if constexpr (MKQ) tdec_load_window_sb<Q16>(a, lane, w * BETA_W, r);
-    else tdec_load_window<DEC2, FIRST, Q16>(a, lane, w * BETA_W, r);
+    if constexpr (MKQ) tdec_load_window_sb<FIRST, Q16>(a, lane, w * BETA_W, r);
+    else tdec_load_window<DEC2, FIRST, Q16, SQB>(a, lane, w * BETA_W, r);
   };
   auto beta = [&](const TdecWin<Q16>& r, uint32_t w) {
     if constexpr (MKQ) tdec_beta_window_mkq<Q16>(a, lane, r, w * BETA_W, b);
-    else tdec_beta_window<DEC2, Q16>(r, w * BETA_W, F, b);
+    else tdec_beta_window<DEC2, Q16, SQB>(r, w * BETA_W, F, b);
   };
   load(nw - 1, A);
   for (uint32_t j = nw - 1;; j -= 2) {
@@ -395,16 +436,16 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
   float al[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
-  tdec_load_window<DEC2, FIRST, Q16>(a, lane, 0, A);
+  tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, 0, A);
   ck_load_raw<Q16>(a.scr, ck, 1, lane, A);
   for (uint32_t j = 0; j < nw; j += 2) {
-    tdec_load_window<DEC2, FIRST, Q16>(a, lane, (j + 1) * BETA_W, B);
+    tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, (j + 1) * BETA_W, B);
     ck_load_raw<Q16>(a.scr, ck, j + 2, lane, B);
-    tdec_alpha_window<DEC2, Q16>(a, lane, A, j * BETA_W, al, crc);
+    tdec_alpha_window<DEC2, Q16, SQF>(a, lane, A, j * BETA_W, al, crc);
     const uint32_t jn = j + 2 < nw ? j + 2 : nw - 1;   // last round: a harmless reload
-    tdec_load_window<DEC2, FIRST, Q16>(a, lane, jn * BETA_W, A);
+    tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, jn * BETA_W, A);
     ck_load_raw<Q16>(a.scr, ck, jn + 1, lane, A);
-    tdec_alpha_window<DEC2, Q16>(a, lane, B, (j + 1) * BETA_W, al, crc);
+    tdec_alpha_window<DEC2, Q16, SQF>(a, lane, B, (j + 1) * BETA_W, al, crc);
   }
 }
 
@@ -413,12 +454,24 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
     uint32_t crc = 0;
+    constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;   // iteration creating the q rows
     if (it == 0) {
-      tdec_half<false, true, Q16>(a, lane, crc);
-      tdec_half<true, true, Q16>(a, lane, crc);
+      if (MK == 0) {
+        tdec_half<false, true, Q16, SRC_MKQ>(a, lane, crc);
+        tdec_half<true, true, Q16, SRC_Q>(a, lane, crc);
+      } else {
+        tdec_half<false, true, Q16, SRC_SB>(a, lane, crc);
+        tdec_half<true, true, Q16, SRC_SB>(a, lane, crc);
+      }
+    } else if (it < MK) {
+      tdec_half<false, false, Q16, SRC_SB>(a, lane, crc);
+      tdec_half<true, false, Q16, SRC_SB>(a, lane, crc);
+    } else if (it == MK) {
+      tdec_half<false, false, Q16, SRC_MKQ>(a, lane, crc);
+      tdec_half<true, false, Q16, SRC_Q>(a, lane, crc);
     } else {
-      tdec_half<false, false, Q16>(a, lane, crc);
-      tdec_half<true, false, Q16>(a, lane, crc);
+      tdec_half<false, false, Q16, SRC_Q>(a, lane, crc);
+      tdec_half<true, false, Q16, SRC_Q>(a, lane, crc);
     }
     r.its = it + 1;
     r.crc_ok = crc == 0;
