@@ -23,7 +23,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
   if (P.build(cfgs, n, true)) return -1;
   std::vector<float> e(P.e_floats, 0.f), sb(P.sb_floats, 0.f), scr(P.scratch_floats, 0.f);
   std::vector<uint8_t> dec(P.dec_bytes, 0), cbb(P.lanes.size() * mi::CB_BYTES_STRIDE, 0);
-  std::vector<uint32_t> cits(P.lanes.size(), 0), ccrc(P.lanes.size(), 0);
+  std::vector<uint32_t> cits(P.lanes.size(), 0), ccrc(P.lanes.size(), 0), ctbp(P.lanes.size(), 0);
   size_t src = 0;
   for (uint32_t s = 0; s < n; s++) {
     const uint32_t G = P.pds[P.sfs[s].pdsch].G;
@@ -50,6 +50,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.pi = &P.kdata[kt.pi_off];
       a.crc_a = &P.kdata[kt.crca_off];
       a.crc_b = &P.kdata[kt.crcb_off];
+      a.crc_p = &P.kdata[kt.crcp_off];
       a.scr = &scr[g.scratch_off];
       a.dec = &dec[g.dec_off];
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
@@ -57,6 +58,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       mi::TdecLaneResult r = g_q16 ? mi::tdec_lane<true>(a, lane) : mi::tdec_lane<false>(a, lane);
       cits[li] = r.its;
       ccrc[li] = r.crc_ok;
+      ctbp[li] = r.tb_part;
     }
   }
   for (uint32_t t = 0; t < n; t++) {
@@ -70,16 +72,9 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       buf[j] = cbb[(size_t)lanes[r] * mi::CB_BYTES_STRIDE + off];
     }
     memcpy(payload + tb.pay_off, buf.data(), tb.tbs / 8);
-    // parallel-CRC formulation of the GPU kernel with 256 segments
-    const uint32_t seg = (nbytes + 255) / 256;
+    // TB CRC from the decoder's per-code-block partial registers (tb_kernel's formulation)
     uint32_t crc = 0;
-    for (uint32_t th = 0; th < 256; th++) {
-      const uint32_t b0 = th * seg;
-      if (b0 >= nbytes) continue;
-      const uint32_t m = (b0 + seg <= nbytes) ? seg : nbytes - b0;
-      uint32_t c = mi::crc24_bytes(buf.data() + b0, m, mi::CRC24A_POLY);
-      crc ^= mi::gf24_mulmod(c, mi::gf24_xpow8(nbytes - b0 - m, mi::CRC24A_POLY), mi::CRC24A_POLY);
-    }
+    for (uint32_t r = 0; r < tb.C; r++) crc ^= mi::tb_crc_term(tb, r, ctbp[lanes[r]]);
     tb_ok[t] = crc == 0;
     uint32_t its = 0;
     for (uint32_t r = 0; r < tb.C; r++) its = cits[lanes[r]] > its ? cits[lanes[r]] : its;

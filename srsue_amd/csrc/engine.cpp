@@ -77,7 +77,7 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   if (P.has_pdsch || P.cb_n) {
     ok = ok && d_e.ensure(P.e_floats * 4) && d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
          d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
-         d_cbcrc.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
+         d_cbcrc.ensure(P.lanes.size() * 4) && d_cbtbp.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
          d_tbits.ensure(nsf * 4);
     if (alloc_sb) {
       size_t before = d_sb.bytes;
@@ -133,13 +133,15 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC))
       launch_tdec(sb, d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
-                  d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(),
+                  d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+                  d_ktabs.as<MiKTab>(),
                   d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
                   q16(), st);
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
-                d_cbits.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(), d_cblist.as<uint32_t>(), st);
+                d_cbits.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(),
+                d_cblist.as<uint32_t>(), st);
     mark(6);
   } else {
     for (int i = 3; i <= 6; i++) mark(i);
@@ -169,7 +171,8 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
                     (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
   mark(MI_DL_STAGE_TDEC);
   launch_tdec(d_sb.as<float>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
-              d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+              d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
+              d_lanes.as<MiLaneDesc>(),
               d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
               q16(), st);
   mark(MI_DL_STAGE_TB);

@@ -22,15 +22,15 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
                        uint32_t max_ncb, hipStream_t st);
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
 void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
-                 uint32_t* cb_crc, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
-                 const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop,
-                 bool q16, hipStream_t st);
+                 uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
+                 const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
+                 uint32_t early_stop, bool q16, hipStream_t st);
 // raw code-block decoder input [cb][3(K+4)] -> group-interleaved softbuffer layout
 void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, const MiKTab* ktabs,
                        const uint32_t* kdata, uint32_t n_groups, uint32_t K, uint32_t n_cb, hipStream_t st);
 // TB assembly + CRC24A + payload packing
 void launch_tb(const uint8_t* cb_bytes, uint8_t* payload, uint32_t* tb_crc_ok, uint32_t* tb_its,
-               const uint32_t* cb_its, const MiTbDesc* tbs, uint32_t n_tb, const uint32_t* cb_list,
-               hipStream_t st);
+               const uint32_t* cb_its, const uint32_t* cb_tbp, const MiTbDesc* tbs, uint32_t n_tb,
+               const uint32_t* cb_list, hipStream_t st);
 
 }  // namespace mi

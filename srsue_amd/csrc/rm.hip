@@ -12,6 +12,10 @@
 #include "kernels.h"
 #include "rm_body.h"
 
+#ifndef MI_RM_NT
+#define MI_RM_NT 0   // non-temporal softbuffer stores (A/B switch)
+#endif
+
 namespace mi {
 
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
@@ -93,7 +97,11 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       if (rep)
         for (j += nv; j < E; j += nv) v = v + e[ld.e_off + j];
     }
+#if MI_RM_NT
+    __builtin_nontemporal_store(v, &sbg[(size_t)p * LANES + lane]);
+#else
     sbg[(size_t)p * LANES + lane] = v;
+#endif
   }
 }
 

@@ -3,9 +3,10 @@
 // without filler and CB CRC are concatenated, the TB CRC24A is checked (return 0 <=> CRC ok) and
 // the payload is packed MSB-first into bytes (srsUE treats it as bytes: ue/src/mac/demux.cc:180).
 //
-// The CRC is computed in parallel: each lane takes a byte segment, computes its zero-initialised
-// CRC register, and shifts it to the end of the message by multiplying with x^(8 n) mod g in
-// GF(2)[x] (CRC(A||B) = CRC(A) x^|B| + CRC(B)); XOR of all shifted registers is the message CRC.
+// The TB CRC is linear over GF(2): the turbo decoder accumulates, per code block, the register
+// contribution of its decided payload bits (TdecLaneResult::tb_part, per-K table crc_p), and the TB
+// register is XOR_r tb_part_r * x^(bits after code block r) mod g (CRC(A||B) = CRC(A) x^|B| + CRC(B))
+// -- no pass over the TB bytes.
 #pragma once
 #include "dl_common.h"
 #ifndef MI_HD
@@ -51,19 +52,17 @@ MI_HD inline uint32_t gf24_xpow8(uint32_t n, uint32_t poly) {
   return res;
 }
 
-// which code block / byte of that block holds TB byte j (CB payload bytes are byte aligned:
-// K, F and the 24-bit CB CRC are multiples of 8)
-MI_HD inline void tb_byte_src(const MiTbDesc& t, uint32_t j, uint32_t& r, uint32_t& off) {
-  const uint32_t L = t.C > 1 ? 3 : 0;
-  uint32_t start = 0;
-  for (r = 0; r < t.C; r++) {
-    const uint32_t Kr = r < t.Cm ? t.Km : t.Kp;
-    const uint32_t Fr = r == 0 ? t.F : 0;
-    const uint32_t nr = Kr / 8 - Fr / 8 - L;
-    if (j < start + nr) { off = Fr / 8 + (j - start); return; }
-    start += nr;
-  }
-  r = t.C - 1; off = 0;
+// payload bytes code block r contributes to the TB (after filler, without the CB CRC)
+MI_HD inline uint32_t tb_cb_nbytes(const MiTbDesc& t, uint32_t r) {
+  const uint32_t Kr = r < t.Cm ? t.Km : t.Kp;
+  return Kr / 8 - (r == 0 ? t.F / 8 : 0) - (t.C > 1 ? 3 : 0);
+}
+
+// code block r's term of the TB CRC24A register
+MI_HD inline uint32_t tb_crc_term(const MiTbDesc& t, uint32_t r, uint32_t part) {
+  uint32_t after = 0;
+  for (uint32_t j = r + 1; j < t.C; j++) after += tb_cb_nbytes(t, j);
+  return gf24_mulmod(part, gf24_xpow8(after, CRC24A_POLY), CRC24A_POLY);
 }
 
 }  // namespace mi

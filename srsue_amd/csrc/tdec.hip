@@ -5,15 +5,20 @@
 
 namespace mi {
 
+struct TdecOut {            // per code block (lane index li) results
+  uint8_t* cb_bytes;        // [li][CB_BYTES_STRIDE] packed decisions
+  uint32_t* its;            // iterations used
+  uint32_t* crc_ok;         // CB CRC verdict of the last iteration
+  uint32_t* tb_part;        // partial TB-CRC24A register (tb_kernel combines them)
+};
+
 template <bool Q16>
 __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* __restrict__ scratch,
-                                                 uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
-                                                 uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
-                                                 const MiGroupDesc* __restrict__ groups,
-                                                 const MiLaneDesc* __restrict__ lanes,
-                                                 const MiKTab* __restrict__ ktabs,
-                                                 const uint32_t* __restrict__ kdata, uint32_t max_its,
-                                                 uint32_t early_stop) {
+                                           uint8_t* __restrict__ dec, const TdecOut& out,
+                                           const MiGroupDesc* __restrict__ groups,
+                                           const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
+                                           const uint32_t* __restrict__ kdata, uint32_t max_its,
+                                           uint32_t early_stop) {
   const MiGroupDesc g = groups[blockIdx.x];
   const int lane = threadIdx.x;
   const uint32_t li = g.lane0 + lane;
@@ -27,28 +32,29 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
   a.pi = kdata + kt.pi_off;
   a.crc_a = kdata + kt.crca_off;
   a.crc_b = kdata + kt.crcb_off;
+  a.crc_p = kdata + kt.crcp_off;
   a.scr = scratch + g.scratch_off;
   a.dec = dec + g.dec_off;
-  a.cb_bytes = cb_bytes + (size_t)li * CB_BYTES_STRIDE;
+  a.cb_bytes = out.cb_bytes + (size_t)li * CB_BYTES_STRIDE;
   a.K = g.K;
   a.F = ld.F;
   a.max_its = max_its;
   a.early_stop = early_stop;
   a.crc24a = ld.crc24a;
   const TdecLaneResult r = tdec_lane<Q16>(a, lane);
-  cb_its[li] = r.its;
-  cb_crc[li] = r.crc_ok;
+  out.its[li] = r.its;
+  out.crc_ok[li] = r.crc_ok;
+  out.tb_part[li] = r.tb_part;
 }
 
-// float decoder: 163 VGPRs -> 3 waves per SIMD by itself
+// float decoder
 __global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ sb, float* __restrict__ scratch,
-                                                     uint8_t* __restrict__ dec, uint8_t* __restrict__ cb_bytes,
-                                                     uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
+                                                     uint8_t* __restrict__ dec, TdecOut out,
                                                      const MiGroupDesc* __restrict__ groups,
                                                      const MiLaneDesc* __restrict__ lanes,
                                                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata,
                                                      uint32_t max_its, uint32_t early_stop) {
-  tdec_group<false>(sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<false>(sb, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 // int16 decoder: held to MI_TDEC_I16_WAVES waves per SIMD (3: <= 168 VGPRs), enough to keep every
 // group of a 12,500-subframe batch resident (2,540 waves on 1,024 SIMDs)
@@ -56,24 +62,25 @@ __global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ 
 #define MI_TDEC_I16_WAVES 3
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_TDEC_I16_WAVES)))
-void tdec_kernel_i16(const float* __restrict__ sb, float* __restrict__ scratch, uint8_t* __restrict__ dec,
-                     uint8_t* __restrict__ cb_bytes, uint32_t* __restrict__ cb_its, uint32_t* __restrict__ cb_crc,
+void tdec_kernel_i16(const float* __restrict__ sb, float* __restrict__ scratch, uint8_t* __restrict__ dec, TdecOut out,
                      const MiGroupDesc* __restrict__ groups, const MiLaneDesc* __restrict__ lanes,
                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata, uint32_t max_its,
                      uint32_t early_stop) {
-  tdec_group<true>(sb, scratch, dec, cb_bytes, cb_its, cb_crc, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<true>(sb, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 
 void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
-                 const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data,
-                 uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16, hipStream_t st) {
+                 uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
+                 const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,
+                 hipStream_t st) {
   if (!n_groups) return;
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
   if (q16)
-    hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
-                       groups, lanes, ktabs, ktab_data, max_its, early_stop);
+    hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, out, groups, lanes, ktabs,
+                       ktab_data, max_its, early_stop);
   else
-    hipLaunchKernelGGL(tdec_kernel_gen, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, cb_bytes, cb_its, cb_crc,
-                       groups, lanes, ktabs, ktab_data, max_its, early_stop);
+    hipLaunchKernelGGL(tdec_kernel_gen, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, out, groups, lanes, ktabs,
+                       ktab_data, max_its, early_stop);
 }
 
 }  // namespace mi

@@ -53,13 +53,18 @@ struct TdecArgs {
   const uint32_t* pi;     // [K]
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
   const uint32_t* crc_b;  // [K] same for CRC24B
+  const uint32_t* crc_p;  // [K] TB-CRC24A contribution of CB payload bit k when C > 1: x^(K-1-k) mod g_A,
+                          //     0 for the CB-CRC bits (C = 1: crc_a itself)
   float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/(2W)+1)*7][64]
   uint8_t* dec;           // [K][64] decision bytes
   uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
   uint32_t K, F, max_its, early_stop, crc24a;
 };
 
-struct TdecLaneResult { uint32_t its; uint32_t crc_ok; };
+// CRC registers accumulated by linearity during DEC2's forward pass: the code block's own CRC
+// (early stop) and its partial of the TB CRC24A (combined by tb_kernel, tb_body.h)
+struct TdecCrc { uint32_t cb, tb; };
+struct TdecLaneResult { uint32_t its; uint32_t crc_ok; uint32_t tb_part; };
 
 
 MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
@@ -293,7 +298,7 @@ MI_HD inline void tdec_xs_xp(const TdecWin<Q16>& r, int i, uint32_t k, uint32_t 
 // per-step outputs: DEC1 stores llr1; DEC2 updates w, stores the decision and folds it into the CRC
 template <bool DEC2, bool Q16>
 MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, float llr, float xs,
-                            const TdecWin<Q16>& w, uint32_t& crc) {
+                            const TdecWin<Q16>& w, TdecCrc& crc) {
   const uint32_t k = base + i;
   if (!DEC2) {
     scr_st<Q16>(scr_at<Q16>(a.scr, a.K), base, lane, llr, i);           // llr1
@@ -305,7 +310,9 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, f
     const bool bit = llr > 0.0f;
     row_st(a.dec, pk, lane, (uint8_t)(bit ? 1 : 0));                    // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
-    crc ^= bit ? tt : 0u;                                               // CRC by linearity
+    crc.cb ^= bit ? tt : 0u;                                            // CB CRC by linearity
+    const uint32_t tp = a.crc24a ? a.crc_a[pk] : a.crc_p[pk];
+    crc.tb ^= (bit && pk >= a.F) ? tp : 0u;                             // TB CRC partial (no filler)
   }
 }
 
@@ -346,7 +353,7 @@ MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWi
 // closing checkpoint, then alpha and the LLRs
 template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base, float (&al)[8],
-                                    uint32_t& crc) {
+                                    TdecCrc& crc) {
   float xs[BETA_W], xp[BETA_W];
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
@@ -368,7 +375,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 // window j is computed and are first used one window later (K is a multiple of 8 for every LTE
 // code block size, so the window count K/4 is even and the loops have no remainder).
 template <bool DEC2, bool FIRST, bool Q16, int SRC>
-MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
+MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;   // backward pass: softbuffer -> q rows
   constexpr bool SQB = Q16 && SRC == SRC_Q;              // backward pass reads q rows
   constexpr bool SQF = Q16 && SRC != SRC_SB;             // forward pass reads q rows
@@ -451,9 +458,9 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, uint32_t& crc) {
 
 template <bool Q16>
 MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
-  TdecLaneResult r{0, 0};
+  TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
-    uint32_t crc = 0;
+    TdecCrc crc{0, 0};
     constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;   // iteration creating the q rows
     if (it == 0) {
       if (MK == 0) {
@@ -474,7 +481,8 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
       tdec_half<true, false, Q16, SRC_Q>(a, lane, crc);
     }
     r.its = it + 1;
-    r.crc_ok = crc == 0;
+    r.crc_ok = crc.cb == 0;
+    r.tb_part = crc.tb;
     if (a.early_stop && r.crc_ok) break;
   }
   for (uint32_t j = 0; j < a.K / 8; j++) {
