@@ -117,7 +117,6 @@ struct MiKTab {              // per K, device resident
   uint32_t pi_off;           // uint32 offset: pi[K]
   uint32_t crca_off;         // uint32 offset: CRC24A contribution of a single 1 at bit i, [K]
   uint32_t crcb_off;         // uint32 offset: same for CRC24B
-  uint32_t crcp_off;         // uint32 offset: TB-CRC24A contribution of payload bit k of a CB when C > 1
 };
 
 namespace mi {

@@ -17,8 +17,11 @@
 static int g_q16 = 0;   // turbo arithmetic of the emulated decoder (MI_DL_FLAG_TDEC_I16)
 extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 
+static uint32_t crc8[256];
+
 extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
                               uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
+  for (uint32_t b = 0; b < 256; b++) crc8[b] = mi::crc24_byte_entry(b, mi::CRC24A_POLY);
   mi::Plan P;
   if (P.build(cfgs, n, true)) return -1;
   std::vector<float> e(P.e_floats, 0.f), sb(P.sb_floats, 0.f), scr(P.scratch_floats, 0.f);
@@ -50,7 +53,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.pi = &P.kdata[kt.pi_off];
       a.crc_a = &P.kdata[kt.crca_off];
       a.crc_b = &P.kdata[kt.crcb_off];
-      a.crc_p = &P.kdata[kt.crcp_off];
+      a.crc8 = crc8;
       a.scr = &scr[g.scratch_off];
       a.dec = &dec[g.dec_off];
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
@@ -64,12 +67,10 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
   for (uint32_t t = 0; t < n; t++) {
     const MiTbDesc& tb = P.tbs[t];
     const uint32_t* lanes = &P.cb_list[tb.cb_list];
-    const uint32_t nbytes = (tb.tbs + 24) / 8;
-    std::vector<uint8_t> buf(nbytes);
-    for (uint32_t j = 0; j < nbytes; j++) {
-      uint32_t r, off;
-      mi::tb_byte_src(tb, j, r, off);
-      buf[j] = cbb[(size_t)lanes[r] * mi::CB_BYTES_STRIDE + off];
+    std::vector<uint8_t> buf;
+    for (uint32_t r = 0; r < tb.C; r++) {
+      const uint8_t* src = &cbb[(size_t)lanes[r] * mi::CB_BYTES_STRIDE + (r == 0 ? tb.F / 8 : 0)];
+      buf.insert(buf.end(), src, src + mi::tb_cb_nbytes(tb, r));
     }
     memcpy(payload + tb.pay_off, buf.data(), tb.tbs / 8);
     // TB CRC from the decoder's per-code-block partial registers (tb_kernel's formulation)

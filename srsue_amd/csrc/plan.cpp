@@ -18,19 +18,15 @@ static size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 void Plan::add_ktab(uint32_t K) {
   auto& kp = kpos_cache[K];
   if (kp.empty()) {
-    kp.resize(5);
+    kp.resize(4);
     cb_pos_table(K, kp[0]);
     qpp_table(K, kp[1]);
     crc_bit_table(K, 0x864CFBu, kp[2]);
     crc_bit_table(K, 0x800063u, kp[3]);
-    // TB-CRC partial of a code block with a CB CRC (C > 1): its payload bits k < K - 24 form a
-    // message of K - 24 bits; the CB-CRC bits contribute nothing
-    crc_bit_table(K - 24, 0x864CFBu, kp[4]);
-    kp[4].resize(K, 0u);
   }
-  MiKTab t{K, ncb_of(K), 0, 0, 0, 0, 0};
-  uint32_t* offs[5] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off, &t.crcp_off};
-  for (int q = 0; q < 5; q++) {
+  MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
+  uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
+  for (int q = 0; q < 4; q++) {
     *offs[q] = (uint32_t)kdata.size();
     kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
   }

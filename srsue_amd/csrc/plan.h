@@ -42,7 +42,7 @@ struct Plan {
   // cached per-key tables (kept across rebuilds)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<float>> crs_cache;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::vector<uint32_t>> scr_cache;
-  std::map<uint32_t, std::vector<std::vector<uint32_t>>> kpos_cache;   // K -> {pos, pi, crcA, crcB, crcP}
+  std::map<uint32_t, std::vector<std::vector<uint32_t>>> kpos_cache;   // K -> {pos, pi, crcA, crcB}
   void add_ktab(uint32_t K);   // appends K's tables to kdata and a MiKTab to ktabs
   std::map<std::pair<uint32_t, uint32_t>, std::pair<std::vector<int32_t>, uint32_t>> rank_cache;
 

@@ -30,6 +30,13 @@ MI_HD inline uint32_t crc24_bytes(const uint8_t* p, uint32_t n, uint32_t poly) {
   return crc;
 }
 
+// CRC register after one message byte b from the zero state (byte-table entry)
+MI_HD inline uint32_t crc24_byte_entry(uint32_t b, uint32_t poly) {
+  uint32_t c = b << 16;
+  for (int i = 0; i < 8; i++) c = ((c << 1) & 0xFFFFFFu) ^ ((c & 0x800000u) ? poly : 0u);
+  return c;
+}
+
 // a * b mod (x^24 + poly) over GF(2)
 MI_HD inline uint32_t gf24_mulmod(uint32_t a, uint32_t b, uint32_t poly) {
   uint32_t r = 0;

@@ -1,6 +1,7 @@
 // tdec.hip -- turbo decoder launch: one 64-lane wavefront per group of code blocks of equal K
 // (tdec_body.h holds the per-lane algorithm and its bit-exactness contract with the oracle).
 #include "kernels.h"
+#include "tb_body.h"
 #include "tdec_body.h"
 
 namespace mi {
@@ -19,6 +20,10 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
                                            const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                                            const uint32_t* __restrict__ kdata, uint32_t max_its,
                                            uint32_t early_stop) {
+  // CRC24A byte table in LDS (one entry per lane group of 4), for the TB-CRC partial of each lane
+  __shared__ uint32_t crc8[256];
+  for (uint32_t b = threadIdx.x; b < 256; b += 64) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+  __syncthreads();
   const MiGroupDesc g = groups[blockIdx.x];
   const int lane = threadIdx.x;
   const uint32_t li = g.lane0 + lane;
@@ -32,7 +37,7 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
   a.pi = kdata + kt.pi_off;
   a.crc_a = kdata + kt.crca_off;
   a.crc_b = kdata + kt.crcb_off;
-  a.crc_p = kdata + kt.crcp_off;
+  a.crc8 = crc8;
   a.scr = scratch + g.scratch_off;
   a.dec = dec + g.dec_off;
   a.cb_bytes = out.cb_bytes + (size_t)li * CB_BYTES_STRIDE;

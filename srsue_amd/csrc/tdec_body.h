@@ -53,17 +53,15 @@ struct TdecArgs {
   const uint32_t* pi;     // [K]
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
   const uint32_t* crc_b;  // [K] same for CRC24B
-  const uint32_t* crc_p;  // [K] TB-CRC24A contribution of CB payload bit k when C > 1: x^(K-1-k) mod g_A,
-                          //     0 for the CB-CRC bits (C = 1: crc_a itself)
+  const uint32_t* crc8;   // [256] byte table of CRC24A (register update of one message byte)
   float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/(2W)+1)*7][64]
   uint8_t* dec;           // [K][64] decision bytes
   uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
   uint32_t K, F, max_its, early_stop, crc24a;
 };
 
-// CRC registers accumulated by linearity during DEC2's forward pass: the code block's own CRC
-// (early stop) and its partial of the TB CRC24A (combined by tb_kernel, tb_body.h)
-struct TdecCrc { uint32_t cb, tb; };
+// the code block's own CRC register, accumulated by linearity during DEC2's forward pass (early stop)
+struct TdecCrc { uint32_t cb; };
 struct TdecLaneResult { uint32_t its; uint32_t crc_ok; uint32_t tb_part; };
 
 
@@ -311,8 +309,6 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, f
     row_st(a.dec, pk, lane, (uint8_t)(bit ? 1 : 0));                    // decision
     const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
     crc.cb ^= bit ? tt : 0u;                                            // CB CRC by linearity
-    const uint32_t tp = a.crc24a ? a.crc_a[pk] : a.crc_p[pk];
-    crc.tb ^= (bit && pk >= a.F) ? tp : 0u;                             // TB CRC partial (no filler)
   }
 }
 
@@ -460,7 +456,7 @@ template <bool Q16>
 MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
-    TdecCrc crc{0, 0};
+    TdecCrc crc{0};
     constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;   // iteration creating the q rows
     if (it == 0) {
       if (MK == 0) {
@@ -482,15 +478,21 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
     }
     r.its = it + 1;
     r.crc_ok = crc.cb == 0;
-    r.tb_part = crc.tb;
     if (a.early_stop && r.crc_ok) break;
   }
+  // pack the final decisions MSB first; the bytes of the TB payload part (after filler, before the CB
+  // CRC when C > 1) also run through a byte-wise CRC24A: the code block's partial TB-CRC register
+  // (tb_kernel combines the partials, tb_body.h)
+  const uint32_t b0 = a.F / 8, b1 = a.K / 8 - (a.crc24a ? 0 : 3);
+  uint32_t tb = 0;
   for (uint32_t j = 0; j < a.K / 8; j++) {
     uint32_t v = 0;
 #pragma unroll
     for (int q = 0; q < 8; q++) v |= (uint32_t)row_ld(a.dec, 8 * j + q, lane) << (7 - q);
     a.cb_bytes[j] = (uint8_t)v;
+    if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
   }
+  r.tb_part = tb;
   return r;
 }
 
