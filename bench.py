@@ -292,6 +292,33 @@ def bench_codeblocks(args, world, rank, dev):
     return out
 
 
+def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
+    """IQ resident in page-locked host memory, each step copied H2D and decoded through the
+    double-buffered pipeline (copy of step i+1 overlaps the decode of step i)."""
+    B = len(cfgs)
+    pipe = abi.Pipe(cfgs, max_its=args.max_its, tdec_i16=args.tdec == "i16")
+    nfl = 2 * batch.iq_samples
+    hb = abi.HostBuffer(nfl * 4)
+    for i in range(B):
+        o = 2 * batch.iq_offset(i)
+        iq = pool_iq[i % len(pool_iq)]
+        hb.array[o:o + len(iq)] = iq
+    for _ in range(max(2, args.warmup)):
+        pipe.wait(pipe.submit(hb.ptr))
+    t0 = time.perf_counter()
+    last = [pipe.submit(hb.ptr) for _ in range(args.steps)]
+    pipe.wait(last[-1] ^ 1)
+    pipe.wait(last[-1])
+    dt = time.perf_counter() - t0
+    ok = pipe.batch(last[-1]).download(abi.BUF_TB_CRC, np.uint32)[:B]
+    pipe.close()
+    hb.close()
+    return {"value": round(bits_ok * args.steps / dt / 1e6, 2), "unit": "Mbps", "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "pcie_GBps": round(nfl * 4 * args.steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
+            "what": "IQ (cf32, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy stream "
+                    "overlapped with the previous batch's decode"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,6 +334,9 @@ def main():
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
     ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
     ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
+    ap.add_argument("--h2d", action="store_true",
+                    help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
+                         "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
     args = ap.parse_args()
@@ -416,6 +446,8 @@ def main():
                          "algorithmic_bytes_per_launch": tdec_bytes,
                          "avg_launch_ms": round(tdec_ms, 4), "launches_averaged": nprof},
         }
+        if args.h2d:
+            out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
                                                args.tdec == "i16")

@@ -116,6 +116,25 @@ int    mi_sf_len(uint32_t nof_prb);
 /* number of PDSCH bits G of a configuration (RE count x Qm, 36.211 6.3.5 / 6.4) */
 int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
 
+/* ---- host-IQ streaming pipeline -------------------------------------
+ * Double buffering for IQ that arrives in host memory (srsUE's sync thread writes the worker's
+ * buffer, phch_recv.cc:321-322): two batches of the same configuration, one copy stream and one
+ * compute stream.  submit() enqueues the H2D copy of host_iq (mi_dl_batch_iq_samples cf32, batch
+ * layout; pinned memory from mi_host_alloc for full PCIe rate) into the free slot behind that
+ * slot's previous decode, then the decode behind the copy, and returns the slot (0/1) without
+ * blocking: the copy of one batch overlaps the decode of the other.  wait() blocks until the slot's
+ * decode is done; its outputs (mi_dl_pipe_batch + mi_dl_batch_download/device_ptr) stay valid
+ * until the slot is submitted again, i.e. for one further submit(). */
+typedef struct mi_dl_pipe mi_dl_pipe_t;
+mi_dl_pipe_t  *mi_dl_pipe_create(const mi_dl_sf_cfg_t *cfgs, uint32_t n_sf, uint32_t max_its, uint32_t flags);
+void           mi_dl_pipe_destroy(mi_dl_pipe_t *p);
+int            mi_dl_pipe_submit(mi_dl_pipe_t *p, const void *host_iq);   /* slot, or -1 */
+int            mi_dl_pipe_wait(mi_dl_pipe_t *p, int slot);
+mi_dl_batch_t *mi_dl_pipe_batch(mi_dl_pipe_t *p, int slot);
+/* page-locked host memory (hipHostMalloc) for IQ buffers */
+void  *mi_host_alloc(size_t bytes);
+void   mi_host_free(void *p);
+
 /* ---- device / runtime helpers ------------------------------------------------------------ */
 int    mi_device_count(void);
 int    mi_set_device(int dev);

@@ -87,6 +87,13 @@ def lib():
             "mi_tdec_algo_bytes": (C.c_double, [vp]),
             "mi_sf_len": (C.c_int, [u32]),
             "mi_pdsch_G": (C.c_int, [vp]),
+            "mi_dl_pipe_create": (vp, [vp, u32, u32, u32]),
+            "mi_dl_pipe_destroy": (None, [vp]),
+            "mi_dl_pipe_submit": (C.c_int, [vp, vp]),
+            "mi_dl_pipe_wait": (C.c_int, [vp, C.c_int]),
+            "mi_dl_pipe_batch": (vp, [vp, C.c_int]),
+            "mi_host_alloc": (vp, [sz]),
+            "mi_host_free": (None, [vp]),
             "mi_device_count": (C.c_int, []),
             "mi_set_device": (C.c_int, [C.c_int]),
             "mi_last_error": (C.c_char_p, []),
@@ -146,10 +153,17 @@ class Batch:
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())
 
+    @classmethod
+    def view(cls, handle, cfgs):
+        """Non-owning wrapper of a batch owned elsewhere (a pipe slot)."""
+        b = cls.__new__(cls)
+        b.cfgs, b._arr, b.h, b._owned = list(cfgs), None, handle, False
+        return b
+
     def close(self):
-        if self.h:
+        if self.h and getattr(self, "_owned", True):
             lib().mi_dl_batch_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -215,6 +229,64 @@ class Batch:
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)
         off = lib().mi_dl_batch_payload_offset(self.h, sf)
         return p[off:off + self.cfgs[sf].tbs // 8]
+
+
+class HostBuffer:
+    """Page-locked host memory (mi_host_alloc) viewed as a numpy array."""
+
+    def __init__(self, nbytes, dtype=np.float32):
+        self.ptr = lib().mi_host_alloc(nbytes)
+        if not self.ptr:
+            raise RuntimeError("mi_host_alloc: " + last_error())
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr)).view(dtype)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            lib().mi_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Pipe:
+    """Double-buffered host-IQ pipeline (mi_dl_pipe_*): submit() returns a slot without blocking."""
+
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True):
+        self.cfgs = list(cfgs)
+        self._arr = cfg_array(self.cfgs)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
+        self.h = lib().mi_dl_pipe_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
+        if not self.h:
+            raise RuntimeError("mi_dl_pipe_create: " + last_error())
+
+    def submit(self, host_ptr):
+        s = lib().mi_dl_pipe_submit(self.h, C.c_void_p(host_ptr))
+        if s < 0:
+            raise RuntimeError("mi_dl_pipe_submit: " + last_error())
+        return s
+
+    def wait(self, slot):
+        if lib().mi_dl_pipe_wait(self.h, slot):
+            raise RuntimeError("mi_dl_pipe_wait: " + last_error())
+
+    def batch(self, slot):
+        return Batch.view(lib().mi_dl_pipe_batch(self.h, slot), self.cfgs)
+
+    def close(self):
+        if self.h:
+            lib().mi_dl_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def turbo_encode(bits, K, F=0):

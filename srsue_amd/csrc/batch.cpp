@@ -162,6 +162,86 @@ int mi_tdec_stage_ms(mi_tdec_batch_t* b, float* ms, uint32_t* nruns) { return b-
 void mi_tdec_profile_reset(mi_tdec_batch_t* b) { b->eng.profile_reset(); }
 double mi_tdec_algo_bytes(const mi_tdec_batch_t* b) { return b->eng.plan.stage_bytes[MI_DL_STAGE_TDEC]; }
 
+// ---- host-IQ pipeline (double buffering) ---------------------------------------
+}  // extern "C"
+
+struct mi_dl_pipe {
+  mi_dl_batch_t* slot[2] = {nullptr, nullptr};
+  mi::DevBuf iq[2];
+  hipStream_t copy = nullptr, comp = nullptr;
+  hipEvent_t copied[2] = {nullptr, nullptr}, decoded[2] = {nullptr, nullptr};
+  bool busy[2] = {false, false};
+  int next = 0;
+  size_t iq_bytes = 0;
+  ~mi_dl_pipe() {
+    if (comp) (void)hipStreamSynchronize(comp);
+    if (copy) (void)hipStreamSynchronize(copy);
+    for (int s = 0; s < 2; s++) {
+      if (copied[s]) (void)hipEventDestroy(copied[s]);
+      if (decoded[s]) (void)hipEventDestroy(decoded[s]);
+      delete slot[s];
+    }
+    if (copy) (void)hipStreamDestroy(copy);
+    if (comp) (void)hipStreamDestroy(comp);
+  }
+};
+
+extern "C" {
+
+mi_dl_pipe_t* mi_dl_pipe_create(const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf, uint32_t max_its, uint32_t flags) {
+  auto* p = new mi_dl_pipe();
+  bool ok = mi::hip_ok(hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking), "stream") &&
+            mi::hip_ok(hipStreamCreateWithFlags(&p->comp, hipStreamNonBlocking), "stream");
+  for (int s = 0; ok && s < 2; s++) {
+    p->slot[s] = mi_dl_batch_create(cfgs, n_sf, max_its, flags);
+    ok = p->slot[s] != nullptr;
+    if (ok) {
+      p->iq_bytes = mi_dl_batch_iq_samples(p->slot[s]) * 8;
+      ok = p->iq[s].ensure(p->iq_bytes) &&
+           mi::hip_ok(hipEventCreateWithFlags(&p->copied[s], hipEventDisableTiming), "event") &&
+           mi::hip_ok(hipEventCreateWithFlags(&p->decoded[s], hipEventDisableTiming), "event");
+    }
+  }
+  if (!ok) { delete p; return nullptr; }
+  return p;
+}
+
+void mi_dl_pipe_destroy(mi_dl_pipe_t* p) { delete p; }
+
+int mi_dl_pipe_submit(mi_dl_pipe_t* p, const void* host_iq) {
+  if (!p || !host_iq) { mi::set_error("null argument"); return -1; }
+  const int s = p->next;
+  // the slot's previous decode must have consumed its device IQ before the copy overwrites it
+  bool ok = (!p->busy[s] || mi::hip_ok(hipStreamWaitEvent(p->copy, p->decoded[s], 0), "wait")) &&
+            mi::hip_ok(hipMemcpyAsync(p->iq[s].p, host_iq, p->iq_bytes, hipMemcpyHostToDevice, p->copy), "H2D") &&
+            mi::hip_ok(hipEventRecord(p->copied[s], p->copy), "record") &&
+            mi::hip_ok(hipStreamWaitEvent(p->comp, p->copied[s], 0), "wait") &&
+            p->slot[s]->eng.run(p->iq[s].p, p->comp, 0xFFFFFFFFu, nullptr) == 0 &&
+            mi::hip_ok(hipEventRecord(p->decoded[s], p->comp), "record");
+  if (!ok) return -1;
+  p->busy[s] = true;
+  p->next ^= 1;
+  return s;
+}
+
+int mi_dl_pipe_wait(mi_dl_pipe_t* p, int slot) {
+  if (!p || slot < 0 || slot > 1) { mi::set_error("bad slot"); return -1; }
+  if (!p->busy[slot]) return 0;
+  return mi::hip_ok(hipEventSynchronize(p->decoded[slot]), "event sync") ? 0 : -1;
+}
+
+mi_dl_batch_t* mi_dl_pipe_batch(mi_dl_pipe_t* p, int slot) {
+  return (p && slot >= 0 && slot < 2) ? p->slot[slot] : nullptr;
+}
+
+void* mi_host_alloc(size_t bytes) {
+  void* h = nullptr;
+  return mi::hip_ok(hipHostMalloc(&h, bytes, hipHostMallocDefault), "hipHostMalloc") ? h : nullptr;
+}
+void mi_host_free(void* h) {
+  if (h) (void)hipHostFree(h);
+}
+
 int mi_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -100,3 +100,27 @@ def test_turbo_bit_exact_on_identical_llrs(snr, i16):
         assert bool(crc[i]) == ok
         assert its[i] == onoi
         assert np.array_equal(b.payload(i, pay), opay)
+
+
+def test_host_iq_pipeline_matches_batch():
+    """mi_dl_pipe_* (SURVEY 8f-3): host IQ in page-locked memory, double-buffered H2D + decode on two
+    streams; each slot's outputs equal a plain batch run on the same IQ, across slot reuse."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + (i % 4), tbs=75376, Qm=6) for i in range(6)]
+    iqs, tbs = make_subframes(cfgs, snr_db=30.0, seed0=40)
+    ref = run_batch(cfgs, iqs)
+    want = ref.download(abi.BUF_PAYLOAD, np.uint8)
+    p = abi.Pipe(cfgs)
+    nfl = 2 * ref.iq_samples
+    hb = abi.HostBuffer(nfl * 4)
+    for i, iq in enumerate(iqs):
+        o = 2 * ref.iq_offset(i)
+        hb.array[o:o + len(iq)] = iq
+    slots = [p.submit(hb.ptr) for _ in range(3)]      # slot 0, 1, 0 again (reuse behind its decode)
+    assert slots == [0, 1, 0]
+    for s in (1, 0):
+        p.wait(s)
+        b = p.batch(s)
+        assert np.array_equal(b.download(abi.BUF_PAYLOAD, np.uint8), want)
+        assert np.all(b.download(abi.BUF_TB_CRC, np.uint32)[:len(cfgs)] == 1)
+    p.close()
+    hb.close()
