@@ -296,12 +296,15 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
     """IQ resident in page-locked host memory, each step copied H2D and decoded through the
     double-buffered pipeline (copy of step i+1 overlaps the decode of step i)."""
     B = len(cfgs)
-    pipe = abi.Pipe(cfgs, max_its=args.max_its, tdec_i16=args.tdec == "i16")
+    sc16 = args.iq == "sc16"
+    pipe = abi.Pipe(cfgs, max_its=args.max_its, tdec_i16=args.tdec == "i16", iq_sc16=sc16)
     nfl = 2 * batch.iq_samples
-    hb = abi.HostBuffer(nfl * 4)
+    esz = 2 if sc16 else 4
+    hb = abi.HostBuffer(nfl * esz, np.int16 if sc16 else np.float32)
+    pool = [abi.to_sc16(x) for x in pool_iq] if sc16 else pool_iq
     for i in range(B):
         o = 2 * batch.iq_offset(i)
-        iq = pool_iq[i % len(pool_iq)]
+        iq = pool[i % len(pool)]
         hb.array[o:o + len(iq)] = iq
     for _ in range(max(2, args.warmup)):
         pipe.wait(pipe.submit(hb.ptr))
@@ -314,9 +317,9 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
     pipe.close()
     hb.close()
     return {"value": round(bits_ok * args.steps / dt / 1e6, 2), "unit": "Mbps", "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "pcie_GBps": round(nfl * 4 * args.steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
-            "what": "IQ (cf32, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy stream "
-                    "overlapped with the previous batch's decode"}
+            "pcie_GBps": round(nfl * esz * args.steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
+            "what": f"IQ ({args.iq}, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy "
+                    "stream overlapped with the previous batch's decode"}
 
 
 def main():
@@ -337,6 +340,8 @@ def main():
     ap.add_argument("--h2d", action="store_true",
                     help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
                          "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
+    ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
+                    help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
     args = ap.parse_args()

@@ -55,6 +55,9 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * srsLTE-gen decoder (srslte_tdec_gen, the non-SSE build).  Both are bit-exact to their oracle. */
 #define MI_DL_FLAG_TDEC_I16 2u
 #define MI_DL_FLAG_TDEC_GEN 4u
+/* IQ input in UHD's sc16 wire format (int16 I/Q, fc32 = sc16 / 32768) instead of fc32: half the
+ * bytes over PCIe for host-resident IQ; the OFDM stage converts on load (exact). */
+#define MI_DL_FLAG_IQ_SC16 8u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 
@@ -119,7 +122,8 @@ int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
 /* ---- host-IQ streaming pipeline -------------------------------------
  * Double buffering for IQ that arrives in host memory (srsUE's sync thread writes the worker's
  * buffer, phch_recv.cc:321-322): two batches of the same configuration, one copy stream and one
- * compute stream.  submit() enqueues the H2D copy of host_iq (mi_dl_batch_iq_samples cf32, batch
+ * compute stream.  submit() enqueues the H2D copy of host_iq (mi_dl_batch_iq_samples cf32, or sc16
+ * with MI_DL_FLAG_IQ_SC16, batch
  * layout; pinned memory from mi_host_alloc for full PCIe rate) into the free slot behind that
  * slot's previous decode, then the decode behind the copy, and returns the slot (0/1) without
  * blocking: the copy of one batch overlaps the decode of the other.  wait() blocks until the slot's

@@ -19,6 +19,7 @@ BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF
 FLAG_PROFILE = 1
 FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic (the default), see include/mi_dl.h
 FLAG_TDEC_GEN = 4   # float srsLTE-gen turbo arithmetic
+FLAG_IQ_SC16 = 8    # IQ input as UHD sc16 (int16 I/Q, fc32 = sc16 / 32768)
 
 
 class SfCfg(C.Structure):
@@ -145,10 +146,11 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
-        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
+            (FLAG_IQ_SC16 if iq_sc16 else 0)
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())
@@ -256,10 +258,11 @@ class HostBuffer:
 class Pipe:
     """Double-buffered host-IQ pipeline (mi_dl_pipe_*): submit() returns a slot without blocking."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
-        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
+            (FLAG_IQ_SC16 if iq_sc16 else 0)
         self.h = lib().mi_dl_pipe_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_pipe_create: " + last_error())
@@ -287,6 +290,11 @@ class Pipe:
             self.close()
         except Exception:
             pass
+
+
+def to_sc16(iq_f32):
+    """fc32 interleaved I/Q -> UHD sc16 (round to nearest, saturate): the wire format of FLAG_IQ_SC16."""
+    return np.clip(np.rint(np.asarray(iq_f32, np.float32) * 32768.0), -32768, 32767).astype(np.int16)
 
 
 def turbo_encode(bits, K, F=0):

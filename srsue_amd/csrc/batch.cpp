@@ -196,7 +196,7 @@ mi_dl_pipe_t* mi_dl_pipe_create(const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf, uint3
     p->slot[s] = mi_dl_batch_create(cfgs, n_sf, max_its, flags);
     ok = p->slot[s] != nullptr;
     if (ok) {
-      p->iq_bytes = mi_dl_batch_iq_samples(p->slot[s]) * 8;
+      p->iq_bytes = mi_dl_batch_iq_samples(p->slot[s]) * ((flags & MI_DL_FLAG_IQ_SC16) ? 4 : 8);
       ok = p->iq[s].ensure(p->iq_bytes) &&
            mi::hip_ok(hipEventCreateWithFlags(&p->copied[s], hipEventDisableTiming), "event") &&
            mi::hip_ok(hipEventCreateWithFlags(&p->decoded[s], hipEventDisableTiming), "event");

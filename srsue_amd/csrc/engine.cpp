@@ -110,7 +110,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   if (mask & (1u << MI_DL_STAGE_OFDM)) {
     for (size_t i = 0; i < P.fft_lists.size(); i++) {
       const int N = P.fft_lists[i].first;
-      launch_ofdm_rx(N, reinterpret_cast<const float2*>(d_iq), d_grid.as<float2>(), d_sfs.as<MiSfDesc>(),
+      launch_ofdm_rx(N, d_iq, (flags & MI_DL_FLAG_IQ_SC16) != 0, d_grid.as<float2>(), d_sfs.as<MiSfDesc>(),
                      d_fftlist.as<uint32_t>() + P.fft_list_off[i], (uint32_t)P.fft_lists[i].second.size(),
                      d_tw.as<float2>() + tw_off[N], P.fft_W[i], st);
     }

@@ -7,7 +7,7 @@
 namespace mi {
 
 // OFDM RX (srslte_ofdm_rx_sf): one workgroup per subframe, 14 FFTs of size N
-void launch_ofdm_rx(int N, const float2* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
+void launch_ofdm_rx(int N, const void* iq, bool sc16, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
                     uint32_t n, const float2* tw, uint32_t W, hipStream_t st);
 // channel estimation (srslte_chest_dl_estimate): one workgroup per subframe, all ports
 void launch_chest(const float2* grid, float2* ce, const MiSfDesc* sfs, const MiCellDesc* cells,

@@ -57,8 +57,15 @@ template <> __device__ __forceinline__ void dft<8>(float2 (&v)[8]) {
 
 // One Stockham stage (decimation in time): butterfly j reads x[j + r N/R], twiddles by
 // W_{Ns R}^{(j mod Ns) r}, writes y[(j / Ns) Ns R + j mod Ns + r Ns].
-template <int N, int R, bool FIRST>
-__device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict__ gsrc, const float2* tw, int Ns) {
+// IQ sample i of a symbol: fc32, or UHD sc16 (fc32 = sc16 / 32768, exact in fp32) -- MI_DL_FLAG_IQ_SC16
+__device__ __forceinline__ float2 load_iq(const float2* __restrict__ p, int i) { return p[i]; }
+__device__ __forceinline__ float2 load_iq(const short2* __restrict__ p, int i) {
+  const short2 v = p[i];
+  return make_float2((float)v.x * (1.0f / 32768.0f), (float)v.y * (1.0f / 32768.0f));
+}
+
+template <int N, int R, bool FIRST, typename IQ>
+__device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gsrc, const float2* tw, int Ns) {
   constexpr int NB = N / R;
   constexpr int PER = (NB + 255) / 256;
   const int tid = threadIdx.x;
@@ -68,7 +75,7 @@ __device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict_
     const int j = tid + p * 256;
     if (j < NB) {
 #pragma unroll
-      for (int r = 0; r < R; r++) v[p][r] = FIRST ? gsrc[j + r * NB] : buf[j + r * NB];
+      for (int r = 0; r < R; r++) v[p][r] = FIRST ? load_iq(gsrc, j + r * NB) : buf[j + r * NB];
     }
   }
   __syncthreads();
@@ -91,32 +98,32 @@ __device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict_
   __syncthreads();
 }
 
-template <int N>
-__device__ __forceinline__ void fft_symbol(float2* buf, const float2* __restrict__ src, const float2* tw) {
+template <int N, typename IQ>
+__device__ __forceinline__ void fft_symbol(float2* buf, const IQ* __restrict__ src, const float2* tw) {
   if constexpr (N == 2048) {
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
-    fft_stage<N, 8, false>(buf, src, tw, 64); fft_stage<N, 4, false>(buf, src, tw, 512);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 8, false, IQ>(buf, src, tw, 64); fft_stage<N, 4, false, IQ>(buf, src, tw, 512);
   } else if constexpr (N == 1536) {
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
-    fft_stage<N, 8, false>(buf, src, tw, 64); fft_stage<N, 3, false>(buf, src, tw, 512);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 8, false, IQ>(buf, src, tw, 64); fft_stage<N, 3, false, IQ>(buf, src, tw, 512);
   } else if constexpr (N == 1024) {
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
-    fft_stage<N, 4, false>(buf, src, tw, 64); fft_stage<N, 4, false>(buf, src, tw, 256);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 4, false, IQ>(buf, src, tw, 64); fft_stage<N, 4, false, IQ>(buf, src, tw, 256);
   } else if constexpr (N == 512) {
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
-    fft_stage<N, 8, false>(buf, src, tw, 64);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 8, false, IQ>(buf, src, tw, 64);
   } else if constexpr (N == 256) {
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 8, false>(buf, src, tw, 8);
-    fft_stage<N, 4, false>(buf, src, tw, 64);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 4, false, IQ>(buf, src, tw, 64);
   } else {
     static_assert(N == 128, "unsupported FFT size");
-    fft_stage<N, 8, true>(buf, src, tw, 1); fft_stage<N, 4, false>(buf, src, tw, 8);
-    fft_stage<N, 4, false>(buf, src, tw, 32);
+    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 4, false, IQ>(buf, src, tw, 8);
+    fft_stage<N, 4, false, IQ>(buf, src, tw, 32);
   }
 }
 
-template <int N>
-__global__ __launch_bounds__(256) void ofdm_rx_kernel(const float2* __restrict__ iq, float2* __restrict__ grid,
+template <int N, typename IQ>
+__global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
                                                       const MiSfDesc* __restrict__ sfs,
                                                       const uint32_t* __restrict__ list,
                                                       const float2* __restrict__ twg, uint32_t W) {
@@ -125,28 +132,35 @@ __global__ __launch_bounds__(256) void ofdm_rx_kernel(const float2* __restrict__
   const MiSfDesc d = sfs[list[blockIdx.x]];
   for (int t = threadIdx.x; t < N; t += 256) tw[t] = twg[t];
   __syncthreads();
-  const float2* src_sf = iq + d.iq_off;
+  const IQ* src_sf = iq + d.iq_off;
   float2* dst = grid + d.grid_off;
   for (int l = 0; l < NSYMB; l++) {
-    fft_symbol<N>(buf, src_sf + symbol_offset(N, l), tw);
+    fft_symbol<N, IQ>(buf, src_sf + symbol_offset(N, l), tw);
     for (int k = threadIdx.x; k < (int)W; k += 256) dst[l * W + k] = buf[sc_bin(k, (int)W, N)];
     __syncthreads();
   }
 }
 
-void launch_ofdm_rx(int N, const float2* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
-                    uint32_t n, const float2* tw, uint32_t W, hipStream_t st) {
-  if (n == 0) return;
+template <typename IQ>
+static void launch_ofdm_rx_t(int N, const IQ* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list, uint32_t n,
+                             const float2* tw, uint32_t W, hipStream_t st) {
   dim3 g(n), b(256);
   switch (N) {
-    case 2048: hipLaunchKernelGGL(ofdm_rx_kernel<2048>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 1536: hipLaunchKernelGGL(ofdm_rx_kernel<1536>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 1024: hipLaunchKernelGGL(ofdm_rx_kernel<1024>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 512: hipLaunchKernelGGL(ofdm_rx_kernel<512>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 256: hipLaunchKernelGGL(ofdm_rx_kernel<256>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 128: hipLaunchKernelGGL(ofdm_rx_kernel<128>, g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 2048: hipLaunchKernelGGL((ofdm_rx_kernel<2048, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 1536: hipLaunchKernelGGL((ofdm_rx_kernel<1536, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 1024: hipLaunchKernelGGL((ofdm_rx_kernel<1024, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 512: hipLaunchKernelGGL((ofdm_rx_kernel<512, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 256: hipLaunchKernelGGL((ofdm_rx_kernel<256, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 128: hipLaunchKernelGGL((ofdm_rx_kernel<128, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
     default: break;
   }
+}
+
+void launch_ofdm_rx(int N, const void* iq, bool sc16, float2* grid, const MiSfDesc* sfs, const uint32_t* list,
+                    uint32_t n, const float2* tw, uint32_t W, hipStream_t st) {
+  if (n == 0) return;
+  if (sc16) launch_ofdm_rx_t(N, static_cast<const short2*>(iq), grid, sfs, list, n, tw, W, st);
+  else launch_ofdm_rx_t(N, static_cast<const float2*>(iq), grid, sfs, list, n, tw, W, st);
 }
 
 }  // namespace mi
