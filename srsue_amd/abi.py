@@ -292,9 +292,13 @@ class Pipe:
             pass
 
 
-def to_sc16(iq_f32):
-    """fc32 interleaved I/Q -> UHD sc16 (round to nearest, saturate): the wire format of FLAG_IQ_SC16."""
-    return np.clip(np.rint(np.asarray(iq_f32, np.float32) * 32768.0), -32768, 32767).astype(np.int16)
+SC16_GAIN = 0.25   # receive gain before sc16 quantisation: the synthetic TX peaks at ~2.5 (a radio's AGC
+                   # keeps samples inside [-1, 1)); a power of two, so gain * x is exact
+
+
+def to_sc16(iq_f32, gain=SC16_GAIN):
+    """fc32 interleaved I/Q -> UHD sc16 (gain, round to nearest, saturate): FLAG_IQ_SC16's wire format."""
+    return np.clip(np.rint(np.asarray(iq_f32, np.float32) * (gain * 32768.0)), -32768, 32767).astype(np.int16)
 
 
 def turbo_encode(bits, K, F=0):
