@@ -130,6 +130,41 @@ int      or_simd_decode_batch(const float *in, uint32_t stride, uint32_t n, uint
                               int early_stop, int crc_type, uint8_t *bits, uint32_t *its, uint8_t *ok,
                               uint32_t nthreads);
 
+/* ---- DL control channels (o_ctrl.c): PHICH/PCFICH REG allocation, PDCCH, DCI ---- */
+#define OR_DCI_MAX_BITS 64
+enum { OR_DCI_0 = 0, OR_DCI_1 = 1, OR_DCI_1A = 2 };
+typedef struct {
+  or_cell_t cell;
+  uint32_t  ng;        /* PHICH resources Ng: 0 = 1/6, 1 = 1/2, 2 = 1, 3 = 2 (srslte_phich_resources_t) */
+  uint32_t  cfi, sf;   /* PHICH duration normal, normal CP */
+} or_ctrl_t;
+typedef struct { uint32_t rb_start, L_crb, mcs, harq, ndi, rv, tpc; } or_dci1a_t;
+typedef struct { uint32_t format, nbits, L, ncce; uint8_t bits[OR_DCI_MAX_BITS]; } or_dci_found_t;
+uint32_t or_phich_ngroups(uint32_t nof_prb, uint32_t ng);
+/* PDCCH REGs (not PCFICH/PHICH) in 36.211 6.8.5 mapping order, 4 RE indices (l*W + k) each;
+ * returns N_REG, *n_cce = N_REG / 9.  re4 may be NULL (count only). */
+int      or_pdcch_regs(const or_ctrl_t *q, uint32_t *re4, uint32_t *n_cce);
+void     or_pdcch_quad_perm(uint32_t M, uint32_t cell_id, uint32_t *log_of_reg);
+/* PDCCH soft bits [8 N_REG] in logical (CCE) order, descrambled; srslte_pdcch_extract_llr */
+int      or_pdcch_llr(const or_ctrl_t *q, const float *grid, const float *ce, float noise, float *llr,
+                      uint32_t *n_cce);
+void     or_conv_encode_tb(const uint8_t *c, uint32_t D, uint8_t *d /* d0 | d1 | d2 */);
+int      or_conv_rm_tx(const uint8_t *d, uint32_t D, uint32_t E, uint8_t *e);
+void     or_conv_rm_rx(const float *e, uint32_t E, uint32_t D, float *d);
+void     or_viterbi_tb(const float *d, uint32_t D, uint8_t *c);
+uint32_t or_dci_size(uint32_t format, uint32_t nof_prb);
+uint32_t or_riv(uint32_t nof_prb, uint32_t rb_start, uint32_t L);
+int      or_dci1a_pack(uint32_t nof_prb, const or_dci1a_t *g, uint8_t *bits);
+int      or_dci1a_unpack(uint32_t nof_prb, const uint8_t *bits, uint32_t nbits, or_dci1a_t *g);
+int      or_dci_encode(const uint8_t *a, uint32_t A, uint16_t rnti, uint32_t L, uint8_t *e /* 72 L */);
+int      or_dci_decode(const float *e, uint32_t L, uint32_t A, uint16_t rnti, uint8_t *a);   /* 1 = CRC ok */
+int      or_search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, int common, uint32_t *L, uint32_t *ncce);
+int      or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int ul,
+                     or_dci_found_t *out);
+/* adds one noiseless DCI (L CCEs at ncce) to iq (2 * SF_LEN floats), flat per-port channel h */
+int      or_tx_pdcch(const or_ctrl_t *q, uint16_t rnti, uint32_t L, uint32_t ncce, const uint8_t *a, uint32_t A,
+                     const float *h_re_im, float *iq);
+
 /* ---- PHY TX (o_tx.c): synthetic subframe generator (ground truth) ----------------------- */
 typedef struct {
   or_cell_t cell;

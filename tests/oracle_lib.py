@@ -25,6 +25,22 @@ class CbSegm(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("C", "Cp", "Cm", "Kp", "Km", "F", "B")]
 
 
+class CtrlCfg(C.Structure):
+    _fields_ = [("cell", Cell), ("ng", C.c_uint32), ("cfi", C.c_uint32), ("sf", C.c_uint32)]
+
+
+class Dci1a(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("rb_start", "L_crb", "mcs", "harq", "ndi", "rv", "tpc")]
+
+
+class DciFound(C.Structure):
+    _fields_ = [("format", C.c_uint32), ("nbits", C.c_uint32), ("L", C.c_uint32), ("ncce", C.c_uint32),
+                ("bits", C.c_uint8 * 64)]
+
+
+DCI_0, DCI_1, DCI_1A = 0, 1, 2
+
+
 class TxCfg(C.Structure):
     _fields_ = [
         ("cell", Cell),
@@ -90,6 +106,25 @@ def lib():
                                                C.c_int, u8, u32, u8, C.c_uint32]),
             "or_set_tdec_mode": (None, [C.c_int]),
             "or_get_tdec_mode": (C.c_int, []),
+            "or_phich_ngroups": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+            "or_pdcch_regs": (C.c_int, [C.POINTER(CtrlCfg), C.c_void_p, C.POINTER(C.c_uint32)]),
+            "or_pdcch_quad_perm": (None, [C.c_uint32, C.c_uint32, u32]),
+            "or_pdcch_llr": (C.c_int, [C.POINTER(CtrlCfg), f32, f32, C.c_float, f32, C.POINTER(C.c_uint32)]),
+            "or_conv_encode_tb": (None, [u8, C.c_uint32, u8]),
+            "or_conv_rm_tx": (C.c_int, [u8, C.c_uint32, C.c_uint32, u8]),
+            "or_conv_rm_rx": (None, [f32, C.c_uint32, C.c_uint32, f32]),
+            "or_viterbi_tb": (None, [f32, C.c_uint32, u8]),
+            "or_dci_size": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+            "or_riv": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+            "or_dci1a_pack": (C.c_int, [C.c_uint32, C.POINTER(Dci1a), u8]),
+            "or_dci1a_unpack": (C.c_int, [C.c_uint32, u8, C.c_uint32, C.POINTER(Dci1a)]),
+            "or_dci_encode": (C.c_int, [u8, C.c_uint32, C.c_uint16, C.c_uint32, u8]),
+            "or_dci_decode": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint16, C.c_void_p]),
+            "or_search_space": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_int, u32, u32]),
+            "or_find_dci": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint16, C.c_int,
+                                      C.POINTER(DciFound)]),
+            "or_tx_pdcch": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint16, C.c_uint32, C.c_uint32, u8, C.c_uint32,
+                                      C.c_void_p, f32]),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -145,6 +180,26 @@ class tdec_mode:
 
     def __exit__(self, *a):
         lib().or_set_tdec_mode(self.prev)
+
+
+def ctrl_cfg(cell_id=1, nof_prb=100, nof_ports=1, ng=2, cfi=1, sf=1):
+    return CtrlCfg(Cell(cell_id, nof_prb, nof_ports), ng, cfi, sf)
+
+
+def pdcch_llr(q, grid, ce):
+    """Oracle PDCCH soft bits (logical CCE order) of a subframe's grid / channel estimates."""
+    n = C.c_uint32()
+    M = lib().or_pdcch_regs(C.byref(q), None, C.byref(n))
+    llr = np.zeros(8 * M, np.float32)
+    lib().or_pdcch_llr(C.byref(q), np.ascontiguousarray(grid, np.float32), np.ascontiguousarray(ce, np.float32),
+                       0.0, llr, C.byref(n))
+    return llr, n.value
+
+
+def find_dci(llr, n_cce, nof_prb, sf, rnti, ul=False):
+    out = DciFound()
+    ok = lib().or_find_dci(np.ascontiguousarray(llr, np.float32), n_cce, nof_prb, sf, rnti, int(ul), C.byref(out))
+    return (out.format, np.array(out.bits[:out.nbits], np.uint8), out.L, out.ncce) if ok else None
 
 
 def cbsegm(tbs):
