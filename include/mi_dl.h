@@ -119,6 +119,26 @@ int    mi_sf_len(uint32_t nof_prb);
 /* number of PDSCH bits G of a configuration (RE count x Qm, 36.211 6.3.5 / 6.4) */
 int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
 
+/* ---- DL control channels ----------------------------------------------
+ * PCFICH -> CFI, PDCCH soft bits and DCI blind search (srslte_pdcch_extract_llr +
+ * srslte_ue_dl_find_dl_dci / _find_ul_dci) over the grid and channel estimates a batch's front end
+ * left in HBM.  Per subframe the search uses that subframe's cfg.rnti and cfg.cfi; PHICH resources
+ * phich_ng = 0..3 (Ng = 1/6, 1/2, 1, 2; normal duration).  run() enqueues three kernels (stage mask:
+ * 1 PCFICH, 2 PDCCH soft bits, 4 blind search); result() returns the first DCI of the subframe in
+ * search order (UE-specific L = 1, 2, 4, 8, then common L = 4, 8): 1 found, 0 not found, -1 error. */
+typedef struct mi_dl_ctrl mi_dl_ctrl_t;
+mi_dl_ctrl_t *mi_dl_ctrl_create(mi_dl_batch_t *b, uint32_t phich_ng);
+void          mi_dl_ctrl_destroy(mi_dl_ctrl_t *c);
+int           mi_dl_ctrl_run(mi_dl_ctrl_t *c, void *stream);
+int           mi_dl_ctrl_run_stages(mi_dl_ctrl_t *c, uint32_t mask, void *stream);
+int           mi_dl_ctrl_result(mi_dl_ctrl_t *c, uint32_t sf, int ul, uint32_t *cfi, uint32_t *format, uint32_t *L,
+                                uint32_t *ncce, uint8_t *bits /* 64 */, uint32_t *nbits);
+size_t        mi_dl_ctrl_llr_floats(const mi_dl_ctrl_t *c);
+size_t        mi_dl_ctrl_llr_offset(const mi_dl_ctrl_t *c, uint32_t sf);
+uint32_t      mi_dl_ctrl_n_cce(const mi_dl_ctrl_t *c, uint32_t sf);
+/* copy PDCCH soft bits between host and device (upload != 0: host -> device) */
+int           mi_dl_ctrl_llr(mi_dl_ctrl_t *c, float *host, size_t n, int upload);
+
 /* ---- host-IQ streaming pipeline -------------------------------------
  * Double buffering for IQ that arrives in host memory (srsUE's sync thread writes the worker's
  * buffer, phch_recv.cc:321-322): two batches of the same configuration, one copy stream and one

@@ -88,6 +88,15 @@ def lib():
             "mi_tdec_algo_bytes": (C.c_double, [vp]),
             "mi_sf_len": (C.c_int, [u32]),
             "mi_pdsch_G": (C.c_int, [vp]),
+            "mi_dl_ctrl_create": (vp, [vp, u32]),
+            "mi_dl_ctrl_destroy": (None, [vp]),
+            "mi_dl_ctrl_run": (C.c_int, [vp, vp]),
+            "mi_dl_ctrl_run_stages": (C.c_int, [vp, u32, vp]),
+            "mi_dl_ctrl_result": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp, vp, vp]),
+            "mi_dl_ctrl_llr_floats": (sz, [vp]),
+            "mi_dl_ctrl_llr_offset": (sz, [vp, u32]),
+            "mi_dl_ctrl_n_cce": (u32, [vp, u32]),
+            "mi_dl_ctrl_llr": (C.c_int, [vp, vp, sz, C.c_int]),
             "mi_dl_pipe_create": (vp, [vp, u32, u32, u32]),
             "mi_dl_pipe_destroy": (None, [vp]),
             "mi_dl_pipe_submit": (C.c_int, [vp, vp]),
@@ -231,6 +240,60 @@ class Batch:
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)
         off = lib().mi_dl_batch_payload_offset(self.h, sf)
         return p[off:off + self.cfgs[sf].tbs // 8]
+
+
+class Ctrl:
+    """DL control channels over a batch's grid / channel estimates (mi_dl_ctrl_*)."""
+    PCFICH, LLR, SEARCH = 1, 2, 4
+
+    def __init__(self, batch, phich_ng=2):
+        self.batch = batch
+        self.h = lib().mi_dl_ctrl_create(batch.h, phich_ng)
+        if not self.h:
+            raise RuntimeError("mi_dl_ctrl_create: " + last_error())
+
+    def run(self, stream_ptr=None, mask=7):
+        if lib().mi_dl_ctrl_run_stages(self.h, mask, C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_dl_ctrl_run: " + last_error())
+
+    def result(self, sf, ul=False):
+        """(cfi, found DCI or None); DCI = (format, bits, L, ncce)"""
+        v = [C.c_uint32() for _ in range(5)]
+        bits = np.zeros(64, np.uint8)
+        rc = lib().mi_dl_ctrl_result(self.h, sf, int(ul), C.byref(v[0]), C.byref(v[1]), C.byref(v[2]), C.byref(v[3]),
+                                     bits.ctypes.data, C.byref(v[4]))
+        if rc < 0:
+            raise RuntimeError("mi_dl_ctrl_result: " + last_error())
+        return v[0].value, ((v[1].value, bits[:v[4].value].copy(), v[2].value, v[3].value) if rc == 1 else None)
+
+    def llr(self):
+        n = lib().mi_dl_ctrl_llr_floats(self.h)
+        out = np.zeros(n, np.float32)
+        if lib().mi_dl_ctrl_llr(self.h, out.ctypes.data, n, 0):
+            raise RuntimeError("mi_dl_ctrl_llr: " + last_error())
+        return out
+
+    def set_llr(self, host):
+        a = np.ascontiguousarray(host, np.float32)
+        if lib().mi_dl_ctrl_llr(self.h, a.ctypes.data, a.size, 1):
+            raise RuntimeError("mi_dl_ctrl_llr: " + last_error())
+
+    def llr_offset(self, sf):
+        return lib().mi_dl_ctrl_llr_offset(self.h, sf)
+
+    def n_cce(self, sf):
+        return lib().mi_dl_ctrl_n_cce(self.h, sf)
+
+    def close(self):
+        if self.h:
+            lib().mi_dl_ctrl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class HostBuffer:

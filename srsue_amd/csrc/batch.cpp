@@ -6,10 +6,7 @@
 
 namespace mi { const char* last_error(); }
 
-struct mi_dl_batch {
-  mi::Engine eng;
-  std::vector<mi_dl_sf_cfg_t> cfgs;
-};
+#include "batch_impl.h"
 
 extern "C" {
 

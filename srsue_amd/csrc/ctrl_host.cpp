@@ -1,0 +1,226 @@
+// ctrl.cpp -- host planner of the DL control stage (ctrl.h) and the mi_dl_ctrl_* C ABI.
+#include "ctrl.h"
+
+#include <string.h>
+
+#include <map>
+#include <tuple>
+
+#include "kernels.h"
+#include "tables.h"
+
+namespace mi {
+
+int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t phich_ng,
+                      const std::vector<uint16_t>& rnti) {
+  const size_t n = P.sfs.size();
+  if (cfi.size() != n || rnti.size() != n) { set_error("ctrl: per-subframe cfi / rnti"); return -1; }
+  sfs.clear(); cdata.clear(); jobs.clear(); job_begin.clear(); nof_prb.clear();
+  llr_floats = 0; max_regs = 0;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> reg_cache;  // -> (off, M)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> scr_cache, pcf_cache;
+  std::map<uint32_t, uint32_t> rank_cache;   // D -> cdata offset
+  for (size_t s = 0; s < n; s++) {
+    const MiSfDesc& sd = P.sfs[s];
+    const MiCellDesc& c = P.cells[sd.cell];
+    if (cfi[s] < 1 || cfi[s] > 3) { set_error("ctrl: cfi"); return -1; }
+    MiCtrlSf d{};
+    d.grid_off = sd.grid_off;
+    d.ce_off = sd.ce_off;
+    d.plane = NSYMB * c.W;
+    d.ports = c.nof_ports;
+    auto rk = std::make_tuple(c.id, c.nof_prb, phich_ng, cfi[s]);
+    auto it = reg_cache.find(rk);
+    if (it == reg_cache.end()) {
+      std::vector<uint32_t> re4, lg;
+      const uint32_t M = pdcch_regs(c.id, c.nof_prb, phich_ng, cfi[s], &re4);
+      pdcch_quad_perm(M, c.id, lg);
+      const uint32_t off = (uint32_t)cdata.size();
+      cdata.insert(cdata.end(), re4.begin(), re4.end());
+      cdata.insert(cdata.end(), lg.begin(), lg.end());
+      it = reg_cache.emplace(rk, std::make_pair(off, M)).first;
+    }
+    d.reg_off = it->second.first;
+    d.M = it->second.second;
+    d.n_cce = d.M / 9;
+    auto sk = std::make_tuple(c.id, sd.sf_idx, d.M, 0u);
+    auto si = scr_cache.find(sk);
+    if (si == scr_cache.end()) {
+      std::vector<uint32_t> w((8 * d.M + 31) / 32);
+      gold_words(sd.sf_idx * 512 + c.id, 8 * d.M, w.data());    // 36.211 6.8.2
+      si = scr_cache.emplace(sk, (uint32_t)cdata.size()).first;
+      cdata.insert(cdata.end(), w.begin(), w.end());
+    }
+    d.scr_off = si->second;
+    auto pk = std::make_tuple(c.id, c.nof_prb, sd.sf_idx, 0u);
+    auto pi = pcf_cache.find(pk);
+    if (pi == pcf_cache.end()) {
+      uint32_t k16[16], w = 0;
+      pcfich_k(c.id, c.nof_prb, k16);
+      gold_words(pcfich_cinit(c.id, sd.sf_idx), 32, &w);
+      pi = pcf_cache.emplace(pk, (uint32_t)cdata.size()).first;
+      cdata.insert(cdata.end(), k16, k16 + 16);
+      cdata.push_back(w);
+    }
+    d.pcfich_off = pi->second;
+    d.llr_off = (uint32_t)llr_floats;
+    llr_floats += (size_t)8 * d.M;
+    max_regs = std::max(max_regs, d.M);
+    sfs.push_back(d);
+    nof_prb.push_back(c.nof_prb);
+    // jobs in search order: UE-specific (sizes 1A/0 then 1), then common (1A/0)
+    job_begin.push_back((uint32_t)jobs.size());
+    const uint32_t A1a = dci_size(DCI_1A, c.nof_prb), A1 = dci_size(DCI_1, c.nof_prb);
+    for (int common = 0; common < 2; common++) {
+      uint32_t Ls[16], nc[16];
+      const int nk = search_space(d.n_cce, sd.sf_idx, rnti[s], common != 0, Ls, nc);
+      for (int k = 0; k < nk; k++)
+        for (int f = 0; f < (common ? 1 : 2); f++) {
+          const uint32_t A = f ? A1 : A1a, D = A + 16;
+          auto ri = rank_cache.find(D);
+          if (ri == rank_cache.end()) {
+            std::vector<uint32_t> rank;
+            conv_rank_table(D, rank);
+            ri = rank_cache.emplace(D, (uint32_t)cdata.size()).first;
+            cdata.insert(cdata.end(), rank.begin(), rank.end());
+          }
+          jobs.push_back(MiDciJob{(uint32_t)s, d.llr_off, Ls[k], nc[k], A, D, ri->second, rnti[s]});
+        }
+    }
+  }
+  job_begin.push_back((uint32_t)jobs.size());
+  return 0;
+}
+
+int CtrlEngine::upload(hipStream_t st) {
+  auto up = [&](DevBuf& b, const void* h, size_t bytes) {
+    return b.ensure(bytes) && (bytes == 0 || hip_ok(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, st), "H2D"));
+  };
+  const bool ok = up(d_sfs, sfs.data(), sfs.size() * sizeof(MiCtrlSf)) &&
+                  up(d_cdata, cdata.data(), cdata.size() * 4) && up(d_jobs, jobs.data(), jobs.size() * sizeof(MiDciJob)) &&
+                  d_llr.ensure(llr_floats * 4) && d_res.ensure(jobs.size() * sizeof(MiDciRes)) &&
+                  d_cfi.ensure(sfs.size() * 4) && hip_ok(hipStreamSynchronize(st), "ctrl upload");
+  return ok ? 0 : -1;
+}
+
+int CtrlEngine::run(const float2* grid, const float2* ce, uint32_t mask, float noise, hipStream_t st) {
+  const uint32_t n = (uint32_t)sfs.size();
+  if (mask & 1u) launch_pcfich(grid, ce, d_sfs.as<MiCtrlSf>(), d_cdata.as<uint32_t>(), d_cfi.as<uint32_t>(), n, st);
+  if (mask & 2u)
+    launch_pdcch_llr(grid, ce, d_sfs.as<MiCtrlSf>(), d_cdata.as<uint32_t>(), d_llr.as<float>(), n, max_regs, noise, st);
+  if (mask & 4u)
+    launch_dci_search(d_llr.as<float>(), d_jobs.as<MiDciJob>(), d_cdata.as<uint32_t>(), d_res.as<MiDciRes>(),
+                      (uint32_t)jobs.size(), st);
+  return hip_ok(hipGetLastError(), "ctrl launch") ? 0 : -1;
+}
+
+int CtrlEngine::download(hipStream_t st) {
+  res.resize(jobs.size());
+  return hip_ok(hipMemcpyAsync(res.data(), d_res.p, res.size() * sizeof(MiDciRes), hipMemcpyDeviceToHost, st), "D2H") &&
+                 hip_ok(hipStreamSynchronize(st), "sync")
+             ? 0
+             : -1;
+}
+
+DciFound CtrlEngine::select(uint32_t s, bool ul, bool common_only) const {
+  DciFound out{};
+  const uint32_t A1a = dci_size(DCI_1A, nof_prb[s]);
+  for (uint32_t j = job_begin[s]; j < job_begin[s + 1]; j++) {
+    const MiDciJob& jb = jobs[j];
+    const MiDciRes& r = res[j];
+    if (!r.found) continue;
+    const uint32_t flag = (r.bits[0] >> 31) & 1u;
+    int fmt;
+    if (jb.A == A1a) fmt = flag ? DCI_1A : DCI_0;
+    else fmt = DCI_1;
+    if (ul ? fmt != DCI_0 : fmt == DCI_0) continue;
+    if (common_only) {
+      // common-space candidates are the last ones of the subframe's job list (L = 4 / 8, one size)
+      uint32_t Ls[16], nc[16];
+      const uint32_t ncommon = (uint32_t)search_space(sfs[s].n_cce, 0, 0, true, Ls, nc);
+      if (j < job_begin[s + 1] - ncommon) continue;
+    }
+    out.found = 1;
+    out.format = (uint32_t)fmt;
+    out.nbits = jb.A;
+    out.L = jb.L;
+    out.ncce = jb.ncce;
+    for (uint32_t i = 0; i < jb.A; i++) out.bits[i] = (uint8_t)((r.bits[i >> 5] >> (31 - (i & 31))) & 1u);
+    return out;
+  }
+  return out;
+}
+
+}  // namespace mi
+
+// ---- C ABI (include/mi_dl.h) -----------------------------------------------------------------
+#include "batch_impl.h"
+
+struct mi_dl_ctrl {
+  mi::CtrlEngine ce;
+  mi_dl_batch_t* b = nullptr;
+  hipStream_t last = nullptr;
+  bool have_res = false;
+  std::vector<uint32_t> cfi;
+};
+
+extern "C" {
+
+mi_dl_ctrl_t* mi_dl_ctrl_create(mi_dl_batch_t* b, uint32_t phich_ng) {
+  if (!b) { mi::set_error("null batch"); return nullptr; }
+  auto* c = new mi_dl_ctrl();
+  c->b = b;
+  std::vector<uint32_t> cfi;
+  std::vector<uint16_t> rnti;
+  for (const mi_dl_sf_cfg_t& s : b->cfgs) { cfi.push_back(s.cfi); rnti.push_back((uint16_t)s.rnti); }
+  if (c->ce.build(b->eng.plan, cfi, phich_ng, rnti) || c->ce.upload(nullptr)) { delete c; return nullptr; }
+  return c;
+}
+
+void mi_dl_ctrl_destroy(mi_dl_ctrl_t* c) { delete c; }
+
+int mi_dl_ctrl_run_stages(mi_dl_ctrl_t* c, uint32_t mask, void* stream) {
+  if (!c) { mi::set_error("null argument"); return -1; }
+  c->last = reinterpret_cast<hipStream_t>(stream);
+  c->have_res = false;
+  return c->ce.run(c->b->eng.d_grid.as<float2>(), c->b->eng.d_ce.as<float2>(), mask, 0.0f, c->last);
+}
+int mi_dl_ctrl_run(mi_dl_ctrl_t* c, void* stream) { return mi_dl_ctrl_run_stages(c, 7u, stream); }
+
+int mi_dl_ctrl_result(mi_dl_ctrl_t* c, uint32_t sf, int ul, uint32_t* cfi, uint32_t* format, uint32_t* L,
+                      uint32_t* ncce, uint8_t* bits, uint32_t* nbits) {
+  if (!c || sf >= c->ce.sfs.size()) { mi::set_error("bad subframe"); return -1; }
+  if (!c->have_res) {
+    c->cfi.resize(c->ce.sfs.size());
+    if (c->ce.download(c->last) ||
+        !mi::hip_ok(hipMemcpy(c->cfi.data(), c->ce.d_cfi.p, c->cfi.size() * 4, hipMemcpyDeviceToHost), "D2H"))
+      return -1;
+    c->have_res = true;
+  }
+  if (cfi) *cfi = c->cfi[sf];
+  const mi::DciFound f = c->ce.select(sf, ul != 0, false);
+  if (!f.found) return 0;
+  if (format) *format = f.format;
+  if (L) *L = f.L;
+  if (ncce) *ncce = f.ncce;
+  if (nbits) *nbits = f.nbits;
+  if (bits) memcpy(bits, f.bits, f.nbits);
+  return 1;
+}
+
+size_t mi_dl_ctrl_llr_floats(const mi_dl_ctrl_t* c) { return c ? c->ce.llr_floats : 0; }
+size_t mi_dl_ctrl_llr_offset(const mi_dl_ctrl_t* c, uint32_t sf) {
+  return (c && sf < c->ce.sfs.size()) ? c->ce.sfs[sf].llr_off : 0;
+}
+uint32_t mi_dl_ctrl_n_cce(const mi_dl_ctrl_t* c, uint32_t sf) {
+  return (c && sf < c->ce.sfs.size()) ? c->ce.sfs[sf].n_cce : 0;
+}
+int mi_dl_ctrl_llr(mi_dl_ctrl_t* c, float* host, size_t n, int upload) {
+  if (!c || n > c->ce.llr_floats) { mi::set_error("llr size"); return -1; }
+  const bool ok = upload ? mi::hip_ok(hipMemcpy(c->ce.d_llr.p, host, n * 4, hipMemcpyHostToDevice), "H2D")
+                         : (mi::hip_ok(hipStreamSynchronize(c->last), "sync") &&
+                            mi::hip_ok(hipMemcpy(host, c->ce.d_llr.p, n * 4, hipMemcpyDeviceToHost), "D2H"));
+  return ok ? 0 : -1;
+}
+
+}  // extern "C"

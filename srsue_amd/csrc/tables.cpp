@@ -267,4 +267,107 @@ void cfi_codeword(uint32_t cfi, uint8_t* b) {
   for (int i = 0; i < 32; i++) b[i] = (cfi >= 1 && cfi <= 3) ? pat[cfi - 1][i % 3] : 0;
 }
 
+// ---- DL control ---------------------------------------------------------------------------------
+static const uint8_t P_CONV[32] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
+                                   0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
+
+uint32_t phich_ngroups(uint32_t nof_prb, uint32_t ng) {
+  static const uint32_t num[4] = {1, 3, 6, 12};   // Ng = num / 6; N_group = ceil(Ng N_RB / 8)
+  return (num[ng & 3] * nof_prb + 47) / 48;
+}
+
+uint32_t pdcch_regs(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t cfi, std::vector<uint32_t>* re4) {
+  const uint32_t W = 12 * nof_prb, L = (uint32_t)ctrl_symbols(nof_prb, cfi), n0 = 2 * nof_prb;
+  std::vector<uint8_t> used0(n0, 0);
+  const uint32_t kbar = 6 * (id % (2 * nof_prb));
+  for (uint32_t i = 0; i < 4; i++) used0[((kbar + (i * nof_prb / 2) * 6) % W) / 6] = 1;   // PCFICH
+  std::vector<uint32_t> free0;
+  for (uint32_t r = 0; r < n0; r++) if (!used0[r]) free0.push_back(r);
+  const uint32_t nf = (uint32_t)free0.size(), ngr = phich_ngroups(nof_prb, ng);
+  for (uint32_t m = 0; m < ngr; m++)                                                      // PHICH
+    for (uint32_t i = 0; i < 3; i++) used0[free0[(id + m + (i * nf) / 3) % nf]] = 2;
+  if (re4) re4->clear();
+  const uint32_t vs3 = (id % 6) % 3;
+  uint32_t n = 0;
+  for (uint32_t k = 0; k < W; k++)
+    for (uint32_t l = 0; l < L; l++) {
+      const bool start = l == 0 ? (k % 6 == 0) : (k % 4 == 0);
+      if (!start || (l == 0 && used0[k / 6])) continue;
+      if (re4) {
+        if (l == 0) {
+          for (uint32_t kk = k; kk < k + 6; kk++) if (kk % 3 != vs3) re4->push_back(kk);
+        } else {
+          for (uint32_t i = 0; i < 4; i++) re4->push_back(l * W + k + i);
+        }
+      }
+      n++;
+    }
+  return n;
+}
+
+void pdcch_quad_perm(uint32_t M, uint32_t id, std::vector<uint32_t>& log_of_reg) {
+  const uint32_t R = (M + 31) / 32, ND = 32 * R - M;
+  std::vector<uint32_t> w;
+  w.reserve(M);
+  for (uint32_t col = 0; col < 32; col++)
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t y = r * 32 + P_CONV[col];
+      if (y >= ND) w.push_back(y - ND);
+    }
+  log_of_reg.resize(M);
+  for (uint32_t i = 0; i < M; i++) log_of_reg[i] = w[(i + id) % M];
+}
+
+static uint32_t ceil_log2(uint32_t x) {
+  uint32_t n = 0;
+  while ((1u << n) < x) n++;
+  return n;
+}
+static bool dci_ambiguous(uint32_t n) {
+  return n == 12 || n == 14 || n == 16 || n == 20 || n == 24 || n == 26 || n == 32 || n == 40 || n == 44 || n == 56;
+}
+uint32_t dci_size(int format, uint32_t nof_prb) {
+  const uint32_t rba = ceil_log2(nof_prb * (nof_prb + 1) / 2);
+  uint32_t n01a = 15 + rba;   // 1A = 15 + RBA >= format 0 = 14 + RBA (FDD)
+  if (dci_ambiguous(n01a)) n01a++;
+  if (format != DCI_1) return n01a;
+  const uint32_t P = nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4;
+  uint32_t s1 = (nof_prb > 10 ? 1 : 0) + (nof_prb + P - 1) / P + 13;
+  if (s1 == n01a) s1++;
+  while (dci_ambiguous(s1)) s1++;
+  return s1;
+}
+
+void conv_rank_table(uint32_t D, std::vector<uint32_t>& rank) {
+  const uint32_t R = (D + 31) / 32, KP = 32 * R, ND = KP - D;
+  rank.assign(3 * D, 0);
+  uint32_t cnt = 0;
+  for (uint32_t i = 0; i < 3; i++)
+    for (uint32_t col = 0; col < 32; col++)
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t y = r * 32 + P_CONV[col];
+        if (y >= ND) rank[i * D + (y - ND)] = cnt++;
+      }
+}
+
+int search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, bool common, uint32_t* Ls, uint32_t* ncce) {
+  static const uint32_t LU[4] = {1, 2, 4, 8}, MU[4] = {6, 6, 2, 2}, LC[2] = {4, 8}, MC[2] = {4, 2};
+  uint32_t Y = 0;
+  if (!common) {
+    Y = rnti;
+    for (uint32_t k = 0; k <= sf; k++) Y = (39827u * Y) % 65537u;
+  }
+  int n = 0;
+  for (int li = 0; li < (common ? 2 : 4); li++) {
+    const uint32_t L = common ? LC[li] : LU[li], M = common ? MC[li] : MU[li], nl = n_cce / L;
+    if (!nl) continue;
+    for (uint32_t m = 0; m < M; m++) {
+      Ls[n] = L;
+      ncce[n] = L * ((Y + m) % nl);
+      n++;
+    }
+  }
+  return n;
+}
+
 }  // namespace mi

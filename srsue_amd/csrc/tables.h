@@ -37,4 +37,19 @@ void pcfich_k(uint32_t id, uint32_t nof_prb, uint32_t* k16);
 uint32_t pcfich_cinit(uint32_t id, uint32_t sf);
 void cfi_codeword(uint32_t cfi, uint8_t* b32);                       // 36.212 Table 5.3.4-1
 
+// ---- DL control: 36.211 6.2.4 / 6.7.4 / 6.8.5 / 6.9.3, 36.212 5.1.4.2 / 5.3.3,
+// 36.213 9.1.1.  Same restatement as oracle/o_ctrl.c (which documents the spec walk-through).
+uint32_t phich_ngroups(uint32_t nof_prb, uint32_t ng);               // ng: 0..3 = Ng 1/6, 1/2, 1, 2
+// PDCCH REGs (not PCFICH / PHICH) in 6.8.5 mapping order, 4 RE indices each; returns N_REG
+uint32_t pdcch_regs(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t cfi, std::vector<uint32_t>* re4);
+// logical quadruplet carried by each physical REG (quadruplet sub-block interleaver + shift by N_ID)
+void pdcch_quad_perm(uint32_t M, uint32_t id, std::vector<uint32_t>& log_of_reg);
+enum { DCI_0 = 0, DCI_1 = 1, DCI_1A = 2 };
+uint32_t dci_size(int format, uint32_t nof_prb);
+// circular-buffer rank of each coded bit p of the rate-1/3 tail-biting code (d0 | d1 | d2, D each):
+// e_k lands on the position of rank k mod 3D
+void conv_rank_table(uint32_t D, std::vector<uint32_t>& rank);
+// 36.213 9.1.1 candidates (L, first CCE) in search order; returns the count (<= 16)
+int search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, bool common, uint32_t* L, uint32_t* ncce);
+
 }  // namespace mi
