@@ -138,10 +138,37 @@ typedef struct SRSLTE_API {
   uint32_t ncce;
 } srslte_dci_location_t;
 
+/* PDCCH (srslte_pdcch_extract_llr, phch_worker.cc:260): soft bits and blind search on the GPU
+ * (srsue_amd/csrc/ctrl.hip); ctx = the owning srslte_ue_dl_t's device context */
 typedef struct SRSLTE_API {
-  srslte_cell_t cell;   /* PDCCH decoding stays on the host in srsLTE */
+  srslte_cell_t cell;
   uint32_t nof_cce;
+  struct mi_ue_dl_ctx *ctx;
 } srslte_pdcch_t;
+
+#define SRSLTE_DCI_MAX_BITS 64
+typedef enum { SRSLTE_DCI_FORMAT0 = 0, SRSLTE_DCI_FORMAT1, SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1C,
+               SRSLTE_DCI_FORMAT_ERROR } srslte_dci_format_t;
+typedef enum { SRSLTE_RA_ALLOC_TYPE0 = 0, SRSLTE_RA_ALLOC_TYPE1, SRSLTE_RA_ALLOC_TYPE2 } srslte_ra_type_t;
+/* DCI message (srslte_ue_dl_find_dl_dci_type output, phch_worker.cc:293; srsUE reads nof_bits, data) */
+typedef struct SRSLTE_API {
+  uint8_t data[SRSLTE_DCI_MAX_BITS];
+  uint32_t nof_bits;
+  srslte_dci_format_t format;
+} srslte_dci_msg_t;
+/* unpacked DL DCI (srslte_dci_msg_to_dl_grant, phch_worker.cc:297; srsUE reads ndi, harq_process,
+ * rv_idx at :304-308) */
+typedef struct SRSLTE_API {
+  srslte_ra_type_t alloc_type;
+  uint32_t type2_start, type2_len;   /* RIV-decoded localized allocation (format 1A) */
+  uint32_t type0_alloc;              /* RBG bitmap (format 1), RBG 0 = MSB of the field */
+  uint32_t mcs_idx;
+  uint32_t harq_process;
+  bool ndi;
+  uint32_t rv_idx;
+  uint32_t tpc_pucch;
+  srslte_dci_format_t dci_format;
+} srslte_ra_dl_dci_t;
 
 /* srslte_ue_dl_t, owned by value per phch_worker (phch_worker.h:111) */
 typedef struct SRSLTE_API {
@@ -174,6 +201,24 @@ SRSLTE_API void srslte_ue_dl_set_rnti(srslte_ue_dl_t *q, uint16_t rnti);
 SRSLTE_API int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t *q, cf_t *input, uint32_t sf_idx, uint32_t *cfi);
 SRSLTE_API int srslte_ue_dl_cfg_grant(srslte_ue_dl_t *q, srslte_ra_dl_grant_t *grant, uint32_t cfi, uint32_t sf_idx,
                                       uint32_t rvidx);
+
+/* ---- PDCCH / DCI (phch_worker.cc:260, 293, 297, 314, 426) --------------------------------------
+ * Blind search order: UE-specific space L = 1, 2, 4, 8 (formats 1A then 1), then the common space
+ * L = 4, 8 (format 1A); SI/RA/P-RNTI search the common space only.  find_* return 1 when found.
+ * dci_msg_to_dl_grant: formats 1A (localized RIV) and 1 (type-0 RBG bitmap); the TBS comes from the
+ * spot columns this library carries (N_PRB = 6, 25, 50, 100), other allocations return an error. */
+SRSLTE_API int srslte_pdcch_extract_llr(srslte_pdcch_t *q, cf_t *sf_symbols, cf_t *ce[SRSLTE_MAX_PORTS],
+                                        float noise_estimate, uint32_t nsubframe, uint32_t cfi);
+SRSLTE_API int srslte_ue_dl_find_dl_dci(srslte_ue_dl_t *q, srslte_dci_msg_t *dci_msg, uint32_t cfi, uint32_t sf_idx,
+                                        uint16_t rnti);
+SRSLTE_API int srslte_ue_dl_find_dl_dci_type(srslte_ue_dl_t *q, srslte_dci_msg_t *dci_msg, uint32_t cfi,
+                                             uint32_t sf_idx, uint16_t rnti, srslte_rnti_type_t rnti_type);
+SRSLTE_API int srslte_ue_dl_find_ul_dci(srslte_ue_dl_t *q, srslte_dci_msg_t *dci_msg, uint32_t cfi, uint32_t sf_idx,
+                                        uint16_t rnti);
+SRSLTE_API uint32_t srslte_ue_dl_get_ncce(srslte_ue_dl_t *q);
+SRSLTE_API int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t *msg, uint16_t msg_rnti, uint32_t nof_prb,
+                                          srslte_ra_dl_dci_t *dl_dci, srslte_ra_dl_grant_t *grant);
+SRSLTE_API char *srslte_ra_dl_dci_string(srslte_ra_dl_dci_t *dci);
 
 /* ---- PDSCH (phch_worker.cc:347-348, :360, :848; :88) ------------------------------------------ */
 SRSLTE_API int srslte_pdsch_decode_rnti(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,

@@ -6,11 +6,14 @@
 // (srsUE reads them on the host for PDCCH, phch_worker.cc:260).  Re-entrant per instance, no
 // global mutable state besides the cached read-only spec tables inside each Engine.
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/srslte/srslte.h"
+#include "ctrl.h"
 #include "engine.h"
+#include "tables.h"
 
 struct mi_ue_dl_ctx {
   mi::Engine eng;
@@ -21,54 +24,31 @@ struct mi_ue_dl_ctx {
   bool fft_done = false;
   cf_t* host_grid = nullptr;
   cf_t* host_ce[SRSLTE_MAX_PORTS] = {};
+  mi::CtrlEngine ctrl;     // PCFICH / PDCCH / DCI blind search over eng's grid and ce (ctrl.hip)
+  uint32_t phich_ng = 0;
+  bool llr_done = false;
 };
 
 namespace {
 
-void pcfich_host(const srslte_cell_t& cell, uint32_t sf, const cf_t* grid, cf_t* const* ce, uint32_t* cfi_out) {
-  uint32_t kk[16];
-  mi::pcfich_k(cell.id, cell.nof_prb, kk);
-  const float* g = reinterpret_cast<const float*>(grid);
-  const float* h0 = reinterpret_cast<const float*>(ce[0]);
-  const float* h1 = cell.nof_ports == 2 ? reinterpret_cast<const float*>(ce[1]) : nullptr;
-  float xr[16], xi[16];
-  for (int i = 0; i < 16; i += (h1 ? 2 : 1)) {
-    if (!h1) {
-      const float yr = g[2 * kk[i]], yi = g[2 * kk[i] + 1], hr = h0[2 * kk[i]], hi = h0[2 * kk[i] + 1];
-      const float den = hr * hr + hi * hi + 1e-9f;
-      xr[i] = (yr * hr + yi * hi) / den;
-      xi[i] = (yi * hr - yr * hi) / den;
-    } else {
-      const uint32_t a = kk[i], b = kk[i + 1];
-      const float r0r = g[2 * a], r0i = g[2 * a + 1], r1r = g[2 * b], r1i = g[2 * b + 1];
-      const float h00r = h0[2 * a], h00i = h0[2 * a + 1], h01r = h0[2 * b], h01i = h0[2 * b + 1];
-      const float h10r = h1[2 * a], h10i = h1[2 * a + 1], h11r = h1[2 * b], h11i = h1[2 * b + 1];
-      float hh = h00r * h00r + h00i * h00i + h11r * h11r + h11i * h11i;
-      if (hh <= 0) hh = 1e-9f;
-      const float s = 1.41421356f / hh;
-      xr[i] = s * ((h00r * r0r + h00i * r0i) + (h11r * r1r + h11i * r1i));
-      xi[i] = s * ((h00r * r0i - h00i * r0r) + (h11i * r1r - h11r * r1i));
-      xr[i + 1] = s * (-(h10r * r0r + h10i * r0i) + (h01r * r1r + h01i * r1i));
-      xi[i + 1] = s * (-(h10i * r0r - h10r * r0i) + (h01r * r1i - h01i * r1r));
-    }
-  }
-  uint8_t sc[32];
-  mi::gold_bits(mi::pcfich_cinit(cell.id, sf), 32, sc);
-  float llr[32];
-  for (int i = 0; i < 16; i++) {   // QPSK max-log LLR (> 0 => bit 1), descrambled
-    llr[2 * i] = -xr[i] * (sc[2 * i] ? -1.f : 1.f);
-    llr[2 * i + 1] = -xi[i] * (sc[2 * i + 1] ? -1.f : 1.f);
-  }
-  float best = -1e30f;
-  uint32_t bc = 0;
-  for (uint32_t c = 1; c <= 3; c++) {
-    uint8_t cw[32];
-    mi::cfi_codeword(c, cw);
-    float s = 0;
-    for (int i = 0; i < 32; i++) s += cw[i] ? llr[i] : -llr[i];
-    if (s > best) { best = s; bc = c; }
-  }
-  *cfi_out = bc;
+// plan the control stage for the instance's single subframe (cheap: tables of one cell / sf / cfi)
+bool ctrl_plan(mi_ue_dl_ctx* c, uint32_t cfi, uint16_t rnti) {
+  return c->ctrl.build(c->eng.plan, std::vector<uint32_t>{cfi}, c->phich_ng, std::vector<uint16_t>{rnti}) == 0 &&
+         c->ctrl.upload(c->st) == 0;
+}
+
+// grid / ce on the device: the copies decode_fft_estimate left are reused when the caller passes this
+// instance's own host mirrors (srsUE passes ue_dl.sf_symbols / ue_dl.ce); other buffers are uploaded
+bool device_grid(mi_ue_dl_ctx* c, const srslte_cell_t& cell, cf_t* sf_symbols, cf_t* const* ce) {
+  const size_t n = (size_t)mi::NSYMB * 12 * cell.nof_prb;
+  bool own = c->fft_done && sf_symbols == c->host_grid;
+  for (uint32_t p = 0; p < cell.nof_ports; p++) own = own && ce[p] == c->host_ce[p];
+  if (own) return true;
+  bool ok = mi::hip_ok(hipMemcpyAsync(c->eng.d_grid.p, sf_symbols, n * 8, hipMemcpyHostToDevice, c->st), "H2D grid");
+  for (uint32_t p = 0; p < cell.nof_ports && ok; p++)
+    ok = mi::hip_ok(hipMemcpyAsync(c->eng.d_ce.as<float2>() + p * n, ce[p], n * 8, hipMemcpyHostToDevice, c->st),
+                    "H2D ce");
+  return ok;
 }
 
 uint32_t mod_bits(srslte_mod_t m) {
@@ -167,8 +147,10 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, srslte_cell_t cell) {
   ctx->cfg.nl_td = 2;
   ctx->host_grid = q->sf_symbols;
   for (int p = 0; p < SRSLTE_MAX_PORTS; p++) ctx->host_ce[p] = q->ce[p];
+  ctx->phich_ng = (uint32_t)cell.phich_resources;
   q->ctx = ctx;
   q->pdsch.ctx = ctx;
+  q->pdcch.ctx = ctx;
   return SRSLTE_SUCCESS;
 }
 
@@ -201,18 +183,23 @@ int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t* q, cf_t* input, uint32_t sf
     return SRSLTE_ERROR;
   if (c->eng.plan.build(&c->cfg, 1, false) || c->eng.upload(c->st, false)) return SRSLTE_ERROR;
   if (c->eng.run(c->d_iq.p, c->st, (1u << MI_DL_STAGE_OFDM) | (1u << MI_DL_STAGE_CHEST), nullptr)) return SRSLTE_ERROR;
+  // PCFICH -> CFI on the GPU (the control plan's PCFICH tables do not depend on the CFI)
+  if (!ctrl_plan(c, 1, q->current_rnti) ||
+      c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 1u, 0.0f, c->st))
+    return SRSLTE_ERROR;
+  uint32_t cf = 0;
   float met[5];
   bool ok = mi::hip_ok(hipMemcpyAsync(q->sf_symbols, c->eng.d_grid.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H");
   for (uint32_t p = 0; p < q->cell.nof_ports && ok; p++)
     ok = mi::hip_ok(hipMemcpyAsync(q->ce[p], c->eng.d_ce.as<float2>() + p * n, n * 8, hipMemcpyDeviceToHost, c->st), "D2H");
   ok = ok && mi::hip_ok(hipMemcpyAsync(met, c->eng.d_metrics.p, sizeof(met), hipMemcpyDeviceToHost, c->st), "D2H") &&
+       mi::hip_ok(hipMemcpyAsync(&cf, c->ctrl.d_cfi.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipStreamSynchronize(c->st), "sync");
   if (!ok) return SRSLTE_ERROR;
   q->chest.rsrp = met[0]; q->chest.rssi = met[1]; q->chest.rsrq = met[2];
   q->chest.noise_estimate = met[3]; q->chest.snr = met[4];
-  uint32_t cf = 0;
-  pcfich_host(q->cell, sf_idx, q->sf_symbols, q->ce, &cf);
   if (cf < 1 || cf > 3) return SRSLTE_ERROR;
+  c->llr_done = false;
   q->cfi = cf;
   c->cfi = cf;
   c->fft_done = true;
@@ -265,19 +252,7 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
   c->eng.max_its = q->dl_sch.max_iterations ? q->dl_sch.max_iterations : SRSLTE_PDSCH_MAX_TDEC_ITERS;
   if (c->eng.plan.build(&s, 1, true) || c->eng.upload(c->st, false)) return SRSLTE_ERROR;
   if (c->eng.plan.sb_floats * sizeof(float) > softbuffer->dev_bytes) return SRSLTE_ERROR;
-  // grid / ce: the device copies left by decode_fft_estimate are reused when the caller passes this
-  // instance's own host mirrors (srsUE passes ue_dl.sf_symbols / ue_dl.ce, phch_worker.cc:347-348);
-  // any other buffers are uploaded.
-  const size_t W = 12 * cell.nof_prb, n = (size_t)mi::NSYMB * W;
-  bool own = c->fft_done && sf_symbols == c->host_grid;
-  for (uint32_t p = 0; p < cell.nof_ports; p++) own = own && ce[p] == c->host_ce[p];
-  bool ok = true;
-  if (!own) {
-    ok = mi::hip_ok(hipMemcpyAsync(c->eng.d_grid.p, sf_symbols, n * 8, hipMemcpyHostToDevice, c->st), "H2D grid");
-    for (uint32_t p = 0; p < cell.nof_ports && ok; p++)
-      ok = mi::hip_ok(hipMemcpyAsync(c->eng.d_ce.as<float2>() + p * n, ce[p], n * 8, hipMemcpyHostToDevice, c->st),
-                      "H2D ce");
-  }
+  bool ok = device_grid(c, cell, sf_symbols, ce);
   if (!ok) return SRSLTE_ERROR;
   const uint32_t stages = (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM) | (1u << MI_DL_STAGE_TDEC) |
                           (1u << MI_DL_STAGE_TB);
@@ -296,6 +271,126 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
 uint32_t srslte_pdsch_last_noi(srslte_pdsch_t* q) { return q ? q->dl_sch.nof_iterations : 0; }
 void srslte_sch_set_max_noi(srslte_sch_t* q, uint32_t max_iterations) {
   if (q && max_iterations > 0) q->max_iterations = max_iterations;
+}
+
+/* ---- PDCCH / DCI --------------------------------------------------------------------------- */
+int srslte_pdcch_extract_llr(srslte_pdcch_t* q, cf_t* sf_symbols, cf_t* ce[SRSLTE_MAX_PORTS], float noise_estimate,
+                             uint32_t nsubframe, uint32_t cfi) {
+  if (!q || !q->ctx || !sf_symbols || !ce || cfi < 1 || cfi > 3 || nsubframe > 9) return SRSLTE_ERROR_INVALID_INPUTS;
+  mi_ue_dl_ctx* c = q->ctx;
+  if (c->sf_idx != nsubframe || !c->fft_done) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (!device_grid(c, q->cell, sf_symbols, ce) || !ctrl_plan(c, cfi, 0) ||
+      c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 2u, noise_estimate, c->st))
+    return SRSLTE_ERROR;
+  c->cfi = cfi;
+  c->llr_done = true;
+  q->nof_cce = c->ctrl.sfs[0].n_cce;
+  return SRSLTE_SUCCESS;
+}
+
+static int find_dci(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t cfi, uint32_t sf_idx, uint16_t rnti, bool ul,
+                    bool common_only) {
+  if (!q || !q->ctx || !msg || cfi < 1 || cfi > 3 || sf_idx > 9) return SRSLTE_ERROR_INVALID_INPUTS;
+  mi_ue_dl_ctx* c = q->ctx;
+  if (!c->llr_done || c->cfi != cfi || c->sf_idx != sf_idx) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (!ctrl_plan(c, cfi, rnti) || c->ctrl.run(nullptr, nullptr, 4u, 0.0f, c->st) || c->ctrl.download(c->st))
+    return SRSLTE_ERROR;
+  const mi::DciFound f = c->ctrl.select(0, ul, common_only);
+  if (!f.found) return 0;
+  memset(msg, 0, sizeof(*msg));
+  memcpy(msg->data, f.bits, f.nbits);
+  msg->nof_bits = f.nbits;
+  msg->format = f.format == mi::DCI_0 ? SRSLTE_DCI_FORMAT0 : f.format == mi::DCI_1 ? SRSLTE_DCI_FORMAT1
+                                                                                  : SRSLTE_DCI_FORMAT1A;
+  q->last_location.L = f.L;
+  q->last_location.ncce = f.ncce;
+  q->last_n_cce = f.ncce;
+  return 1;
+}
+
+int srslte_ue_dl_find_dl_dci_type(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t cfi, uint32_t sf_idx,
+                                  uint16_t rnti, srslte_rnti_type_t type) {
+  const bool common = type == SRSLTE_RNTI_SI || type == SRSLTE_RNTI_RAR || type == SRSLTE_RNTI_PCH;
+  return find_dci(q, msg, cfi, sf_idx, rnti, false, common);
+}
+int srslte_ue_dl_find_dl_dci(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t cfi, uint32_t sf_idx, uint16_t rnti) {
+  return find_dci(q, msg, cfi, sf_idx, rnti, false, false);
+}
+int srslte_ue_dl_find_ul_dci(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t cfi, uint32_t sf_idx, uint16_t rnti) {
+  return find_dci(q, msg, cfi, sf_idx, rnti, true, false);
+}
+uint32_t srslte_ue_dl_get_ncce(srslte_ue_dl_t* q) { return q ? q->last_n_cce : 0; }
+
+static uint32_t take_bits(const uint8_t* b, uint32_t* pos, uint32_t n) {
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < n; i++) v = (v << 1) | b[(*pos)++];
+  return v;
+}
+
+int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t* msg, uint16_t /*msg_rnti*/, uint32_t nof_prb, srslte_ra_dl_dci_t* dci,
+                               srslte_ra_dl_grant_t* grant) {
+  if (!msg || !dci || !grant || mi::symbol_sz(nof_prb) < 0) return SRSLTE_ERROR_INVALID_INPUTS;
+  memset(dci, 0, sizeof(*dci));
+  memset(grant, 0, sizeof(*grant));
+  const uint32_t n1a = mi::dci_size(mi::DCI_1A, nof_prb), n1 = mi::dci_size(mi::DCI_1, nof_prb);
+  uint32_t pos = 0;
+  if (msg->nof_bits == n1a && msg->data[0] == 1) {
+    // format 1A (36.212 5.3.3.1.3): flag, localized VRB, RIV, MCS, HARQ, NDI, RV, TPC
+    uint32_t rba = 0;
+    while ((1u << rba) < nof_prb * (nof_prb + 1) / 2) rba++;
+    pos = 1;
+    if (take_bits(msg->data, &pos, 1)) return SRSLTE_ERROR;   // distributed VRB: not supported
+    const uint32_t riv = take_bits(msg->data, &pos, rba), a = riv / nof_prb, b = riv % nof_prb;
+    uint32_t L, start;
+    if (a + b < nof_prb) { L = a + 1; start = b; }
+    else { L = nof_prb - a + 1; start = nof_prb - 1 - b; }
+    if (start + L > nof_prb) return SRSLTE_ERROR;
+    dci->alloc_type = SRSLTE_RA_ALLOC_TYPE2;
+    dci->type2_start = start;
+    dci->type2_len = L;
+    dci->dci_format = SRSLTE_DCI_FORMAT1A;
+    for (uint32_t p = start; p < start + L; p++) grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
+    grant->nof_prb = L;
+  } else if (msg->nof_bits == n1) {
+    // format 1 (36.212 5.3.3.1.2), type-0 allocation: [header], RBG bitmap, MCS, HARQ, NDI, RV, TPC
+    const uint32_t P = nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4, nrbg = (nof_prb + P - 1) / P;
+    if (nof_prb > 10 && take_bits(msg->data, &pos, 1)) return SRSLTE_ERROR;   // type 1: not supported
+    dci->alloc_type = SRSLTE_RA_ALLOC_TYPE0;
+    dci->dci_format = SRSLTE_DCI_FORMAT1;
+    for (uint32_t g = 0; g < nrbg; g++) {
+      const uint32_t bit = take_bits(msg->data, &pos, 1);
+      dci->type0_alloc = (dci->type0_alloc << 1) | bit;
+      for (uint32_t p = g * P; bit && p < (g + 1) * P && p < nof_prb; p++) {
+        grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
+        grant->nof_prb++;
+      }
+    }
+  } else {
+    return SRSLTE_ERROR;
+  }
+  dci->mcs_idx = take_bits(msg->data, &pos, 5);
+  dci->harq_process = take_bits(msg->data, &pos, 3);
+  dci->ndi = take_bits(msg->data, &pos, 1) != 0;
+  dci->rv_idx = take_bits(msg->data, &pos, 2);
+  dci->tpc_pucch = take_bits(msg->data, &pos, 2);
+  uint32_t qm = 0;
+  const int itbs = mi::mcs_to_itbs(dci->mcs_idx, &qm);
+  const int tbs = itbs < 0 ? -1 : mi::tbs_from_idx((uint32_t)itbs, grant->nof_prb);
+  if (tbs <= 0) return SRSLTE_ERROR;
+  grant->Qm = qm;
+  grant->mcs.idx = dci->mcs_idx;
+  grant->mcs.tbs = tbs;
+  grant->mcs.mod = qm == 2 ? SRSLTE_MOD_QPSK : qm == 4 ? SRSLTE_MOD_16QAM : SRSLTE_MOD_64QAM;
+  return SRSLTE_SUCCESS;
+}
+
+char* srslte_ra_dl_dci_string(srslte_ra_dl_dci_t* dci) {
+  static thread_local char buf[96];
+  if (!dci) return buf;
+  snprintf(buf, sizeof(buf), "format=%s, mcs=%u, harq=%u, ndi=%d, rv=%u",
+           dci->dci_format == SRSLTE_DCI_FORMAT1 ? "1" : "1A", dci->mcs_idx, dci->harq_process, (int)dci->ndi,
+           dci->rv_idx);
+  return buf;
 }
 
 /* ---- chest metrics ------------------------------------------------------------------------- */

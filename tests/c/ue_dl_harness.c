@@ -6,9 +6,14 @@
  *   per TTI:   srslte_ue_dl_decode_fft_estimate (:254), srslte_ue_dl_cfg_grant (:337),
  *              srslte_pdsch_decode_rnti(.., ue_dl.sf_symbols, ue_dl.ce, 0.01, ..) (:347-348),
  *              srslte_pdsch_last_noi (:360), srslte_chest_dl_get_* (:799-848)
- * Input file : int32 hdr[8] = {cell_id, nof_prb, nof_ports, nsf}; per subframe int32 p[8] =
- *              {sf_idx, tbs, Qm, rv, reset_tbs, rnti, max_its, pass_own_buffers} + 2*SF_LEN floats.
- * Output file: per subframe int32 r[8] = {ret, cfi, noi} + float m[5] + tbs/8 payload bytes.
+ *   PDCCH mode (hdr[5] = 1): srslte_pdcch_extract_llr (:260), srslte_ue_dl_find_dl_dci_type (:293),
+ *              srslte_dci_msg_to_dl_grant (:297), srslte_ue_dl_get_ncce (:314); the PDSCH grant and
+ *              rv come from the decoded DCI (p[2], p[3] unused)
+ * Input file : int32 hdr[8] = {cell_id, nof_prb, nof_ports, nsf, phich_ng, pdcch_mode}; per subframe
+ *              int32 p[8] = {sf_idx, tbs, Qm, rv, reset_tbs, rnti, max_its, pass_own_buffers} +
+ *              2*SF_LEN floats.
+ * Output file: per subframe int32 r[8] = {ret, cfi, noi, dci_found, ncce, grant_tbs, harq, rv} +
+ *              float m[5] + tbs/8 payload bytes.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -26,6 +31,9 @@ int main(int argc, char **argv) {
   memset(&cell, 0, sizeof(cell));
   cell.id = (uint32_t)hdr[0]; cell.nof_prb = (uint32_t)hdr[1]; cell.nof_ports = (uint32_t)hdr[2];
   cell.cp = SRSLTE_CP_NORM;
+  cell.phich_length = SRSLTE_PHICH_NORM;
+  cell.phich_resources = (srslte_phich_resources_t)hdr[4];
+  const int pdcch_mode = hdr[5];
   if (!srslte_check_version(1, 0, 0)) { fprintf(stderr, "version\n"); return 3; }
   srslte_ue_dl_t ue_dl;
   if (srslte_ue_dl_init(&ue_dl, cell)) { fprintf(stderr, "ue_dl_init\n"); return 3; }
@@ -44,15 +52,36 @@ int main(int argc, char **argv) {
     float m[5] = {0};
     uint32_t cfi = 0;
     int ret = srslte_ue_dl_decode_fft_estimate(&ue_dl, buf, (uint32_t)p[0], &cfi);
-    if (ret >= 0) {
-      srslte_ra_dl_grant_t grant;
-      memset(&grant, 0, sizeof(grant));
+    if (ret < 0) ret = -9;
+    srslte_ra_dl_grant_t grant;
+    memset(&grant, 0, sizeof(grant));
+    uint32_t rv = (uint32_t)p[3];
+    if (ret >= 0 && pdcch_mode) {
+      srslte_dci_msg_t msg;
+      srslte_ra_dl_dci_t dci;
+      if (srslte_pdcch_extract_llr(&ue_dl.pdcch, ue_dl.sf_symbols, ue_dl.ce, 0, (uint32_t)p[0], cfi)) {
+        ret = -11;
+      } else if ((r[3] = srslte_ue_dl_find_dl_dci_type(&ue_dl, &msg, cfi, (uint32_t)p[0], (uint16_t)p[5],
+                                                        SRSLTE_RNTI_USER)) != 1) {
+        ret = -12;
+      } else if (srslte_dci_msg_to_dl_grant(&msg, (uint16_t)p[5], cell.nof_prb, &dci, &grant)) {
+        ret = -13;
+      } else {
+        r[4] = (int32_t)srslte_ue_dl_get_ncce(&ue_dl);
+        r[5] = grant.mcs.tbs;
+        r[6] = (int32_t)dci.harq_process;
+        r[7] = (int32_t)dci.rv_idx;
+        rv = dci.rv_idx;
+      }
+    } else if (ret >= 0) {
       for (uint32_t q = 0; q < cell.nof_prb; q++) grant.prb_idx[0][q] = grant.prb_idx[1][q] = true;
       grant.nof_prb = cell.nof_prb;
       grant.Qm = (uint32_t)p[2];
       grant.mcs.mod = p[2] == 2 ? SRSLTE_MOD_QPSK : p[2] == 4 ? SRSLTE_MOD_16QAM : SRSLTE_MOD_64QAM;
       grant.mcs.tbs = p[1];
-      if (srslte_ue_dl_cfg_grant(&ue_dl, &grant, cfi, (uint32_t)p[0], (uint32_t)p[3])) {
+    }
+    if (ret >= 0) {
+      if (srslte_ue_dl_cfg_grant(&ue_dl, &grant, cfi, (uint32_t)p[0], rv)) {
         ret = -10;
       } else if (ue_dl.pdsch_cfg.grant.mcs.mod > 0 && ue_dl.pdsch_cfg.grant.mcs.tbs >= 0) {
         cf_t *grid = ue_dl.sf_symbols;
@@ -75,6 +104,7 @@ int main(int argc, char **argv) {
       }
     }
     r[0] = ret; r[1] = (int32_t)cfi; r[2] = (int32_t)srslte_pdsch_last_noi(&ue_dl.pdsch);
+    if (!pdcch_mode) r[3] = r[4] = r[5] = r[6] = r[7] = 0;
     m[0] = srslte_chest_dl_get_rsrp(&ue_dl.chest); m[1] = srslte_chest_dl_get_rssi(&ue_dl.chest);
     m[2] = srslte_chest_dl_get_rsrq(&ue_dl.chest); m[3] = srslte_chest_dl_get_noise_estimate(&ue_dl.chest);
     m[4] = srslte_chest_dl_get_snr(&ue_dl.chest);

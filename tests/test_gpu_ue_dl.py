@@ -17,12 +17,12 @@ pytestmark = pytest.mark.gpu
 HARNESS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "ue_dl_harness")
 
 
-def run_harness(cell_id, nof_prb, nof_ports, subframes):
+def run_harness(cell_id, nof_prb, nof_ports, subframes, phich_ng=0, pdcch=False, full=False):
     """subframes: list of (cfg, iq, reset_tbs, max_its, own_buffers)"""
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
         with open(fin, "wb") as f:
-            f.write(struct.pack("8i", cell_id, nof_prb, nof_ports, len(subframes), 0, 0, 0, 0))
+            f.write(struct.pack("8i", cell_id, nof_prb, nof_ports, len(subframes), phich_ng, int(pdcch), 0, 0))
             for cfg, iq, reset, max_its, own in subframes:
                 f.write(struct.pack("8i", cfg.sf_idx, cfg.tbs, cfg.Qm, cfg.rv, int(reset), cfg.rnti, max_its,
                                     int(own)))
@@ -34,7 +34,7 @@ def run_harness(cell_id, nof_prb, nof_ports, subframes):
             r = struct.unpack_from("8i", raw, pos); pos += 32
             m = struct.unpack_from("5f", raw, pos); pos += 20
             pay = np.frombuffer(raw[pos:pos + cfg.tbs // 8], np.uint8); pos += cfg.tbs // 8
-            out.append((r[0], r[1], r[2], m, pay))
+            out.append((r[0], r[1], r[2], m, pay) + ((r[3:],) if full else ()))
         return out
 
 
@@ -77,3 +77,45 @@ def test_ue_dl_harq_soft_combining():
     assert res[0][2] == noi0
     assert res[1][0] == 0 and ok1
     assert np.array_equal(res[1][4], tb) and np.array_equal(res[1][4], pay1) and res[1][2] == noi1
+
+
+def test_ue_dl_pdcch_to_pdsch_srsue_call_order():
+    """SURVEY 8f-1 end to end through the per-TTI ABI in srsUE's order: the grant is NOT given to the
+    harness -- it blind-decodes the DCI 1A the transmitter put on the PDCCH (GPU PCFICH, PDCCH soft
+    bits, blind search), converts it with srslte_dci_msg_to_dl_grant and decodes the PDSCH with it."""
+    import ctypes as C
+    import oracle_lib as O
+    from test_oracle_ctrl import tx_with_dci
+    rnti, ng = 0x3C, 2
+    subs, truth = [], []
+    for i, (ports, cfi, sf, mcs) in enumerate([(1, 1, 1, 28), (2, 2, 3, 20), (1, 3, 6, 9)]):
+        qm, itbs = (2, mcs) if mcs <= 9 else (4, mcs - 1) if mcs <= 16 else (6, mcs - 2)
+        tbs = O.lib().or_tbs(itbs, 100)
+        cfg = abi.sf_cfg(cell_id=11, nof_prb=100, nof_ports=ports, sf_idx=sf, cfi=cfi, tbs=tbs, Qm=qm, rnti=rnti,
+                         rv=i % 2 * 2)
+        tb = tb_bytes(50 + i, tbs)
+        q = O.ctrl_cfg(11, 100, ports, ng, cfi, sf)
+        n = C.c_uint32()
+        O.lib().or_pdcch_regs(C.byref(q), None, C.byref(n))
+        Ls = np.zeros(32, np.uint32)
+        nc = np.zeros(32, np.uint32)
+        k = O.lib().or_search_space(n.value, sf, rnti, 0, Ls, nc)
+        bits = np.zeros(64, np.uint8)
+        A = O.lib().or_dci1a_pack(100, C.byref(O.Dci1a(0, 100, mcs, i + 1, 1, cfg.rv, 1)), bits)
+        h = [0.8 + 0.3j, -0.4 + 0.5j] if ports == 2 else None
+        iq = abi.tx_subframe(cfg, tb, h=h, snr_db=300.0, seed=i)
+        qq = O.ctrl_cfg(11, 100, ports, ng, cfi, sf)
+        hh = None if h is None else np.array([v for z in h for v in (z.real, z.imag)], np.float32)
+        assert O.lib().or_tx_pdcch(C.byref(qq), rnti, int(Ls[k - 1]), int(nc[k - 1]), bits[:A], A,
+                                   None if hh is None else hh.ctypes.data, iq) == 0
+        iq = (iq + np.random.default_rng(i).normal(0, np.sqrt(10 ** -3.0 / 2), iq.shape)).astype(np.float32)
+        subs.append((cfg, iq, True, 4, True))
+        truth.append((tb, int(nc[k - 1]), i + 1, cfg.rv, tbs))
+    res = run_harness(11, 100, 1, subs[:1], phich_ng=ng, pdcch=True, full=True)
+    res += run_harness(11, 100, 2, subs[1:2], phich_ng=ng, pdcch=True, full=True)
+    res += run_harness(11, 100, 1, subs[2:], phich_ng=ng, pdcch=True, full=True)
+    for (cfg, *_), (ret, cf, noi, met, pay, extra), (tb, ncce, harq, rv, tbs) in zip(subs, res, truth):
+        found, gncce, gtbs, gharq, grv = extra
+        assert cf == cfg.cfi and found == 1 and gncce == ncce
+        assert (gtbs, gharq, grv) == (tbs, harq, rv)
+        assert ret == 0 and np.array_equal(pay, tb)
