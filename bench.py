@@ -292,6 +292,28 @@ def bench_codeblocks(args, world, rank, dev):
     return out
 
 
+def bench_ctrl(args, batch, dev):
+    """PCFICH + PDCCH soft bits + DCI blind search (UE-specific + common space, formats 1A / 1) of every
+    subframe of the batch, on the grid / channel estimates the timed steps left in HBM."""
+    ctl = abi.Ctrl(batch, phich_ng=2)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(max(1, args.warmup)):
+        ctl.run(sptr)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctl.run(sptr)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / args.steps
+    B = len(batch.cfgs)
+    cfi = [ctl.result(i)[0] for i in range(0, B, max(1, B // 16))]
+    ctl.close()
+    return {"ms_per_step": round(dt * 1e3, 3), "subframes_per_s": round(B / dt, 1),
+            "cfi_ok": all(c == batch.cfgs[0].cfi for c in cfi),
+            "what": "PCFICH + PDCCH soft bits + blind search (38 candidate x size decodes per subframe) for "
+                    f"{B} subframes per step"}
+
+
 def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
     """IQ resident in page-locked host memory, each step copied H2D and decoded through the
     double-buffered pipeline (copy of step i+1 overlaps the decode of step i)."""
@@ -340,6 +362,9 @@ def main():
     ap.add_argument("--h2d", action="store_true",
                     help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
                          "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
+    ap.add_argument("--ctrl", action="store_true",
+                    help="also time the DL control stage (SURVEY 8f-1: PCFICH + PDCCH soft bits + DCI blind search "
+                         "for each subframe's RNTI) on the batch's grid; reported beside value")
     ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
                     help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
@@ -453,6 +478,8 @@ def main():
         }
         if args.h2d:
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
+        if args.ctrl:
+            out["ctrl"] = bench_ctrl(args, batch, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
                                                args.tdec == "i16")
