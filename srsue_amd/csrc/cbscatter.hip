@@ -2,7 +2,7 @@
 // contract, BASELINE configs[0] = srsLTE turbodecoder_test): decoder inputs d[cb][3(K+4)] in
 // triplet order are written into the group-interleaved layout [N_cb][64] the turbo kernel reads,
 // through the same per-K position table (LDS transpose: coalesced reads of each code block's row,
-// 256-B coalesced row writes).
+// 256-B coalesced row writes); every row is materialised in the sparse-row map.
 #include "kernels.h"
 
 namespace mi {
@@ -28,6 +28,11 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict
   for (uint32_t i = w; i < (uint32_t)SC_T; i += 4) {
     const uint32_t t = t0 + i;
     if (t < T) sbg[(size_t)pos[t] * LANES + q] = tile[q][i];
+  }
+  if (blockIdx.x == 0) {   // every row written: the whole map materialised, plus the zero row
+    uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb));
+    for (uint32_t p = tid; p < g.Ncb; p += 256) map[p] = 1;
+    if (tid < LANES) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;
   }
 }
 

@@ -36,6 +36,7 @@ constexpr int TDEC_CK_Q16 = MI_TDEC_CK_Q16;   // same for the int16 decoder (few
 constexpr int TDEC_CK_MIN = TDEC_CK < TDEC_CK_Q16 ? TDEC_CK : TDEC_CK_Q16;   // scratch sizing
 constexpr float FILLER_LLR = -10000.0f;
 constexpr int RM_CHUNK = 128;        // circular-buffer positions per rate-dematch workgroup
+constexpr int WM_STRIDE = KMAX / BETA_W + 4;   // turbo window masks per group (rowmask_kernel)
 
 __host__ __device__ inline int symbol_sz(uint32_t nof_prb) {
   return nof_prb <= 6 ? 128 : nof_prb <= 15 ? 256 : nof_prb <= 25 ? 512 : nof_prb <= 50 ? 1024
@@ -106,7 +107,7 @@ struct MiGroupDesc {         // one per wavefront group of <= 64 code blocks of 
   uint32_t K, Ncb;
   uint32_t lane0;            // first MiLaneDesc index (64 consecutive entries)
   uint32_t ktab;             // K-table index (pos / pi tables)
-  uint64_t sb_off;           // float offset of the group's softbuffer region [Ncb][64]
+  uint64_t sb_off;           // float offset of the group's softbuffer region (mi::sb_group_floats: rows, zero row, map)
   uint64_t scratch_off;      // float offset of the group's turbo scratch (w, llr1, beta ckpt)
   uint64_t dec_off;          // byte offset of decision bytes [K][64]
 };
@@ -131,6 +132,20 @@ __host__ __device__ inline float q16f(float x) { return clampf(rintf(x * I16_SCA
 // first pass from the softbuffer and read by every later pass.  Fits: 3K + 12 <= 2K + 7 (K/4 + 1) for K >= 7.
 __host__ __device__ inline size_t q16_elem_off(uint32_t K) {
   return (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
+}
+}  // namespace mi
+
+namespace mi {
+// ---- softbuffer region of one group (sparse rows) -------------------------------------------------
+// [Ncb][64] fp32 rows, then one all-zero row (row index Ncb), then the row map: one byte per
+// circular-buffer position, 1 = the row holds the values of all 64 lanes ("materialised"), 0 = every
+// lane's value there is 0 (RX_NULL / never received).  The rate de-matcher writes only rows that
+// receive an LLR (or must keep a HARQ history) and rewrites the map; the turbo decoder fetches
+// unmaterialised rows from the zero row (L2-resident) instead of HBM.  Punctured positions never
+// cost HBM traffic and a reset only needs the map cleared.
+__host__ __device__ inline size_t sb_map_off(uint32_t Ncb) { return (size_t)(Ncb + 1) * LANES; }   // floats
+__host__ __device__ inline size_t sb_group_floats(uint32_t Ncb) {
+  return sb_map_off(Ncb) + (size_t)((Ncb + 255) / 256) * LANES;
 }
 }  // namespace mi
 

@@ -34,20 +34,21 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
     src += G;
   }
   for (const MiGroupDesc& g : P.groups) {
-    for (int lane = 0; lane < mi::LANES; lane++) {
-      const MiLaneDesc& ld = P.lanes[g.lane0 + lane];
-      if (!ld.valid) continue;
-      const int32_t* rank = reinterpret_cast<const int32_t*>(&P.kdata[ld.rank_off]);
-      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_one(ld, rank, e.data(), &sb[g.sb_off], p, lane);
-    }
+    float* sbg = &sb[g.sb_off];
+    uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
+    for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p);
     const MiKTab& kt = P.ktabs[g.ktab];
+    std::vector<uint32_t> wm(g.K / mi::BETA_W + 1);
+    for (uint32_t w = 0; w < wm.size(); w++) wm[w] = mi::tdec_window_mask(map, &P.kdata[kt.pos_off], w);
     int16_t* q16 = reinterpret_cast<int16_t*>(&scr[g.scratch_off]) + mi::q16_elem_off(g.K);
     for (int lane = 0; lane < mi::LANES; lane++) {
       const uint32_t li = g.lane0 + lane;
       const MiLaneDesc& ld = P.lanes[li];
       if (!ld.valid) continue;
       mi::TdecArgs a;
-      a.sb = &sb[g.sb_off];
+      a.sb = sbg;
+      a.wm = wm.data();
+      a.zrow = g.Ncb;
       a.q16 = q16;
       a.pos = &P.kdata[kt.pos_off];
       a.pi = &P.kdata[kt.pi_off];

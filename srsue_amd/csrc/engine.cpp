@@ -75,7 +75,8 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
   ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
   if (P.has_pdsch || P.cb_n) {
-    ok = ok && d_e.ensure(P.e_floats * 4) && d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
+    ok = ok && d_e.ensure(P.e_floats * 4) && d_wm.ensure(P.groups.size() * WM_STRIDE * 4) &&
+         d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
          d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
          d_cbcrc.ensure(P.lanes.size() * 4) && d_cbtbp.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
          d_tbits.ensure(nsf * 4);
@@ -131,12 +132,15 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
     mark(4);
-    if (mask & (1u << MI_DL_STAGE_TDEC))
-      launch_tdec(sb, d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
+    if (mask & (1u << MI_DL_STAGE_TDEC)) {
+      launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
+                     (uint32_t)P.groups.size(), st);
+      launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
                   d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                   d_ktabs.as<MiKTab>(),
                   d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
                   q16(), st);
+    }
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
@@ -170,7 +174,9 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
   launch_cb_scatter(d_in, d_sb.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                     (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
   mark(MI_DL_STAGE_TDEC);
-  launch_tdec(d_sb.as<float>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
+  launch_rowmask(d_sb.as<float>(), d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(),
+                 d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), st);
+  launch_tdec(d_sb.as<float>(), d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
               d_lanes.as<MiLaneDesc>(),
               d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,

@@ -32,7 +32,7 @@ struct Engine {
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,
       d_fftlist, d_tw;
   // data buffers
-  DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,
+  DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_wm, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,
       d_tbits;
   std::map<int, size_t> tw_off;   // FFT size -> float2 offset in d_tw
   hipStream_t last_stream = nullptr;

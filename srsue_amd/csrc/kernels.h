@@ -21,7 +21,10 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
                        const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups,
                        uint32_t max_ncb, hipStream_t st);
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
-void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
+// window masks of the sparse softbuffer rows (which decoder inputs have a materialised row)
+void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,
+                    const uint32_t* kdata, uint32_t n_groups, hipStream_t st);
+void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
                  uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                  const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
                  uint32_t early_stop, bool q16, hipStream_t st);

@@ -175,7 +175,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       g.sb_off = sb_floats;
       g.scratch_off = scratch_floats;
       g.dec_off = dec_bytes;
-      sb_floats += (size_t)Ncb * LANES;
+      sb_floats += sb_group_floats(Ncb);
       scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
       dec_bytes += (size_t)K * LANES;
       groups.push_back(g);
@@ -285,7 +285,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
     g.sb_off = sb_floats;
     g.scratch_off = scratch_floats;
     g.dec_off = dec_bytes;
-    sb_floats += (size_t)Ncb * LANES;
+    sb_floats += sb_group_floats(Ncb);
     scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
     dec_bytes += (size_t)K * LANES;
     groups.push_back(g);

@@ -15,16 +15,42 @@
 
 namespace mi {
 
-MI_HD inline void rm_combine_one(const MiLaneDesc& ld, const int32_t* rank, const float* e, float* sbg, uint32_t p,
-                                 int lane) {
+// value of position p for one lane: `old` (a combining lane's materialised history, else 0) plus the
+// LLRs received there; *got = at least one LLR lands on p
+MI_HD inline float rm_value(const MiLaneDesc& ld, const int32_t* rank, const float* e, float old, uint32_t p, bool* got) {
   const int32_t rk = rank[p];
-  float v = ld.new_tb ? 0.0f : sbg[(size_t)p * LANES + lane];
+  float v = old;
+  *got = false;
   if (rk >= 0) {
     uint32_t j = ((uint32_t)rk + ld.Nv - ld.r0) % ld.Nv;
     const float* el = e + ld.e_off;
-    for (; j < ld.E; j += ld.Nv) v = v + el[j];
+    for (; j < ld.E; j += ld.Nv) { v = v + el[j]; *got = true; }
   }
-  sbg[(size_t)p * LANES + lane] = v;
+  return v;
+}
+
+// row p of a group (all lanes) with the sparse-row rule of rm_combine_kernel: the row is materialised
+// after the launch iff some lane receives an LLR there, or it was materialised and a lane combines
+MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, const float* e, float* sbg,
+                                 uint8_t* map, uint32_t p) {
+  bool comb = false, any = false;
+  for (int l = 0; l < LANES; l++) comb |= lds[l].valid && !lds[l].new_tb;
+  const bool was = map[p] != 0;
+  float v[LANES];
+  for (int l = 0; l < LANES; l++) {
+    const MiLaneDesc& ld = lds[l];
+    v[l] = 0.0f;
+    if (!ld.valid) continue;
+    bool got;
+    const float old = (was && !ld.new_tb) ? sbg[(size_t)p * LANES + l] : 0.0f;
+    v[l] = rm_value(ld, reinterpret_cast<const int32_t*>(kdata + ld.rank_off), e, old, p, &got);
+    any |= got;
+  }
+  const bool mat = any || (was && comb);
+  if (mat)
+    for (int l = 0; l < LANES; l++)
+      if (lds[l].valid) sbg[(size_t)p * LANES + l] = v[l];
+  map[p] = mat ? 1 : 0;
 }
 
 }  // namespace mi

@@ -14,8 +14,8 @@ struct TdecOut {            // per code block (lane index li) results
 };
 
 template <bool Q16>
-__device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* __restrict__ scratch,
-                                           uint8_t* __restrict__ dec, const TdecOut& out,
+__device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const uint32_t* __restrict__ wm,
+                                           float* __restrict__ scratch, uint8_t* __restrict__ dec, const TdecOut& out,
                                            const MiGroupDesc* __restrict__ groups,
                                            const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                                            const uint32_t* __restrict__ kdata, uint32_t max_its,
@@ -25,13 +25,15 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
   for (uint32_t b = threadIdx.x; b < 256; b += 64) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
   __syncthreads();
   const MiGroupDesc g = groups[blockIdx.x];
+  const MiKTab kt = ktabs[g.ktab];
   const int lane = threadIdx.x;
   const uint32_t li = g.lane0 + lane;
   const MiLaneDesc ld = lanes[li];
   if (!ld.valid) return;
-  const MiKTab kt = ktabs[g.ktab];
   TdecArgs a;
   a.sb = sb + g.sb_off;
+  a.wm = wm + (size_t)blockIdx.x * WM_STRIDE;
+  a.zrow = g.Ncb;
   a.q16 = reinterpret_cast<int16_t*>(scratch + g.scratch_off) + q16_elem_off(g.K);
   a.pos = kdata + kt.pos_off;
   a.pi = kdata + kt.pi_off;
@@ -52,14 +54,34 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, float* 
   out.tb_part[li] = r.tb_part;
 }
 
+// window masks of the sparse softbuffer rows: one thread per 4-step window (12 decoder inputs) of a
+// group; bit i = row pos[12w + i] is materialised (dl_common.h sb_group_floats)
+__global__ __launch_bounds__(256) void rowmask_kernel(const float* __restrict__ sb, uint32_t* __restrict__ wm,
+                                                     const MiGroupDesc* __restrict__ groups,
+                                                     const MiKTab* __restrict__ ktabs,
+                                                     const uint32_t* __restrict__ kdata) {
+  const MiGroupDesc g = groups[blockIdx.y];
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  if (w > g.K / BETA_W) return;
+  const uint8_t* map = reinterpret_cast<const uint8_t*>(sb + g.sb_off + sb_map_off(g.Ncb));
+  wm[(size_t)blockIdx.y * WM_STRIDE + w] = tdec_window_mask(map, kdata + ktabs[g.ktab].pos_off, w);
+}
+
+void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,
+                    const uint32_t* kdata, uint32_t n_groups, hipStream_t st) {
+  if (!n_groups) return;
+  hipLaunchKernelGGL(rowmask_kernel, dim3((WM_STRIDE + 255) / 256, n_groups), dim3(256), 0, st, sb, wm, groups,
+                     ktabs, kdata);
+}
+
 // float decoder
-__global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ sb, float* __restrict__ scratch,
+__global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                                                      uint8_t* __restrict__ dec, TdecOut out,
                                                      const MiGroupDesc* __restrict__ groups,
                                                      const MiLaneDesc* __restrict__ lanes,
                                                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata,
                                                      uint32_t max_its, uint32_t early_stop) {
-  tdec_group<false>(sb, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<false>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 // int16 decoder: held to MI_TDEC_I16_WAVES waves per SIMD (3: <= 168 VGPRs), enough to keep every
 // group of a 12,500-subframe batch resident (2,540 waves on 1,024 SIMDs)
@@ -67,24 +89,24 @@ __global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ 
 #define MI_TDEC_I16_WAVES 3
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_TDEC_I16_WAVES)))
-void tdec_kernel_i16(const float* __restrict__ sb, float* __restrict__ scratch, uint8_t* __restrict__ dec, TdecOut out,
+void tdec_kernel_i16(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch, uint8_t* __restrict__ dec, TdecOut out,
                      const MiGroupDesc* __restrict__ groups, const MiLaneDesc* __restrict__ lanes,
                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata, uint32_t max_its,
                      uint32_t early_stop) {
-  tdec_group<true>(sb, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 
-void launch_tdec(const float* sb, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
+void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,
                  hipStream_t st) {
   if (!n_groups) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
   if (q16)
-    hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, out, groups, lanes, ktabs,
+    hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
                        ktab_data, max_its, early_stop);
   else
-    hipLaunchKernelGGL(tdec_kernel_gen, dim3(n_groups), dim3(64), 0, st, sb, scratch, dec, out, groups, lanes, ktabs,
+    hipLaunchKernelGGL(tdec_kernel_gen, dim3(n_groups), dim3(64), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
                        ktab_data, max_its, early_stop);
 }
 

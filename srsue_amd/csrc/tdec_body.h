@@ -46,7 +46,10 @@ MI_HD constexpr int tr_prev_u(int sp, int j) {
 }
 
 struct TdecArgs {
-  const float* sb;        // group softbuffer [Ncb][64]                         (float decoder)
+  const float* sb;        // group softbuffer [Ncb][64] + zero row Ncb (dl_common.h sb_group_floats)
+  const uint32_t* wm;     // [K/4 + 1] window masks (rowmask_kernel): bit i of wm[w] = the softbuffer
+                          // row of decoder input 12w + i is materialised (else its value is 0)
+  uint32_t zrow;          // row index of the group's all-zero softbuffer row (= Ncb)
   int16_t* q16;           // group quantised decoder inputs [3(K+4)][64], natural order (int16 decoder;
                           // written by the first pass of the first iteration, read by all others)
   const uint32_t* pos;    // [3(K+4)] circular-buffer position of decoder input t = 3k+i
@@ -207,32 +210,66 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
   else row_st(scr, row, lane, v, crow);
 }
 
+// window mask of decoder inputs 12w .. 12w+11 (tail: w = K/4): bit i = row pos[12w+i] materialised
+MI_HD inline uint32_t tdec_window_mask(const uint8_t* map, const uint32_t* pos, uint32_t w) {
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < 12; i++) m |= (uint32_t)(map[pos[12 * w + i]] != 0) << i;
+  return m;
+}
+// the mask of window w (a scalar load, batched with the window's position-table loads)
+MI_HD inline uint32_t wmask(const TdecArgs& a, uint32_t w) { return a.wm[w]; }
+// softbuffer float of decoder input t0 + dt (t0 = 12 w, m = wmask(w)): materialised rows through the
+// position table; an unmaterialised row is 0 without HBM traffic.  Two ways: read the group's zero
+// row instead (one scalar select; the row stays cache-resident) -- the default for both decoders --
+// or (MI_SB_ZROW_* = 0) a lane offset beyond the descriptor's range (2^31), for which the hardware
+// returns 0 without a memory access.  Same-box A/B (gpurun_out ab_sparse2): int16 tdec 9.60 ms with
+// the zero row, 9.80 ms out of range, 9.83 ms with every row materialised, 10.5 ms before.
+#ifndef MI_SB_ZROW_GEN
+#define MI_SB_ZROW_GEN 1
+#endif
+#ifndef MI_SB_ZROW_I16
+#define MI_SB_ZROW_I16 1
+#endif
+template <bool Q16>
+MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
+  const bool on = (m >> dt) & 1u;
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  if constexpr (!(Q16 ? MI_SB_ZROW_I16 : MI_SB_ZROW_GEN)) {
+    const uint32_t so = a.pos[t0 + dt] * (uint32_t)(LANES * sizeof(float));
+    const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb), vo, so, 0));
+  }
+#endif
+  return row_ld(a.sb, on ? a.pos[t0 + dt] : a.zrow, lane);
+}
+
 // raw decoder input t (= 3k + i): softbuffer float at position pos[t], or the int16 q row t
 template <bool Q16>
-MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t t0, uint32_t dt, int lane) {
+MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
   if constexpr (Q16) return (int32_t)row_ld(a.q16, t0, lane, dt);
-  else return row_ld(a.sb, a.pos[t0 + dt], lane);
+  else return sb_in<Q16>(a, m, t0, dt, lane);
 }
 
 template <bool DEC2, bool FIRST, bool Q16, bool SQ>
 MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
   const float* llr1 = scr_at<Q16>(a.scr, a.K);
+  const uint32_t m = (Q16 && SQ) ? 0u : wmask(a, base / BETA_W);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
       if constexpr (Q16 && !SQ) {
-        r.f0[i] = row_ld(a.sb, a.pos[3 * k], lane);
-        r.f1[i] = row_ld(a.sb, a.pos[3 * k + 1], lane);
+        r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i, lane);
+        r.f1[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
       } else {
-        r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i, lane);
-        r.s1[i] = dec_in<Q16>(a, 3 * base, 3 * i + 1, lane);
+        r.s0[i] = dec_in<Q16>(a, m, 3 * base, 3 * i, lane);
+        r.s1[i] = dec_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
       }
       r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
     } else {
       const uint32_t pk = a.pi[k];
-      if constexpr (Q16 && !SQ) r.f0[i] = row_ld(a.sb, a.pos[3 * k + 2], lane);
-      else r.s0[i] = dec_in<Q16>(a, 3 * base, 3 * i + 2, lane);
+      if constexpr (Q16 && !SQ) r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
+      else r.s0[i] = dec_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
       r.r0[i] = scr_raw<Q16>(llr1, pk, lane);
       r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, pk, lane);
     }
@@ -244,12 +281,12 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
 // writes the q rows
 template <bool FIRST, bool Q16>
 MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
+  const uint32_t m = wmask(a, base / BETA_W);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
-    const uint32_t t = 3 * (base + i);
-    r.f0[i] = row_ld(a.sb, a.pos[t], lane);
-    r.f1[i] = row_ld(a.sb, a.pos[t + 1], lane);
-    r.f2[i] = row_ld(a.sb, a.pos[t + 2], lane);
+    r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i, lane);
+    r.f1[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
+    r.f2[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
     r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
   }
 }
@@ -382,13 +419,13 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
 #pragma unroll
   for (int s = 0; s < 8; s++) b[s] = s ? NINF : 0.0f;
   {
-    const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
+    const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0), tm = (Q16 && SQB) ? 0u : wmask(a, nw);
     float tx[3], tp[3];
     if constexpr (MKQ) {
       // all 12 tail inputs (both constituent codes) quantised into their q rows
       float tq[12];
 #pragma unroll
-      for (int j = 0; j < 12; j++) tq[j] = q16f(row_ld(a.sb, a.pos[3 * K + j], lane));
+      for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, 3 * K, j, lane));
 #pragma unroll
       for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
 #pragma unroll
@@ -396,14 +433,14 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     } else if constexpr (Q16 && !SQB) {
 #pragma unroll
       for (int j = 0; j < 3; j++) {
-        tx[j] = q16f(row_ld(a.sb, a.pos[t0 + 2 * j], lane));
-        tp[j] = q16f(row_ld(a.sb, a.pos[t0 + 2 * j + 1], lane));
+        tx[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
+        tp[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 3; j++) {
-        tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0, 2 * j, lane));
-        tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, t0, 2 * j + 1, lane));
+        tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
+        tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
       }
     }
 #pragma unroll

@@ -107,7 +107,7 @@ int srslte_softbuffer_rx_init(srslte_softbuffer_rx_t* q, uint32_t nof_prb) {
   memset(q, 0, sizeof(*q));
   // max code blocks of the largest single-layer TBS at nof_prb (13 at 100 PRB)
   q->max_cb = (nof_prb * 12 * 14 * 6 + 6119) / 6120 + 1;
-  q->dev_bytes = (uint64_t)2 * mi::NCB_MAX * mi::LANES * sizeof(float);
+  q->dev_bytes = (uint64_t)2 * mi::sb_group_floats(mi::NCB_MAX) * sizeof(float);
   if (hipMalloc(&q->dev, q->dev_bytes) != hipSuccess) { q->dev = nullptr; return SRSLTE_ERROR; }
   srslte_softbuffer_rx_reset(q);
   return SRSLTE_SUCCESS;

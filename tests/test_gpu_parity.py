@@ -147,3 +147,34 @@ def test_sc16_wire_format_is_exact():
     pay = b.download(abi.BUF_PAYLOAD, np.uint8)
     for i in range(len(cfgs)):
         assert np.array_equal(b.payload(i, pay), tbs[i])
+
+
+@pytest.mark.parametrize("i16", [False, True])
+def test_batch_harq_combining_sparse_rows(i16):
+    """HARQ in the batch path with the sparse softbuffer rows (dl_common.h sb_group_floats): one
+    64-lane group mixes first transmissions (rv 0, overwrite) and retransmissions (rv 2 / rv 3,
+    combine).  Two launches with different LLRs: combining lanes must equal the oracle's dense float
+    softbuffer after both, the fresh lanes the oracle's single decode -- rows that only one lane
+    materialises, rows dropped by a fresh lane and the zero row all take part."""
+    spec = [(0, 1), (2, 0), (0, 1), (3, 0)]
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i, tbs=75376, Qm=6, rv=rv, new_tb=nt) for i, (rv, nt) in enumerate(spec)]
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16)
+    flat_len = b.download(abi.BUF_LLR, np.float32).shape
+    osb = [None] * len(cfgs)
+    for run, snr in enumerate((14.0, 16.0)):
+        iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=90 + 10 * run)
+        llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
+        flat = np.zeros(flat_len, np.float32)
+        for i, l in enumerate(llrs):
+            flat[b.offset(abi.BUF_LLR, i):b.offset(abi.BUF_LLR, i) + len(l)] = l
+        b.upload(abi.BUF_LLR, flat)
+        b.run_stages(S_RM_TDEC_TB)
+        pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+        crc = b.download(abi.BUF_TB_CRC, np.uint32)
+        its = b.download(abi.BUF_TB_ITS, np.uint32)
+        for i, c in enumerate(cfgs):
+            ok, opay, onoi, osb[i] = oracle_dlsch(c, llrs[i], sb=None if c.new_tb else osb[i], new_tb=bool(c.new_tb),
+                                                  i16=i16)
+            assert bool(crc[i]) == ok, (run, i)
+            assert its[i] == onoi, (run, i)
+            assert np.array_equal(b.payload(i, pay), opay), (run, i)
