@@ -169,6 +169,16 @@ enum { SRC_SB = 0, SRC_MKQ = 1, SRC_Q = 2 };
 #ifndef MI_TDEC_MKQ_IT
 #define MI_TDEC_MKQ_IT 1
 #endif
+// software-pipelining depth (windows ahead) of a pass, by where it reads its channel inputs: the
+// softbuffer passes 1 (ping-pong), the q-row passes 2 (three buffers).  Same-box A/B (ab_pf,
+// ab_tord): 2 for every pass made the one-iteration headline 3 % slower and the 8-iteration
+// configs[0] 6-10 % faster.
+#ifndef MI_TDEC_PF_SB
+#define MI_TDEC_PF_SB 1
+#endif
+#ifndef MI_TDEC_PF_Q
+#define MI_TDEC_PF_Q 2
+#endif
 
 // Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats or
 // int16 words as int) and converted only when the window is computed, so that the loads of the next
@@ -404,14 +414,16 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 // One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then the
 // K info steps, checkpointed every BETA_W steps.  Forward pass: per window the beta values are
 // recomputed from the window's closing checkpoint, alpha and the LLRs follow.  Both passes are
-// unrolled by two windows with ping-pong buffers A/B: the loads of window j+1 are issued before
-// window j is computed and are first used one window later (K is a multiple of 8 for every LTE
-// code block size, so the window count K/4 is even and the loops have no remainder).
+// software-pipelined PF windows deep: PF = 2 unrolls by three windows with rotating buffers A/B/C
+// (the loads of window j+2 are issued before window j is computed; the passes may exit after any
+// window of the rotation), PF = 1 by two with ping-pong buffers (K is a multiple of 8 for every LTE
+// code block size, so the window count K/4 is even and that loop has no remainder).
 template <bool DEC2, bool FIRST, bool Q16, int SRC>
 MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;   // backward pass: softbuffer -> q rows
   constexpr bool SQB = Q16 && SRC == SRC_Q;              // backward pass reads q rows
   constexpr bool SQF = Q16 && SRC != SRC_SB;             // forward pass reads q rows
+  constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_PF_Q;
   const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
   const size_t ck = (size_t)2 * K;  // beta checkpoints (row)
   const float NINF = -INFINITY;
@@ -452,8 +464,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     }
   }
   ck_store<Q16>(a.scr, ck, nw, lane, b);
-  TdecWin<Q16> A, B;
-  // ---- backward pass: windows nw-1 (A), nw-2 (B), ...
+  // ---- backward pass (window j closes with checkpoint j; window 0's betas are not stored)
   auto load = [&](uint32_t w, TdecWin<Q16>& r) {
     if constexpr (MKQ) tdec_load_window_sb<FIRST, Q16>(a, lane, w * BETA_W, r);
     else tdec_load_window<DEC2, FIRST, Q16, SQB>(a, lane, w * BETA_W, r);
@@ -462,30 +473,71 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     if constexpr (MKQ) tdec_beta_window_mkq<Q16>(a, lane, r, w * BETA_W, b);
     else tdec_beta_window<DEC2, Q16, SQB>(r, w * BETA_W, F, b);
   };
-  load(nw - 1, A);
-  for (uint32_t j = nw - 1;; j -= 2) {
-    load(j - 1, B);
-    beta(A, j);
-    ck_store<Q16>(a.scr, ck, j, lane, b);
-    load(j >= 3 ? j - 2 : 1, A);   // last round: a harmless reload
-    beta(B, j - 1);
-    if (j == 1) break;
-    ck_store<Q16>(a.scr, ck, j - 1, lane, b);
-  }
-  // ---- forward pass: windows 0 (A), 1 (B), ...; window j closes with checkpoint j + 1
+  auto fload = [&](uint32_t w, TdecWin<Q16>& r) {
+    tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
+    ck_load_raw<Q16>(a.scr, ck, w + 1, lane, r);
+  };
   float al[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) al[s] = s ? NINF : 0.0f;
-  tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, 0, A);
-  ck_load_raw<Q16>(a.scr, ck, 1, lane, A);
-  for (uint32_t j = 0; j < nw; j += 2) {
-    tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, (j + 1) * BETA_W, B);
-    ck_load_raw<Q16>(a.scr, ck, j + 2, lane, B);
-    tdec_alpha_window<DEC2, Q16, SQF>(a, lane, A, j * BETA_W, al, crc);
-    const uint32_t jn = j + 2 < nw ? j + 2 : nw - 1;   // last round: a harmless reload
-    tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, jn * BETA_W, A);
-    ck_load_raw<Q16>(a.scr, ck, jn + 1, lane, A);
-    tdec_alpha_window<DEC2, Q16, SQF>(a, lane, B, (j + 1) * BETA_W, al, crc);
+  if constexpr (PF >= 2) {
+    // three rotating buffers: the loads of window j-2 are issued before window j is computed, so two
+    // windows of compute cover each load's latency (out-of-range window indices are clamped: harmless
+    // reloads at the ends)
+    TdecWin<Q16> A, B, C;
+    const int last = (int)nw - 1;
+    auto lo = [](int w) { return (uint32_t)(w > 0 ? w : 0); };
+    auto hi = [last](int w) { return (uint32_t)(w < last ? w : last); };
+    load(last, A);
+    load(lo(last - 1), B);
+    for (int j = last;; j -= 3) {
+      load(lo(j - 2), C);
+      beta(A, j);
+      if (j == 0) break;
+      ck_store<Q16>(a.scr, ck, j, lane, b);
+      load(lo(j - 3), A);
+      beta(B, j - 1);
+      if (j == 1) break;
+      ck_store<Q16>(a.scr, ck, j - 1, lane, b);
+      load(lo(j - 4), B);
+      beta(C, j - 2);
+      if (j == 2) break;
+      ck_store<Q16>(a.scr, ck, j - 2, lane, b);
+    }
+    // ---- forward pass: window j closes with checkpoint j + 1
+    fload(0, A);
+    fload(1, B);
+    for (int j = 0;; j += 3) {
+      fload(hi(j + 2), C);
+      tdec_alpha_window<DEC2, Q16, SQF>(a, lane, A, j * BETA_W, al, crc);
+      if (j == last) break;
+      fload(hi(j + 3), A);
+      tdec_alpha_window<DEC2, Q16, SQF>(a, lane, B, (j + 1) * BETA_W, al, crc);
+      if (j + 1 == last) break;
+      fload(hi(j + 4), B);
+      tdec_alpha_window<DEC2, Q16, SQF>(a, lane, C, (j + 2) * BETA_W, al, crc);
+      if (j + 2 == last) break;
+    }
+  } else {
+    TdecWin<Q16> A, B;
+    load(nw - 1, A);
+    for (uint32_t j = nw - 1;; j -= 2) {
+      load(j - 1, B);
+      beta(A, j);
+      ck_store<Q16>(a.scr, ck, j, lane, b);
+      load(j >= 3 ? j - 2 : 1, A);   // last round: a harmless reload
+      beta(B, j - 1);
+      if (j == 1) break;
+      ck_store<Q16>(a.scr, ck, j - 1, lane, b);
+    }
+    // ---- forward pass: windows 0 (A), 1 (B), ...; window j closes with checkpoint j + 1
+    fload(0, A);
+    for (uint32_t j = 0; j < nw; j += 2) {
+      fload(j + 1, B);
+      tdec_alpha_window<DEC2, Q16, SQF>(a, lane, A, j * BETA_W, al, crc);
+      fload(j + 2 < nw ? j + 2 : nw - 1, A);   // last round: a harmless reload
+      tdec_alpha_window<DEC2, Q16, SQF>(a, lane, B, (j + 1) * BETA_W, al, crc);
+    }
   }
 }
 
