@@ -72,7 +72,24 @@ MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
   return u ? (z ? luz : lu) : (z ? lp : 0.0f);
 }
 
-// one backward step: beta_k from beta_{k+1}
+// State-metric normalisation (subtract state 0).  The float decoder normalises every step, as the
+// srsLTE-gen order it reproduces does (its rounding depends on magnitudes).  In the int16 design every
+// metric is an exact integer and an LLR is a difference of two maxima over alpha + gamma + beta, so
+// adding a constant to all states of alpha_k or beta_k never changes an LLR: the int16 decoder
+// normalises once per window (before a checkpoint is stored, at the end of each forward window) --
+// values then grow by at most 4 x (1535 + 1023 + 511) within a window, far inside fp32's exact range
+// -- and its LLRs, extrinsics and decisions stay bit-identical to the per-step oracle.
+template <bool NORM>
+MI_HD inline void norm8(float (&v)[8]) {
+  if constexpr (NORM) {
+    const float v0 = v[0];
+#pragma unroll
+    for (int s = 0; s < 8; s++) v[s] = v[s] - v0;
+  }
+}
+
+// one backward step: beta_k from beta_{k+1} (NORM: normalised)
+template <bool NORM = true>
 MI_HD inline void beta_step(const float (&bn)[8], float xs, float xp, float (&bk)[8]) {
   const float luz = xs + xp;
   float m[8];
@@ -82,11 +99,17 @@ MI_HD inline void beta_step(const float (&bn)[8], float xs, float xp, float (&bk
     float b1 = bn[tr_next(s, 1)] + gam(1, tr_par(s, 1), xs, xp, luz);
     m[s] = fmaxf(b0, b1);
   }
+  if constexpr (NORM) {
 #pragma unroll
-  for (int s = 0; s < 8; s++) bk[s] = m[s] - m[0];
+    for (int s = 0; s < 8; s++) bk[s] = m[s] - m[0];
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; s++) bk[s] = m[s];
+  }
 }
 
-// one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1}
+// one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1} (NORM: alpha normalised)
+template <bool NORM = true>
 MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, float xp) {
   const float luz = xs + xp;
   const float NINF = -INFINITY;
@@ -105,8 +128,13 @@ MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, fl
 #pragma unroll
   for (int sp = 0; sp < 8; sp++)
     na[sp] = fmaxf(c[tr_prev_s(sp, 0)][tr_prev_u(sp, 0)], c[tr_prev_s(sp, 1)][tr_prev_u(sp, 1)]);
+  if constexpr (NORM) {
 #pragma unroll
-  for (int s = 0; s < 8; s++) al[s] = na[s] - na[0];
+    for (int s = 0; s < 8; s++) al[s] = na[s] - na[0];
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; s++) al[s] = na[s];
+  }
   return llr;
 }
 
@@ -366,10 +394,11 @@ MI_HD inline void tdec_beta_window(const TdecWin<Q16>& w, uint32_t base, uint32_
   for (int i = BETA_W - 1; i >= 0; i--) {
     float xs, xp, nb[8];
     tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, F, xs, xp);
-    beta_step(b, xs, xp, nb);
+    beta_step<!Q16>(b, xs, xp, nb);
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
   }
+  norm8<Q16>(b);
 }
 
 // the same for the int16 decoder's first pass: quantise the window's softbuffer inputs, store them as
@@ -386,10 +415,11 @@ MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWi
     row_st(a.q16, 3 * base, lane, (int16_t)q2, 3 * i + 2);
     const bool fill = base + i < a.F;
     float nb[8];
-    beta_step(b, (fill ? FILL : q0) + scr_cvt<Q16>(w.r0[i]), fill ? FILL : q1, nb);
+    beta_step<!Q16>(b, (fill ? FILL : q0) + scr_cvt<Q16>(w.r0[i]), fill ? FILL : q1, nb);
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
   }
+  norm8<Q16>(b);
 }
 
 // forward steps of one window: beta_{base+1..base+W} recomputed in registers from the window's
@@ -405,10 +435,11 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
 #pragma unroll
   for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = scr_cvt<Q16>(w.ck[s - 1]);
 #pragma unroll
-  for (int i = BETA_W - 2; i >= 0; i--) beta_step(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+  for (int i = BETA_W - 2; i >= 0; i--) beta_step<!Q16>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++)
-    tdec_emit<DEC2, Q16>(a, lane, base, i, alpha_step(al, bw[i], xs[i], xp[i]), xs[i], w, crc);
+    tdec_emit<DEC2, Q16>(a, lane, base, i, alpha_step<!Q16>(al, bw[i], xs[i], xp[i]), xs[i], w, crc);
+  norm8<Q16>(al);
 }
 
 // One constituent decoder (half iteration).  Backward pass: beta over the 3 tail steps and then the
@@ -458,10 +489,11 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
 #pragma unroll
     for (int j = 2; j >= 0; j--) {
       float nb[8];
-      beta_step(b, tx[j], tp[j], nb);
+      beta_step<!Q16>(b, tx[j], tp[j], nb);
 #pragma unroll
       for (int s = 0; s < 8; s++) b[s] = nb[s];
     }
+    norm8<Q16>(b);
   }
   ck_store<Q16>(a.scr, ck, nw, lane, b);
   // ---- backward pass (window j closes with checkpoint j; window 0's betas are not stored)
