@@ -123,9 +123,12 @@ int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
  * PCFICH -> CFI, PDCCH soft bits and DCI blind search (srslte_pdcch_extract_llr +
  * srslte_ue_dl_find_dl_dci / _find_ul_dci) over the grid and channel estimates a batch's front end
  * left in HBM.  Per subframe the search uses that subframe's cfg.rnti and cfg.cfi; PHICH resources
- * phich_ng = 0..3 (Ng = 1/6, 1/2, 1, 2; normal duration).  run() enqueues three kernels (stage mask:
- * 1 PCFICH, 2 PDCCH soft bits, 4 blind search); result() returns the first DCI of the subframe in
- * search order (UE-specific L = 1, 2, 4, 8, then common L = 4, 8): 1 found, 0 not found, -1 error. */
+ * phich_ng = 0..3 (Ng = 1/6, 1/2, 1, 2; normal duration).  run() enqueues four kernels (stage mask:
+ * 1 PCFICH, 2 PDCCH soft bits, 4 blind search, 8 PHICH); result() returns the first DCI of the
+ * subframe in search order (UE-specific L = 1, 2, 4, 8, then common L = 4, 8): 1 found, 0 not found,
+ * -1 error.  PHICH (srslte_ue_dl_decode_phich, phch_worker.cc:381): set_phich() sets per subframe the
+ * UL grant's lowest PRB index and DMRS cyclic shift (36.213 9.1.2; default 0, 0), phich() returns the
+ * HARQ indicator (1 ACK, 0 NACK, -1 error) and its soft value (> 0 favours ACK). */
 typedef struct mi_dl_ctrl mi_dl_ctrl_t;
 mi_dl_ctrl_t *mi_dl_ctrl_create(mi_dl_batch_t *b, uint32_t phich_ng);
 void          mi_dl_ctrl_destroy(mi_dl_ctrl_t *c);
@@ -138,6 +141,8 @@ size_t        mi_dl_ctrl_llr_offset(const mi_dl_ctrl_t *c, uint32_t sf);
 uint32_t      mi_dl_ctrl_n_cce(const mi_dl_ctrl_t *c, uint32_t sf);
 /* copy PDCCH soft bits between host and device (upload != 0: host -> device) */
 int           mi_dl_ctrl_llr(mi_dl_ctrl_t *c, float *host, size_t n, int upload);
+int           mi_dl_ctrl_set_phich(mi_dl_ctrl_t *c, const uint32_t *i_lowest, const uint32_t *n_dmrs);
+int           mi_dl_ctrl_phich(mi_dl_ctrl_t *c, uint32_t sf, float *soft);
 
 /* ---- host-IQ streaming pipeline -------------------------------------
  * Double buffering for IQ that arrives in host memory (srsUE's sync thread writes the worker's

@@ -216,6 +216,10 @@ SRSLTE_API int srslte_ue_dl_find_dl_dci_type(srslte_ue_dl_t *q, srslte_dci_msg_t
 SRSLTE_API int srslte_ue_dl_find_ul_dci(srslte_ue_dl_t *q, srslte_dci_msg_t *dci_msg, uint32_t cfi, uint32_t sf_idx,
                                         uint16_t rnti);
 SRSLTE_API uint32_t srslte_ue_dl_get_ncce(srslte_ue_dl_t *q);
+/* PHICH (phch_worker.cc:381): HARQ indicator of the UL grant with lowest PRB index n_prb_lowest and
+ * DMRS cyclic shift n_dmrs (36.213 9.1.2, FDD) in the subframe decode_fft_estimate processed; true =
+ * ACK (maximum-likelihood decision on the despread soft value, GPU phich_kernel). */
+SRSLTE_API bool srslte_ue_dl_decode_phich(srslte_ue_dl_t *q, uint32_t sf_idx, uint32_t n_prb_lowest, uint32_t n_dmrs);
 SRSLTE_API int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t *msg, uint16_t msg_rnti, uint32_t nof_prb,
                                           srslte_ra_dl_dci_t *dl_dci, srslte_ra_dl_grant_t *grant);
 SRSLTE_API char *srslte_ra_dl_dci_string(srslte_ra_dl_dci_t *dci);

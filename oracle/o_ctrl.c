@@ -373,10 +373,53 @@ int or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf,
 }
 
 /* ---- transmit side (ground truth): one DCI on the air, noiseless, added to iq ---- */
+/* OFDM modulation of the first Lc symbols of a per-port grid (double, [P][14][W] complex) through the
+   flat per-port channel h (NULL: port 0 only, h = 1), added to the subframe IQ */
+static void add_ctrl_grid(const or_cell_t *c, uint32_t Lc, const double *grid, const float *h_re_im, float *iq) {
+  const uint32_t W = 12 * c->nof_prb, N = (uint32_t)or_symbol_sz(c->nof_prb), P = c->nof_ports;
+  double *X = (double *)malloc(sizeof(double) * 2 * N), *x = (double *)malloc(sizeof(double) * 2 * N);
+  const double nrm = 1.0 / sqrt((double)N);
+  for (uint32_t p = 0; p < P; p++) {
+    double hr = h_re_im ? h_re_im[2 * p] : (p == 0 ? 1.0 : 0.0), hi = h_re_im ? h_re_im[2 * p + 1] : 0.0;
+    size_t pos = 0;
+    for (uint32_t l = 0; l < OR_NSYMB; l++) {
+      const uint32_t cp = (uint32_t)or_cp_len(N, l % 7);
+      if (l < Lc) {
+        memset(X, 0, sizeof(double) * 2 * N);
+        const double *gl = grid + ((size_t)p * OR_NSYMB * W + l * W) * 2;
+        for (uint32_t k = 0; k < W; k++) {
+          const uint32_t bin = (k < W / 2) ? (N - W / 2 + k) : (k - W / 2 + 1);
+          X[2 * bin] = gl[2 * k]; X[2 * bin + 1] = gl[2 * k + 1];
+        }
+        or_dft(X, x, N, 1);
+        for (uint32_t t = 0; t < N + cp; t++) {
+          const uint32_t src = (t + N - cp) % N;
+          const double vr = x[2 * src] * nrm, vi = x[2 * src + 1] * nrm;
+          iq[2 * (pos + t)] += (float)(vr * hr - vi * hi);
+          iq[2 * (pos + t) + 1] += (float)(vr * hi + vi * hr);
+        }
+      }
+      pos += N + cp;
+    }
+  }
+  free(X); free(x);
+}
+
+/* SFBC (36.211 6.3.4.3) of one RE pair (r0, r1) of the control region onto ports 0 / 1 */
+static void sfbc_put(double *grid, size_t plane, uint32_t r0, uint32_t r1, double x0r, double x0i, double x1r,
+                     double x1i) {
+  const double s2 = 1.0 / sqrt(2.0);
+  double *g0 = grid, *g1 = grid + 2 * plane;
+  g0[2 * r0] += s2 * x0r;  g0[2 * r0 + 1] += s2 * x0i;
+  g1[2 * r0] += -s2 * x1r; g1[2 * r0 + 1] += s2 * x1i;
+  g0[2 * r1] += s2 * x1r;  g0[2 * r1 + 1] += s2 * x1i;
+  g1[2 * r1] += s2 * x0r;  g1[2 * r1 + 1] += -s2 * x0i;
+}
+
 int or_tx_pdcch(const or_ctrl_t *q, uint16_t rnti, uint32_t L, uint32_t ncce, const uint8_t *a, uint32_t A,
                 const float *h_re_im, float *iq) {
   const or_cell_t *c = &q->cell;
-  const uint32_t W = 12 * c->nof_prb, N = (uint32_t)or_symbol_sz(c->nof_prb), P = c->nof_ports;
+  const uint32_t W = 12 * c->nof_prb, P = c->nof_ports;
   uint32_t n_cce;
   const uint32_t M = (uint32_t)or_pdcch_regs(q, NULL, &n_cce);
   if (ncce + L > n_cce) return -1;
@@ -411,33 +454,110 @@ int or_tx_pdcch(const or_ctrl_t *q, uint16_t rnti, uint32_t L, uint32_t ncce, co
       }
     }
   }
-  /* OFDM modulation of the control symbols with the flat per-port channel, added to iq */
-  double *X = (double *)malloc(sizeof(double) * 2 * N), *x = (double *)malloc(sizeof(double) * 2 * N);
-  const double nrm = 1.0 / sqrt((double)N);
-  const uint32_t Lc = (uint32_t)or_ctrl_symbols(c, q->cfi);
-  for (uint32_t p = 0; p < P; p++) {
-    double hr = h_re_im ? h_re_im[2 * p] : (p == 0 ? 1.0 : 0.0), hi = h_re_im ? h_re_im[2 * p + 1] : 0.0;
-    size_t pos = 0;
-    for (uint32_t l = 0; l < OR_NSYMB; l++) {
-      const uint32_t cp = (uint32_t)or_cp_len(N, l % 7);
-      if (l < Lc) {
-        memset(X, 0, sizeof(double) * 2 * N);
-        const double *gl = grid + ((size_t)p * OR_NSYMB * W + l * W) * 2;
-        for (uint32_t k = 0; k < W; k++) {
-          const uint32_t bin = (k < W / 2) ? (N - W / 2 + k) : (k - W / 2 + 1);
-          X[2 * bin] = gl[2 * k]; X[2 * bin + 1] = gl[2 * k + 1];
-        }
-        or_dft(X, x, N, 1);
-        for (uint32_t t = 0; t < N + cp; t++) {
-          const uint32_t src = (t + N - cp) % N;
-          const double vr = x[2 * src] * nrm, vi = x[2 * src + 1] * nrm;
-          iq[2 * (pos + t)] += (float)(vr * hr - vi * hi);
-          iq[2 * (pos + t) + 1] += (float)(vr * hi + vi * hr);
-        }
-      }
-      pos += N + cp;
+  add_ctrl_grid(c, (uint32_t)or_ctrl_symbols(c, q->cfi), grid, h_re_im, iq);
+  free(re); free(lg); free(b); free(on); free(cs); free(grid);
+  return 0;
+}
+
+/* ---- PHICH (36.211 6.9, 36.212 5.3.5, 36.213 9.1.2) ------------------------------------------
+   srsUE: *ack = srslte_ue_dl_decode_phich(&ue_dl, tti % 10, I_lowest, n_dmrs)  (phch_worker.cc:381)
+   Resource (FDD, I_PHICH = 0): group = (I_lowest + n_dmrs) mod N_group,
+                                seq = (floor(I_lowest / N_group) + n_dmrs) mod 2 N_SF (N_SF = 4).
+   HI (1 = ACK) -> 3 repeated bits -> BPSK z (bit 0 -> (1+j)/sqrt2) -> d(i) = w_seq(i mod 4) (1 - 2 c(i))
+   z(floor(i / 4)), i < 12, c_init = (sf + 1)(2 N_ID + 1) 2^9 + N_ID; quadruplet i of the group on
+   REG n_i of symbol 0 (normal duration); 2 ports: SFBC per RE pair as the PDCCH.
+   Receiver contract (the GPU's phich_kernel): equalise as the PDCCH (noise 0), despread
+   s = sum_i Re(conj(w(i mod 4)) (1 - 2 c(i)) x(i) (1 - j) / sqrt2) over i = 0..11 in order;
+   hi_soft = -s (> 0 favours ACK); ACK iff hi_soft > 0 (maximum likelihood; no erasure threshold). */
+static const int8_t PHICH_W[8][4][2] = {   /* Table 6.9.1-2 (normal CP): (re, im) */
+    {{1, 0}, {1, 0}, {1, 0}, {1, 0}},  {{1, 0}, {-1, 0}, {1, 0}, {-1, 0}},
+    {{1, 0}, {1, 0}, {-1, 0}, {-1, 0}}, {{1, 0}, {-1, 0}, {-1, 0}, {1, 0}},
+    {{0, 1}, {0, 1}, {0, 1}, {0, 1}},  {{0, 1}, {0, -1}, {0, 1}, {0, -1}},
+    {{0, 1}, {0, 1}, {0, -1}, {0, -1}}, {{0, 1}, {0, -1}, {0, -1}, {0, 1}}};
+
+void or_phich_calc(uint32_t nof_prb, uint32_t ng, uint32_t I_lowest, uint32_t n_dmrs, uint32_t *group,
+                   uint32_t *seq) {
+  const uint32_t N = or_phich_ngroups(nof_prb, ng);
+  *group = (I_lowest + n_dmrs) % N;
+  *seq = (I_lowest / N + n_dmrs) % 8;
+}
+
+uint32_t or_phich_cinit(uint32_t cell_id, uint32_t sf) { return (sf + 1) * (2 * cell_id + 1) * 512 + cell_id; }
+
+int or_phich_res(const or_ctrl_t *q, uint32_t group, uint32_t *re12) {
+  const or_cell_t *c = &q->cell;
+  const uint32_t W = 12 * c->nof_prb, n0 = 2 * c->nof_prb;
+  if (group >= or_phich_ngroups(c->nof_prb, q->ng)) return -1;
+  uint8_t used0[2 * OR_NRB_MAX] = {0};
+  const uint32_t kbar = 6 * (c->id % (2 * c->nof_prb));
+  for (uint32_t i = 0; i < 4; i++) used0[((kbar + (i * c->nof_prb / 2) * 6) % W) / 6] = 1;
+  uint32_t free0[2 * OR_NRB_MAX], nf = 0;
+  for (uint32_t r = 0; r < n0; r++) if (!used0[r]) free0[nf++] = r;
+  for (uint32_t i = 0; i < 3; i++) reg_res(c, 0, 6 * free0[(c->id + group + (i * nf) / 3) % nf], re12 + 4 * i);
+  return 0;
+}
+
+float or_phich_soft(const or_ctrl_t *q, const float *grid, const float *ce, uint32_t group, uint32_t seq) {
+  const or_cell_t *c = &q->cell;
+  const uint32_t plane = OR_NSYMB * 12 * c->nof_prb;
+  uint32_t re[12];
+  if (or_phich_res(q, group, re) || seq > 7) return 0.0f;
+  uint8_t cs[12];
+  or_gold(or_phich_cinit(c->id, q->sf), cs, 12);
+  double x[24];
+  const int tm2 = c->nof_ports == 2;
+  for (int j = 0; j < 12; j += tm2 ? 2 : 1) {
+    if (!tm2) {
+      double yr = grid[2 * re[j]], yi = grid[2 * re[j] + 1], hr = ce[2 * re[j]], hi = ce[2 * re[j] + 1];
+      double den = hr * hr + hi * hi;
+      if (den <= 0) den = 1e-9;
+      x[2 * j] = (yr * hr + yi * hi) / den;
+      x[2 * j + 1] = (yi * hr - yr * hi) / den;
+    } else {
+      const float *c0 = ce, *c1 = ce + 2 * plane;
+      const uint32_t a = re[j], b = re[j + 1];
+      double r0r = grid[2 * a], r0i = grid[2 * a + 1], r1r = grid[2 * b], r1i = grid[2 * b + 1];
+      double h00r = c0[2 * a], h00i = c0[2 * a + 1], h01r = c0[2 * b], h01i = c0[2 * b + 1];
+      double h10r = c1[2 * a], h10i = c1[2 * a + 1], h11r = c1[2 * b], h11i = c1[2 * b + 1];
+      double hh = h00r * h00r + h00i * h00i + h11r * h11r + h11i * h11i;
+      if (hh <= 0) hh = 1e-9;
+      double s = sqrt(2.0) / hh;
+      x[2 * j] = s * ((h00r * r0r + h00i * r0i) + (h11r * r1r + h11i * r1i));
+      x[2 * j + 1] = s * ((h00r * r0i - h00i * r0r) + (h11i * r1r - h11r * r1i));
+      x[2 * j + 2] = s * (-(h10r * r0r + h10i * r0i) + (h01r * r1r + h01i * r1i));
+      x[2 * j + 3] = s * (-(h10i * r0r - h10r * r0i) + (h01r * r1i - h01i * r1r));
     }
   }
-  free(re); free(lg); free(b); free(on); free(cs); free(grid); free(X); free(x);
+  double s = 0.0;
+  for (int i = 0; i < 12; i++) {
+    const double wr = PHICH_W[seq][i % 4][0], wi = PHICH_W[seq][i % 4][1], sg = cs[i] ? -1.0 : 1.0;
+    const double yr = wr * x[2 * i] + wi * x[2 * i + 1], yi = wr * x[2 * i + 1] - wi * x[2 * i];   /* conj(w) x */
+    s += sg * (yr + yi) / sqrt(2.0);
+  }
+  return (float)(-s);
+}
+
+int or_tx_phich(const or_ctrl_t *q, uint32_t group, uint32_t seq, int ack, const float *h_re_im, float *iq) {
+  const or_cell_t *c = &q->cell;
+  const uint32_t W = 12 * c->nof_prb, P = c->nof_ports;
+  const size_t plane = (size_t)OR_NSYMB * W;
+  uint32_t re[12];
+  if (or_phich_res(q, group, re) || seq > 7) return -1;
+  uint8_t cs[12];
+  or_gold(or_phich_cinit(c->id, q->sf), cs, 12);
+  double d[24];
+  const double s2 = 1.0 / sqrt(2.0), zb = ack ? -s2 : s2;   /* bit = HI, BPSK (1 - 2b)(1 + j)/sqrt2 */
+  for (int i = 0; i < 12; i++) {
+    const double wr = PHICH_W[seq][i % 4][0], wi = PHICH_W[seq][i % 4][1], sg = cs[i] ? -1.0 : 1.0;
+    d[2 * i] = sg * (wr * zb - wi * zb);        /* w * z, z = zb (1 + j) */
+    d[2 * i + 1] = sg * (wr * zb + wi * zb);
+  }
+  double *grid = (double *)calloc((size_t)2 * P * plane, sizeof(double));
+  for (int j = 0; j < 12; j += (P == 2 ? 2 : 1)) {
+    if (P == 1) { grid[2 * re[j]] = d[2 * j]; grid[2 * re[j] + 1] = d[2 * j + 1]; }
+    else sfbc_put(grid, plane, re[j], re[j + 1], d[2 * j], d[2 * j + 1], d[2 * j + 2], d[2 * j + 3]);
+  }
+  add_ctrl_grid(c, 1, grid, h_re_im, iq);
+  free(grid);
   return 0;
 }

@@ -162,6 +162,13 @@ int      or_search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, int common,
 int      or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int ul,
                      or_dci_found_t *out);
 /* adds one noiseless DCI (L CCEs at ncce) to iq (2 * SF_LEN floats), flat per-port channel h */
+/* PHICH (o_ctrl.c): resource of an UL grant, its 12 REs, soft HI (> 0 favours ACK), transmitter */
+void     or_phich_calc(uint32_t nof_prb, uint32_t ng, uint32_t I_lowest, uint32_t n_dmrs, uint32_t *group,
+                       uint32_t *seq);
+uint32_t or_phich_cinit(uint32_t cell_id, uint32_t sf);
+int      or_phich_res(const or_ctrl_t *q, uint32_t group, uint32_t *re12);
+float    or_phich_soft(const or_ctrl_t *q, const float *grid, const float *ce, uint32_t group, uint32_t seq);
+int      or_tx_phich(const or_ctrl_t *q, uint32_t group, uint32_t seq, int ack, const float *h_re_im, float *iq);
 int      or_tx_pdcch(const or_ctrl_t *q, uint16_t rnti, uint32_t L, uint32_t ncce, const uint8_t *a, uint32_t A,
                      const float *h_re_im, float *iq);
 

@@ -97,6 +97,8 @@ def lib():
             "mi_dl_ctrl_llr_offset": (sz, [vp, u32]),
             "mi_dl_ctrl_n_cce": (u32, [vp, u32]),
             "mi_dl_ctrl_llr": (C.c_int, [vp, vp, sz, C.c_int]),
+            "mi_dl_ctrl_set_phich": (C.c_int, [vp, vp, vp]),
+            "mi_dl_ctrl_phich": (C.c_int, [vp, u32, vp]),
             "mi_dl_pipe_create": (vp, [vp, u32, u32, u32]),
             "mi_dl_pipe_destroy": (None, [vp]),
             "mi_dl_pipe_submit": (C.c_int, [vp, vp]),
@@ -244,7 +246,7 @@ class Batch:
 
 class Ctrl:
     """DL control channels over a batch's grid / channel estimates (mi_dl_ctrl_*)."""
-    PCFICH, LLR, SEARCH = 1, 2, 4
+    PCFICH, LLR, SEARCH, PHICH = 1, 2, 4, 8
 
     def __init__(self, batch, phich_ng=2):
         self.batch = batch
@@ -252,7 +254,22 @@ class Ctrl:
         if not self.h:
             raise RuntimeError("mi_dl_ctrl_create: " + last_error())
 
-    def run(self, stream_ptr=None, mask=7):
+    def set_phich(self, i_lowest, n_dmrs):
+        """per-subframe PHICH queries: the UL grant's lowest PRB index and DMRS cyclic shift"""
+        a = np.ascontiguousarray(i_lowest, np.uint32)
+        b = np.ascontiguousarray(n_dmrs, np.uint32)
+        if lib().mi_dl_ctrl_set_phich(self.h, a.ctypes.data, b.ctypes.data):
+            raise RuntimeError("mi_dl_ctrl_set_phich: " + last_error())
+
+    def phich(self, sf):
+        """(ack, soft HI) of subframe sf after a run with the PHICH stage"""
+        s = C.c_float()
+        rc = lib().mi_dl_ctrl_phich(self.h, sf, C.byref(s))
+        if rc < 0:
+            raise RuntimeError("mi_dl_ctrl_phich: " + last_error())
+        return rc == 1, s.value
+
+    def run(self, stream_ptr=None, mask=15):
         if lib().mi_dl_ctrl_run_stages(self.h, mask, C.c_void_p(stream_ptr or 0)):
             raise RuntimeError("mi_dl_ctrl_run: " + last_error())
 

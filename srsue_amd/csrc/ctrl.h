@@ -19,6 +19,7 @@ struct MiCtrlSf {            // one per subframe
   uint32_t scr_off;          // cdata offset: scrambling words (8 M bits)
   uint32_t pcfich_off;       // cdata offset: 16 PCFICH REs + 1 scrambling word
   uint32_t llr_off;          // float offset of this subframe's PDCCH soft bits [8 M]
+  uint32_t phich_off;        // cdata offset: PHICH query: 12 REs, scrambling word (12 bits), sequence
 };
 
 struct MiDciJob {            // one (candidate, DCI size) of one subframe
@@ -32,6 +33,8 @@ void launch_pdcch_llr(const float2* grid, const float2* ce, const MiCtrlSf* sfs,
                       uint32_t n_sf, uint32_t max_regs, float noise, hipStream_t st);
 void launch_dci_search(const float* llr, const MiDciJob* jobs, const uint32_t* cdata, MiDciRes* res, uint32_t n_jobs,
                        hipStream_t st);
+void launch_phich(const float2* grid, const float2* ce, const MiCtrlSf* sfs, const uint32_t* cdata, float* soft,
+                  uint32_t n_sf, hipStream_t st);
 
 struct DciFound { uint32_t found, format, nbits, L, ncce; uint8_t bits[DCI_MAX_BITS]; };
 
@@ -41,14 +44,16 @@ struct CtrlEngine {
   std::vector<MiDciJob> jobs;
   std::vector<uint32_t> job_begin;   // per subframe: jobs [job_begin[s], job_begin[s+1]) in search order
   std::vector<uint32_t> nof_prb;     // per subframe
-  DevBuf d_sfs, d_cdata, d_llr, d_jobs, d_res, d_cfi;
+  DevBuf d_sfs, d_cdata, d_llr, d_jobs, d_res, d_cfi, d_phich;
   size_t llr_floats = 0;
   uint32_t max_regs = 0;
   std::vector<MiDciRes> res;         // host copy after download
-  // plan over the subframes of P (cells, grid / ce layout) with per-subframe CFI and RNTI
-  int build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t phich_ng, const std::vector<uint16_t>& rnti);
+  // plan over the subframes of P (cells, grid / ce layout) with per-subframe CFI and RNTI; phich: per
+  // subframe the PHICH query I_lowest | n_dmrs << 16 (36.213 9.1.2), empty = (0, 0)
+  int build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t phich_ng, const std::vector<uint16_t>& rnti,
+            const std::vector<uint32_t>& phich = {});
   int upload(hipStream_t st);
-  // stages: 1 = PCFICH, 2 = PDCCH soft bits, 4 = blind search
+  // stages: 1 = PCFICH, 2 = PDCCH soft bits, 4 = blind search, 8 = PHICH
   int run(const float2* grid, const float2* ce, uint32_t mask, float noise, hipStream_t st);
   int download(hipStream_t st);
   // first match in search order: DL = format 1A (flag 1) or 1; UL = format 0 (flag 0)

@@ -1,5 +1,5 @@
 // ctrl.hip -- DL control channels on the GPU: PCFICH -> CFI, PDCCH soft-bit
-// extraction, DCI blind search (rate de-matching + tail-biting Viterbi + RNTI-masked CRC16).
+// extraction, DCI blind search (rate de-matching + tail-biting Viterbi + RNTI-masked CRC16), PHICH.
 //
 // Replaces the host work behind srslte_pdcch_extract_llr (/root/reference/ue/src/phy/
 // phch_worker.cc:260) and srslte_ue_dl_find_dl_dci_type / _find_ul_dci (:293, :426); the arithmetic
@@ -196,6 +196,57 @@ __global__ __launch_bounds__(64) void dci_search_kernel(const float* __restrict_
     for (uint32_t i = 0; i < A; i++) r.bits[i >> 5] |= (uint32_t)c[i] << (31 - (i & 31));
     res[blockIdx.x] = r;
   }
+}
+
+// PHICH (36.211 6.9): one wavefront per subframe; lanes equalise the group's 12 REs (SFBC: 6 pairs),
+// lane 0 despreads them in order i = 0..11 (oracle or_phich_soft's contract, in fp32):
+// s = sum_i Re(conj(w(i mod 4)) (1 - 2 c(i)) x(i) (1 - j) / sqrt2), soft HI = -s (> 0 favours ACK)
+__global__ __launch_bounds__(64) void phich_kernel(const float2* __restrict__ grid, const float2* __restrict__ ce,
+                                                  const MiCtrlSf* __restrict__ sfs,
+                                                  const uint32_t* __restrict__ cdata, float* __restrict__ soft) {
+  __shared__ float2 x[12];
+  const MiCtrlSf d = sfs[blockIdx.x];
+  const uint32_t t = threadIdx.x;
+  const float2* g = grid + d.grid_off;
+  const float2* c0 = ce + d.ce_off;
+  const float2* c1 = c0 + d.plane;
+  const uint32_t* re = cdata + d.phich_off;
+  if (d.ports == 2) {
+    if (t < 6) {
+      float2 a, b;
+      const uint32_t r0 = re[2 * t], r1 = re[2 * t + 1];
+      eq_tm2(g[r0], g[r1], c0[r0], c0[r1], c1[r0], c1[r1], a, b);
+      x[2 * t] = a;
+      x[2 * t + 1] = b;
+    }
+  } else if (t < 12) {
+    const float2 h = c0[re[t]];
+    float den = h.x * h.x + h.y * h.y;
+    if (den <= 0.f) den = 1e-9f;
+    const float2 y = g[re[t]];
+    x[t] = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t cs = re[12], seq = re[13];
+    float s = 0.0f;
+    for (int i = 0; i < 12; i++) {
+      // w(i mod 4) of Table 6.9.1-2: sign pattern by seq & 3, times j for seq >= 4
+      const int c = i & 3, m = (int)(seq & 3);
+      const float sw = ((m == 1 && (c & 1)) || (m == 2 && c >= 2) || (m == 3 && (c == 1 || c == 2))) ? -1.f : 1.f;
+      const float wr = seq < 4 ? sw : 0.f, wi = seq < 4 ? 0.f : sw;
+      const float yr = wr * x[i].x + wi * x[i].y, yi = wr * x[i].y - wi * x[i].x;
+      const float sg = ((cs >> i) & 1u) ? -1.f : 1.f;
+      s = s + sg * (yr + yi) * 0.70710678118654752f;
+    }
+    soft[blockIdx.x] = -s;
+  }
+}
+
+void launch_phich(const float2* grid, const float2* ce, const MiCtrlSf* sfs, const uint32_t* cdata, float* soft,
+                  uint32_t n_sf, hipStream_t st) {
+  if (!n_sf) return;
+  hipLaunchKernelGGL(phich_kernel, dim3(n_sf), dim3(64), 0, st, grid, ce, sfs, cdata, soft);
 }
 
 void launch_pcfich(const float2* grid, const float2* ce, const MiCtrlSf* sfs, const uint32_t* cdata, uint32_t* cfi,

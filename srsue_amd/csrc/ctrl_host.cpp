@@ -12,9 +12,13 @@
 namespace mi {
 
 int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t phich_ng,
-                      const std::vector<uint16_t>& rnti) {
+                      const std::vector<uint16_t>& rnti, const std::vector<uint32_t>& phich) {
   const size_t n = P.sfs.size();
-  if (cfi.size() != n || rnti.size() != n) { set_error("ctrl: per-subframe cfi / rnti"); return -1; }
+  if (cfi.size() != n || rnti.size() != n || (!phich.empty() && phich.size() != n)) {
+    set_error("ctrl: per-subframe cfi / rnti / phich");
+    return -1;
+  }
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> phich_cache;
   sfs.clear(); cdata.clear(); jobs.clear(); job_begin.clear(); nof_prb.clear();
   llr_floats = 0; max_regs = 0;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> reg_cache;  // -> (off, M)
@@ -63,6 +67,23 @@ int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t 
       cdata.push_back(w);
     }
     d.pcfich_off = pi->second;
+    {   // PHICH query of this subframe
+      uint32_t grp, seq;
+      const uint32_t qv = phich.empty() ? 0u : phich[s];
+      phich_calc(c.nof_prb, phich_ng, qv & 0xFFFFu, qv >> 16, &grp, &seq);
+      auto hk = std::make_tuple(c.id, (c.nof_prb << 8) | (phich_ng << 4) | seq, sd.sf_idx, grp);
+      auto hi = phich_cache.find(hk);
+      if (hi == phich_cache.end()) {
+        uint32_t re12[12], w = 0;
+        if (phich_res(c.id, c.nof_prb, phich_ng, grp, re12)) { set_error("ctrl: phich group"); return -1; }
+        gold_words(phich_cinit(c.id, sd.sf_idx), 12, &w);
+        hi = phich_cache.emplace(hk, (uint32_t)cdata.size()).first;
+        cdata.insert(cdata.end(), re12, re12 + 12);
+        cdata.push_back(w);
+        cdata.push_back(seq);
+      }
+      d.phich_off = hi->second;
+    }
     d.llr_off = (uint32_t)llr_floats;
     llr_floats += (size_t)8 * d.M;
     max_regs = std::max(max_regs, d.M);
@@ -99,7 +120,8 @@ int CtrlEngine::upload(hipStream_t st) {
   const bool ok = up(d_sfs, sfs.data(), sfs.size() * sizeof(MiCtrlSf)) &&
                   up(d_cdata, cdata.data(), cdata.size() * 4) && up(d_jobs, jobs.data(), jobs.size() * sizeof(MiDciJob)) &&
                   d_llr.ensure(llr_floats * 4) && d_res.ensure(jobs.size() * sizeof(MiDciRes)) &&
-                  d_cfi.ensure(sfs.size() * 4) && hip_ok(hipStreamSynchronize(st), "ctrl upload");
+                  d_cfi.ensure(sfs.size() * 4) && d_phich.ensure(sfs.size() * 4) &&
+                  hip_ok(hipStreamSynchronize(st), "ctrl upload");
   return ok ? 0 : -1;
 }
 
@@ -111,6 +133,7 @@ int CtrlEngine::run(const float2* grid, const float2* ce, uint32_t mask, float n
   if (mask & 4u)
     launch_dci_search(d_llr.as<float>(), d_jobs.as<MiDciJob>(), d_cdata.as<uint32_t>(), d_res.as<MiDciRes>(),
                       (uint32_t)jobs.size(), st);
+  if (mask & 8u) launch_phich(grid, ce, d_sfs.as<MiCtrlSf>(), d_cdata.as<uint32_t>(), d_phich.as<float>(), n, st);
   return hip_ok(hipGetLastError(), "ctrl launch") ? 0 : -1;
 }
 
@@ -160,8 +183,10 @@ struct mi_dl_ctrl {
   mi::CtrlEngine ce;
   mi_dl_batch_t* b = nullptr;
   hipStream_t last = nullptr;
-  bool have_res = false;
+  bool have_res = false, have_phich = false;
+  uint32_t phich_ng = 0;
   std::vector<uint32_t> cfi;
+  std::vector<float> phich;
 };
 
 extern "C" {
@@ -170,6 +195,7 @@ mi_dl_ctrl_t* mi_dl_ctrl_create(mi_dl_batch_t* b, uint32_t phich_ng) {
   if (!b) { mi::set_error("null batch"); return nullptr; }
   auto* c = new mi_dl_ctrl();
   c->b = b;
+  c->phich_ng = phich_ng;
   std::vector<uint32_t> cfi;
   std::vector<uint16_t> rnti;
   for (const mi_dl_sf_cfg_t& s : b->cfgs) { cfi.push_back(s.cfi); rnti.push_back((uint16_t)s.rnti); }
@@ -183,9 +209,37 @@ int mi_dl_ctrl_run_stages(mi_dl_ctrl_t* c, uint32_t mask, void* stream) {
   if (!c) { mi::set_error("null argument"); return -1; }
   c->last = reinterpret_cast<hipStream_t>(stream);
   c->have_res = false;
+  c->have_phich = false;
   return c->ce.run(c->b->eng.d_grid.as<float2>(), c->b->eng.d_ce.as<float2>(), mask, 0.0f, c->last);
 }
-int mi_dl_ctrl_run(mi_dl_ctrl_t* c, void* stream) { return mi_dl_ctrl_run_stages(c, 7u, stream); }
+int mi_dl_ctrl_run(mi_dl_ctrl_t* c, void* stream) { return mi_dl_ctrl_run_stages(c, 15u, stream); }
+
+int mi_dl_ctrl_set_phich(mi_dl_ctrl_t* c, const uint32_t* i_lowest, const uint32_t* n_dmrs) {
+  if (!c || !i_lowest || !n_dmrs) { mi::set_error("null argument"); return -1; }
+  std::vector<uint32_t> cfi, q;
+  std::vector<uint16_t> rnti;
+  for (size_t s = 0; s < c->b->cfgs.size(); s++) {
+    cfi.push_back(c->b->cfgs[s].cfi);
+    rnti.push_back((uint16_t)c->b->cfgs[s].rnti);
+    if (i_lowest[s] > 0xFFFFu || n_dmrs[s] > 7) { mi::set_error("phich query"); return -1; }
+    q.push_back(i_lowest[s] | (n_dmrs[s] << 16));
+  }
+  if (c->last && !mi::hip_ok(hipStreamSynchronize(c->last), "sync")) return -1;
+  return (c->ce.build(c->b->eng.plan, cfi, c->phich_ng, rnti, q) || c->ce.upload(nullptr)) ? -1 : 0;
+}
+
+int mi_dl_ctrl_phich(mi_dl_ctrl_t* c, uint32_t sf, float* soft) {
+  if (!c || sf >= c->ce.sfs.size()) { mi::set_error("bad subframe"); return -1; }
+  if (!c->have_phich) {
+    c->phich.resize(c->ce.sfs.size());
+    if (!mi::hip_ok(hipStreamSynchronize(c->last), "sync") ||
+        !mi::hip_ok(hipMemcpy(c->phich.data(), c->ce.d_phich.p, c->phich.size() * 4, hipMemcpyDeviceToHost), "D2H"))
+      return -1;
+    c->have_phich = true;
+  }
+  if (soft) *soft = c->phich[sf];
+  return c->phich[sf] > 0.0f ? 1 : 0;
+}
 
 int mi_dl_ctrl_result(mi_dl_ctrl_t* c, uint32_t sf, int ul, uint32_t* cfi, uint32_t* format, uint32_t* L,
                       uint32_t* ncce, uint8_t* bits, uint32_t* nbits) {

@@ -305,6 +305,31 @@ uint32_t pdcch_regs(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t cfi, st
   return n;
 }
 
+void phich_calc(uint32_t nof_prb, uint32_t ng, uint32_t I_lowest, uint32_t n_dmrs, uint32_t* group, uint32_t* seq) {
+  const uint32_t N = phich_ngroups(nof_prb, ng);
+  *group = (I_lowest + n_dmrs) % N;
+  *seq = (I_lowest / N + n_dmrs) % 8;
+}
+
+// REG n_i = (N_ID + m + floor(i n0' / 3)) mod n0' of the symbol-0 REGs not used by the PCFICH
+// (36.211 6.9.3, normal duration), its 4 non-CRS REs each
+int phich_res(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t group, uint32_t* re12) {
+  if (group >= phich_ngroups(nof_prb, ng)) return -1;
+  const uint32_t W = 12 * nof_prb, n0 = 2 * nof_prb, vs3 = (id % 6) % 3;
+  std::vector<uint8_t> used0(n0, 0);
+  const uint32_t kbar = 6 * (id % (2 * nof_prb));
+  for (uint32_t i = 0; i < 4; i++) used0[((kbar + (i * nof_prb / 2) * 6) % W) / 6] = 1;
+  std::vector<uint32_t> free0;
+  for (uint32_t r = 0; r < n0; r++) if (!used0[r]) free0.push_back(r);
+  const uint32_t nf = (uint32_t)free0.size();
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < 3; i++) {
+    const uint32_t k0 = 6 * free0[(id + group + (i * nf) / 3) % nf];
+    for (uint32_t k = k0; k < k0 + 6; k++) if (k % 3 != vs3) re12[n++] = k;
+  }
+  return 0;
+}
+
 void pdcch_quad_perm(uint32_t M, uint32_t id, std::vector<uint32_t>& log_of_reg) {
   const uint32_t R = (M + 31) / 32, ND = 32 * R - M;
   std::vector<uint32_t> w;

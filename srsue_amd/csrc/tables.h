@@ -40,6 +40,10 @@ void cfi_codeword(uint32_t cfi, uint8_t* b32);                       // 36.212 T
 // ---- DL control: 36.211 6.2.4 / 6.7.4 / 6.8.5 / 6.9.3, 36.212 5.1.4.2 / 5.3.3,
 // 36.213 9.1.1.  Same restatement as oracle/o_ctrl.c (which documents the spec walk-through).
 uint32_t phich_ngroups(uint32_t nof_prb, uint32_t ng);               // ng: 0..3 = Ng 1/6, 1/2, 1, 2
+// PHICH (36.213 9.1.2 FDD): group / orthogonal sequence of an UL grant; the group's 12 symbol-0 REs
+void phich_calc(uint32_t nof_prb, uint32_t ng, uint32_t I_lowest, uint32_t n_dmrs, uint32_t* group, uint32_t* seq);
+int phich_res(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t group, uint32_t* re12);
+inline uint32_t phich_cinit(uint32_t id, uint32_t sf) { return (sf + 1) * (2 * id + 1) * 512 + id; }
 // PDCCH REGs (not PCFICH / PHICH) in 6.8.5 mapping order, 4 RE indices each; returns N_REG
 uint32_t pdcch_regs(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t cfi, std::vector<uint32_t>* re4);
 // logical quadruplet carried by each physical REG (quadruplet sub-block interleaver + shift by N_ID)

@@ -32,8 +32,9 @@ struct mi_ue_dl_ctx {
 namespace {
 
 // plan the control stage for the instance's single subframe (cheap: tables of one cell / sf / cfi)
-bool ctrl_plan(mi_ue_dl_ctx* c, uint32_t cfi, uint16_t rnti) {
-  return c->ctrl.build(c->eng.plan, std::vector<uint32_t>{cfi}, c->phich_ng, std::vector<uint16_t>{rnti}) == 0 &&
+bool ctrl_plan(mi_ue_dl_ctx* c, uint32_t cfi, uint16_t rnti, uint32_t phich_q = 0) {
+  return c->ctrl.build(c->eng.plan, std::vector<uint32_t>{cfi}, c->phich_ng, std::vector<uint16_t>{rnti},
+                       std::vector<uint32_t>{phich_q}) == 0 &&
          c->ctrl.upload(c->st) == 0;
 }
 
@@ -320,6 +321,21 @@ int srslte_ue_dl_find_ul_dci(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t 
   return find_dci(q, msg, cfi, sf_idx, rnti, true, false);
 }
 uint32_t srslte_ue_dl_get_ncce(srslte_ue_dl_t* q) { return q ? q->last_n_cce : 0; }
+
+bool srslte_ue_dl_decode_phich(srslte_ue_dl_t* q, uint32_t sf_idx, uint32_t n_prb_lowest, uint32_t n_dmrs) {
+  if (!q || !q->ctx || !q->ctx->fft_done || sf_idx != q->ctx->sf_idx || n_prb_lowest > 0xFFFFu || n_dmrs > 7)
+    return false;
+  mi_ue_dl_ctx* c = q->ctx;
+  float soft = 0.0f;
+  // the grid / ce of the last decode_fft_estimate are still in HBM (device_grid keeps them)
+  if (!ctrl_plan(c, c->cfi ? c->cfi : 1, q->current_rnti, n_prb_lowest | (n_dmrs << 16)) ||
+      c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 8u, 0.0f, c->st) ||
+      !mi::hip_ok(hipMemcpyAsync(&soft, c->ctrl.d_phich.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") ||
+      !mi::hip_ok(hipStreamSynchronize(c->st), "sync"))
+    return false;
+  // the rebuilt plan has the same CFI: the PDCCH soft bits stay valid for find_ul_dci (:426)
+  return soft > 0.0f;
+}
 
 static uint32_t take_bits(const uint8_t* b, uint32_t* pos, uint32_t n) {
   uint32_t v = 0;

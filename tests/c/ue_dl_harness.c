@@ -9,11 +9,13 @@
  *   PDCCH mode (hdr[5] = 1): srslte_pdcch_extract_llr (:260), srslte_ue_dl_find_dl_dci_type (:293),
  *              srslte_dci_msg_to_dl_grant (:297), srslte_ue_dl_get_ncce (:314); the PDSCH grant and
  *              rv come from the decoded DCI (p[2], p[3] unused)
- * Input file : int32 hdr[8] = {cell_id, nof_prb, nof_ports, nsf, phich_ng, pdcch_mode}; per subframe
+ *   PHICH (hdr[6] = 1): srslte_ue_dl_decode_phich(&ue_dl, sf, I_lowest, n_dmrs) (:381) after the PDSCH,
+ *              with I_lowest = hdr[7] & 0xffff, n_dmrs = hdr[7] >> 16
+ * Input file : int32 hdr[8] = {cell_id, nof_prb, nof_ports, nsf, phich_ng, pdcch_mode, phich, query}; per subframe
  *              int32 p[8] = {sf_idx, tbs, Qm, rv, reset_tbs, rnti, max_its, pass_own_buffers} +
  *              2*SF_LEN floats.
  * Output file: per subframe int32 r[8] = {ret, cfi, noi, dci_found, ncce, grant_tbs, harq, rv} +
- *              float m[5] + tbs/8 payload bytes.
+ *              float m[5] + int32 phich (1 ACK, 0 NACK, -1 not asked) + tbs/8 payload bytes.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -108,8 +110,11 @@ int main(int argc, char **argv) {
     m[0] = srslte_chest_dl_get_rsrp(&ue_dl.chest); m[1] = srslte_chest_dl_get_rssi(&ue_dl.chest);
     m[2] = srslte_chest_dl_get_rsrq(&ue_dl.chest); m[3] = srslte_chest_dl_get_noise_estimate(&ue_dl.chest);
     m[4] = srslte_chest_dl_get_snr(&ue_dl.chest);
+    int32_t ph = -1;
+    if (hdr[6]) ph = srslte_ue_dl_decode_phich(&ue_dl, (uint32_t)p[0], (uint32_t)hdr[7] & 0xffffu, (uint32_t)hdr[7] >> 16);
     fwrite(r, 4, 8, fo);
     fwrite(m, 4, 5, fo);
+    fwrite(&ph, 4, 1, fo);
     fwrite(payload, 1, (size_t)p[1] / 8, fo);
   }
   srslte_softbuffer_rx_free(&sb);

@@ -125,6 +125,12 @@ def lib():
                                       C.POINTER(DciFound)]),
             "or_tx_pdcch": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint16, C.c_uint32, C.c_uint32, u8, C.c_uint32,
                                       C.c_void_p, f32]),
+            "or_phich_calc": (None, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32)]),
+            "or_phich_cinit": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+            "or_phich_res": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint32, u32]),
+            "or_phich_soft": (C.c_float, [C.POINTER(CtrlCfg), f32, f32, C.c_uint32, C.c_uint32]),
+            "or_tx_phich": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, f32]),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -194,6 +200,18 @@ def pdcch_llr(q, grid, ce):
     lib().or_pdcch_llr(C.byref(q), np.ascontiguousarray(grid, np.float32), np.ascontiguousarray(ce, np.float32),
                        0.0, llr, C.byref(n))
     return llr, n.value
+
+
+def phich_calc(nof_prb, ng, i_lowest, n_dmrs):
+    g, q = C.c_uint32(), C.c_uint32()
+    lib().or_phich_calc(nof_prb, ng, i_lowest, n_dmrs, C.byref(g), C.byref(q))
+    return g.value, q.value
+
+
+def phich_soft(q, grid, ce, group, seq):
+    """Oracle soft HI of PHICH (group, seq): > 0 favours ACK."""
+    return lib().or_phich_soft(C.byref(q), np.ascontiguousarray(grid, np.float32),
+                               np.ascontiguousarray(ce, np.float32), group, seq)
 
 
 def find_dci(llr, n_cce, nof_prb, sf, rnti, ul=False):

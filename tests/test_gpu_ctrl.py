@@ -111,3 +111,33 @@ def test_blind_search_bit_exact_on_identical_soft_bits(snr):
                 assert got[0] == ref[0] and np.array_equal(got[1], ref[1]) and got[2:] == ref[2:]
     assert 0 <= nfound <= 2 * n_sf
     ctl.close()
+
+
+@pytest.mark.parametrize("ng", [0, 2, 3])
+def test_phich_batch_round_trip_and_oracle_parity(ng):
+    """PHICH (36.211 6.9) through mi_dl_ctrl_set_phich / _phich: per subframe an UL grant (I_lowest,
+    n_dmrs) -> (group, seq); the oracle's transmitter puts ACK or NACK there (plus an interfering
+    PHICH on another sequence of the same group); the GPU HI equals the transmitted one and its soft
+    value the oracle's on the oracle's own front end within 1e-3 relative."""
+    from test_oracle_ctrl import tx_with_phich
+    cases = [(100, 1, 1, 7, 0, 1, None), (100, 2, 4, 33, 3, 0, 6.0), (25, 1, 0, 5, 1, 1, 4.0),
+             (6, 2, 9, 2, 7, 0, None), (50, 1, 6, 49, 2, 1, 8.0)]   # nprb, ports, sf, I_lowest, n_dmrs, ack, snr
+    cfgs, iqs, want = [], [], []
+    for i, (nprb, ports, sf, il, nd, ack, snr) in enumerate(cases):
+        cfg = abi.sf_cfg(cell_id=11 + 5 * i, nof_prb=nprb, nof_ports=ports, sf_idx=sf, cfi=1, tbs=1000, Qm=2)
+        g, sq = O.phich_calc(nprb, ng, il, nd)
+        h = [0.8 + 0.3j, -0.4 + 0.5j] if ports == 2 else None
+        iq, q = tx_with_phich(cfg, ng, [(g, sq, ack), (g, (sq + 3) % 8, 1 - ack)], h=h, snr_db=snr, seed=i + 1)
+        grid, ce, _, _ = oracle_front(cfg, iq)
+        cfgs.append(cfg)
+        iqs.append(iq)
+        want.append((ack, O.phich_soft(q, grid, ce, g, sq)))
+    b, d = front_batch(cfgs, iqs)
+    c = abi.Ctrl(b, phich_ng=ng)
+    c.set_phich([x[3] for x in cases], [x[4] for x in cases])
+    c.run(torch.cuda.current_stream().cuda_stream, mask=abi.Ctrl.PHICH)
+    for i, (ack, osoft) in enumerate(want):
+        got, soft = c.phich(i)
+        assert got == bool(ack) and (osoft > 0) == bool(ack), (i, got, soft, osoft)
+        assert abs(soft - osoft) <= 1e-3 * max(1.0, abs(osoft)), (i, soft, osoft)
+    c.close()

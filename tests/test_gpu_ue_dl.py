@@ -10,6 +10,7 @@ import tempfile
 import numpy as np
 import pytest
 
+import oracle_lib as O
 from helpers import oracle_dlsch, oracle_front, tb_bytes
 from srsue_amd import abi
 
@@ -17,12 +18,15 @@ pytestmark = pytest.mark.gpu
 HARNESS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "ue_dl_harness")
 
 
-def run_harness(cell_id, nof_prb, nof_ports, subframes, phich_ng=0, pdcch=False, full=False):
-    """subframes: list of (cfg, iq, reset_tbs, max_its, own_buffers)"""
+def run_harness(cell_id, nof_prb, nof_ports, subframes, phich_ng=0, pdcch=False, full=False, phich=None):
+    """subframes: list of (cfg, iq, reset_tbs, max_its, own_buffers); phich = (I_lowest, n_dmrs) asks
+    srslte_ue_dl_decode_phich every subframe (full: its result is the last entry of the extras)"""
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
         with open(fin, "wb") as f:
-            f.write(struct.pack("8i", cell_id, nof_prb, nof_ports, len(subframes), phich_ng, int(pdcch), 0, 0))
+            q = 0 if phich is None else phich[0] | (phich[1] << 16)
+            f.write(struct.pack("8i", cell_id, nof_prb, nof_ports, len(subframes), phich_ng, int(pdcch),
+                                int(phich is not None), q))
             for cfg, iq, reset, max_its, own in subframes:
                 f.write(struct.pack("8i", cfg.sf_idx, cfg.tbs, cfg.Qm, cfg.rv, int(reset), cfg.rnti, max_its,
                                     int(own)))
@@ -33,8 +37,9 @@ def run_harness(cell_id, nof_prb, nof_ports, subframes, phich_ng=0, pdcch=False,
         for cfg, *_ in subframes:
             r = struct.unpack_from("8i", raw, pos); pos += 32
             m = struct.unpack_from("5f", raw, pos); pos += 20
+            ph, = struct.unpack_from("i", raw, pos); pos += 4
             pay = np.frombuffer(raw[pos:pos + cfg.tbs // 8], np.uint8); pos += cfg.tbs // 8
-            out.append((r[0], r[1], r[2], m, pay) + ((r[3:],) if full else ()))
+            out.append((r[0], r[1], r[2], m, pay) + ((r[3:] + (ph,),) if full else ()))
         return out
 
 
@@ -115,7 +120,30 @@ def test_ue_dl_pdcch_to_pdsch_srsue_call_order():
     res += run_harness(11, 100, 2, subs[1:2], phich_ng=ng, pdcch=True, full=True)
     res += run_harness(11, 100, 1, subs[2:], phich_ng=ng, pdcch=True, full=True)
     for (cfg, *_), (ret, cf, noi, met, pay, extra), (tb, ncce, harq, rv, tbs) in zip(subs, res, truth):
-        found, gncce, gtbs, gharq, grv = extra
+        found, gncce, gtbs, gharq, grv, _ = extra
         assert cf == cfg.cfi and found == 1 and gncce == ncce
         assert (gtbs, gharq, grv) == (tbs, harq, rv)
         assert ret == 0 and np.array_equal(pay, tb)
+
+
+def test_ue_dl_decode_phich_srsue_call_order():
+    """srslte_ue_dl_decode_phich (phch_worker.cc:381) after the PDSCH of the same TTI: the HI the
+    oracle's transmitter put on the UL grant's PHICH (36.213 9.1.2) is returned, alternating ACK /
+    NACK over subframes; the PDSCH of those subframes still decodes."""
+    from test_oracle_ctrl import tx_with_phich
+    ng, il, nd = 2, 17, 3
+    g, sq = O.phich_calc(100, ng, il, nd)
+    subs, tbs = [], []
+    for i, sf in enumerate((1, 2, 3, 4)):
+        c = abi.sf_cfg(nof_prb=100, sf_idx=sf, tbs=75376, Qm=6)
+        ack = i % 2
+        iq, _ = tx_with_phich(c, ng, [(g, sq, ack)], snr_db=None, seed=i)
+        tb = tb_bytes(200 + i, c.tbs)
+        iq = iq + abi.tx_subframe(c, tb, snr_db=30.0, seed=i) - abi.tx_subframe(c, np.zeros(c.tbs // 8, np.uint8),
+                                                                               snr_db=300.0, seed=i)
+        subs.append((c, iq.astype(np.float32), True, 0, True))
+        tbs.append((tb, ack))
+    res = run_harness(1, 100, 1, subs, phich_ng=ng, full=True, phich=(il, nd))
+    for (ret, cf, noi, met, pay, extra), (tb, ack) in zip(res, tbs):
+        assert ret == 0 and np.array_equal(pay, tb)
+        assert extra[-1] == ack

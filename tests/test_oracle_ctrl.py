@@ -169,3 +169,72 @@ def test_pdcch_round_trip_blind_search(nprb, ports, cfi, ng, sf, snr):
     assert fmt == O.DCI_1A and np.array_equal(b, bits[:A]) and L <= Ls[pick] and ncce == nc[pick]
     assert O.find_dci(llr, n_cce, nprb, sf, 0x47) is None
     assert O.find_dci(llr, n_cce, nprb, sf, rnti, ul=True) is None    # a 1A is not a format 0
+
+
+# ---- PHICH (36.211 6.9, 36.213 9.1.2) -----------------------------------------------------------
+@pytest.mark.parametrize("nprb,ng", [(100, 2), (25, 0), (6, 3), (50, 1)])
+def test_phich_resource_36213(nprb, ng):
+    """group = (I_lowest + n_dmrs) mod N_group, seq = (floor(I_lowest / N_group) + n_dmrs) mod 8."""
+    N = O.lib().or_phich_ngroups(nprb, ng)
+    for i_low in range(0, nprb, 3):
+        for n_dmrs in range(8):
+            assert O.phich_calc(nprb, ng, i_low, n_dmrs) == ((i_low + n_dmrs) % N, (i_low // N + n_dmrs) % 8)
+
+
+@pytest.mark.parametrize("nprb,ports,ng,cid", [(100, 1, 2, 1), (25, 2, 3, 11), (6, 1, 0, 301), (50, 2, 1, 7)])
+def test_phich_res_disjoint(nprb, ports, ng, cid):
+    """The 3 REGs of every PHICH group: 12 symbol-0 REs, no CRS, disjoint across groups, from the
+    PCFICH REs and from every PDCCH REG."""
+    q = O.ctrl_cfg(cid, nprb, ports, ng, 1, 0)
+    N = O.lib().or_phich_ngroups(nprb, ng)
+    seen = set()
+    for g in range(N):
+        re = np.zeros(12, np.uint32)
+        assert O.lib().or_phich_res(C.byref(q), g, re) == 0
+        assert all(int(r) < 12 * nprb for r in re)                          # symbol 0
+        assert all(int(r) % 3 != (cid % 6) % 3 for r in re)                 # not a CRS RE
+        assert not (set(int(r) for r in re) & seen) and len(set(re)) == 12
+        seen |= set(int(r) for r in re)
+    assert O.lib().or_phich_res(C.byref(q), N, np.zeros(12, np.uint32)) == -1
+    k16 = np.zeros(16, np.uint32)
+    O.lib().or_pcfich_k(C.byref(O.Cell(cid, nprb, 1)), k16.ctypes.data_as(C.c_void_p))
+    assert not (set(int(k) for k in k16) & seen)
+    n = C.c_uint32()
+    M = O.lib().or_pdcch_regs(C.byref(q), None, C.byref(n))
+    re4 = np.zeros(4 * M, np.uint32)
+    O.lib().or_pdcch_regs(C.byref(q), re4.ctypes.data, C.byref(n))
+    assert not (set(int(r) for r in re4) & seen)
+
+
+def tx_with_phich(cfg, ng, hs, h=None, snr_db=None, seed=0):
+    """Product-TX subframe + the oracle's PHICHs hs = [(group, seq, ack)], then AWGN (numpy)."""
+    iq = abi.tx_subframe(cfg, np.zeros(cfg.tbs // 8, np.uint8), h=h, snr_db=300.0, seed=seed)
+    q = O.ctrl_cfg(cfg.cell_id, cfg.nof_prb, cfg.nof_ports, ng, cfg.cfi, cfg.sf_idx)
+    hh = None if h is None else np.array([v for z in h for v in (z.real, z.imag)], np.float32)
+    for g, sq, ack in hs:
+        assert O.lib().or_tx_phich(C.byref(q), g, sq, int(ack), None if hh is None else hh.ctypes.data, iq) == 0
+    if snr_db is not None:
+        rng = np.random.default_rng(seed)
+        iq = iq + rng.normal(0, np.sqrt(10 ** (-snr_db / 10) / 2), iq.shape).astype(np.float32)
+    return iq.astype(np.float32), q
+
+
+@pytest.mark.parametrize("nprb,ports,ng,sf,snr", [(100, 1, 2, 1, None), (100, 2, 1, 4, 5.0), (25, 1, 3, 0, 3.0),
+                                                  (6, 2, 0, 9, None)])
+def test_phich_round_trip(nprb, ports, ng, sf, snr):
+    """Transmit-chain ground truth: ACK / NACK on two orthogonal sequences of one group (and a third
+    PHICH in another group when there is one) decode to the transmitted HI; noiseless soft = +-12
+    (12 despread chips); an unused sequence of the group reads ~0."""
+    cfg = abi.sf_cfg(cell_id=3 + nprb, nof_prb=nprb, nof_ports=ports, sf_idx=sf, cfi=1, tbs=1000, Qm=2)
+    N = O.lib().or_phich_ngroups(nprb, ng)
+    hs = [(0, 1, 1), (0, 6, 0)] + ([(N - 1, 3, 1)] if N > 1 else [])
+    h = [0.8 + 0.3j, -0.4 + 0.5j] if ports == 2 else None
+    iq, q = tx_with_phich(cfg, ng, hs, h=h, snr_db=snr, seed=sf + 1)
+    grid, ce, _, _ = oracle_front(cfg, iq)
+    for g, sq, ack in hs:
+        s = O.phich_soft(q, grid, ce, g, sq)
+        assert (s > 0) == bool(ack), (g, sq, ack, s)
+        if snr is None:
+            assert abs(abs(s) - 12.0) < 1e-3
+    if snr is None:
+        assert abs(O.phich_soft(q, grid, ce, 0, 2)) < 1e-3
