@@ -60,16 +60,22 @@ def tb_payload(seed, nbytes):
 
 
 def kernel_src_hash():
-    """Content hash of the HIP/C++ sources: a committed PMC traffic figure is only reported when it
-    was measured on exactly these kernels (profiles/traffic.json, written by tools/profile.sh)."""
+    """Content hash of the sources that define the measured PDSCH path (its kernels, their layouts and
+    the planner): a committed PMC traffic figure is only reported when it was measured on exactly these
+    (profiles/traffic.json, written by tools/profile.sh).  Other rows (control, sync, per-TTI glue)
+    do not enter the default bench."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(ROOT, "srsue_amd", "csrc")
-    for f in sorted(os.listdir(d)):
-        if f.endswith((".h", ".hip", ".cpp")) and f != "emu.cpp":
-            h.update(f.encode())
-            h.update(open(os.path.join(d, f), "rb").read())
+    for f in PATH_SOURCES:
+        h.update(f.encode())
+        h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
+
+
+PATH_SOURCES = ("cbscatter.hip", "chest.hip", "demap.hip", "dl_common.h", "engine.cpp", "engine.h", "kernels.h",
+                "kernels_consts.h", "ofdm.hip", "plan.cpp", "plan.h", "rm.hip", "rm_body.h", "tables.cpp", "tables.h",
+                "tb.hip", "tb_body.h", "tdec.hip", "tdec_body.h")
 
 
 def pmc_traffic(sf_per_gpu, tdec):

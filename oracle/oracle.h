@@ -211,6 +211,19 @@ int      or_decode_subframe(const or_cell_t *c, uint32_t sf, uint32_t cfi, const
                             const float *iq, float *sb, uint32_t sb_stride, int new_tb,
                             uint32_t max_its, uint8_t *payload, uint32_t *noi_out);
 
+/* ---- sync front end (o_sync.c) ------------------------------------------- */
+typedef struct { uint32_t nid2, lag; float rho, cfo; } or_pss_res_t;
+void     or_pss_seq(uint32_t nid2, float *d /* 62 complex */);
+void     or_sss_m(uint32_t nid1, uint32_t *m0, uint32_t *m1);
+void     or_sss_seq(uint32_t nid1, uint32_t nid2, uint32_t sf5, float *d /* 62 real */);
+void     or_pss_time(uint32_t nid2, uint32_t nof_prb, float *x /* 2N: PSS symbol useful part */);
+uint32_t or_sync_sym_off(uint32_t N, uint32_t l);
+int      or_tx_sync(uint32_t cell_id, uint32_t nof_prb, uint32_t sf_idx, float amp, float *iq);
+int      or_pss_find(const float *x, uint32_t nof_prb, uint32_t nid2_mask, uint32_t nlag, or_pss_res_t *r);
+void     or_cfo_correct(const float *x, uint32_t n, float cfo, uint32_t N, float *y);
+int      or_sss_detect(const float *sf_iq, uint32_t nof_prb, uint32_t nid2, uint32_t *nid1, uint32_t *sf5,
+                       float *score);
+
 #ifdef __cplusplus
 }
 #endif

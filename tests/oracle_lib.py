@@ -131,6 +131,16 @@ def lib():
             "or_phich_res": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint32, u32]),
             "or_phich_soft": (C.c_float, [C.POINTER(CtrlCfg), f32, f32, C.c_uint32, C.c_uint32]),
             "or_tx_phich": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, f32]),
+            "or_pss_seq": (None, [C.c_uint32, f32]),
+            "or_sss_m": (None, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+            "or_sss_seq": (None, [C.c_uint32, C.c_uint32, C.c_uint32, f32]),
+            "or_pss_time": (None, [C.c_uint32, C.c_uint32, f32]),
+            "or_sync_sym_off": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+            "or_tx_sync": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_float, f32]),
+            "or_pss_find": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(PssRes)]),
+            "or_cfo_correct": (None, [f32, C.c_uint32, C.c_float, C.c_uint32, f32]),
+            "or_sss_detect": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_float)]),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -186,6 +196,29 @@ class tdec_mode:
 
     def __exit__(self, *a):
         lib().or_set_tdec_mode(self.prev)
+
+
+class PssRes(C.Structure):
+    _fields_ = [("nid2", C.c_uint32), ("lag", C.c_uint32), ("rho", C.c_float), ("cfo", C.c_float)]
+
+
+def pss_find(x, nof_prb, nid2_mask, nlag):
+    r = PssRes()
+    assert lib().or_pss_find(np.ascontiguousarray(x, np.float32), nof_prb, nid2_mask, nlag, C.byref(r)) == 0
+    return r.nid2, r.lag, r.rho, r.cfo
+
+
+def cfo_correct(x, cfo, N):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.zeros_like(x)
+    lib().or_cfo_correct(x, len(x) // 2, cfo, N, y)
+    return y
+
+
+def sss_detect(sf_iq, nof_prb, nid2):
+    a, b, s = C.c_uint32(), C.c_uint32(), C.c_float()
+    lib().or_sss_detect(np.ascontiguousarray(sf_iq, np.float32), nof_prb, nid2, C.byref(a), C.byref(b), C.byref(s))
+    return a.value, b.value, s.value
 
 
 def ctrl_cfg(cell_id=1, nof_prb=100, nof_ports=1, ng=2, cfi=1, sf=1):
