@@ -144,6 +144,29 @@ int           mi_dl_ctrl_llr(mi_dl_ctrl_t *c, float *host, size_t n, int upload)
 int           mi_dl_ctrl_set_phich(mi_dl_ctrl_t *c, const uint32_t *i_lowest, const uint32_t *n_dmrs);
 int           mi_dl_ctrl_phich(mi_dl_ctrl_t *c, uint32_t sf, float *soft);
 
+/* ---- sync front end ----------------------------------------------------
+ * The data-parallel part of srslte_ue_sync_zerocopy (phch_recv.cc:321): PSS timing + N_ID_2 search,
+ * the PSS CFO estimate, SSS detection (N_ID_1, subframe 0 or 5) and CFO correction, batched over
+ * device-resident IQ (cf32 offsets in samples).  pss(): window i starts at d_iq[off[i]], candidate
+ * lags 0..nlag-1 (the PSS symbol's useful part, N samples, starting at the lag), N_ID_2 candidates in
+ * nid2_mask (bit u); rho = |sum x conj(p)|^2 / (E_x E_p); cfo in subcarrier spacings (|cfo| < 1).
+ * sss(): subframe i starts at d_iq[sf_off[i]].  correct(): len samples of d_src[src_off[i]] rotated
+ * by exp(-j 2 pi cfo[i] n / N) into d_dst[dst_off[i]] (enqueued on stream); pss / sss are synchronous.
+ * mi_tx_sync adds the PSS / SSS of subframes 0 and 5 to a subframe's IQ (synthetic transmitter). */
+typedef struct mi_sync mi_sync_t;
+typedef struct { uint32_t nid2, lag; float rho, cfo; } mi_pss_result_t;
+typedef struct { uint32_t nid1, sf5; float score; } mi_sss_result_t;
+mi_sync_t *mi_sync_create(uint32_t nof_prb);
+void       mi_sync_destroy(mi_sync_t *s);
+uint32_t   mi_sync_fft_size(const mi_sync_t *s);
+int        mi_sync_pss(mi_sync_t *s, const void *d_iq, const uint64_t *off, uint32_t n, uint32_t nlag,
+                       uint32_t nid2_mask, mi_pss_result_t *out, void *stream);
+int        mi_sync_sss(mi_sync_t *s, const void *d_iq, const uint64_t *sf_off, const uint32_t *nid2, const float *cfo,
+                       uint32_t n, mi_sss_result_t *out, void *stream);
+int        mi_sync_correct(mi_sync_t *s, const void *d_src, const uint64_t *src_off, void *d_dst,
+                           const uint64_t *dst_off, const float *cfo, uint32_t n, uint32_t len, void *stream);
+int        mi_tx_sync(uint32_t cell_id, uint32_t nof_prb, uint32_t sf_idx, float amp, float *iq);
+
 /* ---- host-IQ streaming pipeline -------------------------------------
  * Double buffering for IQ that arrives in host memory (srsUE's sync thread writes the worker's
  * buffer, phch_recv.cc:321-322): two batches of the same configuration, one copy stream and one

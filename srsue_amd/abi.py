@@ -99,6 +99,13 @@ def lib():
             "mi_dl_ctrl_llr": (C.c_int, [vp, vp, sz, C.c_int]),
             "mi_dl_ctrl_set_phich": (C.c_int, [vp, vp, vp]),
             "mi_dl_ctrl_phich": (C.c_int, [vp, u32, vp]),
+            "mi_sync_create": (vp, [u32]),
+            "mi_sync_destroy": (None, [vp]),
+            "mi_sync_fft_size": (u32, [vp]),
+            "mi_sync_pss": (C.c_int, [vp, vp, vp, u32, u32, u32, vp, vp]),
+            "mi_sync_sss": (C.c_int, [vp, vp, vp, vp, vp, u32, vp, vp]),
+            "mi_sync_correct": (C.c_int, [vp, vp, vp, vp, vp, vp, u32, u32, vp]),
+            "mi_tx_sync": (C.c_int, [u32, u32, u32, C.c_float, vp]),
             "mi_dl_pipe_create": (vp, [vp, u32, u32, u32]),
             "mi_dl_pipe_destroy": (None, [vp]),
             "mi_dl_pipe_submit": (C.c_int, [vp, vp]),
@@ -304,6 +311,70 @@ class Ctrl:
     def close(self):
         if self.h:
             lib().mi_dl_ctrl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PssResult(C.Structure):
+    _fields_ = [("nid2", C.c_uint32), ("lag", C.c_uint32), ("rho", C.c_float), ("cfo", C.c_float)]
+
+
+class SssResult(C.Structure):
+    _fields_ = [("nid1", C.c_uint32), ("sf5", C.c_uint32), ("score", C.c_float)]
+
+
+def tx_sync(cell_id, nof_prb, sf_idx, iq, amp=1.0):
+    """add the PSS / SSS of subframe 0 / 5 to iq (float32 interleaved, in place)"""
+    assert iq.dtype == np.float32 and iq.flags.c_contiguous
+    rc = lib().mi_tx_sync(cell_id, nof_prb, sf_idx, amp, iq.ctypes.data)
+    if rc < 0:
+        raise RuntimeError("mi_tx_sync: " + last_error())
+    return rc
+
+
+class Sync:
+    """Sync front end (mi_sync_*) over device-resident IQ (offsets in cf32 samples)."""
+
+    def __init__(self, nof_prb):
+        self.h = lib().mi_sync_create(nof_prb)
+        if not self.h:
+            raise RuntimeError("mi_sync_create: " + last_error())
+        self.N = lib().mi_sync_fft_size(self.h)
+
+    def pss(self, d_iq, offsets, nlag, nid2_mask=7, stream_ptr=None):
+        off = np.ascontiguousarray(offsets, np.uint64)
+        out = (PssResult * max(len(off), 1))()
+        if lib().mi_sync_pss(self.h, C.c_void_p(d_iq), off.ctypes.data, len(off), nlag, nid2_mask, out,
+                             C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_sync_pss: " + last_error())
+        return [(r.nid2, r.lag, r.rho, r.cfo) for r in out[:len(off)]]
+
+    def sss(self, d_iq, sf_offsets, nid2, cfo, stream_ptr=None):
+        off = np.ascontiguousarray(sf_offsets, np.uint64)
+        n2 = np.ascontiguousarray(nid2, np.uint32)
+        cf = np.ascontiguousarray(cfo, np.float32)
+        out = (SssResult * max(len(off), 1))()
+        if lib().mi_sync_sss(self.h, C.c_void_p(d_iq), off.ctypes.data, n2.ctypes.data, cf.ctypes.data, len(off), out,
+                             C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_sync_sss: " + last_error())
+        return [(r.nid1, r.sf5, r.score) for r in out[:len(off)]]
+
+    def correct(self, d_src, src_off, d_dst, dst_off, cfo, length, stream_ptr=None):
+        a = np.ascontiguousarray(src_off, np.uint64)
+        b = np.ascontiguousarray(dst_off, np.uint64)
+        c = np.ascontiguousarray(cfo, np.float32)
+        if lib().mi_sync_correct(self.h, C.c_void_p(d_src), a.ctypes.data, C.c_void_p(d_dst), b.ctypes.data,
+                                 c.ctypes.data, len(a), length, C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_sync_correct: " + last_error())
+
+    def close(self):
+        if self.h:
+            lib().mi_sync_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -13,6 +13,7 @@
 #include "dl_common.h"
 #include "mi_dl.h"
 #include "tables.h"
+#include "sync.h"
 
 namespace mi {
 
@@ -264,6 +265,41 @@ extern "C" int mi_pdsch_G(const mi_dl_sf_cfg_t* c) {
   std::vector<uint32_t> re;
   return (int)(mi::pdsch_re_list(c->cell_id, c->nof_prb, c->nof_ports, c->cfi, c->sf_idx, c->prb_mask, re) * c->Qm);
 }
+// PSS (symbol 6) + SSS (symbol 5) of subframes 0 / 5 (36.211 6.11), amplitude amp per RE, added to the
+// subframe's IQ through the same 1/sqrt(N) OFDM modulation as the PDSCH (a direct 62-bin IDFT)
+extern "C" int mi_tx_sync(uint32_t cell_id, uint32_t nof_prb, uint32_t sf_idx, float amp, float* iq) {
+  if (sf_idx != 0 && sf_idx != 5) return 0;
+  const int Ni = mi::symbol_sz(nof_prb);
+  if (Ni < 0 || !iq || cell_id > 503) return -1;
+  const uint32_t N = (uint32_t)Ni;
+  float2 pss[62];
+  float sss[62];
+  mi::pss_seq(cell_id % 3, pss);
+  mi::sss_seq(cell_id / 3, cell_id % 3, sf_idx == 5, sss);
+  const double nrm = amp / sqrt((double)N);
+  for (uint32_t l = 5; l <= 6; l++) {
+    const uint32_t cp = (uint32_t)mi::cp_len((int)N, (int)(l % 7)), s0 = (uint32_t)mi::symbol_offset((int)N, (int)l) - cp;
+    for (uint32_t n = 0; n < N; n++) {
+      double re = 0, im = 0;
+      for (uint32_t m = 0; m < 62; m++) {
+        const double dr = l == 6 ? pss[m].x : sss[m], di = l == 6 ? pss[m].y : 0.0;
+        const double ph = 2.0 * M_PI * (double)((uint64_t)mi::sync_bin(m, nof_prb, N) * n % N) / N;
+        re += dr * cos(ph) - di * sin(ph);
+        im += dr * sin(ph) + di * cos(ph);
+      }
+      re *= nrm;
+      im *= nrm;
+      iq[2 * (s0 + cp + n)] += (float)re;
+      iq[2 * (s0 + cp + n) + 1] += (float)im;
+      if (n >= N - cp) {   // cyclic prefix
+        iq[2 * (s0 + n - (N - cp))] += (float)re;
+        iq[2 * (s0 + n - (N - cp)) + 1] += (float)im;
+      }
+    }
+  }
+  return 1;
+}
+
 extern "C" int mi_sf_len(uint32_t nof_prb) {
   const int N = mi::symbol_sz(nof_prb);
   return N < 0 ? -1 : mi::sf_len(N);

@@ -90,3 +90,17 @@ def test_sync_round_trip(cell_id, nof_prb, sf, tau, cfo, snr):
     y = O.cfo_correct(x[2 * sf_start:2 * (sf_start + 15 * N)], est, N)
     nid1, sf5, score = O.sss_detect(y, nof_prb, nid2)
     assert (nid1, sf5) == (cell_id // 3, int(sf == 5)) and score > 0
+
+
+@pytest.mark.parametrize("cell_id,nof_prb,sf", [(1, 100, 0), (302, 25, 5), (503, 6, 5), (77, 75, 0)])
+def test_product_tx_sync_matches_oracle(cell_id, nof_prb, sf):
+    """mi_tx_sync (the product's synthetic transmitter, host code) puts the same PSS / SSS samples on
+    the air as the oracle's or_tx_sync; other subframes get nothing."""
+    n = 2 * 15 * O.lib().or_symbol_sz(nof_prb)
+    a = np.zeros(n, np.float32)
+    b = np.zeros(n, np.float32)
+    assert abi.tx_sync(cell_id, nof_prb, sf, a) == 1
+    assert O.lib().or_tx_sync(cell_id, nof_prb, sf, 1.0, b) == 1
+    assert np.max(np.abs(a - b)) < 1e-5 and np.max(np.abs(b)) > 0.01
+    c = np.zeros(n, np.float32)
+    assert abi.tx_sync(cell_id, nof_prb, 3, c) == 0 and not c.any()
