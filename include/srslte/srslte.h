@@ -19,6 +19,7 @@
 #include <stdbool.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <time.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -256,6 +257,47 @@ SRSLTE_API int srslte_cbsegm(srslte_cbsegm_t *s, uint32_t tbs);
 SRSLTE_API int srslte_symbol_sz(uint32_t nof_prb);
 SRSLTE_API void *srslte_vec_malloc(uint32_t size);   /* 256-B aligned, free()-compatible (phch_worker.cc:102) */
 SRSLTE_API void srslte_vec_free(void *ptr);
+
+/* ---- sync front end (phch_recv.cc:108-120, 231-240, 321-335) ----------------
+ * srslte_ue_sync in tracking mode on the GPU (srsue_amd/csrc/sync.hip, ue_sync.cpp): the first
+ * zerocopy() calls search a half frame for the cell's PSS (its N_ID_2 = cell.id % 3), check the SSS
+ * (N_ID_1, subframe 0 or 5) and align the stream to a subframe boundary (return 0); afterwards every
+ * call reads one subframe through the receive callback, re-times and re-estimates the CFO on the PSS
+ * of subframes 0 and 5 (an exponential average, srslte_sync_set_em_alpha), corrects the CFO on the GPU
+ * into input_buffer and returns 1.  get_cfo / set_cfo: Hz; get_sfo: mean timing drift in samples/s.
+ * Cell search (srslte_ue_cellsearch_*), MIB decoding (srslte_ue_mib_*) and AGC stay in srsLTE;
+ * start_agc() returns an error, set_agc_period() is accepted. */
+typedef struct SRSLTE_API { time_t full_secs; double frac_secs; } srslte_timestamp_t;
+typedef struct SRSLTE_API { float threshold; float em_alpha; } srslte_sync_t;
+typedef struct SRSLTE_API { float gain; } srslte_agc_t;
+typedef struct mi_ue_sync_ctx mi_ue_sync_ctx;
+typedef struct SRSLTE_API {
+  srslte_cell_t cell;
+  srslte_sync_t strack;
+  srslte_agc_t agc;
+  cf_t *input_buffer;       /* the last delivered subframe (get_buffer) */
+  mi_ue_sync_ctx *ctx;
+} srslte_ue_sync_t;
+SRSLTE_API int srslte_ue_sync_init(srslte_ue_sync_t *q, srslte_cell_t cell,
+                                   int(recv_callback)(void *, void *, uint32_t, srslte_timestamp_t *),
+                                   void *stream_handler);
+SRSLTE_API void srslte_ue_sync_free(srslte_ue_sync_t *q);
+SRSLTE_API int srslte_ue_sync_zerocopy(srslte_ue_sync_t *q, cf_t *input_buffer);
+SRSLTE_API int srslte_ue_sync_get_buffer(srslte_ue_sync_t *q, cf_t **sf_symbols);
+SRSLTE_API uint32_t srslte_ue_sync_get_sfidx(srslte_ue_sync_t *q);
+SRSLTE_API float srslte_ue_sync_get_cfo(srslte_ue_sync_t *q);
+SRSLTE_API float srslte_ue_sync_get_sfo(srslte_ue_sync_t *q);
+SRSLTE_API void srslte_ue_sync_set_cfo(srslte_ue_sync_t *q, float cfo);
+SRSLTE_API void srslte_ue_sync_decode_sss_on_track(srslte_ue_sync_t *q, bool enabled);
+SRSLTE_API void srslte_ue_sync_get_last_timestamp(srslte_ue_sync_t *q, srslte_timestamp_t *timestamp);
+SRSLTE_API void srslte_ue_sync_set_agc_period(srslte_ue_sync_t *q, uint32_t period);
+SRSLTE_API int srslte_ue_sync_start_agc(srslte_ue_sync_t *q, double(set_gain_callback)(void *, double),
+                                        float init_gain_value);
+SRSLTE_API void srslte_sync_set_threshold(srslte_sync_t *q, float threshold);
+SRSLTE_API void srslte_sync_set_em_alpha(srslte_sync_t *q, float alpha);
+SRSLTE_API int srslte_sampling_freq_hz(uint32_t nof_prb);
+SRSLTE_API void srslte_timestamp_copy(srslte_timestamp_t *dest, srslte_timestamp_t *src);
+SRSLTE_API int srslte_timestamp_add(srslte_timestamp_t *t, time_t full_secs, double frac_secs);
 
 #ifdef __cplusplus
 }
