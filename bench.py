@@ -320,6 +320,87 @@ def bench_ctrl(args, batch, dev):
                     f"{B} subframes per step"}
 
 
+def bench_sync(args, batch, dev):
+    """Sync front end over the batch: every subframe arrives in a raw slot of
+    15 N + 64 samples at an unknown offset (1..63) with a CFO (+-0.4 subcarriers); per step the PSS of
+    every subframe 0 / 5 is tracked (+-31 lags around the expected position, mi_sync_pss) and every
+    subframe is realigned + CFO-corrected into the batch's IQ buffer (mi_sync_correct), i.e. exactly
+    what the DL chain then consumes.  Roofline: the correction kernel (one read + one write of each
+    sample)."""
+    B = len(batch.cfgs)
+    N = 2048
+    L, M, slot = 15 * N, 31, 15 * N + 64
+    rng = np.random.default_rng(123)
+    npool = 20
+    raw = np.zeros((npool, 2 * slot), np.float32)
+    taus = rng.integers(1, 64, npool)
+    cfos = rng.uniform(-0.4, 0.4, npool).astype(np.float32)
+    for k in range(npool):
+        c = abi.sf_cfg(cell_id=1, nof_prb=100, sf_idx=k % 10, tbs=61664 if k % 10 in (0, 5) else 75376, Qm=6)
+        iq = abi.tx_subframe(c, tb_payload(900 + k, c.tbs // 8), snr_db=30.0, seed=900 + k)
+        abi.tx_sync(1, 100, k % 10, iq)
+        z = iq[0::2] + 1j * iq[1::2]
+        z = z * np.exp(2j * np.pi * cfos[k] * np.arange(L) / N)
+        raw[k, 2 * taus[k]:2 * (taus[k] + L):2], raw[k, 2 * taus[k] + 1:2 * (taus[k] + L):2] = z.real, z.imag
+    d_pool = torch.from_numpy(raw).to(dev)
+    d_raw = d_pool[torch.arange(B, device=dev) % npool].contiguous()   # [B][2 slot]
+    d_iq = torch.zeros(2 * batch.iq_samples, dtype=torch.float32, device=dev)
+    s = abi.Sync(100)
+    sym6 = (160 + N) + 5 * (144 + N) + 144                            # useful part of symbol 6 (N = 2048)
+    idx = np.arange(B)
+    pss_idx = idx[(idx % npool) % 10 % 5 == 0]                        # subframes 0 / 5
+    pss_off = pss_idx.astype(np.uint64) * slot + 32 + sym6 - M        # receiver expects offset 32
+    half = idx - (idx % npool) % 5                                    # the subframe carrying each one's PSS
+    dst = np.array([batch.iq_offset(i) for i in range(B)], np.uint64)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    tmr = {"pss": 0.0}
+
+    def step():
+        t = time.perf_counter()
+        res = np.array(s.pss(d_raw.data_ptr(), pss_off, 2 * M + 1, 1 << 1, sptr), np.float64)
+        tmr["pss"] += time.perf_counter() - t
+        tau = np.full(B, 32.0)
+        cf = np.zeros(B, np.float32)
+        tau[pss_idx] = 32 + res[:, 1] - M
+        cf[pss_idx] = res[:, 3]
+        # the other subframes take the timing / CFO of their half frame's PSS (the pool's per-subframe
+        # offsets stand in for a drifting stream)
+        src = idx.astype(np.uint64) * slot + tau[half].astype(np.uint64)
+        s.correct(d_raw.data_ptr(), src, d_iq.data_ptr(), dst, cf[half], L, sptr)
+        return res
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    tmr["pss"] = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / args.steps
+    # correction kernel alone (HIP events on the launch stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    src = idx.astype(np.uint64) * slot + 32
+    cf1 = np.full(B, 0.1, np.float32)
+    e0.record()
+    for _ in range(args.steps):
+        s.correct(d_raw.data_ptr(), src, d_iq.data_ptr(), dst, cf1, L, sptr)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    cms = e0.elapsed_time(e1) / args.steps
+    k = pss_idx % npool
+    ok = bool(np.all(np.abs(32 + res[:, 1] - M - taus[k]) <= 1) and np.all(np.abs(res[:, 3] - cfos[k]) < 0.05))
+    s.close()
+    gbs = 2 * 8 * L * B / (cms * 1e-3) / 1e9
+    return {"ms_per_step": round(dt * 1e3, 3), "subframes_per_s": round(B / dt, 1), "timing_cfo_ok": ok,
+            "pss_tracks_per_step": int(len(pss_idx)), "pss_ms": round(tmr["pss"] / args.steps * 1e3, 3),
+            "correct_kernel_ms": round(cms, 3),
+            "correct_roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                                 "frac": round(gbs / 8000.0, 4)},
+            "what": f"PSS tracking (+-{M} lags) of the {len(pss_idx)} subframes 0/5 + realignment and CFO "
+                    f"correction of all {B} subframes into the batch IQ buffer, per step"}
+
+
 def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
     """IQ resident in page-locked host memory, each step copied H2D and decoded through the
     double-buffered pipeline (copy of step i+1 overlaps the decode of step i)."""
@@ -368,6 +449,8 @@ def main():
     ap.add_argument("--h2d", action="store_true",
                     help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
                          "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
+    ap.add_argument("--sync", action="store_true",
+                    help="also time the sync front end (PSS tracking + CFO correction, SURVEY 8f-2) on the batch")
     ap.add_argument("--ctrl", action="store_true",
                     help="also time the DL control stage (SURVEY 8f-1: PCFICH + PDCCH soft bits + DCI blind search "
                          "for each subframe's RNTI) on the batch's grid; reported beside value")
@@ -486,6 +569,8 @@ def main():
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
         if args.ctrl:
             out["ctrl"] = bench_ctrl(args, batch, dev)
+        if args.sync:
+            out["sync"] = bench_sync(args, batch, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
                                                args.tdec == "i16")

@@ -14,7 +14,7 @@ struct MiSssRes { uint32_t nid1, sf5; float score, pad; };
 struct MiCfoJob { uint64_t src, dst; float cfo; uint32_t pad; };
 
 void launch_pss_search(const float2* iq, const float2* tmpl, const MiPssJob* jobs, MiPssRes* res, uint32_t n, uint32_t N,
-                       hipStream_t st);
+                       uint32_t max_nlag, hipStream_t st);
 void launch_sss_detect(const float2* iq, const MiSssJob* jobs, MiSssRes* res, uint32_t n, uint32_t N, uint32_t nof_prb,
                        uint32_t l5, uint32_t l6, hipStream_t st);
 void launch_cfo_correct(const float2* src, float2* dst, const MiCfoJob* jobs, uint32_t n, uint32_t len, uint32_t N,

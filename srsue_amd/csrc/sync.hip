@@ -4,10 +4,10 @@
 //
 // MI355X layout:
 //   * pss_search_kernel: one workgroup per search window; the three time-domain PSS templates of the
-//     bandwidth are staged in LDS (3 x N complex), each thread owns lags t = tid, tid + 256, ... and
-//     streams the window once for all candidates (coalesced: consecutive threads read consecutive
-//     samples), keeping the two half-window sums per candidate for the CFO estimate; the (rho, N_ID_2,
-//     lag) maximum is reduced in LDS with the oracle's tie order;
+//     bandwidth are staged in LDS (3 x N complex); 1, 2 or 4 threads share a lag (a tracking window of
+//     63 lags keeps 252 threads busy) and stream their segment once for all candidates in the job's
+//     mask, keeping the two half-window sums per candidate for the CFO estimate; partial sums combine
+//     by lane shuffles and the (rho, N_ID_2, lag) maximum is reduced in LDS with the oracle's tie order;
 //   * sss_detect_kernel: one workgroup per subframe: the SSS and PSS symbols are CFO-corrected into LDS
 //     with an N-entry twiddle table, 124 threads take their 62-bin DFTs, 168 x 2 hypotheses are scored
 //     coherently against the PSS-derived channel, argmax in LDS;
@@ -20,6 +20,9 @@ namespace mi {
 
 constexpr int PSS_T = 256;
 
+// TPL threads share a lag (consecutive lanes, each a contiguous N / TPL segment, combined by shuffles);
+// only the candidates in the job's mask are correlated
+template <int TPL>
 __global__ __launch_bounds__(PSS_T) void pss_search_kernel(const float2* __restrict__ iq, const float2* __restrict__ tmpl,
                                                           const MiPssJob* __restrict__ jobs, MiPssRes* __restrict__ res,
                                                           uint32_t N) {
@@ -28,36 +31,54 @@ __global__ __launch_bounds__(PSS_T) void pss_search_kernel(const float2* __restr
   __shared__ uint32_t s_key[PSS_T];
   __shared__ float s_cfo[PSS_T];
   const MiPssJob jb = jobs[blockIdx.x];
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, part = tid % TPL, slot = tid / TPL;
+  const bool on[3] = {(jb.mask & 1u) != 0, (jb.mask & 2u) != 0, (jb.mask & 4u) != 0};
   for (uint32_t i = tid; i < 3 * N; i += PSS_T) p[i] = tmpl[i];
   __syncthreads();
   float ep[3];
 #pragma unroll
   for (int u = 0; u < 3; u++) {
     float e = 0.f;
-    for (uint32_t n = 0; n < N; n++) e += p[u * N + n].x * p[u * N + n].x + p[u * N + n].y * p[u * N + n].y;
+    if (on[u])
+      for (uint32_t n = 0; n < N; n++) e += p[u * N + n].x * p[u * N + n].x + p[u * N + n].y * p[u * N + n].y;
     ep[u] = e;   // every thread computes the same sums in the same order
   }
   float best = -1.f, bcfo = 0.f;
   uint32_t bkey = 0xFFFFFFFFu;   // (u << 20) | lag of this thread's best
   const float2* x = iq + jb.off;
-  for (uint32_t t = tid; t < jb.nlag; t += PSS_T) {
+  const uint32_t seg = N / TPL, n0 = part * seg;
+  for (uint32_t t0 = 0; t0 < jb.nlag; t0 += PSS_T / TPL) {   // uniform trip count: shuffles stay convergent
+    const uint32_t t = t0 + slot;
+    const bool live = t < jb.nlag;
     float y1r[3] = {0.f, 0.f, 0.f}, y1i[3] = {0.f, 0.f, 0.f}, y2r[3] = {0.f, 0.f, 0.f}, y2i[3] = {0.f, 0.f, 0.f};
     float ex = 0.f;
-    for (uint32_t n = 0; n < N; n++) {
-      const float2 a = x[t + n];
-      ex += a.x * a.x + a.y * a.y;
-      const bool h2 = n >= N / 2;
+    if (live) {
+      for (uint32_t n = n0; n < n0 + seg; n++) {
+        const float2 a = x[t + n];
+        ex += a.x * a.x + a.y * a.y;
+        const bool h2 = n >= N / 2;
 #pragma unroll
-      for (int u = 0; u < 3; u++) {
-        const float2 b = p[u * N + n];
-        const float cr = a.x * b.x + a.y * b.y, ci = a.y * b.x - a.x * b.y;   // x conj(p)
-        if (h2) { y2r[u] += cr; y2i[u] += ci; } else { y1r[u] += cr; y1i[u] += ci; }
+        for (int u = 0; u < 3; u++) {
+          if (!on[u]) continue;
+          const float2 b = p[u * N + n];
+          const float cr = a.x * b.x + a.y * b.y, ci = a.y * b.x - a.x * b.y;   // x conj(p)
+          if (h2) { y2r[u] += cr; y2i[u] += ci; } else { y1r[u] += cr; y1i[u] += ci; }
+        }
       }
     }
 #pragma unroll
+    for (int o = 1; o < TPL; o <<= 1) {
+      ex += __shfl_xor(ex, o, 64);
+#pragma unroll
+      for (int u = 0; u < 3; u++) {
+        y1r[u] += __shfl_xor(y1r[u], o, 64); y1i[u] += __shfl_xor(y1i[u], o, 64);
+        y2r[u] += __shfl_xor(y2r[u], o, 64); y2i[u] += __shfl_xor(y2i[u], o, 64);
+      }
+    }
+    if (!live || part != 0) continue;
+#pragma unroll
     for (int u = 0; u < 3; u++) {
-      if (!((jb.mask >> u) & 1u)) continue;
+      if (!on[u]) continue;
       const float yr = y1r[u] + y2r[u], yi = y1i[u] + y2i[u];
       const float rho = ex > 0.f ? (yr * yr + yi * yi) / (ex * ep[u]) : 0.f;
       const uint32_t key = ((uint32_t)u << 20) | t;
@@ -188,9 +209,16 @@ __global__ __launch_bounds__(256) void cfo_correct_kernel(const float2* __restri
 }
 
 void launch_pss_search(const float2* iq, const float2* tmpl, const MiPssJob* jobs, MiPssRes* res, uint32_t n, uint32_t N,
-                       hipStream_t st) {
+                       uint32_t max_nlag, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(pss_search_kernel, dim3(n), dim3(PSS_T), 3 * N * sizeof(float2), st, iq, tmpl, jobs, res, N);
+  // threads per lag from the (host-known) largest window: 64 lags or fewer -> 4, 128 or fewer -> 2
+  const size_t lds = 3 * N * sizeof(float2);
+  if (max_nlag <= PSS_T / 4)
+    hipLaunchKernelGGL(pss_search_kernel<4>, dim3(n), dim3(PSS_T), lds, st, iq, tmpl, jobs, res, N);
+  else if (max_nlag <= PSS_T / 2)
+    hipLaunchKernelGGL(pss_search_kernel<2>, dim3(n), dim3(PSS_T), lds, st, iq, tmpl, jobs, res, N);
+  else
+    hipLaunchKernelGGL(pss_search_kernel<1>, dim3(n), dim3(PSS_T), lds, st, iq, tmpl, jobs, res, N);
 }
 void launch_sss_detect(const float2* iq, const MiSssJob* jobs, MiSssRes* res, uint32_t n, uint32_t N, uint32_t nof_prb,
                        uint32_t l5, uint32_t l6, hipStream_t st) {

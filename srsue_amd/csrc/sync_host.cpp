@@ -81,7 +81,10 @@ int SyncEngine::pss(const float2* iq, const std::vector<MiPssJob>& jobs, hipStre
   pres.resize(jobs.size());
   if (jobs.empty()) return 0;
   if (!up_sync(d_pjobs, jobs, st) || !d_pres.ensure(jobs.size() * sizeof(MiPssRes))) return -1;
-  launch_pss_search(iq, d_tmpl.as<float2>(), d_pjobs.as<MiPssJob>(), d_pres.as<MiPssRes>(), (uint32_t)jobs.size(), N, st);
+  uint32_t max_nlag = 0;
+  for (const MiPssJob& j : jobs) max_nlag = std::max(max_nlag, j.nlag);
+  launch_pss_search(iq, d_tmpl.as<float2>(), d_pjobs.as<MiPssJob>(), d_pres.as<MiPssRes>(), (uint32_t)jobs.size(), N,
+                    max_nlag, st);
   return (hip_ok(hipGetLastError(), "pss launch") &&
           hip_ok(hipMemcpyAsync(pres.data(), d_pres.p, pres.size() * sizeof(MiPssRes), hipMemcpyDeviceToHost, st), "D2H") &&
           hip_ok(hipStreamSynchronize(st), "sync"))

@@ -6,7 +6,7 @@
 //   FIND  : read one half frame + one symbol, search every lag for the cell's PSS (N_ID_2 = id % 3) in
 //           parallel chunks, check the SSS (N_ID_1, subframe 0 / 5) at the found boundary, initialise
 //           the CFO from the PSS, align to that subframe (returns 0);
-//   TRACK : per call one subframe (H2D); on subframes 0 / 5 the PSS is searched +-32 samples around
+//   TRACK : per call one subframe (H2D); on subframes 0 / 5 the PSS is searched +-31 samples around
 //           its expected position: the timing error re-times the NEXT subframe boundary and the CFO
 //           estimate enters an exponential average (em_alpha); the CFO is removed on the GPU into the
 //           caller's buffer (D2H), the subframe index advances (returns 1).
@@ -38,7 +38,7 @@ struct mi_ue_sync_ctx {
 
 namespace {
 
-constexpr uint32_t TRACK_M = 32;           // tracking window: +-32 samples around the expected PSS
+constexpr uint32_t TRACK_M = 31;           // tracking window: +-31 samples around the expected PSS (63 lags)
 constexpr float FIND_MIN_RHO = 0.01f;
 
 void ts_add(srslte_timestamp_t* t, double secs) {
