@@ -224,6 +224,24 @@ void     or_cfo_correct(const float *x, uint32_t n, float cfo, uint32_t N, float
 int      or_sss_detect(const float *sf_iq, uint32_t nof_prb, uint32_t nid2, uint32_t *nid1, uint32_t *sf5,
                        float *score);
 
+/* ---- UL PUSCH transmit chain (o_ul.c) ------------------------------------- */
+typedef struct {
+  uint32_t cell_id, nof_prb, sf_idx, rnti;
+  uint32_t n_prb, L_prb, tbs, Qm, rv;                 /* allocation (no hopping), TB, modulation, rv */
+  uint32_t group_hopping, sequence_hopping, delta_ss;  /* DMRS cell configuration */
+  uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI 0 cyclic-shift field (0..7) */
+} or_ul_cfg_t;
+double   or_pam_level(const uint8_t *b, uint32_t Qm);
+uint32_t or_pusch_G(const or_ul_cfg_t *c);
+int      or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *f);
+int      or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *f, float *x /* 12 M complex, symbol-major */);
+void     or_dft_m(const float *in, uint32_t M, float *out, int inverse);
+int      or_dmrs_params(const or_ul_cfg_t *c, uint32_t ns, uint32_t *u, uint32_t *v, uint32_t *ncs);
+int      or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r);
+int      or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid /* 14 x 12 N_RB complex */);
+int      or_scfdma_tx(uint32_t nof_prb, const float *grid, float *iq);
+int      or_pusch_encode(const or_ul_cfg_t *c, const uint8_t *tb, float *iq);
+
 #ifdef __cplusplus
 }
 #endif

@@ -141,6 +141,16 @@ def lib():
             "or_cfo_correct": (None, [f32, C.c_uint32, C.c_float, C.c_uint32, f32]),
             "or_sss_detect": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_float)]),
+            "or_pusch_G": (C.c_uint32, [C.POINTER(UlCfg)]),
+            "or_ulsch_encode": (C.c_int, [C.POINTER(UlCfg), u8, u8]),
+            "or_pusch_mod": (C.c_int, [C.POINTER(UlCfg), u8, f32]),
+            "or_dft_m": (None, [f32, C.c_uint32, f32, C.c_int]),
+            "or_dmrs_params": (C.c_int, [C.POINTER(UlCfg), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32)]),
+            "or_dmrs_pusch": (C.c_int, [C.POINTER(UlCfg), C.c_uint32, f32]),
+            "or_pusch_grid": (C.c_int, [C.POINTER(UlCfg), u8, f32]),
+            "or_scfdma_tx": (C.c_int, [C.c_uint32, f32, f32]),
+            "or_pusch_encode": (C.c_int, [C.POINTER(UlCfg), u8, f32]),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -196,6 +206,16 @@ class tdec_mode:
 
     def __exit__(self, *a):
         lib().or_set_tdec_mode(self.prev)
+
+
+class UlCfg(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "sf_idx", "rnti", "n_prb", "L_prb", "tbs", "Qm", "rv",
+                                          "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2")]
+
+
+def ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=0, Qm=4, rv=0, gh=0, sh=0, dss=0,
+           cs=0, n2=0):
+    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2)
 
 
 class PssRes(C.Structure):

@@ -1,0 +1,152 @@
+"""CPU: the UL PUSCH oracle (oracle/o_ul.c) against 36.211 / 36.212 properties and
+round trips: the UL-SCH coded bits decode back to the TB through the DL-SCH decoder (same channel
+coding, N_L = 1), an independent numpy restatement of the channel interleaver + scrambling +
+modulation, DMRS structure (constant amplitude, ZC periodic autocorrelation, cyclic shift), and the
+SC-FDMA signal demodulated by a plain FFT receiver back to the data symbols."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+
+def tb_of(seed, tbs):
+    return np.random.default_rng(seed).integers(0, 256, tbs // 8, dtype=np.uint8)
+
+
+def cfg(**kw):
+    c = O.ul_cfg(**kw)
+    if not c.tbs:
+        c.tbs = 8 * (O.lib().or_pusch_G(C.byref(c)) // 8 // 3)   # rate ~ 1/3
+    return c
+
+
+@pytest.mark.parametrize("L,Qm,tbs,rv", [(100, 4, 30576, 0), (3, 2, 256, 0), (25, 6, 14112, 0), (25, 6, 5736, 2),
+                                       (50, 4, 5000, 1)])  # rv 1 / 2 alone decode only at low code rates
+def test_ulsch_bits_decode_through_dlsch(L, Qm, tbs, rv):
+    c = cfg(L_prb=L, Qm=Qm, tbs=tbs, rv=rv)
+    G = O.lib().or_pusch_G(C.byref(c))
+    assert G == 12 * 12 * L * Qm
+    tb = tb_of(L, tbs)
+    f = np.zeros(G, np.uint8)
+    assert O.lib().or_ulsch_encode(C.byref(c), tb, f) == G
+    llr = (2.0 * f.astype(np.float32) - 1.0) * 8.0   # LLR > 0 => bit 1
+    s = O.cbsegm(tbs)
+    ncb = O.lib().or_ncb(s.Kp)
+    sb = np.zeros(s.C * ncb, np.float32)
+    pay = np.zeros(tbs // 8, np.uint8)
+    noi, cbok = C.c_uint32(), C.c_uint32()
+    rc = O.lib().or_dlsch_decode(llr, G, tbs, Qm, 1, rv, 1, sb, ncb, 4, pay, C.byref(noi), C.byref(cbok))
+    assert rc == 0 and np.array_equal(pay, tb)
+
+
+def gold(cinit, n):
+    x1 = np.zeros(n + 1600 + 31, np.uint8)
+    x2 = np.zeros(n + 1600 + 31, np.uint8)
+    x1[0] = 1
+    for i in range(31):
+        x2[i] = (cinit >> i) & 1
+    for i in range(n + 1600):
+        x1[i + 31] = x1[i + 3] ^ x1[i]
+        x2[i + 31] = x2[i + 3] ^ x2[i + 2] ^ x2[i + 1] ^ x2[i]
+    return (x1[1600:1600 + n] ^ x2[1600:1600 + n]).astype(np.uint8)
+
+
+def pam(b, Qm):
+    if Qm == 2:
+        return (1 - 2 * b[0]) / np.sqrt(2)
+    if Qm == 4:
+        return (1 - 2 * b[0]) * (1 + 2 * b[1]) / np.sqrt(10)
+    return (1 - 2 * b[0]) * (4 - (1 - 2 * b[1]) * (2 - (1 - 2 * b[2]))) / np.sqrt(42)
+
+
+@pytest.mark.parametrize("L,Qm", [(6, 2), (4, 4), (3, 6)])
+def test_interleave_scramble_modulate_independent(L, Qm):
+    """36.212 5.2.2.8 (no UCI) + 36.211 5.3.1 / 7.1 restated in numpy from the specification text."""
+    c = cfg(L_prb=L, Qm=Qm, cell_id=123, sf_idx=7, rnti=0x3A1)
+    G = O.lib().or_pusch_G(C.byref(c))
+    f = np.random.default_rng(3).integers(0, 2, G).astype(np.uint8)
+    x = np.zeros(2 * G // Qm, np.float32)
+    O.lib().or_pusch_mod(C.byref(c), f, x)
+    M = 12 * L
+    g = f.reshape(M * 12, Qm)                       # row-major: row m, column l -> g[m * 12 + l]
+    h = g.reshape(M, 12, Qm).transpose(1, 0, 2).reshape(-1)   # read column by column
+    h = (h ^ gold((0x3A1 << 14) | (7 << 9) | 123, G)).astype(np.int64)
+    want = np.array([pam(h[s * Qm:(s + 1) * Qm:2], Qm) + 1j * pam(h[s * Qm + 1:(s + 1) * Qm:2], Qm)
+                     for s in range(G // Qm)])
+    assert np.max(np.abs((x[0::2] + 1j * x[1::2]) - want)) < 1e-6
+
+
+@pytest.mark.parametrize("L,gh,sh,cs,n2", [(3, 0, 0, 0, 0), (6, 1, 0, 3, 5), (25, 0, 1, 7, 2), (100, 0, 0, 1, 1)])
+def test_dmrs_structure(L, gh, sh, cs, n2):
+    c = cfg(L_prb=L, cell_id=201, gh=gh, sh=sh, dss=3, cs=cs, n2=n2)
+    M = 12 * L
+    nzc = max(p for p in range(2, M) if all(p % d for d in range(2, int(p ** 0.5) + 1)))
+    us = set()
+    for ns in (2, 3, 14):
+        r = np.zeros(2 * M, np.float32)
+        assert O.lib().or_dmrs_pusch(C.byref(c), ns, r) == 0
+        z = r[0::2] + 1j * r[1::2]
+        assert np.allclose(np.abs(z), 1.0, atol=1e-6)
+        u, v, ncs = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        O.lib().or_dmrs_params(C.byref(c), ns, C.byref(u), C.byref(v), C.byref(ncs))
+        assert u.value < 30 and v.value in (0, 1) and ncs.value < 12
+        assert v.value == 0 or (sh and not gh and M >= 72)
+        us.add(u.value)
+        base = z * np.exp(-2j * np.pi * ncs.value * np.arange(M) / 12)   # undo the cyclic shift
+        assert np.allclose(base[nzc:], base[:M - nzc], atol=1e-5)         # cyclic extension of x_q
+        x = base[:nzc]
+        for tau in (1, 5, nzc // 2):
+            assert abs(np.vdot(x, np.roll(x, tau))) / nzc < 1e-4        # ZC: ideal periodic autocorrelation
+    if not gh:
+        assert len(us) == 1
+    r = np.zeros(24 * 2, np.float32)
+    assert O.lib().or_dmrs_pusch(C.byref(cfg(L_prb=2)), 2, r) == -1           # 1-2 PRB tables: not carried
+
+
+def scfdma_rx(iq, nprb):
+    N = O.lib().or_symbol_sz(nprb)
+    W = 12 * nprb
+    grid, pos = np.zeros((14, W), np.complex128), 0
+    z = iq[0::2].astype(np.float64) + 1j * iq[1::2]
+    for l in range(14):
+        cp = O.lib().or_cp_len(N, l % 7)
+        u = z[pos + cp:pos + cp + N] * np.exp(-1j * np.pi * np.arange(N) / N)
+        Y = np.fft.fft(u) / np.sqrt(N)
+        grid[l] = Y[(np.arange(W) - W // 2) % N]
+        pos += N + cp
+    return grid
+
+
+@pytest.mark.parametrize("nprb,n_prb,L,Qm", [(100, 0, 100, 4), (25, 5, 15, 2), (50, 40, 10, 6), (6, 1, 3, 4)])
+def test_pusch_end_to_end_symbols(nprb, n_prb, L, Qm):
+    """or_pusch_encode -> FFT receiver (CP removal, half-subcarrier shift) -> the grid's allocated REs:
+    DMRS in symbols 3 / 10, IDFT of the data symbols == the modulated, interleaved, scrambled bits;
+    nothing outside the allocation; the CP equals the spec's continuation of the shifted symbol."""
+    c = cfg(nof_prb=nprb, n_prb=n_prb, L_prb=L, Qm=Qm, cell_id=17, sf_idx=4)
+    tb = tb_of(nprb, c.tbs)
+    N = O.lib().or_symbol_sz(nprb)
+    iq = np.zeros(2 * 15 * N, np.float32)
+    assert O.lib().or_pusch_encode(C.byref(c), tb, iq) == 0
+    grid = scfdma_rx(iq, nprb)
+    M = 12 * L
+    G = O.lib().or_pusch_G(C.byref(c))
+    f = np.zeros(G, np.uint8)
+    O.lib().or_ulsch_encode(C.byref(c), tb, f)
+    x = np.zeros(2 * G // Qm, np.float32)
+    O.lib().or_pusch_mod(C.byref(c), f, x)
+    x = (x[0::2] + 1j * x[1::2]).reshape(12, M)
+    ds = 0
+    for l in range(14):
+        row = grid[l, 12 * n_prb:12 * n_prb + M]
+        outside = np.delete(grid[l], np.arange(12 * n_prb, 12 * n_prb + M))
+        assert outside.size == 0 or np.max(np.abs(outside)) < 1e-5
+        if l % 7 == 3:
+            r = np.zeros(2 * M, np.float32)
+            O.lib().or_dmrs_pusch(C.byref(c), 2 * 4 + l // 7, r)
+            assert np.max(np.abs(row - (r[0::2] + 1j * r[1::2]))) < 1e-5
+        else:
+            d = np.fft.ifft(row) * np.sqrt(M)
+            assert np.max(np.abs(d - x[ds])) < 1e-4
+            ds += 1
