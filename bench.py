@@ -216,6 +216,11 @@ def config_cfgs(config, B, first):
     return cfgs
 
 
+def tdec_kernel_name(win):
+    return ("tdec_win_kernel (max-log-MAP turbo, one workgroup per code block)" if win
+            else "tdec_kernel (max-log-MAP turbo, one code block per lane)")
+
+
 def dtype_of(args):
     """f32 everywhere (front end, softbuffer); in i16 mode the turbo metrics are int16-exact integers."""
     return "f32+i16" if args.tdec == "i16" else "f32"
@@ -230,7 +235,7 @@ def bench_codeblocks(args, world, rank, dev):
     sigma2 = 1.0 / (2 * (K / (3.0 * K + 12)) * 10 ** (args.ebno / 10))
     llr = np.stack([(-2.0 * ((1.0 - 2.0 * abi.turbo_encode(b, K)) + rng.normal(0, np.sqrt(sigma2), 3 * K + 12))
                      / sigma2).astype(np.float32) for b in bits])
-    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True, tdec_i16=args.tdec == "i16")
+    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
     d = torch.from_numpy(llr).to(dev)[torch.arange(n, device=dev) % pool].contiguous()
     sptr = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(args.warmup):
@@ -260,9 +265,10 @@ def bench_codeblocks(args, world, rank, dev):
            "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
            "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
                                   f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
-                      "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec},
+                      "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec,
+                      "turbo_schedule": "latency form" if tb.turbo_win else "lane per code block"},
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
-           "roofline": {"kernel": "tdec_kernel (max-log-MAP turbo)", "bound": "hbm", "achieved": round(ach, 2),
+           "roofline": {"kernel": tdec_kernel_name(tb.turbo_win), "bound": "hbm", "achieved": round(ach, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                         "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(stage["tdec"], 4),
                         "launches_averaged": nprof}}
@@ -456,6 +462,9 @@ def main():
                          "for each subframe's RNTI) on the batch's grid; reported beside value")
     ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
                     help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
+    ap.add_argument("--sched", choices=("auto", "win", "lane"), default="auto",
+                    help="int16 turbo schedule: latency form (one workgroup per code block, exact trellis segments), "
+                         "one code block per lane, or auto (latency form up to 1024 code blocks)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
     args = ap.parse_args()
@@ -492,7 +501,7 @@ def main():
         P = B                                               # every mixed subframe is distinct
     h = [0.8 + 0.3j, -0.4 + 0.5j] if args.config == 3 else None
     pool_iq, pool_tb = make_pool(cfgs[:P], args.snr, threads, first, h)
-    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16")
+    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
     # stage the pool in HBM once, replicate on device into the batch IQ layout
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
     if args.config == 5:
@@ -554,12 +563,13 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
-                       "max_its": args.max_its, "parallelism": f"replicas x{world} (no collective on the data path)"},
+                       "max_its": args.max_its, "turbo_schedule": "latency form" if batch.turbo_win else "lane per code block",
+                       "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
             "payload_spot_mismatches": bad,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
-            "roofline": {"kernel": "tdec_kernel (max-log-MAP turbo)", "bound": "hbm", "achieved": round(achieved, 2),
+            "roofline": {"kernel": tdec_kernel_name(batch.turbo_win), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": tdec_bytes,

@@ -58,6 +58,13 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
 /* IQ input in UHD's sc16 wire format (int16 I/Q, fc32 = sc16 / 32768) instead of fc32: half the
  * bytes over PCIe for host-resident IQ; the OFDM stage converts on load (exact). */
 #define MI_DL_FLAG_IQ_SC16 8u
+/* turbo decoder schedule (int16 arithmetic only; results are identical either way).  Default: the
+ * latency form (one workgroup per code block, exact trellis segments) when the batch
+ * holds at most MI_TDEC_WIN_AUTO_CBS code blocks, else one code block per lane of 64-lane wavefronts.
+ * MI_DL_FLAG_TDEC_WIN / MI_DL_FLAG_TDEC_LANE force one of them. */
+#define MI_DL_FLAG_TDEC_WIN  16u
+#define MI_DL_FLAG_TDEC_LANE 32u
+#define MI_TDEC_WIN_AUTO_CBS 1024u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 
@@ -90,6 +97,8 @@ void   mi_dl_batch_profile_reset(mi_dl_batch_t *b);
 /* Algorithmic HBM bytes of one run (SURVEY.md 8d definitions) */
 double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = compulsory total */);
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
+/* 1 when the batch's turbo stage runs the latency form (MI_DL_FLAG_TDEC_WIN rules), else 0 */
+int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 
 /* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =
@@ -106,6 +115,7 @@ int    mi_tdec_download(mi_tdec_batch_t *b, uint8_t *bits /* n_cb*K/8 */, uint32
 int    mi_tdec_stage_ms(mi_tdec_batch_t *b, float *ms /* MI_DL_NSTAGES */, uint32_t *nruns);
 void   mi_tdec_profile_reset(mi_tdec_batch_t *b);
 double mi_tdec_algo_bytes(const mi_tdec_batch_t *b);
+int    mi_tdec_turbo_win(const mi_tdec_batch_t *b);
 /* 36.212 5.1.3 turbo encoder (host): bits[K] -> d[3(K+4)] triplet order, 2 = <NULL> filler */
 int    mi_turbo_encode(const uint8_t *bits, uint32_t K, uint32_t F, uint8_t *d);
 

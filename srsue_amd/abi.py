@@ -20,6 +20,9 @@ FLAG_PROFILE = 1
 FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic (the default), see include/mi_dl.h
 FLAG_TDEC_GEN = 4   # float srsLTE-gen turbo arithmetic
 FLAG_IQ_SC16 = 8    # IQ input as UHD sc16 (int16 I/Q, fc32 = sc16 / 32768)
+FLAG_TDEC_WIN = 16  # int16 turbo: force the latency form (one workgroup per code block)
+FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wavefronts
+SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE}
 
 
 class SfCfg(C.Structure):
@@ -76,6 +79,8 @@ def lib():
             "mi_dl_batch_profile_reset": (None, [vp]),
             "mi_dl_batch_algo_bytes": (C.c_double, [vp, C.c_int]),
             "mi_dl_batch_n_codeblocks": (u32, [vp]),
+            "mi_dl_batch_turbo_win": (C.c_int, [vp]),
+            "mi_tdec_turbo_win": (C.c_int, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
             "mi_turbo_encode": (C.c_int, [vp, u32, u32, vp]),
@@ -164,11 +169,11 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
         flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
-            (FLAG_IQ_SC16 if iq_sc16 else 0)
+            (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched]
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())
@@ -240,6 +245,11 @@ class Batch:
     @property
     def n_codeblocks(self):
         return lib().mi_dl_batch_n_codeblocks(self.h)
+
+    @property
+    def turbo_win(self):
+        """True when the turbo stage runs the latency form (one workgroup per code block)."""
+        return bool(lib().mi_dl_batch_turbo_win(self.h))
 
     @property
     def n_groups(self):
@@ -464,9 +474,9 @@ def turbo_encode(bits, K, F=0):
 class TdecBatch:
     """Raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* / turbodecoder_test contract)."""
 
-    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False, tdec_i16=True):
+    def __init__(self, K, n_cb, max_its=8, early_stop=False, crc24a=False, profile=False, tdec_i16=True, sched=None):
         self.K, self.n_cb = K, n_cb
-        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN)
+        flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | SCHED_FLAGS[sched]
         self.h = lib().mi_tdec_create(K, n_cb, max_its, int(early_stop), int(crc24a), flags)
         if not self.h:
             raise RuntimeError("mi_tdec_create: " + last_error())
@@ -495,6 +505,10 @@ class TdecBatch:
 
     def algo_bytes(self):
         return lib().mi_tdec_algo_bytes(self.h)
+
+    @property
+    def turbo_win(self):
+        return bool(lib().mi_tdec_turbo_win(self.h))
 
     def close(self):
         if self.h:

@@ -13,11 +13,74 @@
 #include "rm_body.h"
 #include "tb_body.h"
 #include "tdec_body.h"
+#include "tdec_win_body.h"
 
 static int g_q16 = 0;   // turbo arithmetic of the emulated decoder (MI_DL_FLAG_TDEC_I16)
 extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 
 static uint32_t crc8[256];
+
+// latency-form (segment-parallel) int16 decoder: threads per code block, 0 = off (tdec_win_body.h).
+// Each phase of the GPU kernel (between two barriers) runs every segment in turn: within a phase a
+// segment only reads what earlier phases wrote, so this reproduces the kernel exactly.
+static uint32_t g_win = 0;
+static uint64_t g_win_rounds = 0, g_win_halves = 0;
+extern "C" void emu_set_tdec_win(uint32_t threads) { g_win = threads; g_win_rounds = g_win_halves = 0; }
+extern "C" void emu_win_stats(uint64_t* rounds, uint64_t* halves) { *rounds = g_win_rounds; *halves = g_win_halves; }
+
+template <bool DEC2>
+static void emu_win_half(const mi::WinCb& c) {
+  g_win_halves++;
+  for (uint32_t j = 0; j < c.nseg; j++) mi::win_bwd_first<DEC2>(c, j);
+  std::vector<float> v(8 * c.nseg);
+  for (;;) {
+    for (uint32_t j = 0; j + 1 < c.nseg; j++) mi::ck_get(c.bend + (j + 1) * 8, *reinterpret_cast<float(*)[8]>(&v[8 * j]));
+    bool any = false;
+    for (uint32_t j = 0; j + 1 < c.nseg; j++) any |= mi::win_bwd_fix<DEC2>(c, j, *reinterpret_cast<float(*)[8]>(&v[8 * j]));
+    g_win_rounds++;
+    if (!any) break;
+  }
+  for (uint32_t j = 0; j < c.nseg; j++) mi::win_fwd_first<DEC2>(c, j);
+  for (;;) {
+    for (uint32_t j = 1; j < c.nseg; j++) mi::ck_get(c.aend + (j - 1) * 8, *reinterpret_cast<float(*)[8]>(&v[8 * j]));
+    bool any = false;
+    for (uint32_t j = 1; j < c.nseg; j++) any |= mi::win_fwd_fix<DEC2>(c, j, *reinterpret_cast<float(*)[8]>(&v[8 * j]));
+    g_win_rounds++;
+    if (!any) break;
+  }
+}
+
+// one code block (lane `lane` of group g) through the latency-form decoder, as tdec_win_kernel does
+static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, const MiLaneDesc& ld, const float* sbg,
+                                     const uint32_t* kdata, uint32_t lane, uint32_t max_its, uint8_t* row) {
+  const uint32_t K = g.K, P = g_win;
+  mi::WinCb c;
+  c.K = K;
+  mi::win_geometry(K, P, c.S, c.nseg);
+  std::vector<int16_t> q(3 * K + 12), d(K), w(K), bck((K / 4 + 1) * 8), ack((K / 4 + 1) * 8), bend(P * 8), aend(P * 8);
+  std::vector<uint16_t> pi(K);
+  std::vector<uint8_t> dec(K), pk(K / 8);
+  c.q = q.data(); c.pi = pi.data(); c.d = d.data(); c.w = w.data(); c.dec = dec.data();
+  c.bck = bck.data(); c.ack = ack.data(); c.bend = bend.data(); c.aend = aend.data();
+  for (uint32_t t = 0; t < P; t++)
+    mi::win_load(c, t, P, sbg, g.Ncb, kdata + kt.pos_off, kdata + kt.pi_off, lane, ld.F);
+  const uint32_t* tab = kdata + (ld.crc24a ? kt.crca_off : kt.crcb_off);
+  mi::TdecLaneResult r{0, 0, 0};
+  for (uint32_t it = 0; it < max_its; it++) {
+    emu_win_half<false>(c);
+    emu_win_half<true>(c);
+    uint32_t x = 0;
+    for (uint32_t t = 0; t < P; t++) x ^= mi::win_crc_part(c, t, P, tab);
+    r.its = it + 1;
+    r.crc_ok = x == 0;
+    if (r.crc_ok) break;
+  }
+  for (uint32_t t = 0; t < P; t++) mi::win_pack(c, t, P, pk.data());
+  memcpy(row, pk.data(), K / 8);
+  const uint32_t b0 = ld.F / 8, b1 = K / 8 - (ld.crc24a ? 0 : 3);
+  for (uint32_t t = 0; t < P; t++) r.tb_part ^= mi::win_tb_term(c, t, P, pk.data(), b0, b1, crc8);
+  return r;
+}
 
 extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
                               uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
@@ -59,7 +122,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.dec = &dec[g.dec_off];
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
       a.K = g.K; a.F = ld.F; a.max_its = max_its; a.early_stop = 1; a.crc24a = ld.crc24a;
-      mi::TdecLaneResult r = g_q16 ? mi::tdec_lane<true>(a, lane) : mi::tdec_lane<false>(a, lane);
+      mi::TdecLaneResult r = g_win && g_q16 ? emu_win_cb(g, kt, ld, sbg, P.kdata.data(), lane, max_its, a.cb_bytes)
+                           : g_q16 ? mi::tdec_lane<true>(a, lane) : mi::tdec_lane<false>(a, lane);
       cits[li] = r.its;
       ccrc[li] = r.crc_ok;
       ctbp[li] = r.tb_part;

@@ -8,6 +8,7 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -133,13 +134,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC)) {
-      launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
-                     (uint32_t)P.groups.size(), st);
-      launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
-                  d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
-                  d_ktabs.as<MiKTab>(),
-                  d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
-                  q16(), st);
+      launch_turbo(sb, st);
     }
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
@@ -174,16 +169,40 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
   launch_cb_scatter(d_in, d_sb.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                     (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
   mark(MI_DL_STAGE_TDEC);
-  launch_rowmask(d_sb.as<float>(), d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(),
-                 d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), st);
-  launch_tdec(d_sb.as<float>(), d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
-              d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
-              d_lanes.as<MiLaneDesc>(),
-              d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), max_its, early_stop,
-              q16(), st);
+  launch_turbo(d_sb.as<float>(), st);
   mark(MI_DL_STAGE_TB);
   mark(MI_DL_NSTAGES);
   return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
+}
+
+bool Engine::use_win() const {
+  if (!q16()) return false;   // the float decoder is not shift-invariant: lane-per-code-block only
+  if (flags & MI_DL_FLAG_TDEC_WIN) return true;
+  if (flags & MI_DL_FLAG_TDEC_LANE) return false;
+  return plan.n_cb <= MI_TDEC_WIN_AUTO_CBS;
+}
+
+// turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts
+void Engine::launch_turbo(float* sb, hipStream_t st) {
+  const Plan& P = plan;
+  if (use_win()) {
+    uint32_t kmax = 0;
+    for (const MiGroupDesc& g : P.groups) kmax = std::max(kmax, g.K);
+    // threads per code block: segments of >= ~16 trellis steps (fewer fix-up rounds), at most 256
+    uint32_t th = win_threads;
+    if (!th && getenv("MI_TDEC_WIN_THREADS")) th = (uint32_t)atoi(getenv("MI_TDEC_WIN_THREADS"));   // A/B tuning
+    if (!th) th = kmax >= 4096 ? 256 : kmax >= 1024 ? 128 : 64;
+    launch_tdec_win(sb, d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(),
+                    d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
+                    (uint32_t)P.lanes.size(), kmax, max_its, early_stop, th, st);
+    return;
+  }
+  launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
+                 (uint32_t)P.groups.size(), st);
+  launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
+              d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
+              d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(),
+              max_its, early_stop, q16(), st);
 }
 
 int Engine::stage_ms(float* ms, uint32_t* nruns) {

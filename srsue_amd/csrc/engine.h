@@ -27,6 +27,9 @@ struct Engine {
   Plan plan;
   uint32_t max_its = 4, early_stop = 1, flags = 0;
   bool q16() const { return (flags & MI_DL_FLAG_TDEC_GEN) == 0; }   // int16 turbo arithmetic (default)
+  uint32_t win_threads = 0;   // latency-form turbo: threads per code block (0 = by K)
+  bool use_win() const;       // latency-form (segment-parallel) turbo decoder for this plan
+  void launch_turbo(float* sb, hipStream_t st);
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,

@@ -28,6 +28,12 @@ void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* d
                  uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                  const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
                  uint32_t early_stop, bool q16, hipStream_t st);
+// latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
+// (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
+void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,
+                     const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* kdata,
+                     uint32_t n_lanes, uint32_t max_k, uint32_t max_its, uint32_t early_stop, uint32_t threads,
+                     hipStream_t st);
 // raw code-block decoder input [cb][3(K+4)] -> group-interleaved softbuffer layout
 void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, const MiKTab* ktabs,
                        const uint32_t* kdata, uint32_t n_groups, uint32_t K, uint32_t n_cb, hipStream_t st);

@@ -78,3 +78,35 @@ def test_emulated_batch_of_mixed_subframes(built):
         off = abi.emu().emu_payload_offset(C.cast(arr, C.c_void_p), len(cfgs), i)
         assert ok[i] == 1
         assert np.array_equal(pe[off:off + c.tbs // 8], truth[i])
+
+
+@pytest.mark.parametrize("threads", [64, 256])
+@pytest.mark.parametrize("nprb,ports,tbs,qm,snr,sf,rv,cid", CASES)
+def test_emulated_segment_parallel_turbo_bit_exact(built, nprb, ports, tbs, qm, snr, sf, rv, cid, threads):
+    """The latency-form int16 decoder (one workgroup per code block, trellis segments with exact
+    boundary fix-up, tdec_win_body.h), emulated phase by phase, against the oracle's int16 decoder:
+    payload, TB CRC and iteration counts identical -- incl. CRC-failing waterfall decodes, where
+    paths merge late and fix-up rounds cascade over several segments."""
+    cfg = abi.sf_cfg(cell_id=cid, nof_prb=nprb, nof_ports=ports, sf_idx=sf, tbs=tbs, Qm=qm, rv=rv)
+    tb = tb_bytes(sf, tbs)
+    iq = abi.tx_subframe(cfg, tb, snr_db=snr, seed=sf + 7)
+    llr = oracle_front(cfg, iq)[3]
+    with O.tdec_mode(O.TDEC_I16):
+        ok, opay, onoi, _ = oracle_dlsch(cfg, llr)
+    arr = abi.cfg_array([cfg])
+    pe = np.zeros(tbs // 8, np.uint8)
+    eok = np.zeros(1, np.uint32)
+    eits = np.zeros(1, np.uint32)
+    E = abi.emu()
+    E.emu_set_tdec_i16(1)
+    E.emu_set_tdec_win(threads)
+    try:
+        rc = E.emu_decode_llr(C.cast(arr, C.c_void_p), 1, np.ascontiguousarray(llr).ctypes.data, 4,
+                              pe.ctypes.data, eok.ctypes.data, eits.ctypes.data, None)
+    finally:
+        E.emu_set_tdec_i16(0)
+        E.emu_set_tdec_win(0)
+    assert rc == 0
+    assert bool(eok[0]) == ok
+    assert eits[0] == onoi
+    assert np.array_equal(pe, opay)

@@ -19,8 +19,12 @@ TOL = 1e-4
 S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
 
 
-def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False):
-    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16)
+# turbo decoders: float (lane per code block), int16 lane per code block, int16 latency form
+DECODERS = [(False, "lane"), (True, "lane"), (True, "win")]
+
+
+def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None):
+    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16, sched=sched)
     flat = np.zeros(2 * b.iq_samples, np.float32)
     for i, iq in enumerate(iqs):
         o = 2 * b.iq_offset(i)
@@ -49,11 +53,11 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("i16", [False, True])
-def test_mixed_batch_front_end_and_decode(i16):
+@pytest.mark.parametrize("i16,sched", DECODERS)
+def test_mixed_batch_front_end_and_decode(i16, sched):
     cfgs = [abi.sf_cfg(**c) for c in CASES]
     iqs, tbs = make_subframes(cfgs, snr_db=30.0)
-    b = run_batch(cfgs, iqs, tdec_i16=i16)
+    b = run_batch(cfgs, iqs, tdec_i16=i16, sched=sched)
     grid = b.download(abi.BUF_GRID, np.float32)
     ce = b.download(abi.BUF_CE, np.float32)
     llr = b.download(abi.BUF_LLR, np.float32)
@@ -77,13 +81,13 @@ def test_mixed_batch_front_end_and_decode(i16):
         assert its[i] == onoi
 
 
-@pytest.mark.parametrize("i16", [False, True])
+@pytest.mark.parametrize("i16,sched", DECODERS)
 @pytest.mark.parametrize("snr", [15.0, 17.5, 18.5, 19.5, 21.0])
-def test_turbo_bit_exact_on_identical_llrs(snr, i16):
+def test_turbo_bit_exact_on_identical_llrs(snr, i16, sched):
     """Waterfall region: CRC passes and fails; GPU == oracle bit for bit either way."""
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + (i % 4), tbs=75376, Qm=6) for i in range(4)]
     iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=int(snr * 10))
-    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16)
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16, sched=sched)
     llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
     flat = np.zeros(b.download(abi.BUF_LLR, np.float32).shape, np.float32)
     for i, l in enumerate(llrs):
@@ -149,8 +153,8 @@ def test_sc16_wire_format_is_exact():
         assert np.array_equal(b.payload(i, pay), tbs[i])
 
 
-@pytest.mark.parametrize("i16", [False, True])
-def test_batch_harq_combining_sparse_rows(i16):
+@pytest.mark.parametrize("i16,sched", DECODERS)
+def test_batch_harq_combining_sparse_rows(i16, sched):
     """HARQ in the batch path with the sparse softbuffer rows (dl_common.h sb_group_floats): one
     64-lane group mixes first transmissions (rv 0, overwrite) and retransmissions (rv 2 / rv 3,
     combine).  Two launches with different LLRs: combining lanes must equal the oracle's dense float
@@ -158,7 +162,7 @@ def test_batch_harq_combining_sparse_rows(i16):
     materialises, rows dropped by a fresh lane and the zero row all take part."""
     spec = [(0, 1), (2, 0), (0, 1), (3, 0)]
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i, tbs=75376, Qm=6, rv=rv, new_tb=nt) for i, (rv, nt) in enumerate(spec)]
-    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16)
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=i16, sched=sched)
     flat_len = b.download(abi.BUF_LLR, np.float32).shape
     osb = [None] * len(cfgs)
     for run, snr in enumerate((14.0, 16.0)):

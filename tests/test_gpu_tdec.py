@@ -1,7 +1,9 @@
 """GPU: raw code-block turbo decoding (mi_tdec_*, the srslte_tdec_* contract of BASELINE configs[0],
 srsLTE's turbodecoder_test): K = 6144, 8 fixed iterations, no early stop, BPSK/AWGN LLRs across the
 waterfall -- decisions bit-identical to the oracle and to the committed golden fixture, for both the
-float (srsLTE-gen) and the int16 (srsLTE SSE design) arithmetic."""
+float (srsLTE-gen) and the int16 (srsLTE SSE design) arithmetic, and for the int16 decoder in both
+schedules: one code block per lane, and the latency form (one workgroup per code block, exact
+trellis segments; at 0.6-0.8 dB paths merge late, so fix-up rounds cascade)."""
 import os
 
 import numpy as np
@@ -22,12 +24,16 @@ def llr_bpsk(d, K, ebno_db, rng):
     return (-2.0 * y / sigma2).astype(np.float32)
 
 
-@pytest.mark.parametrize("i16", [False, True])
-def test_golden_config1_on_gpu(built, i16):
+# turbo schedules: float decoder (lane per code block), int16 lane per code block, int16 latency form
+MODES = [(False, "lane"), (True, "lane"), (True, "win")]
+
+
+@pytest.mark.parametrize("i16,sched", MODES)
+def test_golden_config1_on_gpu(built, i16, sched):
     g = np.load(os.path.join(GOLDEN, "tdec_K6144_ebno.npz"))
     ref = np.load(os.path.join(GOLDEN, "tdec16_K6144.npz"))["dec"] if i16 else g["dec"]
     n = len(g["ebno"])
-    tb = abi.TdecBatch(6144, n, max_its=8, early_stop=False, tdec_i16=i16)
+    tb = abi.TdecBatch(6144, n, max_its=8, early_stop=False, tdec_i16=i16, sched=sched)
     d = torch.from_numpy(np.ascontiguousarray(g["llr"])).cuda()
     tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
     bits, its, _ = tb.results()
@@ -35,16 +41,16 @@ def test_golden_config1_on_gpu(built, i16):
     assert np.array_equal(bits, ref)
 
 
-@pytest.mark.parametrize("i16", [False, True])
-@pytest.mark.parametrize("K,ebno", [(6144, 0.6), (6144, 0.8), (5824, 1.0), (40, 2.0), (512, 1.5)])
-def test_codeblocks_bit_exact_vs_oracle(built, K, ebno, i16):
+@pytest.mark.parametrize("i16,sched", MODES)
+@pytest.mark.parametrize("K,ebno", [(6144, 0.6), (6144, 0.8), (5824, 1.0), (40, 2.0), (512, 1.5), (1024, 1.0)])
+def test_codeblocks_bit_exact_vs_oracle(built, K, ebno, i16, sched):
     rng = np.random.default_rng(K + int(ebno * 10))
     n = 70                                      # two 64-lane groups, the second partial
     bits = rng.integers(0, 2, (n, K)).astype(np.uint8)
     llr = np.stack([llr_bpsk(abi.turbo_encode(b, K), K, ebno, rng) for b in bits])
     if i16:
         llr *= np.float32(rng.uniform(0.5, 8.0))   # exercise the quantiser range too
-    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, tdec_i16=i16)
+    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, tdec_i16=i16, sched=sched)
     d = torch.from_numpy(llr).cuda()
     tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
     got, its, _ = tb.results()
@@ -53,3 +59,23 @@ def test_codeblocks_bit_exact_vs_oracle(built, K, ebno, i16):
         dec, oits, _ = td.decode_cb(llr[i], K, max_its=8, early_stop=False)
         assert np.array_equal(got[i], dec), f"cb {i}"
     assert np.all(its == 8)
+
+
+@pytest.mark.parametrize("threads", ["64", "128", "256"])
+def test_latency_form_thread_counts(built, threads, monkeypatch):
+    """Segment count does not change results: 64/128/256 segments per code block (MI_TDEC_WIN_THREADS)
+    with CRC early stop, against the oracle's int16 decoder."""
+    monkeypatch.setenv("MI_TDEC_WIN_THREADS", threads)
+    rng = np.random.default_rng(int(threads))
+    K, n = 6144, 24
+    bits = rng.integers(0, 2, (n, K)).astype(np.uint8)
+    llr = np.stack([llr_bpsk(abi.turbo_encode(b, K), K, e, rng) for b, e in zip(bits, np.linspace(0.4, 1.6, n))])
+    tb = abi.TdecBatch(K, n, max_its=6, early_stop=True, tdec_i16=True, sched="win")
+    d = torch.from_numpy(llr).cuda()
+    tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got, its, ok = tb.results()
+    td = O.Tdec(O.TDEC_I16)
+    for i in range(n):
+        dec, oits, ook = td.decode_cb(llr[i], K, max_its=6, early_stop=True)
+        assert its[i] == oits and bool(ok[i]) == bool(ook), f"cb {i}"
+        assert np.array_equal(got[i], dec), f"cb {i}"
