@@ -1,0 +1,59 @@
+/*
+ * mi_ul.h -- batched C ABI of the MI355X UL PUSCH transmit path.
+ *
+ * The per-TTI srsLTE entry points srsUE calls (srslte_ue_ul_cfg_grant + srslte_ue_ul_pusch_encode_
+ * rnti_softbuffer, /root/reference/ue/src/phy/phch_worker.cc:551-560) are in srslte/srslte.h; this is
+ * the throughput form: N PUSCH transmissions planned once, encoded per call on the caller's stream
+ * from device-resident TB payloads into device-resident SC-FDMA IQ.
+ *
+ * Chain (gfx950 kernels, srsue_amd/csrc/ul.hip): TB CRC24A -> segmentation + CRC24B -> turbo encoder
+ * (36.212 5.1.3.2, chunk-parallel recursive encoders) -> rate matching (5.1.4.1, full circular buffer)
+ * -> channel interleaver (5.2.2.8, no UCI) -> scrambling (36.211 5.3.1) -> modulation (7.1) ->
+ * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, no hopping) +
+ * DMRS (5.5.2.1, L_prb >= 3) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
+ * Normalisation: unit average power per used subcarrier (1/sqrt(M) DFT, 1/sqrt(N) IDFT).
+ */
+#ifndef MI_UL_H
+#define MI_UL_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  uint32_t cell_id, nof_prb, sf_idx, rnti;
+  uint32_t n_prb, L_prb, tbs, Qm, rv;                 /* allocation (no hopping), TB bits, 2/4/6, rv 0..3 */
+  uint32_t group_hopping, sequence_hopping, delta_ss;  /* DMRS cell configuration (srslte_refsignal_dmrs_pusch_cfg_t) */
+  uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI format 0 cyclic-shift field (0..7) */
+} mi_ul_cfg_t;
+
+enum { MI_UL_STAGE_CRC = 0, MI_UL_STAGE_ENCODE, MI_UL_STAGE_MOD, MI_UL_NSTAGES };
+#define MI_UL_FLAG_PROFILE 1u
+
+typedef struct mi_ul_batch mi_ul_batch_t;
+
+mi_ul_batch_t *mi_ul_batch_create(const mi_ul_cfg_t *cfgs, uint32_t n, uint32_t flags);
+void   mi_ul_batch_destroy(mi_ul_batch_t *b);
+/* payload layout: TB i (tbs/8 bytes, MSB first) at byte offset mi_ul_batch_payload_offset(b, i) */
+size_t mi_ul_batch_payload_offset(const mi_ul_batch_t *b, uint32_t i);
+size_t mi_ul_batch_payload_bytes(const mi_ul_batch_t *b);
+/* output layout: subframe i (15 N cf32 samples) at cf32 offset mi_ul_batch_iq_offset(b, i) */
+size_t mi_ul_batch_iq_offset(const mi_ul_batch_t *b, uint32_t i);
+size_t mi_ul_batch_iq_samples(const mi_ul_batch_t *b);
+uint32_t mi_ul_batch_n_codeblocks(const mi_ul_batch_t *b);
+/* enqueue the chain on `stream` (hipStream_t, NULL = default): d_payload -> d_iq (both device) */
+int    mi_ul_batch_run(mi_ul_batch_t *b, const void *d_payload, void *d_iq, void *stream);
+/* parity hooks: the 12 M coded symbols of transmission i after the last run (rate-matching output
+ * in channel-interleaver input order, Qm bits per byte, first bit = MSB) */
+int    mi_ul_batch_symbols(mi_ul_batch_t *b, uint32_t i, uint8_t *host);
+int    mi_ul_batch_stage_ms(mi_ul_batch_t *b, float *ms /* MI_UL_NSTAGES */, uint32_t *nruns);
+void   mi_ul_batch_profile_reset(mi_ul_batch_t *b);
+/* algorithmic HBM bytes per run: payload read + IQ write (SURVEY.md 8d convention) */
+double mi_ul_batch_algo_bytes(const mi_ul_batch_t *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

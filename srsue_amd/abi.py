@@ -121,6 +121,18 @@ def lib():
             "mi_device_count": (C.c_int, []),
             "mi_set_device": (C.c_int, [C.c_int]),
             "mi_last_error": (C.c_char_p, []),
+            "mi_ul_batch_create": (vp, [vp, u32, u32]),
+            "mi_ul_batch_destroy": (None, [vp]),
+            "mi_ul_batch_payload_offset": (sz, [vp, u32]),
+            "mi_ul_batch_payload_bytes": (sz, [vp]),
+            "mi_ul_batch_iq_offset": (sz, [vp, u32]),
+            "mi_ul_batch_iq_samples": (sz, [vp]),
+            "mi_ul_batch_n_codeblocks": (u32, [vp]),
+            "mi_ul_batch_run": (C.c_int, [vp, vp, vp, vp]),
+            "mi_ul_batch_symbols": (C.c_int, [vp, u32, vp]),
+            "mi_ul_batch_stage_ms": (C.c_int, [vp, vp, vp]),
+            "mi_ul_batch_profile_reset": (None, [vp]),
+            "mi_ul_batch_algo_bytes": (C.c_double, [vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -524,3 +536,81 @@ class TdecBatch:
 
 def pdsch_G(cfg):
     return lib().mi_pdsch_G(C.byref(cfg))
+
+
+# ---- UL PUSCH transmitter (include/mi_ul.h) ---------------------------------------
+UL_STAGES = ("crc", "encode", "mod")
+
+
+class UlCfg(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "sf_idx", "rnti", "n_prb", "L_prb", "tbs", "Qm", "rv",
+                                          "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2")]
+
+
+def ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=0, Qm=4, rv=0, gh=0, sh=0, dss=0,
+           cs=0, n2=0):
+    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2)
+
+
+class UlBatch:
+    """Owns one mi_ul_batch_t: N PUSCH transmissions planned once; run() enqueues the chain."""
+
+    def __init__(self, cfgs, profile=False):
+        self.cfgs = list(cfgs)
+        self._arr = (UlCfg * len(self.cfgs))(*self.cfgs)
+        self.h = lib().mi_ul_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), 1 if profile else 0)
+        if not self.h:
+            raise RuntimeError("mi_ul_batch_create: " + last_error())
+
+    def close(self):
+        if self.h:
+            lib().mi_ul_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def payload_bytes(self):
+        return lib().mi_ul_batch_payload_bytes(self.h)
+
+    @property
+    def iq_samples(self):
+        return lib().mi_ul_batch_iq_samples(self.h)
+
+    @property
+    def n_codeblocks(self):
+        return lib().mi_ul_batch_n_codeblocks(self.h)
+
+    def payload_offset(self, i):
+        return lib().mi_ul_batch_payload_offset(self.h, i)
+
+    def iq_offset(self, i):
+        return lib().mi_ul_batch_iq_offset(self.h, i)
+
+    def run(self, d_payload_ptr, d_iq_ptr, stream_ptr=None):
+        if lib().mi_ul_batch_run(self.h, C.c_void_p(d_payload_ptr), C.c_void_p(d_iq_ptr), C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_ul_batch_run: " + last_error())
+
+    def symbols(self, i):
+        M = 12 * self.cfgs[i].L_prb
+        out = np.zeros(12 * M, np.uint8)
+        if lib().mi_ul_batch_symbols(self.h, i, out.ctypes.data):
+            raise RuntimeError("mi_ul_batch_symbols: " + last_error())
+        return out
+
+    def stage_ms(self):
+        ms = np.zeros(len(UL_STAGES), np.float32)
+        n = C.c_uint32(0)
+        if lib().mi_ul_batch_stage_ms(self.h, ms.ctypes.data, C.byref(n)):
+            raise RuntimeError("mi_ul_batch_stage_ms: " + last_error())
+        return dict(zip(UL_STAGES, ms.tolist())), n.value
+
+    def profile_reset(self):
+        lib().mi_ul_batch_profile_reset(self.h)
+
+    def algo_bytes(self):
+        return lib().mi_ul_batch_algo_bytes(self.h)

@@ -1,0 +1,177 @@
+// ul_plan.cpp -- UL PUSCH planner (see ul_plan.h).  Spec arithmetic: 36.212 5.2.2 / 5.1.2-5.1.4,
+// 36.211 5.3 / 5.5.1 / 5.5.2.1 / 5.6; the oracle (oracle/o_ul.c) restates the same clauses for the tests.
+#include "ul_plan.h"
+
+#include <math.h>
+
+#include "plan.h"   // set_error
+
+namespace mi {
+
+static const uint32_t N1_DMRS[8] = {0, 2, 3, 4, 6, 8, 9, 10};   // 36.211 Table 5.5.2.1.1-2 (cyclicShift)
+static const uint32_t N2_DMRS[8] = {0, 6, 3, 4, 2, 8, 10, 9};   // 36.211 Table 5.5.2.1.1-1 (DCI format 0)
+
+static bool prime(uint32_t n) {
+  if (n < 2) return false;
+  for (uint32_t d = 2; d * d <= n; d++)
+    if (n % d == 0) return false;
+  return true;
+}
+
+int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc, uint32_t* ncs) {
+  const uint32_t M = 12 * c.L_prb, fss = (c.cell_id + c.delta_ss) % 30;
+  if (M < 36 || ns >= 20) return -1;   // L_prb = 1, 2 use the tabulated base sequences (5.5.1.2)
+  uint32_t fgh = 0;
+  if (c.group_hopping) {               // 5.5.1.3: c_init = floor(N_ID / 30)
+    std::vector<uint8_t> g(160);
+    gold_bits(c.cell_id / 30, 160, g.data());
+    for (int i = 0; i < 8; i++) fgh += (uint32_t)g[8 * ns + i] << i;
+    fgh %= 30;
+  }
+  const uint32_t u = (fgh + fss) % 30;
+  // sequence hopping (5.5.1.4) and n_PRS (5.5.2.1.1) share c_init = floor(N_ID / 30) 2^5 + f_ss
+  std::vector<uint8_t> s(8 * 7 * 20);
+  gold_bits((c.cell_id / 30) * 32 + fss, 8 * 7 * 20, s.data());
+  const uint32_t v = (M >= 72 && !c.group_hopping && c.sequence_hopping) ? s[ns] : 0;
+  uint32_t prs = 0;
+  for (int i = 0; i < 8; i++) prs += (uint32_t)s[8 * 7 * ns + i] << i;
+  *ncs = (N1_DMRS[c.cyclic_shift & 7] + N2_DMRS[c.n_dmrs2 & 7] + prs) % 12;
+  uint32_t N = M - 1;
+  while (!prime(N)) N--;
+  *nzc = N;
+  const double qb = (double)N * (u + 1) / 31.0;
+  const uint32_t odd = (uint32_t)floor(2.0 * qb) & 1u;
+  *q = (uint32_t)floor(qb + 0.5) + (odd ? (uint32_t)-(int32_t)v : v);
+  return 0;
+}
+
+uint32_t ul_radix_plan(uint32_t n) {
+  uint32_t plan = 0, st = 0;
+  auto push = [&](uint32_t r) { plan |= r << (4 * st++); };
+  while (n % 4 == 0 && st < 8) { push(4); n /= 4; }
+  while (n % 2 == 0 && st < 8) { push(2); n /= 2; }
+  while (n % 3 == 0 && st < 8) { push(3); n /= 3; }
+  while (n % 5 == 0 && st < 8) { push(5); n /= 5; }
+  return n == 1 ? plan : 0;
+}
+
+int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
+  txs.clear(); cbs.clear(); kdata.clear(); scr.clear(); tw.clear(); tb_cb0.clear();
+  pi_off.clear(); tw_off.clear(); sel_off.clear(); r0_cache.clear();
+  payload_bytes = sym_bytes = iq_samples = 0;
+  algo_bytes = 0;
+  auto twiddles = [&](uint32_t len) {
+    auto it = tw_off.find(len);
+    if (it != tw_off.end()) return it->second;
+    const uint32_t off = (uint32_t)(tw.size() / 2);
+    for (uint32_t t = 0; t < len; t++) {
+      tw.push_back((float)cos(-2.0 * M_PI * t / len));
+      tw.push_back((float)sin(-2.0 * M_PI * t / len));
+    }
+    tw_off[len] = off;
+    return off;
+  };
+  for (uint32_t i = 0; i < n; i++) {
+    const mi_ul_cfg_t& c = cfgs[i];
+    const int N = symbol_sz(c.nof_prb);
+    if (N < 0 || c.nof_prb == 0 || c.sf_idx > 9 || c.L_prb < 3 || c.n_prb + c.L_prb > c.nof_prb ||
+        (c.Qm != 2 && c.Qm != 4 && c.Qm != 6) || c.tbs == 0 || c.tbs % 8 || c.rv > 3) {
+      set_error("invalid UL configuration (L_prb >= 3, allocation inside the cell, Qm 2/4/6, byte-aligned TBS)");
+      return -1;
+    }
+    MiUlTx t{};
+    t.N = (uint32_t)N;
+    t.W = 12 * c.nof_prb;
+    t.n_prb = c.n_prb;
+    t.M = 12 * c.L_prb;
+    t.Qm = c.Qm;
+    t.fact = ul_radix_plan(t.M);
+    t.fact_n = ul_radix_plan(t.N);
+    if (!t.fact || !t.fact_n) {
+      set_error("L_prb must be 2^a 3^b 5^c (36.211 5.3.3)");
+      return -1;
+    }
+    for (uint32_t s = 0; s < 2; s++)
+      if (ul_dmrs_params(c, 2 * c.sf_idx + s, &t.q[s], &t.nzc, &t.ncs[s])) {
+        set_error("DMRS parameters");
+        return -1;
+      }
+    t.twm_off = twiddles(t.M);
+    t.twn_off = twiddles(t.N);
+    const uint32_t G = 12 * t.M * c.Qm;   // normal CP, no SRS, no UCI: 12 data symbols
+    t.iq_off = iq_samples;
+    iq_samples += 15 * (size_t)N;
+    t.pay_off = (uint32_t)payload_bytes;
+    payload_bytes += c.tbs / 8;
+    t.sym_off = (uint32_t)sym_bytes;
+    sym_bytes += 12 * (size_t)t.M;
+    t.tbs = c.tbs;
+    t.scr_off = (uint32_t)scr.size();
+    scr.resize(scr.size() + (G + 31) / 32 + 1);
+    gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, G, &scr[t.scr_off]);
+    // segmentation of (TB || CRC24A), 36.212 5.1.2
+    CbSegm sg;
+    if (cbsegm(c.tbs, &sg)) {
+      set_error("segmentation");
+      return -1;
+    }
+    tb_cb0.push_back((uint32_t)cbs.size());
+    uint32_t byte0 = 0, sym = 0;
+    for (uint32_t r = 0; r < sg.C; r++) {
+      MiUlCb b{};
+      b.tx = i;
+      b.K = r < sg.Cm ? sg.Km : sg.Kp;
+      b.F = r == 0 ? sg.F : 0;
+      b.C = sg.C;
+      b.r = r;
+      b.E = rm_E(G, sg.C, c.Qm, 1, r);
+      b.byte0 = byte0;
+      b.nbytes = (b.K - b.F - (sg.C > 1 ? 24 : 0)) / 8;
+      byte0 += b.nbytes;
+      b.sym0 = sym;
+      sym += b.E / c.Qm;
+      if (!pi_off.count(b.K)) {
+        std::vector<uint32_t> pi;
+        qpp_table(b.K, pi);
+        pi_off[b.K] = (uint32_t)kdata.size();
+        kdata.insert(kdata.end(), pi.begin(), pi.end());
+      }
+      b.pi_off = pi_off[b.K];
+      const auto key = std::make_pair(b.K, b.F);
+      if (!sel_off.count(key)) {
+        std::vector<uint32_t> pos;
+        std::vector<int32_t> rank;
+        uint32_t Nv = 0;
+        cb_pos_table(b.K, pos);
+        cb_rank_table(b.K, b.F, rank, &Nv);
+        std::vector<uint32_t> sel(Nv, 0);
+        for (uint32_t tt = 0; tt < pos.size(); tt++)
+          if (rank[pos[tt]] >= 0) sel[(uint32_t)rank[pos[tt]]] = tt;
+        sel_off[key] = {(uint32_t)kdata.size(), Nv};
+        kdata.insert(kdata.end(), sel.begin(), sel.end());
+        // rank of the first non-null position at or after k0(rv), per rv
+        auto& r0 = r0_cache[key];
+        for (uint32_t rv = 0; rv < 4; rv++) {
+          const uint32_t k0 = k0_of(b.K, rv);
+          uint32_t cnt = 0;
+          for (uint32_t p = 0; p < k0 && p < rank.size(); p++) cnt += rank[p] >= 0 ? 1 : 0;
+          r0[rv] = cnt % Nv;
+        }
+      }
+      b.sel_off = sel_off[key].first;
+      b.Nv = sel_off[key].second;
+      b.r0 = r0_cache[key][c.rv];
+      cbs.push_back(b);
+    }
+    if (byte0 != c.tbs / 8 + 3 || sym != 12 * t.M) {
+      set_error("UL planner: segmentation / rate-matching bookkeeping");
+      return -1;
+    }
+    txs.push_back(t);
+    algo_bytes += (double)c.tbs / 8 + 15.0 * N * 8;
+  }
+  tb_cb0.push_back((uint32_t)cbs.size());
+  return 0;
+}
+
+}  // namespace mi

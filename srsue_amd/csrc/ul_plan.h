@@ -1,0 +1,36 @@
+// ul_plan.h -- host planner of the UL PUSCH transmit path (no HIP dependency): segmentation, rate
+// matching splits and selection tables, scrambling words, DMRS parameters, DFT radix plans and
+// twiddle tables for a batch of transmissions.
+#pragma once
+#include <array>
+#include <map>
+#include <vector>
+
+#include "mi_ul.h"
+#include "tables.h"
+#include "ul_common.h"
+
+namespace mi {
+
+// 36.211 5.5.2.1 / 5.5.1: DMRS root q, Zadoff-Chu length and cyclic shift of slot ns (0..19)
+int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc, uint32_t* ncs);
+// radix list (4, 2, 3, 5; 4 bits per stage) of an n-point transform, 0 if n has another factor
+uint32_t ul_radix_plan(uint32_t n);
+
+struct UlPlan {
+  std::vector<MiUlTx> txs;
+  std::vector<MiUlCb> cbs;
+  std::vector<uint32_t> kdata;      // QPP and selection tables
+  std::vector<uint32_t> scr;        // scrambling words
+  std::vector<float> tw;            // float2 twiddle tables
+  std::vector<uint32_t> tb_cb0;     // first code block of each transmission (n + 1 entries)
+  size_t payload_bytes = 0, sym_bytes = 0, iq_samples = 0;
+  double algo_bytes = 0;
+
+  std::map<uint32_t, uint32_t> pi_off, tw_off;
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> sel_off;   // (K, F) -> (offset, Nv)
+  std::map<std::pair<uint32_t, uint32_t>, std::array<uint32_t, 4>> r0_cache;        // (K, F) -> r0 per rv
+  int build(const mi_ul_cfg_t* cfgs, uint32_t n);
+};
+
+}  // namespace mi

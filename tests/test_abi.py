@@ -13,7 +13,8 @@ import oracle_lib as O
 from srsue_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "srslte", "srslte.h"), os.path.join(ROOT, "include", "mi_dl.h")]
+HEADERS = [os.path.join(ROOT, "include", "srslte", "srslte.h"), os.path.join(ROOT, "include", "mi_dl.h"),
+           os.path.join(ROOT, "include", "mi_ul.h")]
 
 
 def declared_functions(path):
@@ -40,7 +41,7 @@ def test_library_exports_every_declared_symbol(built):
 
 def test_headers_compile_as_c(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "srslte/srslte.h"\n#include "mi_dl.h"\n'
+    src.write_text('#include "srslte/srslte.h"\n#include "mi_dl.h"\n#include "mi_ul.h"\n'
                    "int main(void){srslte_ue_dl_t q; srslte_softbuffer_rx_t s; (void)q; (void)s;"
                    " return SRSLTE_VERSION_CHECK(1,0,0) ? 0 : 1;}\n")
     subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),

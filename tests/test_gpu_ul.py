@@ -1,0 +1,116 @@
+"""GPU: the UL PUSCH transmitter (include/mi_ul.h, srsue_amd/csrc/ul.hip) against the
+oracle's UL chain (oracle/o_ul.c): the rate-matched coded symbols bit-exact with or_ulsch_encode, and the
+SC-FDMA IQ within 1e-4 (RMS-relative) of or_pusch_encode (double precision) -- over QPSK/16QAM/64QAM,
+every redundancy version, K-/K+ segmentation with filler bits, single code blocks (CRC24A only), partial
+allocations, group / sequence hopping, cyclic shifts, and 1.4-20 MHz cells in one batch."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+from srsue_amd import abi
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2
+    (100, 0, 100, 39232, 4, 0, 1, 1, 0, 0, 0, 0, 0),     # 20 MHz full band, 16QAM (MCS 20)
+    (100, 10, 75, 25456, 6, 2, 4, 7, 0, 1, 3, 2, 5),     # 64QAM, rv 2, sequence hopping
+    (50, 5, 24, 5736, 2, 1, 7, 33, 1, 0, 0, 7, 3),       # group hopping, rv 1
+    (25, 0, 3, 512, 2, 0, 0, 301, 0, 0, 0, 1, 1),        # L = 3 (smallest ZC DMRS), C = 1, 8 filler bits
+    (6, 1, 5, 600, 4, 3, 9, 2, 1, 0, 29, 4, 6),          # 1.4 MHz, rv 3
+    (75, 30, 45, 12216, 4, 0, 5, 11, 0, 1, 0, 3, 0),     # N = 1536
+    (15, 0, 15, 4008, 6, 0, 2, 12, 0, 0, 0, 0, 2),       # 3 MHz, N = 256
+]
+
+
+def mk(c):
+    nof_prb, n_prb, L, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 = c
+    return dict(cell_id=cell, nof_prb=nof_prb, sf_idx=sf, rnti=0x46 + sf, n_prb=n_prb, L_prb=L, tbs=tbs, Qm=Qm, rv=rv,
+                gh=gh, sh=sh, dss=dss, cs=cs, n2=n2)
+
+
+def tb_of(i, tbs):
+    return np.random.default_rng(1000 + i).integers(0, 256, tbs // 8, dtype=np.uint8)
+
+
+def oracle_symbols(oc, tb):
+    G = O.lib().or_pusch_G(C.byref(oc))
+    f = np.zeros(G, np.uint8)
+    assert O.lib().or_ulsch_encode(C.byref(oc), tb, f) == G
+    Qm = oc.Qm
+    w = (1 << np.arange(Qm - 1, -1, -1)).astype(np.uint32)
+    return (f.reshape(-1, Qm).astype(np.uint32) @ w).astype(np.uint8)
+
+
+def oracle_iq(oc, tb):
+    N = {6: 128, 15: 256, 25: 512, 50: 1024, 75: 1536, 100: 2048}[oc.nof_prb]
+    iq = np.zeros(2 * 15 * N, np.float32)
+    assert O.lib().or_pusch_encode(C.byref(oc), tb, iq) == 0
+    return iq
+
+
+def rel_err(a, b):
+    return float(np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(b ** 2)))
+
+
+@pytest.fixture(scope="module")
+def encoded(built):
+    cfgs = [abi.ul_cfg(**mk(c)) for c in CASES]
+    b = abi.UlBatch(cfgs)
+    pay = np.zeros(b.payload_bytes, np.uint8)
+    tbs = []
+    for i, c in enumerate(cfgs):
+        tb = tb_of(i, c.tbs)
+        o = b.payload_offset(i)
+        pay[o:o + len(tb)] = tb
+        tbs.append(tb)
+    d_pay = torch.from_numpy(pay).cuda()
+    d_iq = torch.zeros(2 * b.iq_samples, dtype=torch.float32, device="cuda")
+    b.run(d_pay.data_ptr(), d_iq.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return b, cfgs, tbs, d_iq.cpu().numpy()
+
+
+@pytest.mark.parametrize("i", range(len(CASES)))
+def test_coded_symbols_bit_exact(encoded, i):
+    b, cfgs, tbs, _ = encoded
+    oc = O.ul_cfg(**mk(CASES[i]))
+    assert np.array_equal(b.symbols(i), oracle_symbols(oc, tbs[i]))
+
+
+@pytest.mark.parametrize("i", range(len(CASES)))
+def test_scfdma_iq_matches_oracle(encoded, i):
+    b, cfgs, tbs, iq = encoded
+    oc = O.ul_cfg(**mk(CASES[i]))
+    ref = oracle_iq(oc, tbs[i])
+    o = 2 * b.iq_offset(i)
+    got = iq[o:o + len(ref)]
+    assert rel_err(got, ref) < TOL
+
+
+def test_ul_batch_reuse_and_streams(built):
+    """A second run with other payloads on a side stream overwrites every output sample."""
+    cfgs = [abi.ul_cfg(**mk(CASES[0])), abi.ul_cfg(**mk(CASES[3]))]
+    b = abi.UlBatch(cfgs)
+    s = torch.cuda.Stream()
+    d_iq = torch.full((2 * b.iq_samples,), 7.0, dtype=torch.float32, device="cuda")
+    for seed in (5, 6):
+        pay = np.zeros(b.payload_bytes, np.uint8)
+        tbs = []
+        for i, c in enumerate(cfgs):
+            tb = tb_of(seed * 10 + i, c.tbs)
+            pay[b.payload_offset(i):b.payload_offset(i) + len(tb)] = tb
+            tbs.append(tb)
+        d_pay = torch.from_numpy(pay).cuda()
+        torch.cuda.synchronize()
+        b.run(d_pay.data_ptr(), d_iq.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        iq = d_iq.cpu().numpy()
+        for i, c in enumerate(cfgs):
+            oc = O.ul_cfg(**mk(CASES[[0, 3][i]]))
+            ref = oracle_iq(oc, tbs[i])
+            o = 2 * b.iq_offset(i)
+            assert rel_err(iq[o:o + len(ref)], ref) < TOL
