@@ -8,8 +8,9 @@
  * reads directly (ue_dl.sf_symbols, ue_dl.ce, ue_dl.pdsch, ue_dl.pdsch.dl_sch, ue_dl.pdsch_cfg.grant,
  * ue_dl.chest, ue_dl.pdcch, ue_dl.last_n_cce, ue_dl.last_location) are kept.
  *
- * Out of scope here: PDCCH/DCI, PHICH, sync/cell search, uplink,
- * PRACH, radio -- those still come from srsLTE itself.
+ * Beyond the DL data path the header also carries the SURVEY.md 8f rows built on the GPU: DL control
+ * (PDCCH/DCI, PHICH), the sync tracking subset and the UL PUSCH encoder.  Cell search / MIB, PUCCH,
+ * SRS, PRACH, power control and the radio still come from srsLTE itself.
  *
  * Conventions: 0 = SRSLTE_SUCCESS, -1 = SRSLTE_ERROR; srslte_pdsch_decode_rnti returns 0 iff
  * the TB CRC passes; payload bits are packed MSB first.
@@ -257,6 +258,137 @@ SRSLTE_API int srslte_cbsegm(srslte_cbsegm_t *s, uint32_t tbs);
 SRSLTE_API int srslte_symbol_sz(uint32_t nof_prb);
 SRSLTE_API void *srslte_vec_malloc(uint32_t size);   /* 256-B aligned, free()-compatible (phch_worker.cc:102) */
 SRSLTE_API void srslte_vec_free(void *ptr);
+
+/* ---- UL PUSCH (phch_worker.cc:79-84, 105, 128, 213, 545-590, 748) -------------
+ * srslte_ue_ul on the GPU (srsue_amd/csrc/ul.hip, ue_ul.cpp): cfg_grant plans the transmission,
+ * pusch_encode_rnti_softbuffer copies the payload to HBM, runs TB CRC -> turbo encoder -> rate matching
+ * -> channel interleaver -> scrambling -> modulation -> transform precoding + DMRS -> SC-FDMA and copies
+ * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  Limits: no UCI on PUSCH (uci_data must
+ * carry no ACK / CQI / RI: returns SRSLTE_ERROR), no frequency hopping, L_prb >= 3; PUCCH, SRS and UL
+ * power control stay in srsLTE.  set_cfg uses the DMRS and hopping configurations, the others are
+ * accepted.  set_normalization(true) scales by nof_prb / (15 sqrt(L_prb)) (srsLTE's factor as recorded
+ * in DESIGN.md, unverified: srsLTE is not in the container); set_cfo(cfo) shifts the output by cfo
+ * subcarrier spacings when set_cfo_enable(true). */
+#define SRSLTE_CQI_MAX_BITS 64
+typedef struct SRSLTE_API {
+  uint32_t n_prb[2];                /* first PRB of slots 0 / 1 (read at phch_worker.cc:580) */
+  uint32_t n_prb_tilde[2];          /* (read at :223) */
+  uint32_t L_prb;
+  uint32_t freq_hopping;
+  uint32_t nof_re, nof_symb;
+  srslte_ra_mcs_t mcs;
+  uint32_t Qm;
+  uint32_t ncs_dmrs;                /* DCI format 0 cyclic-shift field (read at :223) */
+} srslte_ra_ul_grant_t;
+typedef struct SRSLTE_API {
+  srslte_ra_type_t alloc_type;
+  uint32_t type2_start, type2_len;  /* RIV-decoded allocation */
+  uint32_t mcs_idx, rv_idx, n_dmrs, freq_hop_fl, tpc_pusch;
+  bool ndi, cqi_request;
+} srslte_ra_ul_dci_t;
+typedef struct SRSLTE_API {           /* random-access response grant, 36.213 6.2 (phch_worker.cc:412) */
+  bool hopping_flag;
+  uint32_t rba;
+  uint32_t trunc_mcs;
+  uint32_t tpc_pusch;
+  bool ul_delay;
+  bool cqi_request;
+} srslte_dci_rar_grant_t;
+typedef struct SRSLTE_API {           /* phch_worker.cc:681-685 */
+  bool group_hopping_en;
+  bool sequence_hopping_en;
+  uint32_t cyclic_shift;
+  uint32_t delta_ss;
+} srslte_refsignal_dmrs_pusch_cfg_t;
+typedef struct SRSLTE_API {           /* phch_worker.cc:688-693 */
+  enum { SRSLTE_PUSCH_HOP_MODE_INTER_SF = 1, SRSLTE_PUSCH_HOP_MODE_INTRA_SF = 0 } hop_mode;
+  uint32_t hopping_offset;
+  uint32_t n_sb;
+} srslte_pusch_hopping_cfg_t;
+typedef struct SRSLTE_API {           /* accepted by set_cfg, used by srsLTE's SRS (out of scope) */
+  bool configured;
+  uint32_t subframe_config, bw_cfg, I_srs, B, b_hop, n_rrc, k_tc, n_srs;
+} srslte_refsignal_srs_cfg_t;
+typedef struct SRSLTE_API {           /* accepted by set_cfg (PUCCH: out of scope) */
+  uint32_t delta_pucch_shift, N_cs, n_rb_2;
+  bool srs_configured;
+  uint32_t srs_cs_subf_cfg;
+  bool srs_simul_ack;
+} srslte_pucch_cfg_t;
+typedef struct SRSLTE_API {
+  uint32_t n_pucch_1[4];
+  uint32_t N_pucch_1, n_pucch_2, n_pucch_sr;
+} srslte_pucch_sched_t;
+typedef struct SRSLTE_API { uint32_t I_offset_cqi, I_offset_ri, I_offset_ack; } srslte_uci_cfg_t;
+typedef struct SRSLTE_API {           /* accepted by set_cfg (UL power control: out of scope) */
+  float p0_nominal_pusch, alpha, p0_nominal_pucch, delta_f_pucch[5], delta_preamble_msg3, p0_ue_pusch;
+  bool delta_mcs_based, acc_enabled;
+  float p0_ue_pucch, p_srs_offset;
+} srslte_ue_ul_powerctrl_t;
+typedef struct SRSLTE_API {           /* phch_worker.h:118, filled at :481-523 */
+  uint8_t uci_cqi[SRSLTE_CQI_MAX_BITS];
+  uint32_t uci_cqi_len;
+  uint8_t uci_ri;
+  uint32_t uci_ri_len;
+  uint8_t uci_ack;
+  uint32_t uci_ack_len;
+  bool ri_periodic_report;
+  bool scheduling_request;
+} srslte_uci_data_t;
+/* HARQ tx softbuffer: embedded by value in srsUE's ul_harq_process (ul_harq.h:97) */
+typedef struct SRSLTE_API {
+  uint32_t max_cb;
+  uint8_t **buffer_b;     /* kept for layout compatibility; NULL */
+  void *dev;              /* device copy of the last new-data TB (a retransmission re-encodes it) */
+  uint32_t tbs;           /* bits of that TB, 0 = none */
+} srslte_softbuffer_tx_t;
+typedef struct SRSLTE_API {
+  srslte_cbsegm_t cb_segm;
+  srslte_ra_ul_grant_t grant;
+  uint32_t rv;
+  uint32_t sf_idx;
+  uint32_t tti;
+  uint32_t current_tx_nb;
+} srslte_pusch_cfg_t;
+struct mi_ue_ul_ctx;
+typedef struct SRSLTE_API {         /* owned by value per phch_worker (phch_worker.h:116) */
+  srslte_cell_t cell;
+  srslte_pusch_cfg_t pusch_cfg;     /* ue_ul.pusch_cfg.grant.n_prb_tilde (phch_worker.cc:223) */
+  srslte_refsignal_dmrs_pusch_cfg_t dmrs_cfg;
+  srslte_pusch_hopping_cfg_t hopping_cfg;
+  uint16_t current_rnti;
+  bool normalize_en;
+  bool cfo_en;
+  float current_cfo;
+  uint32_t last_pucch_format;
+  struct mi_ue_ul_ctx *ctx;         /* MI355X device context: HIP stream + HBM workspace */
+} srslte_ue_ul_t;
+
+SRSLTE_API int srslte_ue_ul_init(srslte_ue_ul_t *q, srslte_cell_t cell);
+SRSLTE_API void srslte_ue_ul_free(srslte_ue_ul_t *q);
+SRSLTE_API void srslte_ue_ul_set_rnti(srslte_ue_ul_t *q, uint16_t rnti);
+SRSLTE_API void srslte_ue_ul_set_normalization(srslte_ue_ul_t *q, bool enabled);
+SRSLTE_API void srslte_ue_ul_set_cfo_enable(srslte_ue_ul_t *q, bool enabled);
+SRSLTE_API void srslte_ue_ul_set_cfo(srslte_ue_ul_t *q, float cur_cfo);
+SRSLTE_API void srslte_ue_ul_set_cfg(srslte_ue_ul_t *q, srslte_refsignal_dmrs_pusch_cfg_t *dmrs_cfg,
+                                     srslte_refsignal_srs_cfg_t *srs_cfg, srslte_pucch_cfg_t *pucch_cfg,
+                                     srslte_pucch_sched_t *pucch_sched, srslte_uci_cfg_t *uci_cfg,
+                                     srslte_pusch_hopping_cfg_t *hopping_cfg, srslte_ue_ul_powerctrl_t *power_ctrl);
+SRSLTE_API int srslte_ue_ul_cfg_grant(srslte_ue_ul_t *q, srslte_ra_ul_grant_t *grant, uint32_t tti, uint32_t rvidx,
+                                      uint32_t current_tx_nb);
+SRSLTE_API int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t *q, uint8_t *data, srslte_uci_data_t uci_data,
+                                                         srslte_softbuffer_tx_t *softbuffer, uint16_t rnti,
+                                                         cf_t *output_signal);
+SRSLTE_API int srslte_softbuffer_tx_init(srslte_softbuffer_tx_t *q, uint32_t nof_prb);
+SRSLTE_API void srslte_softbuffer_tx_reset(srslte_softbuffer_tx_t *q);
+SRSLTE_API void srslte_softbuffer_tx_free(srslte_softbuffer_tx_t *q);
+/* DCI format 0 (36.212 5.3.3.1.1, no hopping) / RAR grant (36.213 6.2) -> UL grant: MCS per 36.213
+ * Table 8.6.1-1 (29-31: retransmission, rv 1-3, TBS of the last grant not known here: error); TBS from
+ * the spot columns this library carries (N_PRB = 6, 25, 50, 100). */
+SRSLTE_API int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t *msg, uint32_t nof_prb, uint32_t n_rb_ho,
+                                          srslte_ra_ul_dci_t *ul_dci, srslte_ra_ul_grant_t *grant, uint32_t harq_pid);
+SRSLTE_API int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t *rar, uint32_t nof_prb, uint32_t n_rb_ho,
+                                          srslte_ra_ul_dci_t *ul_dci, srslte_ra_ul_grant_t *grant);
 
 /* ---- sync front end (phch_recv.cc:108-120, 231-240, 321-335) ----------------
  * srslte_ue_sync in tracking mode on the GPU (srsue_amd/csrc/sync.hip, ue_sync.cpp): the first

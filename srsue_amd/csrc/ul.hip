@@ -248,7 +248,7 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
   const uint32_t slot = blockIdx.y, t = threadIdx.x, N = x.N, M = x.M, Qm = x.Qm;
   for (uint32_t i = t; i < N; i += UL_THREADS) twn[i] = twg[x.twn_off + i];
   for (uint32_t i = t; i < M; i += UL_THREADS) twm[i] = twg[x.twm_off + i];
-  const float sM = rsqrtf((float)M), sN = rsqrtf((float)N);
+  const float sM = rsqrtf((float)M), gN = rsqrtf((float)N) * x.scale;
   constexpr int PM = (UL_MMAX + UL_THREADS - 1) / UL_THREADS;
   const int off = (int)(12 * x.n_prb) - (int)(x.W / 2);   // allocation's first subcarrier relative to W/2
   uint32_t pos = slot * (15 * N / 2);                        // first sample of the slot
@@ -320,9 +320,12 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
     for (uint32_t i = t; i < N + cp; i += UL_THREADS) {
       const int n = (int)i - (int)cp;
       const float2 y = buf[(uint32_t)(n + (int)N) % N];
+      // half-subcarrier shift, plus the frequency offset srslte_ue_ul_set_cfo asks for (cfo subcarriers
+      // over the subframe's sample index), in units of pi
+      const float ph = ((float)n + 2.0f * x.cfo * (float)(pos + i)) / (float)N;
       float sv, cv;
-      sincospif((float)n / (float)N, &sv, &cv);
-      dst[i] = make_float2((y.x * cv + y.y * sv) * sN, (y.x * sv - y.y * cv) * sN);
+      sincospif(ph, &sv, &cv);
+      dst[i] = make_float2((y.x * cv + y.y * sv) * gN, (y.x * sv - y.y * cv) * gN);
     }
     __syncthreads();
     pos += N + cp;

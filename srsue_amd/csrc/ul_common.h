@@ -20,6 +20,8 @@ struct MiUlTx {
   uint32_t fact;         // radix list of the M-point DFT, 4 bits per stage (first stage lowest)
   uint32_t fact_n;       // same for the N-point SC-FDMA transform
   uint32_t twm_off, twn_off;   // float2 offsets of exp(-2 pi i t / M) and exp(-2 pi i t / N) tables
+  float scale;           // output amplitude factor (1; srslte_ue_ul_set_normalization)
+  float cfo;             // frequency shift applied to the output, subcarriers (0; srslte_ue_ul_set_cfo)
 };
 
 // one UL-SCH code block

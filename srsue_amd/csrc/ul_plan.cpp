@@ -57,7 +57,7 @@ uint32_t ul_radix_plan(uint32_t n) {
 
 int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
   txs.clear(); cbs.clear(); kdata.clear(); scr.clear(); tw.clear(); tb_cb0.clear();
-  pi_off.clear(); tw_off.clear(); sel_off.clear(); r0_cache.clear();
+  pi_off.clear(); tw_off.clear(); sel_off.clear();
   payload_bytes = sym_bytes = iq_samples = 0;
   algo_bytes = 0;
   auto twiddles = [&](uint32_t len) {
@@ -85,6 +85,8 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     t.n_prb = c.n_prb;
     t.M = 12 * c.L_prb;
     t.Qm = c.Qm;
+    t.scale = 1.0f;
+    t.cfo = 0.0f;
     t.fact = ul_radix_plan(t.M);
     t.fact_n = ul_radix_plan(t.N);
     if (!t.fact || !t.fact_n) {
@@ -131,36 +133,37 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
       b.sym0 = sym;
       sym += b.E / c.Qm;
       if (!pi_off.count(b.K)) {
-        std::vector<uint32_t> pi;
-        qpp_table(b.K, pi);
+        auto& pi = pi_cache[b.K];
+        if (pi.empty()) qpp_table(b.K, pi);
         pi_off[b.K] = (uint32_t)kdata.size();
         kdata.insert(kdata.end(), pi.begin(), pi.end());
       }
       b.pi_off = pi_off[b.K];
       const auto key = std::make_pair(b.K, b.F);
-      if (!sel_off.count(key)) {
+      SelTab& st = sel_cache[key];
+      if (st.sel.empty()) {   // selection table and per-rv start ranks of (K, F), kept across builds
         std::vector<uint32_t> pos;
         std::vector<int32_t> rank;
         uint32_t Nv = 0;
         cb_pos_table(b.K, pos);
         cb_rank_table(b.K, b.F, rank, &Nv);
-        std::vector<uint32_t> sel(Nv, 0);
+        st.sel.assign(Nv, 0);
         for (uint32_t tt = 0; tt < pos.size(); tt++)
-          if (rank[pos[tt]] >= 0) sel[(uint32_t)rank[pos[tt]]] = tt;
-        sel_off[key] = {(uint32_t)kdata.size(), Nv};
-        kdata.insert(kdata.end(), sel.begin(), sel.end());
-        // rank of the first non-null position at or after k0(rv), per rv
-        auto& r0 = r0_cache[key];
-        for (uint32_t rv = 0; rv < 4; rv++) {
+          if (rank[pos[tt]] >= 0) st.sel[(uint32_t)rank[pos[tt]]] = tt;
+        for (uint32_t rv = 0; rv < 4; rv++) {   // rank of the first non-null position at or after k0(rv)
           const uint32_t k0 = k0_of(b.K, rv);
           uint32_t cnt = 0;
           for (uint32_t p = 0; p < k0 && p < rank.size(); p++) cnt += rank[p] >= 0 ? 1 : 0;
-          r0[rv] = cnt % Nv;
+          st.r0[rv] = cnt % Nv;
         }
       }
-      b.sel_off = sel_off[key].first;
-      b.Nv = sel_off[key].second;
-      b.r0 = r0_cache[key][c.rv];
+      if (!sel_off.count(key)) {
+        sel_off[key] = (uint32_t)kdata.size();
+        kdata.insert(kdata.end(), st.sel.begin(), st.sel.end());
+      }
+      b.sel_off = sel_off[key];
+      b.Nv = (uint32_t)st.sel.size();
+      b.r0 = st.r0[c.rv];
       cbs.push_back(b);
     }
     if (byte0 != c.tbs / 8 + 3 || sym != 12 * t.M) {

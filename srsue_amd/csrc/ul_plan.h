@@ -28,8 +28,11 @@ struct UlPlan {
   double algo_bytes = 0;
 
   std::map<uint32_t, uint32_t> pi_off, tw_off;
-  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> sel_off;   // (K, F) -> (offset, Nv)
-  std::map<std::pair<uint32_t, uint32_t>, std::array<uint32_t, 4>> r0_cache;        // (K, F) -> r0 per rv
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> sel_off;   // (K, F) -> kdata offset of this build
+  // per-key tables kept across builds (the per-TTI path re-plans every grant)
+  struct SelTab { std::vector<uint32_t> sel; uint32_t r0[4]; };
+  std::map<std::pair<uint32_t, uint32_t>, SelTab> sel_cache;
+  std::map<uint32_t, std::vector<uint32_t>> pi_cache;
   int build(const mi_ul_cfg_t* cfgs, uint32_t n);
 };
 

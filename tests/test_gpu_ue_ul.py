@@ -1,0 +1,117 @@
+"""Per-TTI srsLTE UL API on the GPU (include/srslte/srslte.h, srsue_amd/csrc/ue_ul.cpp), driven by
+tests/c/ue_ul_harness.c in the call order of srsUE's phch_worker (init / normalisation / CFO / RNTI /
+set_cfg, then per TTI set_cfo, [dci_msg_to_ul_grant], cfg_grant, pusch_encode_rnti_softbuffer).
+Checked against the oracle's PUSCH transmitter (oracle/o_ul.c) on the same TB: direct grants, a grant
+decoded from DCI format 0 bits, a retransmission (rv 2) re-encoded from the HARQ softbuffer with a NULL
+payload, the normalisation factor and the CFO rotation, and the rejection of a retransmission with nothing stored."""
+import ctypes
+import os
+import struct
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_ul_grant import format0
+
+pytestmark = pytest.mark.gpu
+HARNESS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "ue_ul_harness")
+TOL = 1e-4
+NFFT = {6: 128, 15: 256, 25: 512, 50: 1024, 75: 1536, 100: 2048}
+
+
+def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
+    """txs: list of dict(tti, rnti, rv, dci (DciMsg or None), n_prb, L_prb, tbs, Qm, ncs, tb, pass_data)"""
+    N = NFFT[nof_prb]
+    with tempfile.TemporaryDirectory() as d:
+        fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
+        with open(fin, "wb") as f:
+            f.write(struct.pack("8i", cell_id, nof_prb, len(txs), *dmrs, flags))
+            f.write(struct.pack("f", cfo))
+            for t in txs:
+                dci = t.get("dci")
+                f.write(struct.pack("10i", t["tti"], t["rnti"], t["rv"], int(dci is not None), t.get("n_prb", 0),
+                                    t.get("L_prb", 0), t["tbs"], t.get("Qm", 0), t.get("ncs", 0),
+                                    int(t.get("pass_data", True))))
+                f.write(struct.pack("i", dci.nof_bits if dci else 0))
+                f.write(bytes(dci.data) if dci else bytes(64))
+                f.write(np.ascontiguousarray(t["tb"], np.uint8).tobytes())
+        subprocess.check_call([HARNESS, fin, fout], timeout=300)
+        raw = open(fout, "rb").read()
+    out, pos = [], 0
+    for _ in txs:
+        r = struct.unpack_from("6i", raw, pos)
+        pos += 24
+        iq = np.frombuffer(raw[pos:pos + 15 * N * 8], np.float32)
+        pos += 15 * N * 8
+        out.append((r, iq))
+    return out
+
+
+def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None):
+    c = O.ul_cfg(cell_id=cell_id, nof_prb=nof_prb, sf_idx=sf, rnti=t["rnti"], n_prb=t.get("n_prb", 0) if n_prb is None else n_prb,
+                 L_prb=t.get("L_prb") if L is None else L, tbs=t["tbs"], Qm=t.get("Qm") if Qm is None else Qm,
+                 rv=t["rv"], gh=dmrs[0], sh=dmrs[1], dss=dmrs[2], cs=dmrs[3], n2=t.get("ncs", 0) if ncs is None else ncs)
+    iq = np.zeros(2 * 15 * NFFT[nof_prb], np.float32)
+    assert O.lib().or_pusch_encode(ctypes.byref(c), t["tb"], iq) == 0
+    return iq
+
+
+def rel_err(a, b):
+    return float(np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(b ** 2)))
+
+
+def tb(seed, tbs):
+    return np.random.default_rng(seed).integers(0, 256, tbs // 8, dtype=np.uint8)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built(built):
+    assert os.path.exists(HARNESS)
+
+
+def test_direct_grants_match_oracle():
+    dmrs = (0, 1, 2, 3)
+    txs = [dict(tti=14, rnti=0x46, rv=0, n_prb=0, L_prb=100, tbs=43816, Qm=4, ncs=2, tb=tb(1, 43816)),
+           dict(tti=27, rnti=0x1234, rv=0, n_prb=20, L_prb=50, tbs=12216, Qm=6, ncs=5, tb=tb(2, 12216)),
+           dict(tti=9, rnti=0x46, rv=1, n_prb=4, L_prb=3, tbs=256, Qm=2, ncs=0, tb=tb(3, 256))]
+    res = run(7, 100, txs, dmrs=dmrs)
+    for t, (r, iq) in zip(txs, res):
+        assert r[0] == 0
+        assert rel_err(iq, oracle_iq(7, 100, t, t["tti"] % 10, dmrs)) < TOL
+
+
+def test_dci_format0_grant_and_harq_retransmission():
+    """PDCCH-style grant (format 0 bits) -> cfg_grant -> encode; then rv 2 with payload NULL re-encodes the
+    TB the softbuffer kept from the rv 0 transmission."""
+    m = format0(100, 0, 100, 20, ncs=3)        # 16QAM, I_TBS 19
+    T = 43816
+    data = tb(9, T)
+    txs = [dict(tti=33, rnti=0x46, rv=0, dci=m, tbs=T, tb=data),
+           dict(tti=41, rnti=0x46, rv=2, dci=m, tbs=T, tb=np.zeros(T // 8, np.uint8), pass_data=False)]
+    res = run(1, 100, txs)
+    for t, (r, iq) in zip(txs, res):
+        assert r[0] == 0 and r[1:] == (0, 100, T, 4, 3)
+        ref = oracle_iq(1, 100, dict(t, tb=data), t["tti"] % 10, n_prb=0, L=100, Qm=4, ncs=3)
+        assert rel_err(iq, ref) < TOL
+
+
+def test_normalisation_and_cfo():
+    t = dict(tti=5, rnti=0x77, rv=0, n_prb=0, L_prb=25, tbs=5736, Qm=2, ncs=1, tb=tb(4, 5736))
+    cfo = 0.37
+    (r, iq), = run(3, 25, [t], flags=3, cfo=cfo)
+    assert r[0] == 0
+    ref = oracle_iq(3, 25, t, 5).reshape(-1, 2)
+    N = NFFT[25]
+    z = (ref[:, 0] + 1j * ref[:, 1]) * (25 / 15 / np.sqrt(25)) * np.exp(2j * np.pi * cfo * np.arange(len(ref)) / N)
+    ref2 = np.stack([z.real, z.imag], 1).astype(np.float32).ravel()
+    assert rel_err(iq, ref2) < 2e-4
+
+
+def test_retransmission_without_stored_tb_is_rejected():
+    T = 5736
+    txs = [dict(tti=5, rnti=0x46, rv=0, n_prb=0, L_prb=25, tbs=T, Qm=2, ncs=0, tb=tb(5, T), pass_data=False)]
+    (r, _), = run(3, 25, txs)       # nothing stored in the fresh softbuffer and no data: error
+    assert r[0] == -3
