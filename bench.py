@@ -326,6 +326,54 @@ def bench_ctrl(args, batch, dev):
                     f"{B} subframes per step"}
 
 
+def bench_ul(args, B, dev):
+    """UL PUSCH transmitter (include/mi_ul.h): B subframes of 20 MHz full-band PUSCH,
+    16QAM MCS 20 (I_TBS 19, TBS 43,816, 8 code blocks), TB payloads resident in HBM, SC-FDMA IQ written
+    to HBM.  Roofline: pusch_mod_kernel (coded symbols read + IQ write per subframe)."""
+    T = 43816
+    cfgs = [abi.ul_cfg(cell_id=1, nof_prb=100, sf_idx=i % 10, rnti=0x46, n_prb=0, L_prb=100, tbs=T, Qm=4)
+            for i in range(B)]
+    b = abi.UlBatch(cfgs, profile=True)
+    rng = np.random.default_rng(77)
+    pay = rng.integers(0, 256, b.payload_bytes, dtype=np.uint8)
+    d_pay = torch.from_numpy(pay).to(dev)
+    d_iq = torch.empty(2 * b.iq_samples, dtype=torch.float32, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(args.warmup):
+        b.run(d_pay.data_ptr(), d_iq.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    b.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.run(d_pay.data_ptr(), d_iq.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / args.steps
+    st, n = b.stage_ms()
+    mod_bytes = B * (12 * 1200 + 15 * 2048 * 8)
+    out = {"workload": f"{B} x 20 MHz PUSCH, 100 PRB 16QAM MCS 20 (TBS {T}, 8 code blocks)",
+           "ms_per_step": round(el * 1e3, 3), "Mbps": round(B * T / el / 1e6, 1),
+           "subframes_per_s": round(B / el, 1), "stage_ms_per_step": {k: round(v, 4) for k, v in st.items()},
+           "roofline": {"kernel": "pusch_mod_kernel", "bound": "hbm",
+                        "achieved": round(mod_bytes / (st["mod"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(mod_bytes / (st["mod"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import ctypes
+        import oracle_lib as O
+        oc = O.ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=T, Qm=4)
+        iq = np.zeros(2 * 15 * 2048, np.float32)
+        k, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(10.0, args.cpu_seconds):
+            O.lib().or_pusch_encode(ctypes.byref(oc), pay[:T // 8], iq)
+            k += 1
+        dt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": round(k * T / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "port",
+                               "sample": f"{k} subframes through the oracle's UL chain (oracle/o_ul.c, direct "
+                                         f"O(M^2) transform precoding, double precision) in {dt:.1f} s"}
+    b.close()
+    return out
+
+
 def bench_sync(args, batch, dev):
     """Sync front end over the batch: every subframe arrives in a raw slot of
     15 N + 64 samples at an unknown offset (1..63) with a CFO (+-0.4 subcarriers); per step the PSS of
@@ -460,6 +508,8 @@ def main():
     ap.add_argument("--ctrl", action="store_true",
                     help="also time the DL control stage (SURVEY 8f-1: PCFICH + PDCCH soft bits + DCI blind search "
                          "for each subframe's RNTI) on the batch's grid; reported beside value")
+    ap.add_argument("--ul", action="store_true",
+                    help="also time the UL PUSCH transmitter (SURVEY 8f-4) on as many subframes; reported beside value")
     ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
                     help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
     ap.add_argument("--sched", choices=("auto", "win", "lane"), default="auto",
@@ -579,6 +629,8 @@ def main():
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
         if args.ctrl:
             out["ctrl"] = bench_ctrl(args, batch, dev)
+        if args.ul:
+            out["ul"] = bench_ul(args, B, dev)
         if args.sync:
             out["sync"] = bench_sync(args, batch, dev)
         if world == 1 and not args.no_cpu_baseline:

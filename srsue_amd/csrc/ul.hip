@@ -61,42 +61,76 @@ __device__ __forceinline__ void bf5(float2* v) {
   v[3] = csub(p2, q2);
 }
 
-// In-place forward DFT of n <= 2048 points in LDS, Stockham decimation in time over the radix list
-// `plan` (4 bits per stage), twiddles tw[t] = exp(-2 pi i t / n).  Stage with Ns points done so far
-// and radix R: butterfly j (< n / R) reads x[j + r n/R], twiddles by W_{Ns R}^{(j mod Ns) r}, writes
-// y[(j / Ns) Ns R + j mod Ns + r Ns].  All threads of the block take part.
-__device__ void fft_lds(float2* buf, uint32_t n, uint32_t plan, const float2* tw) {
-  constexpr int PER = UL_NMAX / 2 / UL_THREADS;   // butterflies per thread at most (radix 2, n = 2048)
+__device__ __forceinline__ void bf8(float2* v) {
+  float2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+  bf4(e);
+  bf4(o);
+  const float r = 0.70710678118654752440f;
+  o[1] = make_float2((o[1].x + o[1].y) * r, (o[1].y - o[1].x) * r);      // * (1 - j) / sqrt 2
+  o[2] = mul_nj(o[2]);                                                     // * -j
+  o[3] = make_float2((o[3].y - o[3].x) * r, (-o[3].x - o[3].y) * r);     // * (-1 - j) / sqrt 2
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    v[i] = cadd(e[i], o[i]);
+    v[i + 4] = csub(e[i], o[i]);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void bf(float2 (&v)[R]) {
+  if constexpr (R == 2) bf2(v);
+  else if constexpr (R == 3) bf3(v);
+  else if constexpr (R == 4) bf4(v);
+  else if constexpr (R == 5) bf5(v);
+  else bf8(v);
+}
+
+// One Stockham stage (decimation in time) of an n-point forward DFT in LDS, radix R, Ns points done so
+// far: butterfly j (< n / R) reads x[j + r n/R], twiddles by W_{Ns R}^{(j mod Ns) r} (tw[t] =
+// exp(-2 pi i t / n)), writes y[(j / Ns) Ns R + j mod Ns + r Ns].  All threads of the block take part.
+template <int R>
+__device__ __forceinline__ void fft_stage(float2* buf, uint32_t n, uint32_t Ns, const float2* tw) {
+  constexpr int PER = (UL_NMAX / R + UL_THREADS - 1) / UL_THREADS;
+  const uint32_t nb = n / R, tws = n / (Ns * R);
+  float2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; p++) {
+    const uint32_t j = threadIdx.x + p * UL_THREADS;
+    if (j < nb) {
+#pragma unroll
+      for (int r = 0; r < R; r++) v[p][r] = buf[j + r * nb];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < PER; p++) {
+    const uint32_t j = threadIdx.x + p * UL_THREADS;
+    if (j < nb) {
+      const uint32_t k = j % Ns;
+#pragma unroll
+      for (int r = 1; r < R; r++) v[p][r] = cmul(v[p][r], tw[k * r * tws]);   // k r tws < n
+      bf<R>(v[p]);
+      const uint32_t base = (j / Ns) * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; r++) buf[base + r * Ns] = v[p][r];
+    }
+  }
+  __syncthreads();
+}
+
+// In-place forward DFT of n <= 2048 points over the radix list `plan` (4 bits per stage)
+__device__ __forceinline__ void fft_lds(float2* buf, uint32_t n, uint32_t plan, const float2* tw) {
   uint32_t Ns = 1;
   for (int st = 0; st < 8; st++) {
     const uint32_t R = (plan >> (4 * st)) & 15u;
     if (!R) break;
-    const uint32_t nb = n / R, tws = n / (Ns * R);
-    float2 v[PER][5];
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const uint32_t j = threadIdx.x + p * UL_THREADS;
-      if (j < nb)
-        for (uint32_t r = 0; r < R; r++) v[p][r] = buf[j + r * nb];
+    switch (R) {
+      case 2: fft_stage<2>(buf, n, Ns, tw); break;
+      case 3: fft_stage<3>(buf, n, Ns, tw); break;
+      case 4: fft_stage<4>(buf, n, Ns, tw); break;
+      case 5: fft_stage<5>(buf, n, Ns, tw); break;
+      default: fft_stage<8>(buf, n, Ns, tw); break;
     }
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const uint32_t j = threadIdx.x + p * UL_THREADS;
-      if (j < nb) {
-        const uint32_t k = j % Ns;
-        for (uint32_t r = 1; r < R; r++) v[p][r] = cmul(v[p][r], tw[k * r * tws]);   // k r tws < n
-        switch (R) {
-          case 2: bf2(v[p]); break;
-          case 3: bf3(v[p]); break;
-          case 4: bf4(v[p]); break;
-          default: bf5(v[p]); break;
-        }
-        const uint32_t base = (j / Ns) * Ns * R + k;
-        for (uint32_t r = 0; r < R; r++) buf[base + r * Ns] = v[p][r];
-      }
-    }
-    __syncthreads();
     Ns *= R;
   }
 }
@@ -246,6 +280,7 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
   __shared__ float2 twm[UL_MMAX];
   const MiUlTx x = txs[blockIdx.x];
   const uint32_t slot = blockIdx.y, t = threadIdx.x, N = x.N, M = x.M, Qm = x.Qm;
+  const uint32_t dq = slot ? x.q[1] : x.q[0], dncs = slot ? x.ncs[1] : x.ncs[0];   // no dynamic struct index
   for (uint32_t i = t; i < N; i += UL_THREADS) twn[i] = twg[x.twn_off + i];
   for (uint32_t i = t; i < M; i += UL_THREADS) twm[i] = twg[x.twm_off + i];
   const float sM = rsqrtf((float)M), gN = rsqrtf((float)N) * x.scale;
@@ -259,8 +294,8 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
       // DMRS 36.211 5.5.2.1: r(n) = exp(j alpha n) x_q(n mod N_ZC), x_q(m) = exp(-j pi q m (m+1) / N_ZC)
       for (uint32_t n = t; n < M; n += UL_THREADS) {
         const uint32_t m = n % x.nzc;
-        const uint32_t a = (uint32_t)(((uint64_t)x.q[slot] * m * (m + 1)) % (2ull * x.nzc));
-        const uint32_t cs = (x.ncs[slot] * n) % 12;
+        const uint32_t a = (uint32_t)(((uint64_t)dq * m * (m + 1)) % (2ull * x.nzc));
+        const uint32_t cs = (dncs * n) % 12;
         float sv, cv;
         sincospif(-(float)a / (float)x.nzc + (float)cs / 6.0f, &sv, &cv);
         buf[n] = make_float2(cv, sv);

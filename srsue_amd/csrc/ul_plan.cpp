@@ -48,6 +48,7 @@ int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc
 uint32_t ul_radix_plan(uint32_t n) {
   uint32_t plan = 0, st = 0;
   auto push = [&](uint32_t r) { plan |= r << (4 * st++); };
+  while (n % 8 == 0 && n != 16 && n != 32 && st < 8) { push(8); n /= 8; }   // 16 / 32: 4 x 4, 8 x 4
   while (n % 4 == 0 && st < 8) { push(4); n /= 4; }
   while (n % 2 == 0 && st < 8) { push(2); n /= 2; }
   while (n % 3 == 0 && st < 8) { push(3); n /= 3; }

@@ -14,7 +14,7 @@ namespace mi {
 
 // 36.211 5.5.2.1 / 5.5.1: DMRS root q, Zadoff-Chu length and cyclic shift of slot ns (0..19)
 int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc, uint32_t* ncs);
-// radix list (4, 2, 3, 5; 4 bits per stage) of an n-point transform, 0 if n has another factor
+// radix list (8, 4, 2, 3, 5; 4 bits per stage) of an n-point transform, 0 if n has another factor
 uint32_t ul_radix_plan(uint32_t n);
 
 struct UlPlan {
