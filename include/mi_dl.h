@@ -65,6 +65,11 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
 #define MI_DL_FLAG_TDEC_WIN  16u
 #define MI_DL_FLAG_TDEC_LANE 32u
 #define MI_TDEC_WIN_AUTO_CBS 1024u
+/* Keep the LLR stream (MI_DL_BUF_LLR) of a full run.  By default a run that includes both the DEMAP and
+ * the RM stage fuses them: rate de-matching computes each LLR from the grid and channel estimates (the
+ * same arithmetic, demap_body.h) and the LLR stream is never written.  Runs of RM without DEMAP read the
+ * LLR buffer (e.g. uploaded by the caller). */
+#define MI_DL_FLAG_KEEP_LLR  64u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 

@@ -23,6 +23,7 @@ FLAG_IQ_SC16 = 8    # IQ input as UHD sc16 (int16 I/Q, fc32 = sc16 / 32768)
 FLAG_TDEC_WIN = 16  # int16 turbo: force the latency form (one workgroup per code block)
 FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wavefronts
 SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE}
+FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
 
 
 class SfCfg(C.Structure):
@@ -181,11 +182,11 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None, keep_llr=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
         flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
-            (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched]
+            (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched] | (FLAG_KEEP_LLR if keep_llr else 0)
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())

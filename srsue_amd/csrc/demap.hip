@@ -8,44 +8,10 @@
 // One lane per RE (TM1) or per SFBC RE pair (TM2).  The RE list (36.211 6.3.5 mapping order) is
 // a per-configuration device table, so grid/ce reads walk consecutive subcarriers and every lane
 // writes its Qm LLRs contiguously (float2 stores): the LLR stream leaves fully coalesced.
+#include "demap_body.h"
 #include "kernels.h"
 
 namespace mi {
-
-template <int QM>
-__device__ __forceinline__ float pam_level(int lab) {
-  // lab: this dimension's bits, MSB first (36.211 7.1 Gray mapping, separable I/Q)
-  if constexpr (QM == 2) {
-    return (1 - 2 * (lab & 1)) * 0.70710678118654752440f;
-  } else if constexpr (QM == 4) {
-    const int b0 = (lab >> 1) & 1, b1 = lab & 1;
-    return (float)((1 - 2 * b0) * (1 + 2 * b1)) * 0.31622776601683793320f;
-  } else {
-    const int b0 = (lab >> 2) & 1, b1 = (lab >> 1) & 1, b2 = lab & 1;
-    return (float)((1 - 2 * b0) * (4 - (1 - 2 * b1) * (2 - (1 - 2 * b2)))) * 0.15430334996209191026f;
-  }
-}
-
-// writes the QM/2 LLRs of one dimension at llr[0], llr[2], llr[4] (I at even, Q at odd slots)
-template <int QM>
-__device__ __forceinline__ void demap_dim(float x, float* llr) {
-  constexpr int NB = QM / 2, NL = 1 << NB;
-  float d2[NL];
-#pragma unroll
-  for (int lab = 0; lab < NL; lab++) {
-    const float d = x - pam_level<QM>(lab);
-    d2[lab] = d * d;
-  }
-#pragma unroll
-  for (int j = 0; j < NB; j++) {
-    float m0 = 3.0e38f, m1 = 3.0e38f;
-#pragma unroll
-    for (int lab = 0; lab < NL; lab++) {
-      if ((lab >> (NB - 1 - j)) & 1) m1 = fminf(m1, d2[lab]); else m0 = fminf(m0, d2[lab]);
-    }
-    llr[2 * j] = (m0 - m1) * 2.0f;   // / sigma^2, sigma^2 = 0.5
-  }
-}
 
 template <int QM>
 __device__ __forceinline__ void demap_store(float2 x, const uint32_t* __restrict__ scr, uint32_t bit0,

@@ -124,12 +124,20 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   mark(2);
   if (P.has_pdsch) {
     float* sb = sb_override ? sb_override : d_sb.as<float>();
-    if (mask & (1u << MI_DL_STAGE_DEMAP))
+    // fused demap -> rate de-matching unless the caller keeps the LLR stream (or supplies it)
+    const bool fuse = (mask & (1u << MI_DL_STAGE_DEMAP)) && (mask & (1u << MI_DL_STAGE_RM)) &&
+                      !(flags & MI_DL_FLAG_KEEP_LLR);
+    if ((mask & (1u << MI_DL_STAGE_DEMAP)) && !fuse)
       launch_demap(d_grid.as<float2>(), d_ce.as<float2>(), d_e.as<float>(), d_sfs.as<MiSfDesc>(),
                    d_pds.as<MiPdschDesc>(), d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), nsf,
                    P.max_units, noise, st);
     mark(3);
-    if (mask & (1u << MI_DL_STAGE_RM))
+    if (fuse)
+      launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_sfs.as<MiSfDesc>(), d_pds.as<MiPdschDesc>(),
+                      d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), noise, sb,
+                      d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(),
+                      (uint32_t)P.groups.size(), P.max_ncb, st);
+    else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
     mark(4);

@@ -16,6 +16,7 @@
 // in between).  A chunk that receives nothing and holds nothing exits after its first barrier.
 // Punctured positions of a first transmission (60 % of the circular buffer at MCS 28) thus cost no
 // HBM traffic, here or in the decoder.
+#include "demap_body.h"
 #include "kernels.h"
 #include "rm_body.h"
 
@@ -28,14 +29,113 @@
 
 namespace mi {
 
+// Fused demap -> rate de-matching (MI_DL_FLAG_KEEP_LLR off): instead of reading the LLR stream e, the
+// staging computes each LLR from the grid and channel estimates (demap_body.h, the arithmetic of
+// demap_kernel): the 90,000 LLRs of a 20 MHz subframe are never written to or read from HBM.
+struct RmFuse {
+  const float2* grid;
+  const float2* ce;
+  const MiSfDesc* sfs;
+  const MiPdschDesc* pds;
+  const MiCellDesc* cells;
+  const uint32_t* re_tab;
+  const uint32_t* scr_tab;
+  float noise;
+};
+
+// LLR gi of the subframe of descriptor sd
+__device__ __forceinline__ float fused_llr(const RmFuse& f, const MiSfDesc& sd, const MiPdschDesc& pd, uint32_t W,
+                                           uint32_t gi) {
+  const float2* g = f.grid + sd.grid_off;
+  const float2* c0 = f.ce + sd.ce_off;
+  const float2* c1 = c0 + (size_t)NSYMB * W;
+  const uint32_t* re = f.re_tab + pd.re_off;
+  const uint32_t* scr = f.scr_tab + pd.scr_off;
+  switch (pd.Qm) {
+    case 2: return demap_llr<2>(pd, gi, g, c0, c1, re, scr, f.noise);
+    case 4: return demap_llr<4>(pd, gi, g, c0, c1, re, scr, f.noise);
+    default: return demap_llr<6>(pd, gi, g, c0, c1, re, scr, f.noise);
+  }
+}
+
+// Per-lane data of the fused staging (filled once per workgroup): where the lane's subframe keeps its
+// grid / channel estimates, RE list and scrambling words, and its demap kind (Qm, TM2)
+struct RmLaneSrc {
+  uint64_t goff, coff;   // float2 offsets of the grid and of port 0's channel estimates
+  uint32_t c1;           // port 1's estimates: c0 + c1
+  uint32_t re, scr;      // offsets into the RE table / scrambling words
+  uint32_t qm, tm2;
+};
+
+// All LLRs of one demap unit (TM1: one RE, QM LLRs; TM2: one SFBC RE pair, 2 QM LLRs), descrambled, into
+// the tile positions of [ga, gb): demap_kernel's arithmetic (demap_body.h)
+template <int QM, bool TM2>
+__device__ __forceinline__ void fused_unit(const RmFuse& f, const RmLaneSrc& src, uint32_t u, uint32_t ga, uint32_t gb,
+                                           uint32_t ta, float* tile) {
+  const float2* g = f.grid + src.goff;
+  const float2* c0 = f.ce + src.coff;
+  const uint32_t* re = f.re_tab + src.re;
+  const uint32_t* scr = f.scr_tab + src.scr;
+  float2 x[2];
+  if constexpr (!TM2) {
+    const uint32_t rr = re[u];
+    const float2 y = g[rr], h = c0[rr];
+    const float den = h.x * h.x + h.y * h.y + f.noise;
+    x[0] = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
+  } else {
+    const float2* c1 = c0 + src.c1;
+    const uint32_t ra = re[2 * u], rb = re[2 * u + 1];
+    const float2 r0 = g[ra], r1 = g[rb];
+    const float2 h00 = c0[ra], h01 = c0[rb], h10 = c1[ra], h11 = c1[rb];
+    float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
+    if (hh <= 0.f) hh = 1e-9f;
+    const float sc = 1.41421356237309504880f / hh;
+    x[0] = make_float2(sc * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
+                       sc * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
+    x[1] = make_float2(sc * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
+                       sc * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
+  }
+  constexpr int NS = TM2 ? 2 : 1, U = QM * NS;
+  float l[U];
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    demap_dim<QM>(x[k].x, l + k * QM);
+    demap_dim<QM>(x[k].y, l + k * QM + 1);
+  }
+  const uint32_t bit0 = u * U;
+#pragma unroll
+  for (int b = 0; b < U; b++) {
+    const uint32_t i = bit0 + b;
+    const float v = ((scr[i >> 5] >> (i & 31)) & 1u) ? -l[b] : l[b];
+    if (i >= ga && i < gb) tile[ta + (i - ga)] = v;
+  }
+}
+
+__device__ __forceinline__ void fused_unit_any(const RmFuse& f, const RmLaneSrc& src, uint32_t u, uint32_t ga,
+                                               uint32_t gb, uint32_t ta, float* tile) {
+  switch (src.qm + 8 * src.tm2) {
+    case 2: fused_unit<2, false>(f, src, u, ga, gb, ta, tile); break;
+    case 4: fused_unit<4, false>(f, src, u, ga, gb, ta, tile); break;
+    case 6: fused_unit<6, false>(f, src, u, ga, gb, ta, tile); break;
+    case 10: fused_unit<2, true>(f, src, u, ga, gb, ta, tile); break;
+    case 12: fused_unit<4, true>(f, src, u, ga, gb, ta, tile); break;
+    default: fused_unit<6, true>(f, src, u, ga, gb, ta, tile); break;
+  }
+}
+
+template <bool FUSED>
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
-                                                        const uint32_t* __restrict__ kdata) {
+                                                        const uint32_t* __restrict__ kdata, RmFuse fz) {
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
   __shared__ uint32_t s_comb, s_new;
+  // fused staging: per-lane sources, and per wavefront 32 (row, segment) LLR runs -> demap units
+  __shared__ RmLaneSrc s_src[FUSED ? LANES : 1];
+  __shared__ uint32_t rs_ga[FUSED ? 4 : 1][32], rs_gb[FUSED ? 4 : 1][32], rs_ta[FUSED ? 4 : 1][32],
+      rs_u0[FUSED ? 4 : 1][32], rs_pre[FUSED ? 4 : 1][33];
   const MiGroupDesc g = groups[blockIdx.y];
   const uint32_t pa = blockIdx.x * RM_CHUNK;
   if (pa >= g.Ncb) return;
@@ -52,7 +152,21 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       nr = ch[pa / RM_CHUNK + 1] - ra;
       j0 = ra >= ld.r0 ? ra - ld.r0 : ra + ld.Nv - ld.r0;   // LLR index of the chunk's first rank
     }
-    s_j0[tid] = j0; s_nr[tid] = nr; s_nv[tid] = ld.Nv; s_E[tid] = ld.E; s_eoff[tid] = ld.e_off;
+    s_j0[tid] = j0; s_nr[tid] = nr; s_nv[tid] = ld.Nv; s_E[tid] = ld.E;
+    if constexpr (FUSED) {
+      if (ld.valid) {
+        const MiSfDesc sd = fz.sfs[ld.tb];
+        const MiPdschDesc pd = fz.pds[sd.pdsch];
+        s_eoff[tid] = ld.e_off - sd.e_off;   // LLR index of the code block's first LLR within its subframe
+        s_src[tid] = RmLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * fz.cells[sd.cell].W, pd.re_off, pd.scr_off,
+                               pd.Qm, pd.tm == 2 ? 1u : 0u};
+      } else {
+        s_eoff[tid] = 0;
+        s_src[tid] = RmLaneSrc{0, 0, 0, 0, 0, 2, 0};
+      }
+    } else {
+      s_eoff[tid] = ld.e_off;
+    }
     // does any LLR of this lane land in the chunk (LLR indices j0 .. j0+nr-1 mod Nv against [0, E))?
     busy = nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv);
     const uint64_t comb = __ballot(ld.valid && !ld.new_tb), fresh = __ballot(ld.valid && ld.new_tb);
@@ -65,6 +179,50 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
   // all of a wavefront's loads issued before its LDS writes
   constexpr int ROWS = LANES / 4, PER = RM_CHUNK / 64;
+  if constexpr (FUSED) {
+    // Every LLR computed from grid + ce, one demap unit (an RE, or an SFBC RE pair: all its Qm or 2 Qm
+    // LLRs, as demap_kernel computes them) per thread and step.  Wavefront w owns code-block rows
+    // l = w + 4 r; each row's LLR run (j0 + t) mod Nv, t < nr, clipped to [0, E), is at most two
+    // contiguous runs (row-segments); the units of the wavefront's 32 row-segments are dealt to its 64
+    // threads flat, so all threads work and their loads are independent.
+    const uint32_t w = tid >> 6, q = tid & 63;
+#pragma unroll
+    for (int r = 0; r < ROWS; r++)
+      for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + 4 * r][t] = 0.0f;
+    if (q < 32) {
+      const uint32_t l = w + 4 * (q >> 1), seg = q & 1;
+      const uint32_t j0 = s_j0[l], nr = s_nr[l], nv = s_nv[l], E = s_E[l];
+      const uint32_t ta = seg ? nv - j0 : 0, tb = seg ? nr : (nr < nv - j0 ? nr : nv - j0);
+      uint32_t ga = 0, gb = 0, u0 = 0, nu = 0;
+      if (ta < tb) {
+        const uint32_t ja = seg ? 0 : j0, jf = ja + (tb - ta), jb = jf < E ? jf : E;
+        if (ja < jb) {
+          const uint32_t U = s_src[l].qm * (s_src[l].tm2 ? 2 : 1), eb = (uint32_t)s_eoff[l];
+          ga = eb + ja;
+          gb = eb + jb;
+          u0 = ga / U;
+          nu = (gb - 1) / U - u0 + 1;
+        }
+      }
+      rs_ga[w][q] = ga; rs_gb[w][q] = gb; rs_ta[w][q] = ta; rs_u0[w][q] = u0; rs_pre[w][q + 1] = nu;
+    }
+    __syncthreads();
+    if (q == 0) {
+      rs_pre[w][0] = 0;
+      for (int i = 0; i < 32; i++) rs_pre[w][i + 1] += rs_pre[w][i];
+    }
+    __syncthreads();
+    const uint32_t total = rs_pre[w][32];
+    for (uint32_t fi = q; fi < total; fi += 64) {
+      uint32_t lo = 0, hi = 32;   // row-segment rs with rs_pre[rs] <= fi < rs_pre[rs + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rs_pre[w][mid] <= fi) lo = mid; else hi = mid;
+      }
+      const uint32_t l = w + 4 * (lo >> 1);
+      fused_unit_any(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo], tile[l]);
+    }
+  } else {
   {
     float v[ROWS][PER];
     const uint32_t w = tid >> 6, q = tid & 63;
@@ -85,6 +243,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
     for (int r = 0; r < ROWS; r++)
 #pragma unroll
       for (int c = 0; c < PER; c++) tile[w + 4 * r][q + 64 * c] = v[r][c];
+  }
   }
   __syncthreads();
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
@@ -119,8 +278,16 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       uint32_t j = j0 + t;
       if (j >= nv) j -= nv;
       if (j < E) { v = v + tile[lane][t]; c = true; }
-      if (rep)
-        for (j += nv; j < E; j += nv) v = v + e[ld.e_off + j];
+      if (rep) {
+        if constexpr (FUSED) {
+          const MiSfDesc sd = fz.sfs[ld.tb];
+          const MiPdschDesc pd = fz.pds[sd.pdsch];
+          const uint32_t W = fz.cells[sd.cell].W;
+          for (j += nv; j < E; j += nv) v = v + fused_llr(fz, sd, pd, W, (uint32_t)s_eoff[lane] + j);
+        } else {
+          for (j += nv; j < E; j += nv) v = v + e[ld.e_off + j];
+        }
+      }
     }
     const bool any = __ballot(c) != 0, was = (was_m >> i) & 1u;
     const bool mat = MI_RM_DENSE || any || (was && comb);   // row holds data after this launch
@@ -141,7 +308,17 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
                        hipStream_t st) {
   if (!n_groups) return;
   dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
-  hipLaunchKernelGGL(rm_combine_kernel, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data);
+  hipLaunchKernelGGL(rm_combine_kernel<false>, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data, RmFuse{});
+}
+
+void launch_rm_fused(const float2* grid, const float2* ce, const MiSfDesc* sfs, const MiPdschDesc* pds,
+                     const MiCellDesc* cells, const uint32_t* re_tab, const uint32_t* scr_tab, float noise, float* sb,
+                     const MiGroupDesc* groups, const MiLaneDesc* lanes, const uint32_t* ktab_data, uint32_t n_groups,
+                     uint32_t max_ncb, hipStream_t st) {
+  if (!n_groups) return;
+  dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
+  const RmFuse fz{grid, ce, sfs, pds, cells, re_tab, scr_tab, noise};
+  hipLaunchKernelGGL(rm_combine_kernel<true>, g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz);
 }
 
 }  // namespace mi

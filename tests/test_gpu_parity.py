@@ -23,8 +23,8 @@ S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
 DECODERS = [(False, "lane"), (True, "lane"), (True, "win")]
 
 
-def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None):
-    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16, sched=sched)
+def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None, keep_llr=False):
+    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16, sched=sched, keep_llr=keep_llr)
     flat = np.zeros(2 * b.iq_samples, np.float32)
     for i, iq in enumerate(iqs):
         o = 2 * b.iq_offset(i)
@@ -57,7 +57,7 @@ CASES = [
 def test_mixed_batch_front_end_and_decode(i16, sched):
     cfgs = [abi.sf_cfg(**c) for c in CASES]
     iqs, tbs = make_subframes(cfgs, snr_db=30.0)
-    b = run_batch(cfgs, iqs, tdec_i16=i16, sched=sched)
+    b = run_batch(cfgs, iqs, tdec_i16=i16, sched=sched, keep_llr=True)
     grid = b.download(abi.BUF_GRID, np.float32)
     ce = b.download(abi.BUF_CE, np.float32)
     llr = b.download(abi.BUF_LLR, np.float32)
@@ -79,6 +79,26 @@ def test_mixed_batch_front_end_and_decode(i16, sched):
         assert np.array_equal(p, tbs[i]), f"payload vs transmitted TB, case {i}"
         assert np.array_equal(p, opay), f"payload vs oracle, case {i}"
         assert its[i] == onoi
+
+
+@pytest.mark.parametrize("snr", [30.0, 19.0])
+def test_fused_demap_rate_dematching_matches_unfused(snr):
+    """The default full run fuses demap into rate de-matching (LLRs computed from grid + ce inside the rm
+    staging, demap_body.h); it must give the same softbuffer input as the unfused stages: payload, TB CRC
+    and per-code-block iteration counts identical over every configuration of CASES (TM1/TM2, 1.4-20
+    MHz, sync holes, filler bits, rv 2), in the waterfall too."""
+    cfgs = [abi.sf_cfg(**c) for c in CASES]
+    iqs, tbs = make_subframes(cfgs, snr_db=snr, seed0=int(snr))
+    res = []
+    for keep in (True, False):
+        b = run_batch(cfgs, iqs, tdec_i16=True, keep_llr=keep)
+        res.append((b.download(abi.BUF_PAYLOAD, np.uint8), b.download(abi.BUF_TB_CRC, np.uint32),
+                    b.download(abi.BUF_CB_ITS, np.uint32)))
+        b.close()
+    for a, f in zip(res[0], res[1]):
+        assert np.array_equal(a, f)
+    if snr >= 30.0:
+        assert res[1][1].all()
 
 
 @pytest.mark.parametrize("i16,sched", DECODERS)
