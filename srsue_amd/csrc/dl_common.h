@@ -103,6 +103,15 @@ struct MiLaneDesc {          // one per code block (lane of a group)
   uint32_t pad;
 };
 
+struct MiLaneSrc {           // one per code block: where the fused demap stage finds its LLRs' inputs
+  uint64_t goff, coff;       // float2 offsets of its subframe's grid and port-0 channel estimates
+  uint32_t c1;               // port 1's estimates at c0 + c1 (NSYMB x W)
+  uint32_t re, scr;          // offsets of the PDSCH RE list and scrambling words
+  uint32_t qm, tm2;          // bits per symbol, SFBC
+  uint32_t eb;               // LLR index of the code block's first LLR within its subframe
+  uint32_t pad;
+};
+
 struct MiGroupDesc {         // one per wavefront group of <= 64 code blocks of equal K
   uint32_t K, Ncb;
   uint32_t lane0;            // first MiLaneDesc index (64 consecutive entries)

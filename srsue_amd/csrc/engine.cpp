@@ -54,7 +54,7 @@ static bool up(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
 int Engine::upload(hipStream_t st, bool alloc_sb) {
   const Plan& P = plan;
   bool ok = up(d_cells, P.cells, st) && up(d_crs, P.crs, st) && up(d_pds, P.pds, st) && up(d_re, P.re_tab, st) &&
-            up(d_scr, P.scr_tab, st) && up(d_sfs, P.sfs, st) && up(d_lanes, P.lanes, st) &&
+            up(d_scr, P.scr_tab, st) && up(d_sfs, P.sfs, st) && up(d_lanes, P.lanes, st) && up(d_lanesrc, P.lane_src, st) &&
             up(d_groups, P.groups, st) && up(d_ktabs, P.ktabs, st) && up(d_kdata, P.kdata, st) &&
             up(d_tbs, P.tbs, st) && up(d_cblist, P.cb_list, st) && up(d_fftlist, P.fft_list_flat, st);
   if (!ok) return -1;
@@ -133,10 +133,9 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                    P.max_units, noise, st);
     mark(3);
     if (fuse)
-      launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_sfs.as<MiSfDesc>(), d_pds.as<MiPdschDesc>(),
-                      d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), noise, sb,
-                      d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(),
-                      (uint32_t)P.groups.size(), P.max_ncb, st);
+      launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
+                      d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
+                      d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);

@@ -32,7 +32,7 @@ struct Engine {
   void launch_turbo(float* sb, hipStream_t st);
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
-  DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,
+  DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,
       d_fftlist, d_tw;
   // data buffers
   DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_wm, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,

@@ -218,6 +218,16 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     }
     i = j;
   }
+  // fused demap sources of every lane
+  lane_src.assign(lanes.size(), MiLaneSrc{0, 0, 0, 0, 0, 2, 0, 0, 0});
+  for (size_t li = 0; li < lanes.size(); li++) {
+    const MiLaneDesc& ld = lanes[li];
+    if (!ld.valid) continue;
+    const MiSfDesc& sd = sfs[ld.tb];
+    const MiPdschDesc& pd = pds[sd.pdsch];
+    lane_src[li] = MiLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * cells[sd.cell].W, pd.re_off, pd.scr_off, pd.Qm,
+                             pd.tm == 2 ? 1u : 0u, (uint32_t)(ld.e_off - sd.e_off), 0};
+  }
   // rank tables into kdata, patch lane offsets
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rank_off;
   for (size_t gi = 0; gi < groups.size(); gi++) {

@@ -22,6 +22,7 @@ struct Plan {
   std::vector<uint32_t> re_tab, scr_tab;
   std::vector<MiSfDesc> sfs;
   std::vector<MiLaneDesc> lanes;
+  std::vector<MiLaneSrc> lane_src;        // per lane (same index): the fused demap's inputs
   std::vector<MiGroupDesc> groups;
   std::vector<MiKTab> ktabs;
   std::vector<uint32_t> kdata;

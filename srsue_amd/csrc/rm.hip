@@ -35,42 +35,16 @@ namespace mi {
 struct RmFuse {
   const float2* grid;
   const float2* ce;
-  const MiSfDesc* sfs;
-  const MiPdschDesc* pds;
-  const MiCellDesc* cells;
+  const MiLaneSrc* src;      // per lane of the launch (group.lane0 + lane), built by the planner
   const uint32_t* re_tab;
   const uint32_t* scr_tab;
   float noise;
 };
 
-// LLR gi of the subframe of descriptor sd
-__device__ __forceinline__ float fused_llr(const RmFuse& f, const MiSfDesc& sd, const MiPdschDesc& pd, uint32_t W,
-                                           uint32_t gi) {
-  const float2* g = f.grid + sd.grid_off;
-  const float2* c0 = f.ce + sd.ce_off;
-  const float2* c1 = c0 + (size_t)NSYMB * W;
-  const uint32_t* re = f.re_tab + pd.re_off;
-  const uint32_t* scr = f.scr_tab + pd.scr_off;
-  switch (pd.Qm) {
-    case 2: return demap_llr<2>(pd, gi, g, c0, c1, re, scr, f.noise);
-    case 4: return demap_llr<4>(pd, gi, g, c0, c1, re, scr, f.noise);
-    default: return demap_llr<6>(pd, gi, g, c0, c1, re, scr, f.noise);
-  }
-}
-
-// Per-lane data of the fused staging (filled once per workgroup): where the lane's subframe keeps its
-// grid / channel estimates, RE list and scrambling words, and its demap kind (Qm, TM2)
-struct RmLaneSrc {
-  uint64_t goff, coff;   // float2 offsets of the grid and of port 0's channel estimates
-  uint32_t c1;           // port 1's estimates: c0 + c1
-  uint32_t re, scr;      // offsets into the RE table / scrambling words
-  uint32_t qm, tm2;
-};
-
 // All LLRs of one demap unit (TM1: one RE, QM LLRs; TM2: one SFBC RE pair, 2 QM LLRs), descrambled, into
 // the tile positions of [ga, gb): demap_kernel's arithmetic (demap_body.h)
 template <int QM, bool TM2>
-__device__ __forceinline__ void fused_unit(const RmFuse& f, const RmLaneSrc& src, uint32_t u, uint32_t ga, uint32_t gb,
+__device__ __forceinline__ void fused_unit(const RmFuse& f, const MiLaneSrc& src, uint32_t u, uint32_t ga, uint32_t gb,
                                            uint32_t ta, float* tile) {
   const float2* g = f.grid + src.goff;
   const float2* c0 = f.ce + src.coff;
@@ -111,7 +85,7 @@ __device__ __forceinline__ void fused_unit(const RmFuse& f, const RmLaneSrc& src
   }
 }
 
-__device__ __forceinline__ void fused_unit_any(const RmFuse& f, const RmLaneSrc& src, uint32_t u, uint32_t ga,
+__device__ __forceinline__ void fused_unit_any(const RmFuse& f, const MiLaneSrc& src, uint32_t u, uint32_t ga,
                                                uint32_t gb, uint32_t ta, float* tile) {
   switch (src.qm + 8 * src.tm2) {
     case 2: fused_unit<2, false>(f, src, u, ga, gb, ta, tile); break;
@@ -120,6 +94,23 @@ __device__ __forceinline__ void fused_unit_any(const RmFuse& f, const RmLaneSrc&
     case 10: fused_unit<2, true>(f, src, u, ga, gb, ta, tile); break;
     case 12: fused_unit<4, true>(f, src, u, ga, gb, ta, tile); break;
     default: fused_unit<6, true>(f, src, u, ga, gb, ta, tile); break;
+  }
+}
+
+// LLR gi of a lane's subframe, alone (repetition beyond N_v, low code rates only): the single-bit
+// form of the same arithmetic (demap_body.h demap_llr)
+__device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src, uint32_t gi) {
+  MiPdschDesc pd{};
+  pd.tm = src.tm2 ? 2 : 1;
+  const float2* g = f.grid + src.goff;
+  const float2* c0 = f.ce + src.coff;
+  const float2* c1 = c0 + src.c1;
+  const uint32_t* re = f.re_tab + src.re;
+  const uint32_t* scr = f.scr_tab + src.scr;
+  switch (src.qm) {
+    case 2: return demap_llr<2>(pd, gi, g, c0, c1, re, scr, f.noise);
+    case 4: return demap_llr<4>(pd, gi, g, c0, c1, re, scr, f.noise);
+    default: return demap_llr<6>(pd, gi, g, c0, c1, re, scr, f.noise);
   }
 }
 
@@ -133,7 +124,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   __shared__ uint64_t s_eoff[LANES];
   __shared__ uint32_t s_comb, s_new;
   // fused staging: per-lane sources, and per wavefront 32 (row, segment) LLR runs -> demap units
-  __shared__ RmLaneSrc s_src[FUSED ? LANES : 1];
+  __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
   __shared__ uint32_t rs_ga[FUSED ? 4 : 1][32], rs_gb[FUSED ? 4 : 1][32], rs_ta[FUSED ? 4 : 1][32],
       rs_u0[FUSED ? 4 : 1][32], rs_pre[FUSED ? 4 : 1][33];
   const MiGroupDesc g = groups[blockIdx.y];
@@ -154,16 +145,9 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
     }
     s_j0[tid] = j0; s_nr[tid] = nr; s_nv[tid] = ld.Nv; s_E[tid] = ld.E;
     if constexpr (FUSED) {
-      if (ld.valid) {
-        const MiSfDesc sd = fz.sfs[ld.tb];
-        const MiPdschDesc pd = fz.pds[sd.pdsch];
-        s_eoff[tid] = ld.e_off - sd.e_off;   // LLR index of the code block's first LLR within its subframe
-        s_src[tid] = RmLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * fz.cells[sd.cell].W, pd.re_off, pd.scr_off,
-                               pd.Qm, pd.tm == 2 ? 1u : 0u};
-      } else {
-        s_eoff[tid] = 0;
-        s_src[tid] = RmLaneSrc{0, 0, 0, 0, 0, 2, 0};
-      }
+      const MiLaneSrc src = fz.src[g.lane0 + tid];
+      s_src[tid] = src;
+      s_eoff[tid] = src.eb;   // LLR index of the code block's first LLR within its subframe
     } else {
       s_eoff[tid] = ld.e_off;
     }
@@ -280,10 +264,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       if (j < E) { v = v + tile[lane][t]; c = true; }
       if (rep) {
         if constexpr (FUSED) {
-          const MiSfDesc sd = fz.sfs[ld.tb];
-          const MiPdschDesc pd = fz.pds[sd.pdsch];
-          const uint32_t W = fz.cells[sd.cell].W;
-          for (j += nv; j < E; j += nv) v = v + fused_llr(fz, sd, pd, W, (uint32_t)s_eoff[lane] + j);
+          for (j += nv; j < E; j += nv) v = v + fused_llr(fz, s_src[lane], (uint32_t)s_eoff[lane] + j);
         } else {
           for (j += nv; j < E; j += nv) v = v + e[ld.e_off + j];
         }
@@ -311,13 +292,12 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
   hipLaunchKernelGGL(rm_combine_kernel<false>, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data, RmFuse{});
 }
 
-void launch_rm_fused(const float2* grid, const float2* ce, const MiSfDesc* sfs, const MiPdschDesc* pds,
-                     const MiCellDesc* cells, const uint32_t* re_tab, const uint32_t* scr_tab, float noise, float* sb,
-                     const MiGroupDesc* groups, const MiLaneDesc* lanes, const uint32_t* ktab_data, uint32_t n_groups,
-                     uint32_t max_ncb, hipStream_t st) {
+void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
+                     const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
+                     const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, hipStream_t st) {
   if (!n_groups) return;
   dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
-  const RmFuse fz{grid, ce, sfs, pds, cells, re_tab, scr_tab, noise};
+  const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise};
   hipLaunchKernelGGL(rm_combine_kernel<true>, g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz);
 }
 
