@@ -25,7 +25,7 @@ bool hip_ok(hipError_t e, const char* what) {
 }
 
 bool DevBuf::ensure(size_t n) {
-  if (n <= bytes && p) return true;
+  if (n <= bytes && p && !view) return true;
   release();
   size_t a = (n + 255) & ~(size_t)255;
   if (a == 0) a = 256;
@@ -34,12 +34,14 @@ bool DevBuf::ensure(size_t n) {
   return true;
 }
 void DevBuf::release() {
-  if (p) (void)hipFree(p);
+  if (p && !view) (void)hipFree(p);
   p = nullptr;
   bytes = 0;
+  view = false;
 }
 
 Engine::~Engine() {
+  if (h_stage) (void)hipHostFree(h_stage);
   for (auto& set : ev_sets)
     for (auto& e : set) (void)hipEventDestroy(e);
 }
@@ -53,10 +55,32 @@ static bool up(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
 
 int Engine::upload(hipStream_t st, bool alloc_sb) {
   const Plan& P = plan;
-  bool ok = up(d_cells, P.cells, st) && up(d_crs, P.crs, st) && up(d_pds, P.pds, st) && up(d_re, P.re_tab, st) &&
-            up(d_scr, P.scr_tab, st) && up(d_sfs, P.sfs, st) && up(d_lanes, P.lanes, st) && up(d_lanesrc, P.lane_src, st) &&
-            up(d_groups, P.groups, st) && up(d_ktabs, P.ktabs, st) && up(d_kdata, P.kdata, st) &&
-            up(d_tbs, P.tbs, st) && up(d_cblist, P.cb_list, st) && up(d_fftlist, P.fft_list_flat, st);
+  struct Tab { DevBuf* dst; const void* src; size_t bytes; };
+  auto tab = [](DevBuf& d, const auto& v) { return Tab{&d, v.data(), v.size() * sizeof(v[0])}; };
+  const Tab tabs[] = {tab(d_cells, P.cells), tab(d_crs, P.crs), tab(d_pds, P.pds), tab(d_re, P.re_tab),
+                      tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),
+                      tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),
+                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat)};
+  size_t total = 0;
+  for (const Tab& t : tabs) total += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
+  if (total > h_stage_bytes) {
+    if (h_stage) (void)hipHostFree(h_stage);
+    h_stage = nullptr;
+    h_stage_bytes = 0;
+    if (!hip_ok(hipHostMalloc(&h_stage, total, hipHostMallocDefault), "hipHostMalloc tables")) return -1;
+    h_stage_bytes = total;
+  }
+  if (total > d_tables.bytes) {
+    for (const Tab& t : tabs) t.dst->release();   // views into the old arena
+    if (!d_tables.ensure(total)) return -1;
+  }
+  size_t off = 0;
+  for (const Tab& t : tabs) {
+    if (t.bytes) memcpy(static_cast<char*>(h_stage) + off, t.src, t.bytes);
+    t.dst->set_view(static_cast<char*>(d_tables.p) + off, std::max<size_t>(t.bytes, 1));
+    off += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
+  }
+  bool ok = hip_ok(hipMemcpyAsync(d_tables.p, h_stage, total, hipMemcpyHostToDevice, st), "upload tables");
   if (!ok) return -1;
   // twiddles per FFT size (double precision on the host)
   bool need_tw = false;

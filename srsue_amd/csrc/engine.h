@@ -16,8 +16,10 @@ bool hip_ok(hipError_t e, const char* what);
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  bool view = false;       // points into another allocation (the packed table arena): never freed here
   bool ensure(size_t n);   // grow-only
   void release();
+  void set_view(void* ptr, size_t n) { release(); p = ptr; bytes = n; view = true; }
   ~DevBuf() { release(); }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
@@ -38,6 +40,11 @@ struct Engine {
   DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_wm, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,
       d_tbits;
   std::map<int, size_t> tw_off;   // FFT size -> float2 offset in d_tw
+  // the plan's descriptor tables, packed 256-B aligned into one page-locked host buffer and copied to
+  // one device arena with a single DMA per upload (the per-TTI API re-plans every call)
+  DevBuf d_tables;
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
   hipStream_t last_stream = nullptr;
   // profiling: one event set per run since the last reset (MI_DL_FLAG_PROFILE)
   std::vector<std::vector<hipEvent_t>> ev_sets;

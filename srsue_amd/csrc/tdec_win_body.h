@@ -244,13 +244,32 @@ MI_HD inline bool win_fwd_fix(const WinCb& c, uint32_t j, const float (&na)[8]) 
 // q(x) of the materialised rows, 0 for the others; filler steps k < F: DEC1 systematic/parity = -511
 MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb, const uint32_t* pos,
                            const uint32_t* pi32, uint32_t lane, uint32_t F) {
+  // batches of B independent position -> row-map -> value chains per thread, all of a batch's loads of
+  // one kind issued before the next kind (each chain is three dependent global loads)
+  constexpr uint32_t B = 8;
   const uint8_t* map = reinterpret_cast<const uint8_t*>(sbg + sb_map_off(Ncb));
-  for (uint32_t i = t; i < 3 * c.K + 12; i += P) {
-    const uint32_t p = pos[i];
-    float x = map[p] ? sbg[(size_t)p * LANES + lane] : 0.0f;
-    x = q16f(x);
-    if (i < 3 * F && i % 3 != 2) x = -I16_CI;
-    c.q[i] = (int16_t)x;
+  const uint32_t n = 3 * c.K + 12;
+  for (uint32_t i0 = t; i0 < n; i0 += B * P) {
+    uint32_t pp[B];
+    uint8_t mm[B];
+    float xx[B];
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) {
+      const uint32_t i = i0 + b * P;
+      pp[b] = i < n ? pos[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) mm[b] = i0 + b * P < n ? map[pp[b]] : 0;
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) xx[b] = mm[b] ? sbg[(size_t)pp[b] * LANES + lane] : 0.0f;
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) {
+      const uint32_t i = i0 + b * P;
+      if (i >= n) break;
+      float x = q16f(xx[b]);
+      if (i < 3 * F && i % 3 != 2) x = -I16_CI;
+      c.q[i] = (int16_t)x;
+    }
   }
   for (uint32_t k = t; k < c.K; k += P) {
     c.pi[k] = (uint16_t)pi32[k];

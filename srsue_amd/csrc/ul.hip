@@ -274,21 +274,23 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
                                                                const uint32_t* __restrict__ scr,
                                                                const MiUlTx* __restrict__ txs,
                                                                const float2* __restrict__ twg,
-                                                               float2* __restrict__ iq) {
+                                                               float2* __restrict__ iq, uint32_t per) {
   __shared__ float2 buf[UL_NMAX];
   __shared__ float2 twn[UL_NMAX];
   __shared__ float2 twm[UL_MMAX];
   const MiUlTx x = txs[blockIdx.x];
-  const uint32_t slot = blockIdx.y, t = threadIdx.x, N = x.N, M = x.M, Qm = x.Qm;
+  // symbols l0 .. l0 + per - 1 of the subframe (per = 7: one workgroup per slot, twiddles staged once
+  // for 7 symbols -- batches; per = 1: one workgroup per symbol -- the per-TTI latency path)
+  const uint32_t l0 = blockIdx.y * per, slot = l0 / 7, t = threadIdx.x, N = x.N, M = x.M, Qm = x.Qm;
   const uint32_t dq = slot ? x.q[1] : x.q[0], dncs = slot ? x.ncs[1] : x.ncs[0];   // no dynamic struct index
   for (uint32_t i = t; i < N; i += UL_THREADS) twn[i] = twg[x.twn_off + i];
   for (uint32_t i = t; i < M; i += UL_THREADS) twm[i] = twg[x.twm_off + i];
   const float sM = rsqrtf((float)M), gN = rsqrtf((float)N) * x.scale;
   constexpr int PM = (UL_MMAX + UL_THREADS - 1) / UL_THREADS;
   const int off = (int)(12 * x.n_prb) - (int)(x.W / 2);   // allocation's first subcarrier relative to W/2
-  uint32_t pos = slot * (15 * N / 2);                        // first sample of the slot
+  uint32_t pos = (uint32_t)(symbol_offset((int)N, (int)l0) - cp_len((int)N, (int)(l0 % 7)));   // first sample of l0
   __syncthreads();
-  for (uint32_t ls = 0; ls < 7; ls++) {
+  for (uint32_t ls = l0 % 7; ls < l0 % 7 + per; ls++) {
     const uint32_t l = 7 * slot + ls, cp = cp_len((int)N, (int)ls);
     if (ls == 3) {
       // DMRS 36.211 5.5.2.1: r(n) = exp(j alpha n) x_q(n mod N_ZC), x_q(m) = exp(-j pi q m (m+1) / N_ZC)
@@ -373,7 +375,10 @@ void launch_ul(const uint8_t* pay, uint32_t* tbcrc, const MiUlTx* txs, uint32_t 
   if (!n_tx) return;
   if (stage == 0) hipLaunchKernelGGL(ul_tbcrc_kernel, dim3(n_tx), dim3(UL_THREADS), 0, st, pay, txs, tbcrc);
   if (stage == 1) hipLaunchKernelGGL(ul_encode_kernel, dim3(n_cb), dim3(UL_THREADS), 0, st, pay, tbcrc, txs, cbs, kdata, syms);
-  if (stage == 2) hipLaunchKernelGGL(pusch_mod_kernel, dim3(n_tx, 2), dim3(UL_THREADS), 0, st, syms, scr, txs, tw, iq);
+  if (stage == 2) {
+    const uint32_t per = n_tx >= 64 ? 7 : 1;   // small batches: a workgroup per symbol (latency)
+    hipLaunchKernelGGL(pusch_mod_kernel, dim3(n_tx, 14 / per), dim3(UL_THREADS), 0, st, syms, scr, txs, tw, iq, per);
+  }
 }
 
 }  // namespace mi

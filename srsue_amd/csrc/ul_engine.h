@@ -28,10 +28,22 @@ struct UlEngine {
     if (!b.ensure(sizeof(T) * (v.empty() ? 1 : v.size()))) return false;
     return v.empty() || hip_ok(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st), "ul upload");
   }
+  // host copies of the static tables last uploaded: the per-TTI path re-plans every grant, and the
+  // QPP / selection tables and twiddles only change with the code-block sizes and bandwidth
+  std::vector<uint32_t> up_kdata;
+  std::vector<float> up_tw;
   int upload(hipStream_t st) {
     const UlPlan& P = plan;
-    const bool ok = up(d_txs, P.txs, st) && up(d_cbs, P.cbs, st) && up(d_kdata, P.kdata, st) && up(d_scr, P.scr, st) &&
-                    up(d_tw, P.tw, st) && d_tbcrc.ensure(P.txs.size() * 4) && d_syms.ensure(P.sym_bytes);
+    bool ok = up(d_txs, P.txs, st) && up(d_cbs, P.cbs, st) && up(d_scr, P.scr, st) &&
+              d_tbcrc.ensure(P.txs.size() * 4) && d_syms.ensure(P.sym_bytes);
+    if (ok && P.kdata != up_kdata) {
+      ok = up(d_kdata, P.kdata, st);
+      up_kdata = P.kdata;
+    }
+    if (ok && P.tw != up_tw) {
+      ok = up(d_tw, P.tw, st);
+      up_tw = P.tw;
+    }
     return ok ? 0 : -1;
   }
   int run(const void* d_pay, void* d_iq, hipStream_t st) {
