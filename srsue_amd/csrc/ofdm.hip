@@ -122,11 +122,14 @@ __device__ __forceinline__ void fft_symbol(float2* buf, const IQ* __restrict__ s
   }
 }
 
+// symbols [blockIdx.y * per, (blockIdx.y + 1) * per) of a subframe: per = 14 (one workgroup per
+// subframe, twiddles staged once for 14 FFTs -- batches) or 1 (a workgroup per symbol -- small batches,
+// the per-TTI latency path)
 template <int N, typename IQ>
 __global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
                                                       const MiSfDesc* __restrict__ sfs,
                                                       const uint32_t* __restrict__ list,
-                                                      const float2* __restrict__ twg, uint32_t W) {
+                                                      const float2* __restrict__ twg, uint32_t W, int per) {
   __shared__ float2 buf[N];
   __shared__ float2 tw[N];
   const MiSfDesc d = sfs[list[blockIdx.x]];
@@ -134,7 +137,8 @@ __global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq,
   __syncthreads();
   const IQ* src_sf = iq + d.iq_off;
   float2* dst = grid + d.grid_off;
-  for (int l = 0; l < NSYMB; l++) {
+  const int l0 = (int)blockIdx.y * per;
+  for (int l = l0; l < l0 + per; l++) {
     fft_symbol<N, IQ>(buf, src_sf + symbol_offset(N, l), tw);
     for (int k = threadIdx.x; k < (int)W; k += 256) dst[l * W + k] = buf[sc_bin(k, (int)W, N)];
     __syncthreads();
@@ -144,14 +148,15 @@ __global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq,
 template <typename IQ>
 static void launch_ofdm_rx_t(int N, const IQ* iq, float2* grid, const MiSfDesc* sfs, const uint32_t* list, uint32_t n,
                              const float2* tw, uint32_t W, hipStream_t st) {
-  dim3 g(n), b(256);
+  const int per = n >= 256 ? NSYMB : 1;   // small batches: a workgroup per symbol (latency)
+  dim3 g(n, NSYMB / per), b(256);
   switch (N) {
-    case 2048: hipLaunchKernelGGL((ofdm_rx_kernel<2048, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 1536: hipLaunchKernelGGL((ofdm_rx_kernel<1536, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 1024: hipLaunchKernelGGL((ofdm_rx_kernel<1024, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 512: hipLaunchKernelGGL((ofdm_rx_kernel<512, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 256: hipLaunchKernelGGL((ofdm_rx_kernel<256, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
-    case 128: hipLaunchKernelGGL((ofdm_rx_kernel<128, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W); break;
+    case 2048: hipLaunchKernelGGL((ofdm_rx_kernel<2048, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
+    case 1536: hipLaunchKernelGGL((ofdm_rx_kernel<1536, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
+    case 1024: hipLaunchKernelGGL((ofdm_rx_kernel<1024, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
+    case 512: hipLaunchKernelGGL((ofdm_rx_kernel<512, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
+    case 256: hipLaunchKernelGGL((ofdm_rx_kernel<256, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
+    case 128: hipLaunchKernelGGL((ofdm_rx_kernel<128, IQ>), g, b, 0, st, iq, grid, sfs, list, tw, W, per); break;
     default: break;
   }
 }

@@ -16,13 +16,16 @@ __global__ __launch_bounds__(256) void tb_kernel(const uint8_t* __restrict__ cb_
   const MiTbDesc t = tbs[blockIdx.x];
   const uint32_t* lanes = cb_list + t.cb_list;
   const uint32_t pbytes = t.tbs / 8;
-  uint32_t start = 0;
-  for (uint32_t r = 0; r < t.C; r++) {
+  // wavefront w copies code blocks w, w + 4, ...: each block's start in the TB is arithmetic, so the
+  // blocks' loads are independent (no serial chain over the code blocks)
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  for (uint32_t r = wv; r < t.C; r += 4) {
+    uint32_t start = 0;
+    for (uint32_t j = 0; j < r; j++) start += tb_cb_nbytes(t, j);
     const uint32_t n = tb_cb_nbytes(t, r);
     const uint8_t* src = cb_bytes + (size_t)lanes[r] * CB_BYTES_STRIDE + (r == 0 ? t.F / 8 : 0);
     uint8_t* dst = payload + t.pay_off + start;
-    for (uint32_t j = threadIdx.x; j < n && start + j < pbytes; j += 256) dst[j] = src[j];
-    start += n;
+    for (uint32_t j = ln; j < n && start + j < pbytes; j += 64) dst[j] = src[j];
   }
   if (threadIdx.x < 64) {
     uint32_t c = 0, its = 0;

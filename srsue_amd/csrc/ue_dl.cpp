@@ -138,8 +138,15 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, srslte_cell_t cell) {
   auto* ctx = new mi_ue_dl_ctx();
   if (hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) { delete ctx; return SRSLTE_ERROR; }
   const size_t W = 12 * cell.nof_prb, n = (size_t)mi::NSYMB * W;
-  q->sf_symbols = (cf_t*)srslte_vec_malloc((uint32_t)(n * sizeof(cf_t)));
-  for (uint32_t p = 0; p < cell.nof_ports; p++) q->ce[p] = (cf_t*)srslte_vec_malloc((uint32_t)(n * sizeof(cf_t)));
+  // host mirrors of the grid / estimates (srsUE reads them, phch_worker.cc:260): page-locked, so their
+  // per-TTI D2H copies are direct DMA (this library allocates and frees them)
+  auto host_alloc = [](size_t bytes) -> cf_t* {
+    void* p = nullptr;
+    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? (cf_t*)p : nullptr;
+  };
+  q->sf_symbols = host_alloc(n * sizeof(cf_t));
+  for (uint32_t p = 0; p < cell.nof_ports; p++) q->ce[p] = host_alloc(n * sizeof(cf_t));
+  if (!q->sf_symbols || !q->ce[0] || (cell.nof_ports == 2 && !q->ce[1])) { delete ctx; return SRSLTE_ERROR; }
   if (!ctx->d_iq.ensure((size_t)mi::sf_len(mi::symbol_sz(cell.nof_prb)) * 8)) { delete ctx; return SRSLTE_ERROR; }
   ctx->cfg.cell_id = cell.id;
   ctx->cfg.nof_prb = cell.nof_prb;
@@ -161,8 +168,9 @@ void srslte_ue_dl_free(srslte_ue_dl_t* q) {
     if (q->ctx->st) (void)hipStreamDestroy(q->ctx->st);
     delete q->ctx;
   }
-  free(q->sf_symbols);
-  for (int p = 0; p < SRSLTE_MAX_PORTS; p++) free(q->ce[p]);
+  if (q->sf_symbols) (void)hipHostFree(q->sf_symbols);
+  for (int p = 0; p < SRSLTE_MAX_PORTS; p++)
+    if (q->ce[p]) (void)hipHostFree(q->ce[p]);
   memset(q, 0, sizeof(*q));
 }
 
