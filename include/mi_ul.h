@@ -11,6 +11,8 @@
  * -> channel interleaver (5.2.2.8, no UCI) -> scrambling (36.211 5.3.1) -> modulation (7.1) ->
  * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, no hopping) +
  * DMRS (5.5.2.1, L_prb >= 3) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
+ * HARQ-ACK bits (1 or 2) are multiplexed as 36.212 5.2.2.6 / 5.2.2.8 prescribe (Q'_ACK coded symbols
+ * puncturing the data next to the DMRS); CQI / RI on PUSCH are not supported.
  * Normalisation: unit average power per used subcarrier (1/sqrt(M) DFT, 1/sqrt(N) IDFT).
  */
 #ifndef MI_UL_H
@@ -27,6 +29,8 @@ typedef struct {
   uint32_t n_prb, L_prb, tbs, Qm, rv;                 /* allocation (no hopping), TB bits, 2/4/6, rv 0..3 */
   uint32_t group_hopping, sequence_hopping, delta_ss;  /* DMRS cell configuration (srslte_refsignal_dmrs_pusch_cfg_t) */
   uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI format 0 cyclic-shift field (0..7) */
+  uint32_t ack_len, ack, I_offset_ack;                 /* HARQ-ACK on PUSCH (36.212 5.2.2.6): 0, 1 or 2 bits
+                                                          (bit 0 = first), beta_offset index (36.213 8.6.3-1) */
 } mi_ul_cfg_t;
 
 enum { MI_UL_STAGE_CRC = 0, MI_UL_STAGE_ENCODE, MI_UL_STAGE_MOD, MI_UL_NSTAGES };

@@ -263,8 +263,9 @@ SRSLTE_API void srslte_vec_free(void *ptr);
  * srslte_ue_ul on the GPU (srsue_amd/csrc/ul.hip, ue_ul.cpp): cfg_grant plans the transmission,
  * pusch_encode_rnti_softbuffer copies the payload to HBM, runs TB CRC -> turbo encoder -> rate matching
  * -> channel interleaver -> scrambling -> modulation -> transform precoding + DMRS -> SC-FDMA and copies
- * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  Limits: no UCI on PUSCH (uci_data must
- * carry no ACK / CQI / RI: returns SRSLTE_ERROR), no frequency hopping, L_prb >= 3; PUCCH, SRS and UL
+ * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  HARQ-ACK in uci_data (1 or 2 bits) is
+ * multiplexed into the PUSCH (36.212 5.2.2.6, beta_offset from set_cfg's uci_cfg.I_offset_ack).  Limits:
+ * no CQI / RI on PUSCH (returns SRSLTE_ERROR), no frequency hopping, L_prb >= 3; PUCCH, SRS and UL
  * power control stay in srsLTE.  set_cfg uses the DMRS and hopping configurations, the others are
  * accepted.  set_normalization(true) scales by nof_prb / (15 sqrt(L_prb)) (srsLTE's factor as recorded
  * in DESIGN.md, unverified: srsLTE is not in the container); set_cfo(cfo) shifts the output by cfo
@@ -356,6 +357,7 @@ typedef struct SRSLTE_API {         /* owned by value per phch_worker (phch_work
   srslte_pusch_cfg_t pusch_cfg;     /* ue_ul.pusch_cfg.grant.n_prb_tilde (phch_worker.cc:223) */
   srslte_refsignal_dmrs_pusch_cfg_t dmrs_cfg;
   srslte_pusch_hopping_cfg_t hopping_cfg;
+  srslte_uci_cfg_t uci_cfg;         /* beta_offset indices of UCI on PUSCH (set_cfg) */
   uint16_t current_rnti;
   bool normalize_en;
   bool cfo_en;

@@ -30,6 +30,37 @@ static const uint32_t N2_DMRS[8] = {0, 6, 3, 4, 2, 8, 10, 9};   /* Table 5.5.2.1
 
 uint32_t or_pusch_G(const or_ul_cfg_t *c) { return 12 * 12 * c->L_prb * c->Qm; }
 
+/* 36.213 Table 8.6.3-1: beta_offset^HARQ-ACK x 8 for I_offset^HARQ-ACK = 0..14 */
+static const uint32_t BETA8_ACK[15] = {16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160, 248, 400, 640, 1008};
+
+uint32_t or_ack_qprime(const or_ul_cfg_t *c) {
+  if (!c->ack_len) return 0;
+  or_cbsegm_t sg;
+  if (or_cbsegm(c->tbs, &sg)) return 0;
+  const uint64_t sumK = (uint64_t)sg.Cm * sg.Km + (uint64_t)(sg.C - sg.Cm) * sg.Kp, M = 12 * c->L_prb;
+  const uint64_t num = (uint64_t)c->ack_len * M * 12 * BETA8_ACK[c->I_offset_ack > 14 ? 14 : c->I_offset_ack];
+  const uint64_t q = (num + 8 * sumK - 1) / (8 * sumK);
+  return (uint32_t)(q < 4 * M ? q : 4 * M);
+}
+
+/* 36.212 Tables 5.2.2.6-1 / -2 (placeholders: 2 = x, 3 = y) */
+uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk) {
+  const uint32_t Qm = c->Qm, o0 = c->ack & 1, o1 = (c->ack >> 1) & 1, o2 = o0 ^ o1;
+  if (c->ack_len == 1) {
+    blk[0] = (uint8_t)o0;
+    blk[1] = 3;
+    for (uint32_t b = 2; b < Qm; b++) blk[b] = 2;
+    return Qm;
+  }
+  const uint8_t seq[3][2] = {{(uint8_t)o0, (uint8_t)o1}, {(uint8_t)o2, (uint8_t)o0}, {(uint8_t)o1, (uint8_t)o2}};
+  for (uint32_t s = 0; s < 3; s++) {   /* Qm = 2: o0 o1 o2 o0 o1 o2; else each pair padded with x */
+    blk[s * Qm] = seq[s][0];
+    blk[s * Qm + 1] = seq[s][1];
+    for (uint32_t b = 2; b < Qm; b++) blk[s * Qm + b] = 2;
+  }
+  return 3 * Qm;
+}
+
 int or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *f) {
   const uint32_t A = c->tbs, G = or_pusch_G(c);
   if (A == 0 || (c->Qm != 2 && c->Qm != 4 && c->Qm != 6)) return -1;
@@ -63,8 +94,17 @@ int or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *f, float *x) {
   for (uint32_t l = 0; l < 12; l++)          /* interleaver: output symbol l M + m <- input m 12 + l */
     for (uint32_t m = 0; m < M; m++)
       memcpy(h + (size_t)(l * M + m) * Qm, f + (size_t)(m * 12 + l) * Qm, Qm);
+  /* HARQ-ACK symbols overwrite the matrix from the last row up, columns ColumnSet(j), j = 0, 3, 2, 1, ... */
+  static const uint32_t COLSET[4] = {2, 3, 8, 9};
+  uint8_t blk[18];
+  const uint32_t nq = or_ack_qprime(c), nb = c->ack_len ? or_ack_block(c, blk) : Qm;
+  for (uint32_t i = 0, j = 0; i < nq; i++, j = (j + 3) % 4) {
+    const uint32_t r = M - 1 - i / 4, col = COLSET[j];
+    for (uint32_t b = 0; b < Qm; b++) h[(size_t)(col * M + r) * Qm + b] = blk[(i * Qm + b) % nb];
+  }
   or_gold((c->rnti << 14) | (c->sf_idx << 9) | c->cell_id, cs, G);
-  for (uint32_t i = 0; i < G; i++) h[i] ^= cs[i];
+  for (uint32_t i = 0; i < G; i++)            /* 36.211 5.3.1 with the UCI placeholders */
+    h[i] = h[i] == 2 ? 1 : h[i] == 3 ? h[i - 1] : (uint8_t)(h[i] ^ cs[i]);
   for (uint32_t s = 0; s < 12 * M; s++) {
     uint8_t bi[3], bq[3];
     for (uint32_t j = 0; j < Qm / 2; j++) { bi[j] = h[s * Qm + 2 * j]; bq[j] = h[s * Qm + 2 * j + 1]; }

@@ -230,6 +230,7 @@ typedef struct {
   uint32_t n_prb, L_prb, tbs, Qm, rv;                 /* allocation (no hopping), TB, modulation, rv */
   uint32_t group_hopping, sequence_hopping, delta_ss;  /* DMRS cell configuration */
   uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI 0 cyclic-shift field (0..7) */
+  uint32_t ack_len, ack, I_offset_ack;                 /* HARQ-ACK on PUSCH: 0..2 bits (bit 0 = o0), beta index */
 } or_ul_cfg_t;
 double   or_pam_level(const uint8_t *b, uint32_t Qm);
 uint32_t or_pusch_G(const or_ul_cfg_t *c);
@@ -241,6 +242,10 @@ int      or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r);
 int      or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid /* 14 x 12 N_RB complex */);
 int      or_scfdma_tx(uint32_t nof_prb, const float *grid, float *iq);
 int      or_pusch_encode(const or_ul_cfg_t *c, const uint8_t *tb, float *iq);
+/* HARQ-ACK on PUSCH (36.212 5.2.2.6): number of coded modulation symbols Q'_ACK, and the encoded
+ * block (codes 0 / 1 = bit, 2 = placeholder x, 3 = placeholder y), returns its length in bits */
+uint32_t or_ack_qprime(const or_ul_cfg_t *c);
+uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk /* <= 18 */);
 
 #ifdef __cplusplus
 }

@@ -136,8 +136,10 @@ void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint3
     launch_win_p<64>(sb, out, groups, lanes, ktabs, kdata, n_lanes, max_k, max_its, early_stop, st);
   else if (threads <= 128)
     launch_win_p<128>(sb, out, groups, lanes, ktabs, kdata, n_lanes, max_k, max_its, early_stop, st);
-  else
+  else if (threads <= 256)
     launch_win_p<256>(sb, out, groups, lanes, ktabs, kdata, n_lanes, max_k, max_its, early_stop, st);
+  else
+    launch_win_p<512>(sb, out, groups, lanes, ktabs, kdata, n_lanes, max_k, max_its, early_stop, st);
 }
 
 }  // namespace mi

@@ -38,7 +38,7 @@
 
 namespace mi {
 
-constexpr int WIN_MAXP = 256;   // threads (segments) per code block, at most
+constexpr int WIN_MAXP = 512;   // threads (segments) per code block, at most
 
 // per code block state (LDS on the GPU; host arrays in the test emulation)
 struct WinCb {

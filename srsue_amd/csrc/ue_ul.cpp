@@ -115,11 +115,12 @@ void srslte_ue_ul_set_cfo(srslte_ue_ul_t* q, float cur_cfo) {
 }
 
 void srslte_ue_ul_set_cfg(srslte_ue_ul_t* q, srslte_refsignal_dmrs_pusch_cfg_t* dmrs_cfg, srslte_refsignal_srs_cfg_t*,
-                          srslte_pucch_cfg_t*, srslte_pucch_sched_t*, srslte_uci_cfg_t*,
+                          srslte_pucch_cfg_t*, srslte_pucch_sched_t*, srslte_uci_cfg_t* uci_cfg,
                           srslte_pusch_hopping_cfg_t* hopping_cfg, srslte_ue_ul_powerctrl_t*) {
   if (!q) return;
   if (dmrs_cfg) q->dmrs_cfg = *dmrs_cfg;
   if (hopping_cfg) q->hopping_cfg = *hopping_cfg;
+  if (uci_cfg) q->uci_cfg = *uci_cfg;
 }
 
 int srslte_ue_ul_cfg_grant(srslte_ue_ul_t* q, srslte_ra_ul_grant_t* grant, uint32_t tti, uint32_t rvidx,
@@ -162,11 +163,14 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
                                               srslte_softbuffer_tx_t* sb, uint16_t rnti, cf_t* output_signal) {
   if (!q || !q->ctx || !output_signal) return SRSLTE_ERROR_INVALID_INPUTS;
   mi_ue_ul_ctx* c = q->ctx;
-  if (uci.uci_ack_len || uci.uci_cqi_len || uci.uci_ri_len) {
-    mi::set_error("UCI multiplexing on PUSCH is not supported");
+  if (uci.uci_cqi_len || uci.uci_ri_len || uci.uci_ack_len > 2) {
+    mi::set_error("CQI / RI on PUSCH are not supported");
     return SRSLTE_ERROR;
   }
   c->cfg.rnti = rnti;
+  c->cfg.ack_len = uci.uci_ack_len;   // HARQ-ACK on PUSCH (srsUE: 1 bit, phch_worker.cc:486-487)
+  c->cfg.ack = uci.uci_ack & 3u;
+  c->cfg.I_offset_ack = q->uci_cfg.I_offset_ack;
   const uint32_t nbytes = c->cfg.tbs / 8;
   if (nbytes > TX_MAX_BYTES) return SRSLTE_ERROR;
   // the TB: new data from `data`; a retransmission without data re-encodes the softbuffer's copy

@@ -306,13 +306,30 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
     } else {
       const uint32_t ld = l - (l > 3 ? 1 : 0) - (l > 10 ? 1 : 0);   // data symbol 0..11
       for (uint32_t m = t; m < M; m += UL_THREADS) {
-        // channel interleaver (no UCI): data symbol ld, subcarrier m takes coded symbol m * 12 + ld
-        const uint32_t v = syms[x.sym_off + m * 12 + ld];
+        // channel interleaver: data symbol ld, subcarrier m takes coded symbol m * 12 + ld, unless a HARQ-ACK
+        // symbol overwrote that matrix entry: ACK symbol i sits in row M - 1 - i / 4 of column
+        // {2, 9, 8, 3}[i % 4] (36.212 5.2.2.8, ColumnSet {2, 3, 8, 9} walked with j = (j + 3) mod 4)
         const uint32_t i0 = (ld * M + m) * Qm;
+        int ta = -1;
+        if (x.q_ack) ta = ld == 2 ? 0 : ld == 9 ? 1 : ld == 8 ? 2 : ld == 3 ? 3 : -1;
+        const uint32_t ia = 4 * (M - 1 - m) + (uint32_t)ta;
         uint32_t bits = 0;
-        for (uint32_t b = 0; b < Qm; b++) {
-          const uint32_t i = i0 + b;
-          bits = (bits << 1) | (((v >> (Qm - 1 - b)) ^ (scr[x.scr_off + (i >> 5)] >> (i & 31))) & 1u);
+        if (ta >= 0 && ia < x.q_ack) {
+          // 36.211 5.3.1 placeholders: x -> 1, y -> the previous scrambled bit
+          const uint32_t cw = x.ack_nblk == 1 ? x.ack_sym[0] : x.ack_sym[ia % 3];
+          uint32_t prev = 0;
+          for (uint32_t b = 0; b < Qm; b++) {
+            const uint32_t i = i0 + b, code = (cw >> (2 * b)) & 3u;
+            const uint32_t bit = code == 2 ? 1u : code == 3 ? prev : ((code ^ (scr[x.scr_off + (i >> 5)] >> (i & 31))) & 1u);
+            bits = (bits << 1) | bit;
+            prev = bit;
+          }
+        } else {
+          const uint32_t v = syms[x.sym_off + m * 12 + ld];
+          for (uint32_t b = 0; b < Qm; b++) {
+            const uint32_t i = i0 + b;
+            bits = (bits << 1) | (((v >> (Qm - 1 - b)) ^ (scr[x.scr_off + (i >> 5)] >> (i & 31))) & 1u);
+          }
         }
         // 36.211 7.1: bits b0 b1 .. (b0 = MSB); I from b0, b2, b4 and Q from b1, b3, b5
         const uint32_t b0 = (bits >> (Qm - 1)) & 1u, b1 = (bits >> (Qm - 2)) & 1u;

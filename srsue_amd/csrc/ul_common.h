@@ -22,6 +22,9 @@ struct MiUlTx {
   uint32_t twm_off, twn_off;   // float2 offsets of exp(-2 pi i t / M) and exp(-2 pi i t / N) tables
   float scale;           // output amplitude factor (1; srslte_ue_ul_set_normalization)
   float cfo;             // frequency shift applied to the output, subcarriers (0; srslte_ue_ul_set_cfo)
+  uint32_t q_ack;        // HARQ-ACK coded symbols Q'_ACK (0 = none)
+  uint32_t ack_nblk;     // symbols in the encoded ACK block (1 or 3), repeated over the Q'_ACK symbols
+  uint32_t ack_sym[3];   // the block's symbols: 2 bits per coded bit, bit b at bits 2b (0/1, 2 = x, 3 = y)
 };
 
 // one UL-SCH code block

@@ -11,6 +11,9 @@ namespace mi {
 static const uint32_t N1_DMRS[8] = {0, 2, 3, 4, 6, 8, 9, 10};   // 36.211 Table 5.5.2.1.1-2 (cyclicShift)
 static const uint32_t N2_DMRS[8] = {0, 6, 3, 4, 2, 8, 10, 9};   // 36.211 Table 5.5.2.1.1-1 (DCI format 0)
 
+// 36.213 Table 8.6.3-1: beta_offset^HARQ-ACK x 8 for I_offset^HARQ-ACK = 0..14
+static const uint32_t BETA8_ACK[15] = {16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160, 248, 400, 640, 1008};
+
 static bool prime(uint32_t n) {
   if (n < 2) return false;
   for (uint32_t d = 2; d * d <= n; d++)
@@ -166,6 +169,34 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
       b.Nv = (uint32_t)st.sel.size();
       b.r0 = st.r0[c.rv];
       cbs.push_back(b);
+    }
+    // HARQ-ACK on PUSCH (36.212 5.2.2.6): Q'_ACK = min(ceil(O M 12 beta / sum K_r), 4 M), encoded block
+    // of Tables 5.2.2.6-1 / -2 (x / y placeholders), inserted by the modulation kernel
+    if (c.ack_len) {
+      if (c.ack_len > 2) {
+        set_error("HARQ-ACK on PUSCH: 1 or 2 bits");
+        return -1;
+      }
+      uint64_t sumK = 0;
+      for (uint32_t r = 0; r < sg.C; r++) sumK += r < sg.Cm ? sg.Km : sg.Kp;
+      const uint64_t num = (uint64_t)c.ack_len * t.M * 12 * BETA8_ACK[c.I_offset_ack > 14 ? 14 : c.I_offset_ack];
+      const uint64_t qp = (num + 8 * sumK - 1) / (8 * sumK);
+      t.q_ack = (uint32_t)(qp < 4ull * t.M ? qp : 4ull * t.M);
+      const uint32_t o0 = c.ack & 1u, o1 = (c.ack >> 1) & 1u, o2 = o0 ^ o1, X = 2, Y = 3;
+      auto sym = [&](uint32_t a, uint32_t b) {   // [a b x x ...]
+        uint32_t w = a | (b << 2);
+        for (uint32_t k = 2; k < c.Qm; k++) w |= X << (2 * k);
+        return w;
+      };
+      if (c.ack_len == 1) {
+        t.ack_nblk = 1;
+        t.ack_sym[0] = sym(o0, Y);
+      } else {
+        t.ack_nblk = 3;
+        t.ack_sym[0] = sym(o0, o1);
+        t.ack_sym[1] = sym(o2, o0);
+        t.ack_sym[2] = sym(o1, o2);
+      }
     }
     if (byte0 != c.tbs / 8 + 3 || sym != 12 * t.M) {
       set_error("UL planner: segmentation / rate-matching bookkeeping");

@@ -8,8 +8,8 @@
  *              srslte_ue_ul_cfg_grant(&ue_ul, grant, tti + 4, rv, tx_nb) (:551),
  *              srslte_ue_ul_pusch_encode_rnti_softbuffer(.., payload, uci_data, softbuffer, rnti, signal) (:555)
  * Input file : int32 hdr[8] = {cell_id, nof_prb, ntx, group_hopping, sequence_hopping, delta_ss, cyclic_shift,
- *              flags (1 = normalisation, 2 = CFO)} + float cfo; per transmission int32 p[10] = {tti, rnti, rv,
- *              use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data} + int32 dci_nof_bits + 64 DCI bit bytes +
+ *              flags (1 = normalisation, 2 = CFO, bits 8-11 = I_offset_ack)} + float cfo; per transmission int32
+ *              p[12] = {tti, rnti, rv, use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len, ack} + int32 dci_nof_bits + 64 DCI bit bytes +
  *              tbs/8 payload bytes (pass_data = 0: the payload pointer is NULL -- a retransmission from the
  *              softbuffer).
  * Output file: per transmission int32 r[6] = {ret, n_prb, L_prb, tbs, Qm, ncs_dmrs} + SF_LEN cf32 samples.
@@ -48,6 +48,7 @@ int main(int argc, char **argv) {
   memset(&srs_cfg, 0, sizeof(srs_cfg)); memset(&pucch_cfg, 0, sizeof(pucch_cfg));
   memset(&pucch_sched, 0, sizeof(pucch_sched)); memset(&uci_cfg, 0, sizeof(uci_cfg));
   memset(&power_ctrl, 0, sizeof(power_ctrl));
+  uci_cfg.I_offset_ack = (uint32_t)(hdr[7] >> 8) & 15u;
   dmrs_cfg.group_hopping_en = hdr[3] != 0;
   dmrs_cfg.sequence_hopping_en = hdr[4] != 0;
   dmrs_cfg.delta_ss = (uint32_t)hdr[5];
@@ -60,10 +61,10 @@ int main(int argc, char **argv) {
   cf_t *signal = (cf_t *)srslte_vec_malloc(sflen * sizeof(cf_t));
   uint8_t *payload = (uint8_t *)malloc(12288);
   for (int i = 0; i < hdr[2]; i++) {
-    int32_t p[10], nbits;
+    int32_t p[12], nbits;
     srslte_dci_msg_t dci_msg;
     memset(&dci_msg, 0, sizeof(dci_msg));
-    if (fread(p, 4, 10, fi) != 10 || fread(&nbits, 4, 1, fi) != 1 || fread(dci_msg.data, 1, 64, fi) != 64) return 4;
+    if (fread(p, 4, 12, fi) != 12 || fread(&nbits, 4, 1, fi) != 1 || fread(dci_msg.data, 1, 64, fi) != 64) return 4;
     if (fread(payload, 1, (size_t)p[6] / 8, fi) != (size_t)p[6] / 8) return 4;
     dci_msg.nof_bits = (uint32_t)nbits;
     srslte_ue_ul_set_rnti(&ue_ul, (uint16_t)p[1]);
@@ -85,6 +86,8 @@ int main(int argc, char **argv) {
     if (!ret) ret = srslte_ue_ul_cfg_grant(&ue_ul, &grant, (uint32_t)p[0], (uint32_t)p[2], 0) ? -2 : 0;
     srslte_uci_data_t uci_data;
     memset(&uci_data, 0, sizeof(uci_data));
+    uci_data.uci_ack_len = (uint32_t)p[10];   /* phch_worker.cc:486-487 */
+    uci_data.uci_ack = (uint8_t)p[11];
     memset(signal, 0, sflen * sizeof(cf_t));
     if (!ret)
       ret = srslte_ue_ul_pusch_encode_rnti_softbuffer(&ue_ul, p[9] ? payload : NULL, uci_data, &softbuffer,

@@ -151,6 +151,8 @@ def lib():
             "or_pusch_grid": (C.c_int, [C.POINTER(UlCfg), u8, f32]),
             "or_scfdma_tx": (C.c_int, [C.c_uint32, f32, f32]),
             "or_pusch_encode": (C.c_int, [C.POINTER(UlCfg), u8, f32]),
+            "or_ack_qprime": (C.c_uint32, [C.POINTER(UlCfg)]),
+            "or_ack_block": (C.c_uint32, [C.POINTER(UlCfg), u8]),
             "or_tx_subframe": (C.c_int, [C.POINTER(TxCfg), u8, f32, C.POINTER(C.c_uint32)]),
             "or_ofdm_rx": (C.c_int, [C.POINTER(Cell), f32, f32]),
             "or_chest": (C.c_int, [C.POINTER(Cell), C.c_uint32, f32, f32, f32]),
@@ -210,12 +212,13 @@ class tdec_mode:
 
 class UlCfg(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "sf_idx", "rnti", "n_prb", "L_prb", "tbs", "Qm", "rv",
-                                          "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2")]
+                                          "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2",
+                                          "ack_len", "ack", "I_offset_ack")]
 
 
 def ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=0, Qm=4, rv=0, gh=0, sh=0, dss=0,
-           cs=0, n2=0):
-    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2)
+           cs=0, n2=0, ack_len=0, ack=0, ioff=0):
+    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2, ack_len, ack, ioff)
 
 
 class PssRes(C.Structure):

@@ -32,9 +32,9 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
             f.write(struct.pack("f", cfo))
             for t in txs:
                 dci = t.get("dci")
-                f.write(struct.pack("10i", t["tti"], t["rnti"], t["rv"], int(dci is not None), t.get("n_prb", 0),
+                f.write(struct.pack("12i", t["tti"], t["rnti"], t["rv"], int(dci is not None), t.get("n_prb", 0),
                                     t.get("L_prb", 0), t["tbs"], t.get("Qm", 0), t.get("ncs", 0),
-                                    int(t.get("pass_data", True))))
+                                    int(t.get("pass_data", True)), t.get("ack_len", 0), t.get("ack", 0)))
                 f.write(struct.pack("i", dci.nof_bits if dci else 0))
                 f.write(bytes(dci.data) if dci else bytes(64))
                 f.write(np.ascontiguousarray(t["tb"], np.uint8).tobytes())
@@ -50,10 +50,11 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
     return out
 
 
-def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None):
+def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None, ioff=0):
     c = O.ul_cfg(cell_id=cell_id, nof_prb=nof_prb, sf_idx=sf, rnti=t["rnti"], n_prb=t.get("n_prb", 0) if n_prb is None else n_prb,
                  L_prb=t.get("L_prb") if L is None else L, tbs=t["tbs"], Qm=t.get("Qm") if Qm is None else Qm,
-                 rv=t["rv"], gh=dmrs[0], sh=dmrs[1], dss=dmrs[2], cs=dmrs[3], n2=t.get("ncs", 0) if ncs is None else ncs)
+                 rv=t["rv"], gh=dmrs[0], sh=dmrs[1], dss=dmrs[2], cs=dmrs[3], n2=t.get("ncs", 0) if ncs is None else ncs,
+                 ack_len=t.get("ack_len", 0), ack=t.get("ack", 0), ioff=ioff)
     iq = np.zeros(2 * 15 * NFFT[nof_prb], np.float32)
     assert O.lib().or_pusch_encode(ctypes.byref(c), t["tb"], iq) == 0
     return iq
@@ -115,3 +116,17 @@ def test_retransmission_without_stored_tb_is_rejected():
     txs = [dict(tti=5, rnti=0x46, rv=0, n_prb=0, L_prb=25, tbs=T, Qm=2, ncs=0, tb=tb(5, T), pass_data=False)]
     (r, _), = run(3, 25, txs)       # nothing stored in the fresh softbuffer and no data: error
     assert r[0] == -3
+
+
+@pytest.mark.parametrize("ack", [0, 1])
+def test_harq_ack_on_pusch_srsue_call_order(ack):
+    """srsUE multiplexes the DL HARQ-ACK into the PUSCH when both fall in one TTI (uci_ack_len = 1,
+    phch_worker.cc:486-487, 555): the encoded subframe matches the oracle's ACK multiplexing (36.212
+    5.2.2.6 / 5.2.2.8, beta_offset index 6 from set_cfg's uci_cfg)."""
+    txs = [dict(tti=12, rnti=0x46, rv=0, n_prb=0, L_prb=25, tbs=5736, Qm=2, ncs=0, tb=tb(6, 5736), ack_len=1, ack=ack),
+           dict(tti=16, rnti=0x46, rv=0, n_prb=0, L_prb=50, tbs=12216, Qm=4, ncs=1, tb=tb(7, 12216), ack_len=1,
+                ack=1 - ack)]
+    res = run(9, 50, txs, flags=6 << 8)
+    for t, (r, iq) in zip(txs, res):
+        assert r[0] == 0
+        assert rel_err(iq, oracle_iq(9, 50, t, t["tti"] % 10, ioff=6)) < TOL

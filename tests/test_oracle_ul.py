@@ -150,3 +150,60 @@ def test_pusch_end_to_end_symbols(nprb, n_prb, L, Qm):
             d = np.fft.ifft(row) * np.sqrt(M)
             assert np.max(np.abs(d - x[ds])) < 1e-4
             ds += 1
+
+
+BETA8_ACK = [16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160, 248, 400, 640, 1008]   # 36.213 Table 8.6.3-1 x 8
+
+
+@pytest.mark.parametrize("L,Qm,tbs,alen,ack,ioff", [(6, 2, 1000, 1, 1, 0), (6, 4, 2000, 1, 0, 5), (3, 6, 1800, 2, 2, 9),
+                                                    (25, 4, 8000, 2, 3, 14), (10, 2, 600, 2, 1, 12)])
+def test_harq_ack_on_pusch_independent(L, Qm, tbs, alen, ack, ioff):
+    """HARQ-ACK multiplexing (36.212 5.2.2.6 encoding + Q'_ACK, 5.2.2.8 insertion from the last row up in
+    columns 2, 9, 8, 3, 36.211 5.3.1 placeholders x -> 1, y -> previous scrambled bit), restated in numpy
+    from the specification text against or_pusch_mod; the data still decodes through the DL-SCH decoder
+    with the punctured positions erased."""
+    c = cfg(L_prb=L, Qm=Qm, tbs=tbs, cell_id=77, sf_idx=3, rnti=0x1B2, ack_len=alen, ack=ack, ioff=ioff)
+    M, G = 12 * L, O.lib().or_pusch_G(C.byref(c))
+    s = O.cbsegm(tbs)
+    sumK = s.Cm * s.Km + (s.C - s.Cm) * s.Kp
+    qp = min(-(-alen * M * 12 * BETA8_ACK[ioff] // (8 * sumK)), 4 * M)
+    assert O.lib().or_ack_qprime(C.byref(c)) == qp and qp > 0
+    o0, o1 = ack & 1, (ack >> 1) & 1
+    X, Y = 2, 3
+    if alen == 1:
+        blk = [o0, Y] + [X] * (Qm - 2)
+    else:
+        o2 = o0 ^ o1
+        blk = sum(([a, b] + [X] * (Qm - 2) for a, b in ((o0, o1), (o2, o0), (o1, o2))), [])
+    f = np.random.default_rng(5).integers(0, 2, G).astype(np.uint8)
+    h = f.reshape(M, 12, Qm).transpose(1, 0, 2).copy()          # [column l][row m][bit]
+    q = [blk[k % len(blk)] for k in range(qp * Qm)]
+    cols, j = [2, 3, 8, 9], 0
+    for i in range(qp):
+        h[cols[j], M - 1 - i // 4, :] = q[i * Qm:(i + 1) * Qm]
+        j = (j + 3) % 4
+    h = h.reshape(-1).astype(np.int64)
+    cs = gold((0x1B2 << 14) | (3 << 9) | 77, G)
+    for i in range(G):
+        h[i] = 1 if h[i] == X else h[i - 1] if h[i] == Y else h[i] ^ cs[i]
+    want = np.array([pam(h[t * Qm:(t + 1) * Qm:2], Qm) + 1j * pam(h[t * Qm + 1:(t + 1) * Qm:2], Qm)
+                     for t in range(G // Qm)])
+    x = np.zeros(2 * G // Qm, np.float32)
+    O.lib().or_pusch_mod(C.byref(c), f, x)
+    assert np.max(np.abs((x[0::2] + 1j * x[1::2]) - want)) < 1e-6
+    # data decodes with the ACK-punctured symbols erased (rate ~ 1/3 or lower)
+    tb = tb_of(L, tbs)
+    assert O.lib().or_ulsch_encode(C.byref(c), tb, f) == G
+    llr = (2.0 * f.astype(np.float32) - 1.0) * 8.0
+    mask = np.zeros((12, M), bool)
+    j = 0
+    for i in range(qp):
+        mask[cols[j], M - 1 - i // 4] = True
+        j = (j + 3) % 4
+    llr.reshape(M, 12, Qm)[mask.T] = 0.0
+    ncb = O.lib().or_ncb(s.Kp)
+    sb = np.zeros(s.C * ncb, np.float32)
+    pay = np.zeros(tbs // 8, np.uint8)
+    noi, cbok = C.c_uint32(), C.c_uint32()
+    rc = O.lib().or_dlsch_decode(llr, G, tbs, Qm, 1, 0, 1, sb, ncb, 4, pay, C.byref(noi), C.byref(cbok))
+    assert rc == 0 and np.array_equal(pay, tb)
