@@ -25,7 +25,8 @@ CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [
     (15, 0, 15, 4008, 6, 0, 2, 12, 0, 0, 0, 0, 2),       # 3 MHz, N = 256
     (100, 0, 100, 43816, 4, 0, 3, 1, 0, 0, 0, 0, 0, 1, 1, 5),    # HARQ-ACK on PUSCH: 1 bit (ACK)
     (25, 2, 20, 3000, 2, 1, 8, 4, 1, 0, 0, 2, 1, 2, 2, 12),      # 2 ACK bits, QPSK, rv 1, hopping
-    (50, 0, 45, 9000, 6, 0, 6, 5, 0, 1, 0, 0, 4, 1, 0, 14),      # NACK, 64QAM, Q'_ACK capped at 4 M
+    (50, 0, 45, 9000, 6, 0, 6, 5, 0, 1, 0, 0, 4, 1, 0, 14),      # NACK, 64QAM, largest beta_offset
+    (25, 0, 3, 104, 2, 0, 2, 9, 0, 0, 0, 0, 0, 2, 3, 14),        # Q'_ACK capped at 4 M (tiny TB), filler bits
 ]
 
 
