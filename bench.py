@@ -216,9 +216,14 @@ def config_cfgs(config, B, first):
     return cfgs
 
 
-def tdec_kernel_name(win):
-    return ("tdec_win_kernel (max-log-MAP turbo, one workgroup per code block)" if win
-            else "tdec_kernel (max-log-MAP turbo, one code block per lane)")
+SCHED_DESC = {"win": "latency form", "lanex": "lane per code block, crossed (2 wavefronts per group)",
+              "lane": "lane per code block"}
+
+
+def tdec_kernel_name(sched):
+    return {"win": "tdec_win_kernel (max-log-MAP turbo, one workgroup per code block)",
+            "lanex": "tdec_kernel_*x (max-log-MAP turbo, one code block per lane, crossed schedule)"}.get(
+        sched, "tdec_kernel (max-log-MAP turbo, one code block per lane)")
 
 
 def dtype_of(args):
@@ -266,9 +271,9 @@ def bench_codeblocks(args, world, rank, dev):
            "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
                                   f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
                       "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec,
-                      "turbo_schedule": "latency form" if tb.turbo_win else "lane per code block"},
+                      "turbo_schedule": SCHED_DESC[tb.turbo_sched]},
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
-           "roofline": {"kernel": tdec_kernel_name(tb.turbo_win), "bound": "hbm", "achieved": round(ach, 2),
+           "roofline": {"kernel": tdec_kernel_name(tb.turbo_sched), "bound": "hbm", "achieved": round(ach, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                         "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(stage["tdec"], 4),
                         "launches_averaged": nprof}}
@@ -512,7 +517,7 @@ def main():
                     help="also time the UL PUSCH transmitter (SURVEY 8f-4) on as many subframes; reported beside value")
     ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
                     help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
-    ap.add_argument("--sched", choices=("auto", "win", "lane"), default="auto",
+    ap.add_argument("--sched", choices=("auto", "win", "lane", "lanex"), default="auto",
                     help="int16 turbo schedule: latency form (one workgroup per code block, exact trellis segments), "
                          "one code block per lane, or auto (latency form up to 1024 code blocks)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
@@ -613,13 +618,13 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
-                       "max_its": args.max_its, "turbo_schedule": "latency form" if batch.turbo_win else "lane per code block",
+                       "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
             "payload_spot_mismatches": bad,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
-            "roofline": {"kernel": tdec_kernel_name(batch.turbo_win), "bound": "hbm", "achieved": round(achieved, 2),
+            "roofline": {"kernel": tdec_kernel_name(batch.turbo_sched), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": tdec_bytes,

@@ -70,6 +70,12 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * same arithmetic, demap_body.h) and the LLR stream is never written.  Runs of RM without DEMAP read the
  * LLR buffer (e.g. uploaded by the caller). */
 #define MI_DL_FLAG_KEEP_LLR  64u
+/* Lane-per-code-block turbo decoder in the crossed schedule: two wavefronts per 64-code-block group, the
+ * forward and backward recursions of each half-iteration run concurrently and meet in the middle
+ * (bit-identical outputs, tdec_body.h).  Without MI_DL_FLAG_TDEC_X / MI_DL_FLAG_TDEC_LANE the lane form
+ * is crossed when the batch has fewer than 2 groups per SIMD; MI_DL_FLAG_TDEC_LANE alone = one
+ * wavefront per group. */
+#define MI_DL_FLAG_TDEC_X    128u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 
@@ -102,7 +108,8 @@ void   mi_dl_batch_profile_reset(mi_dl_batch_t *b);
 /* Algorithmic HBM bytes of one run (SURVEY.md 8d definitions) */
 double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = compulsory total */);
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
-/* 1 when the batch's turbo stage runs the latency form (MI_DL_FLAG_TDEC_WIN rules), else 0 */
+/* turbo schedule of the batch: 1 = latency form (MI_DL_FLAG_TDEC_WIN rules), 2 = lane per code block in
+ * the crossed schedule (two wavefronts per group), 0 = lane per code block, one wavefront per group */
 int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 

@@ -22,7 +22,8 @@ FLAG_TDEC_GEN = 4   # float srsLTE-gen turbo arithmetic
 FLAG_IQ_SC16 = 8    # IQ input as UHD sc16 (int16 I/Q, fc32 = sc16 / 32768)
 FLAG_TDEC_WIN = 16  # int16 turbo: force the latency form (one workgroup per code block)
 FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wavefronts
-SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE}
+FLAG_TDEC_X = 128  # lane-per-code-block decoder, crossed schedule (two wavefronts per group)
+SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X}
 FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
 
 
@@ -152,6 +153,8 @@ def emu():
                                      C.c_void_p, C.c_void_p]
         E.emu_set_tdec_i16.restype = None
         E.emu_set_tdec_i16.argtypes = [C.c_int]
+        E.emu_set_tdec_x.restype = None
+        E.emu_set_tdec_x.argtypes = [C.c_int]
         E.emu_payload_offset.restype = C.c_size_t
         E.emu_payload_offset.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _emu = E
@@ -262,7 +265,12 @@ class Batch:
     @property
     def turbo_win(self):
         """True when the turbo stage runs the latency form (one workgroup per code block)."""
-        return bool(lib().mi_dl_batch_turbo_win(self.h))
+        return lib().mi_dl_batch_turbo_win(self.h) == 1
+
+    @property
+    def turbo_sched(self):
+        """'win' (latency form), 'lanex' (lane per code block, two wavefronts per group) or 'lane'"""
+        return {1: "win", 2: "lanex"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
 
     @property
     def n_groups(self):
@@ -521,7 +529,11 @@ class TdecBatch:
 
     @property
     def turbo_win(self):
-        return bool(lib().mi_tdec_turbo_win(self.h))
+        return lib().mi_tdec_turbo_win(self.h) == 1
+
+    @property
+    def turbo_sched(self):
+        return {1: "win", 2: "lanex"}.get(lib().mi_tdec_turbo_win(self.h), "lane")
 
     def close(self):
         if self.h:

@@ -20,6 +20,17 @@ extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 
 static uint32_t crc8[256];
 
+// crossed-schedule lane decoder (two wavefronts per group, tdec_body.h tdec_lane_x): 0 = off
+static int g_x = 0;
+extern "C" void emu_set_tdec_x(int on) { g_x = on; }
+template <bool Q16>
+static mi::TdecLaneResult emu_lane_x(const mi::TdecArgs& a, int lane) {
+  mi::TdecExecHost ex;
+  mi::TdecLaneResult r = mi::tdec_lane_x<Q16>(a, lane, ex);
+  r.tb_part = mi::tdec_pack(a, lane);
+  return r;
+}
+
 // latency-form (segment-parallel) int16 decoder: threads per code block, 0 = off (tdec_win_body.h).
 // Each phase of the GPU kernel (between two barriers) runs every segment in turn: within a phase a
 // segment only reads what earlier phases wrote, so this reproduces the kernel exactly.
@@ -123,6 +134,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       a.cb_bytes = &cbb[(size_t)li * mi::CB_BYTES_STRIDE];
       a.K = g.K; a.F = ld.F; a.max_its = max_its; a.early_stop = 1; a.crc24a = ld.crc24a;
       mi::TdecLaneResult r = g_win && g_q16 ? emu_win_cb(g, kt, ld, sbg, P.kdata.data(), lane, max_its, a.cb_bytes)
+                           : g_x ? (g_q16 ? emu_lane_x<true>(a, lane) : emu_lane_x<false>(a, lane))
                            : g_q16 ? mi::tdec_lane<true>(a, lane) : mi::tdec_lane<false>(a, lane);
       cits[li] = r.its;
       ccrc[li] = r.crc_ok;

@@ -213,6 +213,24 @@ bool Engine::use_win() const {
   return plan.n_cb <= MI_TDEC_WIN_AUTO_CBS;
 }
 
+// lane-per-code-block decoder in the crossed schedule (two wavefronts per group, tdec_body.h)
+// Auto: when the batch has fewer than 2 groups per SIMD (a single wavefront per group leaves the SIMDs
+// latency-bound: configs[0] +29 %, configs[2] +54 %); at the headline's 2.5 groups per SIMD the memory
+// system is the limit and the single-wave form is 3 % faster (profiles/r1/ab_x).
+bool Engine::tdec_crossed() const {
+  if (flags & MI_DL_FLAG_TDEC_X) return true;
+  if (flags & MI_DL_FLAG_TDEC_LANE) return false;
+  if (const char* e = getenv("MI_TDEC_X")) return atoi(e) != 0;   // A/B
+  static uint32_t simds = 0;
+  if (!simds) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    simds = 4u * (uint32_t)cus;
+  }
+  return plan.groups.size() < 2ull * simds;
+}
+
 // turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts
 void Engine::launch_turbo(float* sb, hipStream_t st) {
   const Plan& P = plan;
@@ -233,7 +251,7 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
   launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
               d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(),
-              max_its, early_stop, q16(), st);
+              max_its, early_stop, q16(), tdec_crossed(), st);
 }
 
 int Engine::stage_ms(float* ms, uint32_t* nruns) {

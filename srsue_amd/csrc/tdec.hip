@@ -13,7 +13,24 @@ struct TdecOut {            // per code block (lane index li) results
   uint32_t* tb_part;        // partial TB-CRC24A register (tb_kernel combines them)
 };
 
-template <bool Q16>
+// crossed schedule (tdec_body.h tdec_lane_x): wave 0 = F, wave 1 = B of the same 64 code blocks
+struct TdecExecGpu {
+  static constexpr bool SHARED = true;
+  int wave;
+  uint32_t* xcrc;   // LDS [2][64] partial CB-CRC registers
+  template <class F, class B>
+  __device__ void run(F f, B b) {
+    if (wave == 0) f(); else b();
+    __syncthreads();
+  }
+  __device__ uint32_t crc_combine(uint32_t v, int lane) {
+    xcrc[wave * LANES + lane] = v;
+    __syncthreads();
+    return v ^ xcrc[(wave ^ 1) * LANES + lane];
+  }
+};
+
+template <bool Q16, bool X>
 __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const uint32_t* __restrict__ wm,
                                            float* __restrict__ scratch, uint8_t* __restrict__ dec, const TdecOut& out,
                                            const MiGroupDesc* __restrict__ groups,
@@ -22,11 +39,12 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const u
                                            uint32_t early_stop) {
   // CRC24A byte table in LDS (one entry per lane group of 4), for the TB-CRC partial of each lane
   __shared__ uint32_t crc8[256];
-  for (uint32_t b = threadIdx.x; b < 256; b += 64) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+  __shared__ uint32_t xcrc[X ? 2 * LANES : 1];
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
   __syncthreads();
   const MiGroupDesc g = groups[blockIdx.x];
   const MiKTab kt = ktabs[g.ktab];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x % LANES;
   const uint32_t li = g.lane0 + lane;
   const MiLaneDesc ld = lanes[li];
   if (!ld.valid) return;
@@ -48,10 +66,20 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const u
   a.max_its = max_its;
   a.early_stop = early_stop;
   a.crc24a = ld.crc24a;
-  const TdecLaneResult r = tdec_lane<Q16>(a, lane);
-  out.its[li] = r.its;
-  out.crc_ok[li] = r.crc_ok;
-  out.tb_part[li] = r.tb_part;
+  if constexpr (X) {
+    TdecExecGpu ex{(int)(threadIdx.x / LANES), xcrc};
+    TdecLaneResult r = tdec_lane_x<Q16>(a, lane, ex);
+    __syncthreads();   // wave B's decisions are visible to wave F, which packs them
+    if (ex.wave) return;
+    out.its[li] = r.its;
+    out.crc_ok[li] = r.crc_ok;
+    out.tb_part[li] = tdec_pack(a, lane);
+  } else {
+    const TdecLaneResult r = tdec_lane<Q16>(a, lane);
+    out.its[li] = r.its;
+    out.crc_ok[li] = r.crc_ok;
+    out.tb_part[li] = r.tb_part;
+  }
 }
 
 // window masks of the sparse softbuffer rows: one thread per 4-step window (12 decoder inputs) of a
@@ -81,7 +109,7 @@ __global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ 
                                                      const MiLaneDesc* __restrict__ lanes,
                                                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata,
                                                      uint32_t max_its, uint32_t early_stop) {
-  tdec_group<false>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<false, false>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 // int16 decoder: held to MI_TDEC_I16_WAVES waves per SIMD (3: <= 168 VGPRs), enough to keep every
 // group of a 12,500-subframe batch resident (2,540 waves on 1,024 SIMDs)
@@ -93,15 +121,44 @@ void tdec_kernel_i16(const float* __restrict__ sb, const uint32_t* __restrict__ 
                      const MiGroupDesc* __restrict__ groups, const MiLaneDesc* __restrict__ lanes,
                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata, uint32_t max_its,
                      uint32_t early_stop) {
-  tdec_group<true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+  tdec_group<true, false>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
+// crossed schedule: two wavefronts per group (same register budget per wave)
+__global__ __launch_bounds__(128) void tdec_kernel_genx(const float* __restrict__ sb, const uint32_t* __restrict__ wm,
+                                                       float* __restrict__ scratch, uint8_t* __restrict__ dec,
+                                                       TdecOut out, const MiGroupDesc* __restrict__ groups,
+                                                       const MiLaneDesc* __restrict__ lanes,
+                                                       const MiKTab* __restrict__ ktabs,
+                                                       const uint32_t* __restrict__ kdata, uint32_t max_its,
+                                                       uint32_t early_stop) {
+  tdec_group<false, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
+#ifndef MI_TDEC_X_WAVES
+#define MI_TDEC_X_WAVES 4
+#endif
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_X_WAVES)))
+void tdec_kernel_i16x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
+                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
+                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
+                      const uint32_t* __restrict__ kdata, uint32_t max_its, uint32_t early_stop) {
+  tdec_group<true, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,
-                 hipStream_t st) {
+                 bool crossed, hipStream_t st) {
   if (!n_groups) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  if (crossed) {
+    if (q16)
+      hipLaunchKernelGGL(tdec_kernel_i16x, dim3(n_groups), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,
+                         ktabs, ktab_data, max_its, early_stop);
+    else
+      hipLaunchKernelGGL(tdec_kernel_genx, dim3(n_groups), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,
+                         ktabs, ktab_data, max_its, early_stop);
+    return;
+  }
   if (q16)
     hipLaunchKernelGGL(tdec_kernel_i16, dim3(n_groups), dim3(64), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
                        ktab_data, max_its, early_stop);

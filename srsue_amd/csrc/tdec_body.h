@@ -573,6 +573,326 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   }
 }
 
+// ---- crossed schedule: two wavefronts per group --------------------------------------------------
+// The lane-per-code-block kernel runs ~2.5 wavefronts per SIMD at the headline batch (2,540 groups on
+// 1,024 SIMDs) and is latency-bound: each wave walks 4 K dependent trellis steps per iteration.  The
+// crossed schedule gives every group a second wavefront on the same 64 code blocks and splits each
+// half-iteration at the middle window h = K / 8 (windows of BETA_W steps, nw = K / 4 of them):
+//   phase 1  wave F: alpha over windows 0 .. h-1 (no outputs), alpha checkpoints in slots 1 .. h-1
+//            wave B: tail + beta over windows nw-1 .. h, beta checkpoints in slots h+1 .. nw
+//   phase 2  wave F: the usual forward pass over windows h .. nw-1 (beta recomputed per window from
+//            the checkpoints wave B left), LLRs of steps K/2 .. K-1
+//            wave B: backward over windows h-1 .. 0, alpha recomputed per window from wave F's
+//            checkpoints, LLRs of steps 0 .. K/2-1
+// Both recursions stay exact full-length recursions (only the traversal order changes) and every LLR
+// is computed from the same alpha_k, beta_{k+1} and branch metrics with the same operations, so
+// outputs are bit-identical to tdec_lane's (and the oracle's).  Alpha and beta checkpoints occupy
+// disjoint slots of the one checkpoint stream (alpha_k for k >= 4 has every state reachable: no -inf
+// is stored), and the phases only exchange data through checkpoints, so one barrier per phase orders
+// them; within a phase the two waves write disjoint rows (steps k < K/2 vs k >= K/2, and pi is a
+// permutation for the DEC2 rows).  The host emulation runs the phases of both waves in turn.
+
+// the alpha update of alpha_step without the LLR (identical operations)
+template <bool NORM = true>
+MI_HD inline void alpha_fwd(float (&al)[8], float xs, float xp) {
+  const float luz = xs + xp;
+  float c[8][2];
+#pragma unroll
+  for (int s = 0; s < 8; s++)
+#pragma unroll
+    for (int u = 0; u < 2; u++) c[s][u] = al[s] + gam(u, tr_par(s, u), xs, xp, luz);
+  float na[8];
+#pragma unroll
+  for (int sp = 0; sp < 8; sp++)
+    na[sp] = fmaxf(c[tr_prev_s(sp, 0)][tr_prev_u(sp, 0)], c[tr_prev_s(sp, 1)][tr_prev_u(sp, 1)]);
+  if constexpr (NORM) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) al[s] = na[s] - na[0];
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; s++) al[s] = na[s];
+  }
+}
+// the LLR of alpha_step without the alpha update (identical operations)
+MI_HD inline float llr_step(const float (&al)[8], const float (&bn)[8], float xs, float xp) {
+  const float luz = xs + xp;
+  float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const float t = (al[s] + gam(u, tr_par(s, u), xs, xp, luz)) + bn[tr_next(s, u)];
+      if (u) m1 = fmaxf(m1, t); else m0 = fmaxf(m0, t);
+    }
+  }
+  return m1 - m0;
+}
+
+// phase-1 window of wave F: alpha only (regular inputs, or the q-creating first pass)
+template <bool DEC2, bool Q16, bool SQ>
+MI_HD inline void tdec_alpha_only_window(const TdecWin<Q16>& w, uint32_t base, uint32_t F, float (&al)[8]) {
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    float xs, xp;
+    tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, F, xs, xp);
+    alpha_fwd<!Q16>(al, xs, xp);
+  }
+  norm8<Q16>(al);
+}
+template <bool Q16>
+MI_HD inline void tdec_alpha_only_window_mkq(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+                                             float (&al)[8]) {
+  constexpr float FILL = -I16_CI;
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    const float q0 = q16f(w.f0[i]), q1 = q16f(w.f1[i]), q2 = q16f(w.f2[i]);
+    row_st(a.q16, 3 * base, lane, (int16_t)q0, 3 * i);
+    row_st(a.q16, 3 * base, lane, (int16_t)q1, 3 * i + 1);
+    row_st(a.q16, 3 * base, lane, (int16_t)q2, 3 * i + 2);
+    const bool fill = base + i < a.F;
+    alpha_fwd<!Q16>(al, (fill ? FILL : q0) + scr_cvt<Q16>(w.r0[i]), fill ? FILL : q1);
+  }
+  norm8<Q16>(al);
+}
+
+// phase-2 window of wave B: alpha of the window recomputed from its opening checkpoint (window 0:
+// the known start state), then backward steps emitting the LLRs (beta carried in b)
+template <bool DEC2, bool Q16, bool SQ>
+MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+                                        float (&b)[8], TdecCrc& crc) {
+  float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
+  float aw[BETA_W][8];
+  aw[0][0] = 0.0f;
+#pragma unroll
+  for (int s = 1; s < 8; s++) aw[0][s] = base ? scr_cvt<Q16>(w.ck[s - 1]) : -INFINITY;
+#pragma unroll
+  for (int i = 0; i < BETA_W - 1; i++) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) aw[i + 1][s] = aw[i][s];
+    alpha_fwd<!Q16>(aw[i + 1], xs[i], xp[i]);
+  }
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    tdec_emit<DEC2, Q16>(a, lane, base, i, llr_step(aw[i], b, xs[i], xp[i]), xs[i], w, crc);
+    float nb[8];
+    beta_step<!Q16>(b, xs[i], xp[i], nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+  norm8<Q16>(b);
+}
+
+// software-pipelined walk over n windows widx(0), widx(1), ...: PF = 1 ping-pong buffers (loads one
+// window ahead), PF = 2 three rotating buffers (two ahead); the last rounds reload the last window
+// (harmless)
+template <int PF, class Win, class Idx, class Load, class Run>
+MI_HD inline void pipe_windows(int n, Idx widx, Load load, Run run) {
+  if (n <= 0) return;
+  auto at = [&](int i) { return widx(i < n ? i : n - 1); };
+  if constexpr (PF >= 2) {
+    Win A, B, C;
+    load(at(0), A);
+    load(at(1), B);
+    for (int i = 0;; i += 3) {
+      load(at(i + 2), C);
+      run(A, at(i));
+      if (i + 1 >= n) break;
+      load(at(i + 3), A);
+      run(B, at(i + 1));
+      if (i + 2 >= n) break;
+      load(at(i + 4), B);
+      run(C, at(i + 2));
+      if (i + 3 >= n) break;
+    }
+  } else {
+    Win A, B;
+    load(at(0), A);
+    for (int i = 0;; i += 2) {
+      load(at(i + 1), B);
+      run(A, at(i));
+      if (i + 1 >= n) break;
+      load(at(i + 2), A);
+      run(B, at(i + 1));
+      if (i + 2 >= n) break;
+    }
+  }
+}
+
+// pipelining depth of the crossed schedule's q-row passes (twice the waves hide more latency, and the
+// three-buffer rotation spills at the 128-VGPR budget of 4 waves per SIMD)
+#ifndef MI_TDEC_XPF_Q
+#define MI_TDEC_XPF_Q 1
+#endif
+// the four phase bodies of one constituent decoder (same source modes as tdec_half)
+template <bool DEC2, bool FIRST, bool Q16, int SRC>
+struct TdecX {
+  static constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;
+  static constexpr bool SQB = Q16 && SRC == SRC_Q;
+  static constexpr bool SQF = Q16 && SRC != SRC_SB;
+  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_XPF_Q;
+  using Win = TdecWin<Q16>;
+
+  MI_HD static void load1(const TdecArgs& a, int lane, uint32_t w, Win& r) {
+    if constexpr (MKQ) tdec_load_window_sb<FIRST, Q16>(a, lane, w * BETA_W, r);
+    else tdec_load_window<DEC2, FIRST, Q16, SQB>(a, lane, w * BETA_W, r);
+  }
+  // wave F, phase 1: alpha_0 .. alpha_{K/2}
+  MI_HD static void f1(const TdecArgs& a, int lane, float (&al)[8]) {
+    const uint32_t h = a.K / (2 * BETA_W);
+    const size_t ck = (size_t)2 * a.K;
+#pragma unroll
+    for (int s = 0; s < 8; s++) al[s] = s ? -INFINITY : 0.0f;
+    pipe_windows<PF, Win>(
+        (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
+        [&](const Win& r, uint32_t w) {
+          if (w) ck_store<Q16>(a.scr, ck, w, lane, al);
+          if constexpr (MKQ) tdec_alpha_only_window_mkq<Q16>(a, lane, r, w * BETA_W, al);
+          else tdec_alpha_only_window<DEC2, Q16, SQB>(r, w * BETA_W, a.F, al);
+        });
+  }
+  // wave F, phase 2: forward pass over windows h .. nw-1 (LLRs of steps K/2 .. K-1)
+  MI_HD static void f2(const TdecArgs& a, int lane, float (&al)[8], TdecCrc& crc) {
+    const uint32_t nw = a.K / BETA_W, h = nw / 2;
+    const size_t ck = (size_t)2 * a.K;
+    pipe_windows<PF, Win>(
+        (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
+        [&](uint32_t w, Win& r) {
+          tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
+          ck_load_raw<Q16>(a.scr, ck, w + 1, lane, r);
+        },
+        [&](const Win& r, uint32_t w) { tdec_alpha_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, al, crc); });
+  }
+  // wave B, phase 1: tail, then beta_{K} .. beta_{K/2}
+  MI_HD static void b1(const TdecArgs& a, int lane, float (&b)[8]) {
+    const uint32_t K = a.K, nw = K / BETA_W, h = nw / 2;
+    const size_t ck = (size_t)2 * K;
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = s ? -INFINITY : 0.0f;
+    {
+      const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0), tm = SQB ? 0u : wmask(a, nw);
+      float tx[3], tp[3];
+      if constexpr (MKQ) {
+        float tq[12];
+#pragma unroll
+        for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, 3 * K, j, lane));
+#pragma unroll
+        for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
+#pragma unroll
+        for (int j = 0; j < 3; j++) { tx[j] = tq[2 * j]; tp[j] = tq[2 * j + 1]; }
+      } else if constexpr (Q16 && !SQB) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          tx[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
+          tp[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
+          tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+        }
+      }
+#pragma unroll
+      for (int j = 2; j >= 0; j--) {
+        float nb[8];
+        beta_step<!Q16>(b, tx[j], tp[j], nb);
+#pragma unroll
+        for (int s = 0; s < 8; s++) b[s] = nb[s];
+      }
+      norm8<Q16>(b);
+    }
+    ck_store<Q16>(a.scr, ck, nw, lane, b);
+    pipe_windows<PF, Win>(
+        (int)(nw - h), [nw](int i) { return nw - 1 - (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
+        [&](const Win& r, uint32_t w) {
+          if constexpr (MKQ) tdec_beta_window_mkq<Q16>(a, lane, r, w * BETA_W, b);
+          else tdec_beta_window<DEC2, Q16, SQB>(r, w * BETA_W, a.F, b);
+          if (w > h) ck_store<Q16>(a.scr, ck, w, lane, b);
+        });
+  }
+  // wave B, phase 2: windows h-1 .. 0 backward (LLRs of steps 0 .. K/2-1)
+  MI_HD static void b2(const TdecArgs& a, int lane, float (&b)[8], TdecCrc& crc) {
+    const uint32_t h = a.K / (2 * BETA_W);
+    const size_t ck = (size_t)2 * a.K;
+    pipe_windows<PF, Win>(
+        (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
+        [&](uint32_t w, Win& r) {
+          tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
+          ck_load_raw<Q16>(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
+        },
+        [&](const Win& r, uint32_t w) { tdec_beta_emit_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, b, crc); });
+  }
+};
+
+// one half-iteration in the crossed schedule: ex.run(f, b) runs wave F's and wave B's phase body and
+// then orders them (GPU: each wave its own, then a workgroup barrier; host: both in turn)
+template <bool DEC2, bool FIRST, bool Q16, int SRC, class Exec>
+MI_HD inline void tdec_xhalf(const TdecArgs& a, int lane, Exec& ex, TdecCrc& cF, TdecCrc& cB) {
+  using X = TdecX<DEC2, FIRST, Q16, SRC>;
+  float mF[8], mBs[8];
+  float(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
+  ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
+  ex.run([&] { X::f2(a, lane, mF, cF); }, [&] { X::b2(a, lane, mB, cB); });
+}
+
+// the iteration loop of tdec_lane in the crossed schedule (same source-mode sequence); the code-block
+// CRC is the XOR of both waves' partial registers (ex.crc_combine), so both waves stop together
+template <bool Q16, class Exec>
+MI_HD inline TdecLaneResult tdec_lane_x(const TdecArgs& a, int lane, Exec& ex) {
+  TdecLaneResult r{0, 0, 0};
+  for (uint32_t it = 0; it < a.max_its; it++) {
+    TdecCrc cF{0}, cB{0};
+    constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;
+    if (it == 0) {
+      if (MK == 0) {
+        tdec_xhalf<false, true, Q16, SRC_MKQ>(a, lane, ex, cF, cB);
+        tdec_xhalf<true, true, Q16, SRC_Q>(a, lane, ex, cF, cB);
+      } else {
+        tdec_xhalf<false, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
+        tdec_xhalf<true, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
+      }
+    } else if (it < MK) {
+      tdec_xhalf<false, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
+    } else if (it == MK) {
+      tdec_xhalf<false, false, Q16, SRC_MKQ>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
+    } else {
+      tdec_xhalf<false, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
+    }
+    r.its = it + 1;
+    r.crc_ok = ex.crc_combine(cF.cb ^ cB.cb, lane) == 0;
+    if (a.early_stop && r.crc_ok) break;
+  }
+  return r;
+}
+
+// pack the final decisions MSB first; the bytes of the TB payload part (after filler, before the CB
+// CRC when C > 1) also run through a byte-wise CRC24A: the code block's partial TB-CRC register
+// (tb_kernel combines the partials, tb_body.h)
+MI_HD inline uint32_t tdec_pack(const TdecArgs& a, int lane) {
+  const uint32_t b0 = a.F / 8, b1 = a.K / 8 - (a.crc24a ? 0 : 3);
+  uint32_t tb = 0;
+  for (uint32_t j = 0; j < a.K / 8; j++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) v |= (uint32_t)row_ld(a.dec, 8 * j + q, lane) << (7 - q);
+    a.cb_bytes[j] = (uint8_t)v;
+    if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
+  }
+  return tb;
+}
+
+struct TdecExecHost {
+  static constexpr bool SHARED = false;
+  template <class F, class B>
+  void run(F f, B b) { f(); b(); }
+  uint32_t crc_combine(uint32_t v, int) { return v; }
+};
+
 template <bool Q16>
 MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0, 0};
@@ -601,19 +921,7 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
     r.crc_ok = crc.cb == 0;
     if (a.early_stop && r.crc_ok) break;
   }
-  // pack the final decisions MSB first; the bytes of the TB payload part (after filler, before the CB
-  // CRC when C > 1) also run through a byte-wise CRC24A: the code block's partial TB-CRC register
-  // (tb_kernel combines the partials, tb_body.h)
-  const uint32_t b0 = a.F / 8, b1 = a.K / 8 - (a.crc24a ? 0 : 3);
-  uint32_t tb = 0;
-  for (uint32_t j = 0; j < a.K / 8; j++) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) v |= (uint32_t)row_ld(a.dec, 8 * j + q, lane) << (7 - q);
-    a.cb_bytes[j] = (uint8_t)v;
-    if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
-  }
-  r.tb_part = tb;
+  r.tb_part = tdec_pack(a, lane);
   return r;
 }
 
