@@ -35,7 +35,10 @@ constexpr int TDEC_CK = MI_TDEC_CK;  // beta checkpoint spacing: BETA_W (one win
 constexpr int TDEC_CK_Q16 = MI_TDEC_CK_Q16;   // same for the int16 decoder (fewer VGPRs per value)
 constexpr int TDEC_CK_MIN = TDEC_CK < TDEC_CK_Q16 ? TDEC_CK : TDEC_CK_Q16;   // scratch sizing
 constexpr float FILLER_LLR = -10000.0f;
-constexpr int RM_CHUNK = 128;        // circular-buffer positions per rate-dematch workgroup
+#ifndef MI_RM_CHUNK
+#define MI_RM_CHUNK 128
+#endif
+constexpr int RM_CHUNK = MI_RM_CHUNK;  // circular-buffer positions per rate-dematch workgroup (64 or 128)
 constexpr int WM_STRIDE = KMAX / BETA_W + 4;   // turbo window masks per group (rowmask_kernel)
 
 __host__ __device__ inline int symbol_sz(uint32_t nof_prb) {

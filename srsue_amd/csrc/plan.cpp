@@ -228,6 +228,15 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     lane_src[li] = MiLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * cells[sd.cell].W, pd.re_off, pd.scr_off, pd.Qm,
                              pd.tm == 2 ? 1u : 0u, (uint32_t)(ld.e_off - sd.e_off), 0};
   }
+  unit_kind = 0;
+  bool mixed = false;
+  for (size_t li = 0; li < lanes.size(); li++) {
+    if (!lanes[li].valid) continue;
+    const uint32_t k = lane_src[li].qm + 8 * lane_src[li].tm2;
+    if (!unit_kind) unit_kind = k;
+    else if (k != unit_kind) mixed = true;
+  }
+  if (mixed) unit_kind = 0;
   // rank tables into kdata, patch lane offsets
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rank_off;
   for (size_t gi = 0; gi < groups.size(); gi++) {

@@ -23,6 +23,7 @@ struct Plan {
   std::vector<MiSfDesc> sfs;
   std::vector<MiLaneDesc> lanes;
   std::vector<MiLaneSrc> lane_src;        // per lane (same index): the fused demap's inputs
+  uint32_t unit_kind = 0;                 // Qm + 8 (TM2) shared by every valid lane, 0 = mixed
   std::vector<MiGroupDesc> groups;
   std::vector<MiKTab> ktabs;
   std::vector<uint32_t> kdata;

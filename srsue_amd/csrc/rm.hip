@@ -42,25 +42,58 @@ struct RmFuse {
 };
 
 // All LLRs of one demap unit (TM1: one RE, QM LLRs; TM2: one SFBC RE pair, 2 QM LLRs), descrambled, into
-// the tile positions of [ga, gb): demap_kernel's arithmetic (demap_body.h)
+// the tile positions of [ga, gb): demap_kernel's arithmetic (demap_body.h).  Split in three so that the
+// uniform-modulation kernel can software-pipeline units: the RE-table and scrambling-word loads, the
+// grid / channel-estimate loads they address, and the arithmetic.
+struct UnitIdx {
+  uint32_t ra, rb;   // RE indices (rb: TM2 only)
+  uint32_t s0, s1;   // the scrambling words holding the unit's first and last bit
+};
+struct UnitIn {
+  float2 r0, r1, h00, h01, h10, h11;   // TM1: r0, h00
+  uint32_t s0, s1;
+};
 template <int QM, bool TM2>
-__device__ __forceinline__ void fused_unit(const RmFuse& f, const MiLaneSrc& src, uint32_t u, uint32_t ga, uint32_t gb,
-                                           uint32_t ta, float* tile) {
-  const float2* g = f.grid + src.goff;
-  const float2* c0 = f.ce + src.coff;
+__device__ __forceinline__ UnitIdx fused_idx(const RmFuse& f, const MiLaneSrc& src, uint32_t u) {
+  constexpr uint32_t U = QM * (TM2 ? 2 : 1);
   const uint32_t* re = f.re_tab + src.re;
   const uint32_t* scr = f.scr_tab + src.scr;
+  UnitIdx x;
+  x.ra = re[TM2 ? 2 * u : u];
+  x.rb = TM2 ? re[2 * u + 1] : 0u;
+  const uint32_t bit0 = u * U;
+  x.s0 = scr[bit0 >> 5];
+  x.s1 = scr[(bit0 + U - 1) >> 5];
+  return x;
+}
+template <bool TM2>
+__device__ __forceinline__ UnitIn fused_data(const RmFuse& f, const MiLaneSrc& src, const UnitIdx& x) {
+  const float2* g = f.grid + src.goff;
+  const float2* c0 = f.ce + src.coff;
+  UnitIn d;
+  d.r0 = g[x.ra];
+  d.h00 = c0[x.ra];
+  if constexpr (TM2) {
+    const float2* c1 = c0 + src.c1;
+    d.r1 = g[x.rb];
+    d.h01 = c0[x.rb];
+    d.h10 = c1[x.ra];
+    d.h11 = c1[x.rb];
+  }
+  d.s0 = x.s0;
+  d.s1 = x.s1;
+  return d;
+}
+template <int QM, bool TM2>
+__device__ __forceinline__ void fused_compute(const RmFuse& f, const UnitIn& d, uint32_t u, uint32_t ga, uint32_t gb,
+                                              uint32_t ta, float* tile) {
   float2 x[2];
   if constexpr (!TM2) {
-    const uint32_t rr = re[u];
-    const float2 y = g[rr], h = c0[rr];
+    const float2 y = d.r0, h = d.h00;
     const float den = h.x * h.x + h.y * h.y + f.noise;
     x[0] = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
   } else {
-    const float2* c1 = c0 + src.c1;
-    const uint32_t ra = re[2 * u], rb = re[2 * u + 1];
-    const float2 r0 = g[ra], r1 = g[rb];
-    const float2 h00 = c0[ra], h01 = c0[rb], h10 = c1[ra], h11 = c1[rb];
+    const float2 r0 = d.r0, r1 = d.r1, h00 = d.h00, h01 = d.h01, h10 = d.h10, h11 = d.h11;
     float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
     if (hh <= 0.f) hh = 1e-9f;
     const float sc = 1.41421356237309504880f / hh;
@@ -76,13 +109,19 @@ __device__ __forceinline__ void fused_unit(const RmFuse& f, const MiLaneSrc& src
     demap_dim<QM>(x[k].x, l + k * QM);
     demap_dim<QM>(x[k].y, l + k * QM + 1);
   }
-  const uint32_t bit0 = u * U;
+  const uint32_t bit0 = u * U, w0 = bit0 >> 5;
 #pragma unroll
   for (int b = 0; b < U; b++) {
     const uint32_t i = bit0 + b;
-    const float v = ((scr[i >> 5] >> (i & 31)) & 1u) ? -l[b] : l[b];
+    const uint32_t word = (i >> 5) == w0 ? d.s0 : d.s1;
+    const float v = ((word >> (i & 31)) & 1u) ? -l[b] : l[b];
     if (i >= ga && i < gb) tile[ta + (i - ga)] = v;
   }
+}
+template <int QM, bool TM2>
+__device__ __forceinline__ void fused_unit(const RmFuse& f, const MiLaneSrc& src, uint32_t u, uint32_t ga, uint32_t gb,
+                                           uint32_t ta, float* tile) {
+  fused_compute<QM, TM2>(f, fused_data<TM2>(f, src, fused_idx<QM, TM2>(f, src, u)), u, ga, gb, ta, tile);
 }
 
 __device__ __forceinline__ void fused_unit_any(const RmFuse& f, const MiLaneSrc& src, uint32_t u, uint32_t ga,
@@ -114,7 +153,8 @@ __device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src
   }
 }
 
-template <bool FUSED>
+// FQ / FT: the batch's common modulation order and transmission mode (FQ = 0: mixed, per-unit switch)
+template <bool FUSED, int FQ = 0, bool FT = false>
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
@@ -173,11 +213,12 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
 #pragma unroll
     for (int r = 0; r < ROWS; r++)
       for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + 4 * r][t] = 0.0f;
+    uint32_t nu = 0;
     if (q < 32) {
       const uint32_t l = w + 4 * (q >> 1), seg = q & 1;
       const uint32_t j0 = s_j0[l], nr = s_nr[l], nv = s_nv[l], E = s_E[l];
       const uint32_t ta = seg ? nv - j0 : 0, tb = seg ? nr : (nr < nv - j0 ? nr : nv - j0);
-      uint32_t ga = 0, gb = 0, u0 = 0, nu = 0;
+      uint32_t ga = 0, gb = 0, u0 = 0;
       if (ta < tb) {
         const uint32_t ja = seg ? 0 : j0, jf = ja + (tb - ta), jb = jf < E ? jf : E;
         if (ja < jb) {
@@ -188,23 +229,67 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
           nu = (gb - 1) / U - u0 + 1;
         }
       }
-      rs_ga[w][q] = ga; rs_gb[w][q] = gb; rs_ta[w][q] = ta; rs_u0[w][q] = u0; rs_pre[w][q + 1] = nu;
+      rs_ga[w][q] = ga; rs_gb[w][q] = gb; rs_ta[w][q] = ta; rs_u0[w][q] = u0;
     }
-    __syncthreads();
-    if (q == 0) {
-      rs_pre[w][0] = 0;
-      for (int i = 0; i < 32; i++) rs_pre[w][i + 1] += rs_pre[w][i];
+    // units before each row-segment: inclusive wavefront scan of nu (lanes >= 32 contribute 0)
+    uint32_t incl = nu;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, 64);
+      if (q >= (uint32_t)d) incl += t;
     }
+    if (q < 32) rs_pre[w][q + 1] = incl;
+    if (q == 0) rs_pre[w][0] = 0;
+    const uint32_t total = __shfl(incl, 31, 64);
     __syncthreads();
-    const uint32_t total = rs_pre[w][32];
-    for (uint32_t fi = q; fi < total; fi += 64) {
-      uint32_t lo = 0, hi = 32;   // row-segment rs with rs_pre[rs] <= fi < rs_pre[rs + 1]
+    auto locate = [&](uint32_t fi) {   // row-segment rs with rs_pre[rs] <= fi < rs_pre[rs + 1]
+      uint32_t lo = 0, hi = 32;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (rs_pre[w][mid] <= fi) lo = mid; else hi = mid;
       }
-      const uint32_t l = w + 4 * (lo >> 1);
-      fused_unit_any(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo], tile[l]);
+      return lo;
+    };
+    if constexpr (FQ != 0) {
+      // uniform modulation: three-stage software pipeline over the thread's units (fi, fi + 64, ...):
+      // the RE-table / scrambling loads run two units ahead, the grid / channel-estimate loads one
+      // unit ahead, so each unit's two dependent HBM round trips overlap earlier units' arithmetic
+      uint32_t fi = q;
+      if (fi < total) {
+        uint32_t loA = locate(fi), uA = rs_u0[w][loA] + (fi - rs_pre[w][loA]);
+        UnitIn dA = fused_data<FT>(fz, s_src[w + 4 * (loA >> 1)], fused_idx<FQ, FT>(fz, s_src[w + 4 * (loA >> 1)], uA));
+        uint32_t loB = 0, uB = 0;
+        UnitIdx iB{};
+        if (fi + 64 < total) {
+          loB = locate(fi + 64);
+          uB = rs_u0[w][loB] + (fi + 64 - rs_pre[w][loB]);
+          iB = fused_idx<FQ, FT>(fz, s_src[w + 4 * (loB >> 1)], uB);
+        }
+        for (;; fi += 64) {
+          const bool hasB = fi + 64 < total, hasC = fi + 128 < total;
+          UnitIn dB{};
+          if (hasB) dB = fused_data<FT>(fz, s_src[w + 4 * (loB >> 1)], iB);
+          uint32_t loC = 0, uC = 0;
+          UnitIdx iC{};
+          if (hasC) {
+            loC = locate(fi + 128);
+            uC = rs_u0[w][loC] + (fi + 128 - rs_pre[w][loC]);
+            iC = fused_idx<FQ, FT>(fz, s_src[w + 4 * (loC >> 1)], uC);
+          }
+#if !MI_RM_SKIP_UNITS   // diagnostic A/B only: staging without the demap arithmetic (wrong LLRs)
+          fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + 4 * (loA >> 1)]);
+#endif
+          if (!hasB) break;
+          loA = loB; uA = uB; dA = dB;
+          loB = loC; uB = uC; iB = iC;
+        }
+      }
+    } else {
+      for (uint32_t fi = q; fi < total; fi += 64) {
+        const uint32_t lo = locate(fi), l = w + 4 * (lo >> 1);
+        fused_unit_any(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo],
+                       tile[l]);
+      }
     }
   } else {
   {
@@ -294,11 +379,22 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
 
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                     const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, hipStream_t st) {
+                     const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
+                     hipStream_t st) {
   if (!n_groups) return;
   dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise};
-  hipLaunchKernelGGL(rm_combine_kernel<true>, g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz);
+#define MI_RM_LAUNCH(...) hipLaunchKernelGGL((__VA_ARGS__), g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz)
+  switch (unit_kind) {   // Qm + 8 * (TM2)
+    case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
+    case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
+    case 6: MI_RM_LAUNCH(rm_combine_kernel<true, 6, false>); break;
+    case 10: MI_RM_LAUNCH(rm_combine_kernel<true, 2, true>); break;
+    case 12: MI_RM_LAUNCH(rm_combine_kernel<true, 4, true>); break;
+    case 14: MI_RM_LAUNCH(rm_combine_kernel<true, 6, true>); break;
+    default: MI_RM_LAUNCH(rm_combine_kernel<true>); break;
+  }
+#undef MI_RM_LAUNCH
 }
 
 }  // namespace mi
