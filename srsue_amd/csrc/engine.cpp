@@ -60,7 +60,7 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   const Tab tabs[] = {tab(d_cells, P.cells), tab(d_crs, P.crs), tab(d_pds, P.pds), tab(d_re, P.re_tab),
                       tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),
                       tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),
-                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat)};
+                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items)};
   size_t total = 0;
   for (const Tab& t : tabs) total += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
   if (total > h_stage_bytes) {
@@ -159,10 +159,12 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     if (fuse)
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
-                      d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind, st);
+                      d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind, rm_items(),
+                      P.rm_busy, (uint32_t)P.rm_items.size(), st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
-                        d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, st);
+                        d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,
+                        rm_items(), P.rm_busy, (uint32_t)P.rm_items.size(), st);
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC)) {
       launch_turbo(sb, st);

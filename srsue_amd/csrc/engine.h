@@ -44,6 +44,8 @@ struct Engine {
   // the plan's descriptor tables, packed 256-B aligned into one page-locked host buffer and copied to
   // one device arena with a single DMA per upload (the per-TTI API re-plans every call)
   DevBuf d_tables;
+  DevBuf d_rmitems;   // Plan::rm_items (view into d_tables)
+  const uint32_t* rm_items() const { return plan.rm_items.empty() ? nullptr : d_rmitems.as<uint32_t>(); }
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
   hipStream_t last_stream = nullptr;

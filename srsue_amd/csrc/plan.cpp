@@ -6,6 +6,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <set>
+#include <tuple>
 
 namespace mi {
 
@@ -37,7 +39,8 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   has_pdsch = with_pdsch;
   cb_K = cb_n = 0;
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
-  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
   max_units = max_ncb = n_cb = 0;
@@ -264,6 +267,31 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       }
     }
   }
+  // rate de-matching chunks with received LLRs (rm.hip): the kernel's per-lane test
+  // (nr > 0 && (E >= Nv || j0 < E || j0 + nr > Nv)) over the distinct lane parameters of each group
+  {
+    std::vector<uint32_t> idle;
+    rm_items.clear();
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+      const uint32_t Ncb = groups[gi].Ncb, nch = (Ncb + RM_CHUNK - 1) / RM_CHUNK;
+      std::vector<uint8_t> busy(nch, 0);
+      busy[0] = 1;
+      std::set<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>> seen;
+      for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+        const MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
+        if (!ld.valid || !seen.insert(std::make_tuple(ld.rank_off, ld.r0, ld.Nv, ld.E)).second) continue;
+        const uint32_t* ch = &kdata[(size_t)ld.rank_off + Ncb];
+        for (uint32_t c = 0; c < nch; c++) {
+          const uint32_t ra = ch[c], nr = ch[c + 1] - ra;
+          const uint32_t j0 = ra >= ld.r0 ? ra - ld.r0 : ra + ld.Nv - ld.r0;
+          if (nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv)) busy[c] = 1;
+        }
+      }
+      for (uint32_t c = 0; c < nch; c++) (busy[c] ? rm_items : idle).push_back(((uint32_t)gi << 9) | c);
+    }
+    rm_busy = (uint32_t)rm_items.size();
+    rm_items.insert(rm_items.end(), idle.begin(), idle.end());
+  }
   // TB -> lane lists
   std::vector<std::vector<uint32_t>> tb_lanes(n);
   for (size_t gi = 0; gi < groups.size(); gi++)
@@ -284,7 +312,8 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
 int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   if (!cb_size_valid(K) || ncb_req == 0) { set_error("invalid code block size"); return -1; }
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
-  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
   max_units = max_ncb = n_cb = 0;

@@ -24,6 +24,10 @@ struct Plan {
   std::vector<MiLaneDesc> lanes;
   std::vector<MiLaneSrc> lane_src;        // per lane (same index): the fused demap's inputs
   uint32_t unit_kind = 0;                 // Qm + 8 (TM2) shared by every valid lane, 0 = mixed
+  // rate de-matching work list: (group << 9 | chunk) of the chunks where some lane receives LLRs (chunk 0
+  // of every group included: it writes the group's zero row), then the other chunks (rm_busy items first)
+  std::vector<uint32_t> rm_items;
+  uint32_t rm_busy = 0;
   std::vector<MiGroupDesc> groups;
   std::vector<MiKTab> ktabs;
   std::vector<uint32_t> kdata;

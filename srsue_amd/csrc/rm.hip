@@ -23,6 +23,9 @@
 #ifndef MI_RM_NT
 #define MI_RM_NT 0   // non-temporal softbuffer stores (A/B switch)
 #endif
+#ifndef MI_RM_IDLE_OFF
+#define MI_RM_IDLE_OFF 0
+#endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
 #endif
@@ -158,7 +161,8 @@ template <bool FUSED, int FQ = 0, bool FT = false>
 __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
-                                                        const uint32_t* __restrict__ kdata, RmFuse fz) {
+                                                        const uint32_t* __restrict__ kdata, RmFuse fz,
+                                                        const uint32_t* __restrict__ items) {
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
@@ -167,8 +171,15 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
   __shared__ uint32_t rs_ga[FUSED ? 4 : 1][32], rs_gb[FUSED ? 4 : 1][32], rs_ta[FUSED ? 4 : 1][32],
       rs_u0[FUSED ? 4 : 1][32], rs_pre[FUSED ? 4 : 1][33];
-  const MiGroupDesc g = groups[blockIdx.y];
-  const uint32_t pa = blockIdx.x * RM_CHUNK;
+  // the work item: (group, chunk) from the planner's list of chunks with received LLRs, or the 2-D grid
+  uint32_t gi = blockIdx.y, ci = blockIdx.x;
+  if (items) {
+    const uint32_t it = items[blockIdx.x];
+    gi = it >> 9;
+    ci = it & 511u;
+  }
+  const MiGroupDesc g = groups[gi];
+  const uint32_t pa = ci * RM_CHUNK;
   if (pa >= g.Ncb) return;
   const uint32_t tid = threadIdx.x;
   float* sbg = sb + g.sb_off;
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
     busy = nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv);
     const uint64_t comb = __ballot(ld.valid && !ld.new_tb), fresh = __ballot(ld.valid && ld.new_tb);
     if (tid == 0) { s_comb = comb != 0; s_new = fresh != 0; }
-    if (blockIdx.x == 0) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;   // the group's zero row
+    if (ci == 0) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;   // the group's zero row
   }
   if (tid < RM_CHUNK / 4) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
@@ -369,22 +380,82 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   if ((uint32_t)lane < np) map[NP * wave + lane] = (uint8_t)((mat_m >> lane) & 1u);
 }
 
+// Chunks where no lane receives an LLR (the planner's idle list; 60 % of a first transmission's
+// circular buffer at MCS 28): one thread per chunk reads its 128 map bytes and normally finds them all
+// zero.  Rows still materialised from an earlier run are settled exactly as rm_combine_kernel would
+// settle them (nothing is received, so v = old): in a group with combining lanes the row stays
+// materialised and its fresh lanes are zeroed, otherwise the row is dropped from the map.
+__global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, const MiGroupDesc* __restrict__ groups,
+                                                     const MiLaneDesc* __restrict__ lanes,
+                                                     const uint32_t* __restrict__ items, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t it = items[i];
+  const MiGroupDesc g = groups[it >> 9];
+  const uint32_t pa = (it & 511u) * RM_CHUNK;
+  if (pa >= g.Ncb) return;
+  float* sbg = sb + g.sb_off;
+  uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb)) + pa;
+  const uint4* m4 = reinterpret_cast<const uint4*>(map);
+  uint32_t any = 0;
+#pragma unroll
+  for (int k = 0; k < RM_CHUNK / 16; k++) {
+    const uint4 v = m4[k];
+    any |= v.x | v.y | v.z | v.w;
+  }
+  if (!any) return;
+  uint64_t fresh = 0;
+  bool comb = false;
+  for (int l = 0; l < LANES; l++) {
+    const MiLaneDesc ld = lanes[g.lane0 + l];
+    if (!ld.valid) continue;
+    if (ld.new_tb) fresh |= 1ull << l; else comb = true;
+  }
+  const uint32_t np = min((uint32_t)RM_CHUNK, g.Ncb - pa);
+  for (uint32_t p = 0; p < np; p++) {
+    if (!map[p]) continue;
+    if (!comb) { map[p] = 0; continue; }
+    for (int l = 0; l < LANES; l++)
+      if ((fresh >> l) & 1u) sbg[(size_t)(pa + p) * LANES + l] = 0.0f;
+  }
+}
+
+// the chunk work list (busy items with the combine kernel, idle items with rm_idle_kernel), or without
+// one (n_items = 0) every chunk of every group through the combine kernel
+static dim3 rm_grid(const uint32_t* items, uint32_t n_busy, uint32_t n_groups, uint32_t max_ncb) {
+  return items ? dim3(n_busy) : dim3((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
+}
+static void rm_idle(float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes, const uint32_t* items,
+                    uint32_t n_busy, uint32_t n_items, hipStream_t st) {
+#if MI_RM_IDLE_OFF   // A/B only: skip the idle chunks entirely
+  return;
+#endif
+  if (items && n_items > n_busy)
+    hipLaunchKernelGGL(rm_idle_kernel, dim3((n_items - n_busy + 255) / 256), dim3(256), 0, st, sb, groups, lanes,
+                       items + n_busy, n_items - n_busy);
+}
+
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* /*ktabs*/, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
-                       hipStream_t st) {
+                       const uint32_t* items, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
   if (!n_groups) return;
-  dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
-  hipLaunchKernelGGL(rm_combine_kernel<false>, g, dim3(256), 0, st, e, sb, groups, lanes, ktab_data, RmFuse{});
+  if (items && !n_busy) items = nullptr;
+  rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
+  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(256), 0, st, e, sb,
+                     groups, lanes, ktab_data, RmFuse{}, items);
 }
 
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
-                     hipStream_t st) {
+                     const uint32_t* items, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
   if (!n_groups) return;
-  dim3 g((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
+  if (items && !n_busy) items = nullptr;
+  rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
+  const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise};
-#define MI_RM_LAUNCH(...) hipLaunchKernelGGL((__VA_ARGS__), g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz)
+#define MI_RM_LAUNCH(...) \
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items)
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
