@@ -316,7 +316,8 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
         uint32_t bits = 0;
         if (ta >= 0 && ia < x.q_ack) {
           // 36.211 5.3.1 placeholders: x -> 1, y -> the previous scrambled bit
-          const uint32_t cw = x.ack_nblk == 1 ? x.ack_sym[0] : x.ack_sym[ia % 3];
+          const uint32_t ks = x.ack_nblk == 1 ? 0u : ia % 3;   // selects, no dynamic index into x
+          const uint32_t cw = ks == 0 ? x.ack_sym[0] : ks == 1 ? x.ack_sym[1] : x.ack_sym[2];
           uint32_t prev = 0;
           for (uint32_t b = 0; b < Qm; b++) {
             const uint32_t i = i0 + b, code = (cw >> (2 * b)) & 3u;
