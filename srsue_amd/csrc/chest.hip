@@ -4,8 +4,9 @@
 //
 // One 256-thread workgroup per subframe.  Per port: LS estimate on the 4 pilot symbols
 // (p = y conj(r), CRS r from a per-cell device table), 3-tap smoothing [0.1 0.8 0.1] with edge
-// taps renormalised, linear interpolation in frequency into an LDS image [4][12 N_RB], then linear
-// interpolation / extrapolation in time straight to HBM (coalesced rows of ce[port][l][k]).
+// taps renormalised; then each thread owns subcarriers k: linear interpolation in frequency of the
+// 4 pilot symbols at k (registers), linear interpolation / extrapolation in time straight to HBM
+// (coalesced rows of ce[port][l][k]).  LDS holds only the pilot rows (14 KB): 8 workgroups per CU.
 // Metrics are reduced in the workgroup (wave shuffles + LDS) and written once per subframe.
 #include "kernels.h"
 
@@ -31,67 +32,84 @@ __global__ __launch_bounds__(256) void chest_kernel(const float2* __restrict__ g
   constexpr float W1 = 0.1f, W0 = 0.8f;
   __shared__ float2 hp[4][2 * NRB_MAX];
   __shared__ float2 hs[4][2 * NRB_MAX];
-  __shared__ float2 hf[4][12 * NRB_MAX];
   __shared__ float red[4];
   const MiSfDesc d = sfs[blockIdx.x];
   const MiCellDesc c = cells[d.cell];
   const int W = (int)c.W, NP = 2 * (int)c.nof_prb;
   const float2* g = grid + d.grid_off;
   float rsrp = 0.f, noise = 0.f, rssi = 0.f;
+  // every loop runs over (uniform row, thread-strided column): no integer division by runtime sizes
+  const int tid = (int)threadIdx.x;
   for (int p = 0; p < (int)c.nof_ports; p++) {
-    for (int t = threadIdx.x; t < 4 * NP; t += 256) {
-      const int i = t / NP, m = t % NP, l = PL[i], lp = l % 7;
+    int offs[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int lp = PL[i] % 7;
       const int v = (p == 0) ? (lp == 0 ? 0 : 3) : (lp == 0 ? 3 : 0);
-      const int off = (v + (int)(c.id % 6)) % 6;
-      const float2 y = g[l * W + 6 * m + off];
-      const float2 r = crs[c.crs_off + ((2 * d.sf_idx + l / 7) * 2 + (lp == 4)) * (2 * NRB_MAX) + m + NRB_MAX - c.nof_prb];
-      const float2 h = make_float2(y.x * r.x + y.y * r.y, y.y * r.x - y.x * r.y);
-      hp[i][m] = h;
-      if (p == 0) rsrp += h.x * h.x + h.y * h.y;
+      offs[i] = (v + (int)(c.id % 6)) % 6;
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < 4 * NP; t += 256) {
-      const int i = t / NP, m = t % NP;
-      float2 s;
-      if (m == 0) {
-        s = make_float2((W0 * hp[i][0].x + W1 * hp[i][1].x) / (W0 + W1), (W0 * hp[i][0].y + W1 * hp[i][1].y) / (W0 + W1));
-      } else if (m == NP - 1) {
-        s = make_float2((W1 * hp[i][m - 1].x + W0 * hp[i][m].x) / (W0 + W1), (W1 * hp[i][m - 1].y + W0 * hp[i][m].y) / (W0 + W1));
-      } else {
-        s = make_float2(W1 * hp[i][m - 1].x + W0 * hp[i][m].x + W1 * hp[i][m + 1].x,
-                        W1 * hp[i][m - 1].y + W0 * hp[i][m].y + W1 * hp[i][m + 1].y);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int l = PL[i], lp = l % 7;
+      const float2* rr = crs + c.crs_off + ((2 * d.sf_idx + l / 7) * 2 + (lp == 4)) * (2 * NRB_MAX) + NRB_MAX - c.nof_prb;
+      for (int m = tid; m < NP; m += 256) {
+        const float2 y = g[l * W + 6 * m + offs[i]];
+        const float2 r = rr[m];
+        const float2 h = make_float2(y.x * r.x + y.y * r.y, y.y * r.x - y.x * r.y);
+        hp[i][m] = h;
+        if (p == 0) rsrp += h.x * h.x + h.y * h.y;
       }
-      hs[i][m] = s;
-      const float dx = hp[i][m].x - s.x, dy = hp[i][m].y - s.y;
-      noise += dx * dx + dy * dy;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < 4 * W; t += 256) {
-      const int i = t / W, k = t % W, lp = PL[i] % 7;
-      const int v = (p == 0) ? (lp == 0 ? 0 : 3) : (lp == 0 ? 3 : 0);
-      const int off = (v + (int)(c.id % 6)) % 6;
-      int m = (k - off) / 6;
-      if (k < off) m = 0;
-      if (m > NP - 2) m = NP - 2;
-      const float frac = (float)(k - (6 * m + off)) / 6.0f;
-      const float2 a = hs[i][m], b = hs[i][m + 1];
-      hf[i][k] = make_float2(a.x + frac * (b.x - a.x), a.y + frac * (b.y - a.y));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      for (int m = tid; m < NP; m += 256) {
+        float2 s;
+        if (m == 0) {
+          s = make_float2((W0 * hp[i][0].x + W1 * hp[i][1].x) / (W0 + W1), (W0 * hp[i][0].y + W1 * hp[i][1].y) / (W0 + W1));
+        } else if (m == NP - 1) {
+          s = make_float2((W1 * hp[i][m - 1].x + W0 * hp[i][m].x) / (W0 + W1), (W1 * hp[i][m - 1].y + W0 * hp[i][m].y) / (W0 + W1));
+        } else {
+          s = make_float2(W1 * hp[i][m - 1].x + W0 * hp[i][m].x + W1 * hp[i][m + 1].x,
+                          W1 * hp[i][m - 1].y + W0 * hp[i][m].y + W1 * hp[i][m + 1].y);
+        }
+        hs[i][m] = s;
+        const float dx = hp[i][m].x - s.x, dy = hp[i][m].y - s.y;
+        noise += dx * dx + dy * dy;
+      }
     }
     __syncthreads();
+    // frequency interpolation of the 4 pilot symbols at subcarrier k (kept in registers), then the
+    // time interpolation / extrapolation of all 14 symbols at k: coalesced rows of ce[port][l][k]
     float2* cp = ce + d.ce_off + (size_t)p * NSYMB * W;
-    for (int t = threadIdx.x; t < NSYMB * W; t += 256) {
-      const int l = t / W, k = t % W;
-      const int ia = l <= 4 ? 0 : (l <= 7 ? 1 : 2), ib = ia + 1;
-      const float tt = (float)(l - PL[ia]) / (float)(PL[ib] - PL[ia]);
-      const float2 a = hf[ia][k], b = hf[ib][k];
-      cp[t] = make_float2(a.x + tt * (b.x - a.x), a.y + tt * (b.y - a.y));
+    for (int k = tid; k < W; k += 256) {
+      float2 hk[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int off = offs[i];
+        int m = (k - off) / 6;
+        if (k < off) m = 0;
+        if (m > NP - 2) m = NP - 2;
+        const float frac = (float)(k - (6 * m + off)) / 6.0f;
+        const float2 a = hs[i][m], b = hs[i][m + 1];
+        hk[i] = make_float2(a.x + frac * (b.x - a.x), a.y + frac * (b.y - a.y));
+      }
+#pragma unroll
+      for (int l = 0; l < NSYMB; l++) {
+        const int ia = l <= 4 ? 0 : (l <= 7 ? 1 : 2), ib = ia + 1;
+        const float tt = (float)(l - PL[ia]) / (float)(PL[ib] - PL[ia]);
+        const float2 a = hk[ia], b = hk[ib];
+        cp[l * W + k] = make_float2(a.x + tt * (b.x - a.x), a.y + tt * (b.y - a.y));
+      }
     }
     __syncthreads();
   }
-  for (int t = threadIdx.x; t < 4 * W; t += 256) {
-    const float2 y = g[PL[t / W] * W + t % W];
-    rssi += y.x * y.x + y.y * y.y;
-  }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    for (int k = tid; k < W; k += 256) {
+      const float2 y = g[PL[i] * W + k];
+      rssi += y.x * y.x + y.y * y.y;
+    }
   rsrp = block_sum(rsrp, red);
   noise = block_sum(noise, red);
   rssi = block_sum(rssi, red);
