@@ -139,11 +139,11 @@ __host__ __device__ inline float clampf(float x, float c) { return fminf(fmaxf(x
 // decoder-input quantiser q(x) = clamp(rint(32 x), +-511)
 __host__ __device__ inline float q16f(float x) { return clampf(rintf(x * I16_SCALE), I16_CI); }
 // In int16 mode a group's scratch (sized in floats for the float decoder) holds int16 streams: w [K],
-// llr1 [K], beta checkpoints [7 (K/4 + 1)], each [..][64 lanes], then from this int16 element index
+// llr1 [K], beta checkpoints [(K/4 + 1)][64 lanes][8] (tdec_body.h ck_store), then from this int16 element index
 // the quantised decoder inputs q [3 (K + 4)][64] in natural (triplet) order, written by the decoder's
-// first pass from the softbuffer and read by every later pass.  Fits: 3K + 12 <= 2K + 7 (K/4 + 1) for K >= 7.
+// first pass from the softbuffer and read by every later pass.  Fits: 3K + 12 <= 2K + 8 (K/4 + 1) for K >= 4.
 __host__ __device__ inline size_t q16_elem_off(uint32_t K) {
-  return (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
+  return (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
 }
 }  // namespace mi
 

@@ -179,7 +179,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       g.scratch_off = scratch_floats;
       g.dec_off = dec_bytes;
       sb_floats += sb_group_floats(Ncb);
-      scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
+      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
       dec_bytes += (size_t)K * LANES;
       groups.push_back(g);
       for (size_t q = 0; q < (size_t)LANES; q++) {
@@ -334,7 +334,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
     g.scratch_off = scratch_floats;
     g.dec_off = dec_bytes;
     sb_floats += sb_group_floats(Ncb);
-    scratch_floats += (size_t)LANES * (2 * K + 7 * (K / TDEC_CK_MIN + 1));
+    scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
     dec_bytes += (size_t)K * LANES;
     groups.push_back(g);
     for (uint32_t q = 0; q < (uint32_t)LANES; q++) {

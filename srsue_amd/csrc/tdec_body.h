@@ -26,6 +26,8 @@
 //    w = clamp(llr2 - xs2, +-1023).  Every metric is then an integer of magnitude < 2^15, which
 //    fp32 adds/subs/max represent exactly, so the same register code reproduces the int16 decoder.
 #pragma once
+#include <string.h>
+
 #include <type_traits>
 
 #include "dl_common.h"
@@ -57,7 +59,7 @@ struct TdecArgs {
   const uint32_t* crc_a;  // [K] CRC24A contribution of a 1 at bit i (x^(K-1-i+24) mod g)
   const uint32_t* crc_b;  // [K] same for CRC24B
   const uint32_t* crc8;   // [256] byte table of CRC24A (register update of one message byte)
-  float* scr;             // group scratch: w [K][64], llr1 [K][64], beta ckpt [(K/(2W)+1)*7][64]
+  float* scr;             // group scratch: w [K][64], llr1 [K][64], checkpoints [(K/4+1)][64][8]
   uint8_t* dec;           // [K][64] decision bytes
   uint8_t* cb_bytes;      // this lane's packed output row (K/8 bytes, MSB first)
   uint32_t K, F, max_its, early_stop, crc24a;
@@ -214,14 +216,14 @@ enum { SRC_SB = 0, SRC_MKQ = 1, SRC_Q = 2 };
 //   DEC1: s0 = systematic, s1 = parity 1, r0 = w            (FIRST: w = 0, not loaded)
 //   DEC2: s0 = parity 2,   r0 = llr1[pi], r1 = w[pi]         (FIRST: w = 0, not loaded)
 //   (s0/s1: softbuffer floats via the position table, or int16 q[3k+i] rows in int16 mode)
-//   ck  : states 1..7 of the beta checkpoint closing the window (forward pass only)
+//   ck  : the raw record of the checkpoint closing the window (forward pass only)
 //   f0..f2: the three softbuffer inputs of a step, in the int16 decoder's first pass only
 template <bool Q16>
 struct TdecWin {
   using R = typename std::conditional<Q16, int32_t, float>::type;
   R s0[BETA_W], s1[BETA_W];
   R r0[BETA_W], r1[BETA_W];
-  R ck[7];
+  uint32_t ck[Q16 ? 4 : 8];   // raw checkpoint record (ck_state unpacks state s at use)
   float f0[BETA_W], f1[BETA_W], f2[BETA_W];
 };
 
@@ -278,6 +280,11 @@ MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb), vo, so, 0));
   }
 #endif
+#if defined(MI_TDEC_DIAG_Q16SB)   // timing diagnostic only: int16-wide softbuffer reads (wrong values)
+  if constexpr (Q16)
+    return __builtin_bit_cast(float, (uint32_t)(uint16_t)row_ld(reinterpret_cast<const int16_t*>(a.sb),
+                                                                  on ? a.pos[t0 + dt] : a.zrow, lane));
+#endif
   return row_ld(a.sb, on ? a.pos[t0 + dt] : a.zrow, lane);
 }
 
@@ -329,18 +336,61 @@ MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base
   }
 }
 
-// beta checkpoint c (= beta at step c * BETA_W) holds states 1..7 (state 0 is 0 after
-// normalisation); ck0 = row of checkpoint 0 in the scratch stream.  Checkpoints are
-// taken at k <= K, where every state is reachable, so no -inf is ever stored.
+// Checkpoint c (beta, or in the crossed schedule's first half alpha, at step c * BETA_W) holds states
+// 1..7 (state 0 is 0 after normalisation) as ONE record per lane, [c][lane][8] elements (int16 in
+// int16 mode: 16 B, fp32 in float mode: 32 B; element 7 unused), so a checkpoint costs one 128-bit
+// access per lane (two in float mode) instead of seven row accesses: the decoder issues ~6 fewer
+// memory instructions per trellis step.  ck0 = row of checkpoint 0 in the scratch stream (a record is
+// 8 rows' worth of elements).  Checkpoints are taken where every state is reachable (k <= K for
+// beta, k >= 4 for alpha), so no -inf is ever stored.
 template <bool Q16>
 MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
+  constexpr uint32_t NW = Q16 ? 4 : 8, ESZ = Q16 ? 2 : 4;
+  uint32_t w[NW];
+  if constexpr (Q16) {
 #pragma unroll
-  for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + (size_t)c * 7, lane, b[s], s - 1);
+    for (int k = 0; k < 4; k++) {
+      const uint32_t lo = (uint16_t)(int16_t)(int32_t)b[2 * k + 1];
+      const uint32_t hi = k < 3 ? (uint32_t)(uint16_t)(int16_t)(int32_t)b[2 * k + 2] : 0u;
+      w[k] = lo | (hi << 16);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 7; k++) w[k] = __builtin_bit_cast(uint32_t, b[k + 1]);
+    w[7] = 0u;
+  }
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * ESZ), vo = (uint32_t)lane * 8 * ESZ;
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
+#pragma unroll
+  for (uint32_t q = 0; q < NW / 4; q++)
+    __builtin_amdgcn_raw_buffer_store_b128(u4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]}, rs, vo + 16 * q, so, 0);
+#else
+  memcpy(reinterpret_cast<char*>(scr) + so + vo, w, sizeof(w));
+#endif
 }
 template <bool Q16>
 MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane, TdecWin<Q16>& r) {
+  constexpr uint32_t NW = Q16 ? 4 : 8, ESZ = Q16 ? 2 : 4;
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * ESZ), vo = (uint32_t)lane * 8 * ESZ;
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
 #pragma unroll
-  for (int s = 1; s < 8; s++) r.ck[s - 1] = scr_raw<Q16>(scr, ck0 + (size_t)c * 7, lane, s - 1);
+  for (uint32_t q = 0; q < NW / 4; q++) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16 * q, so, 0);
+    r.ck[4 * q] = v.x; r.ck[4 * q + 1] = v.y; r.ck[4 * q + 2] = v.z; r.ck[4 * q + 3] = v.w;
+  }
+#else
+  memcpy(r.ck, reinterpret_cast<const char*>(scr) + so + vo, NW * 4);
+#endif
+}
+// state s (1..7) of a raw checkpoint record
+template <bool Q16>
+MI_HD inline float ck_state(const uint32_t* ck, int s) {
+  if constexpr (Q16) return (float)(int16_t)(uint16_t)(ck[(s - 1) >> 1] >> (16 * ((s - 1) & 1)));
+  else return __builtin_bit_cast(float, ck[s - 1]);
 }
 
 // decoder inputs (xs, xp) of step base+i from the raw window (filler: known-zero bits)
@@ -433,7 +483,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
   float bw[BETA_W][8];
   bw[BETA_W - 1][0] = 0.0f;
 #pragma unroll
-  for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = scr_cvt<Q16>(w.ck[s - 1]);
+  for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = ck_state<Q16>(w.ck, s);
 #pragma unroll
   for (int i = BETA_W - 2; i >= 0; i--) beta_step<!Q16>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
@@ -666,7 +716,7 @@ MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecW
   float aw[BETA_W][8];
   aw[0][0] = 0.0f;
 #pragma unroll
-  for (int s = 1; s < 8; s++) aw[0][s] = base ? scr_cvt<Q16>(w.ck[s - 1]) : -INFINITY;
+  for (int s = 1; s < 8; s++) aw[0][s] = base ? ck_state<Q16>(w.ck, s) : -INFINITY;
 #pragma unroll
   for (int i = 0; i < BETA_W - 1; i++) {
 #pragma unroll
