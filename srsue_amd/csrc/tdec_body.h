@@ -250,6 +250,15 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
   else row_st(scr, row, lane, v, crow);
 }
 
+#if defined(MI_TDEC_DIAG_NOTAB)   // timing diagnostic only: table lookups replaced by hashes (wrong results)
+#define MI_POS(a, t) ((((uint32_t)(t) * 40503u) >> 2) & 16383u)
+#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
+#define MI_CRC(a, pk) 0u
+#else
+#define MI_POS(a, t) ((a).pos[t])
+#define MI_PI(a, k) ((a).pi[k])
+#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
+#endif
 // window mask of decoder inputs 12w .. 12w+11 (tail: w = K/4): bit i = row pos[12w+i] materialised
 MI_HD inline uint32_t tdec_window_mask(const uint8_t* map, const uint32_t* pos, uint32_t w) {
   uint32_t m = 0;
@@ -275,7 +284,7 @@ MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt
   const bool on = (m >> dt) & 1u;
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
   if constexpr (!(Q16 ? MI_SB_ZROW_I16 : MI_SB_ZROW_GEN)) {
-    const uint32_t so = a.pos[t0 + dt] * (uint32_t)(LANES * sizeof(float));
+    const uint32_t so = MI_POS(a, t0 + dt) * (uint32_t)(LANES * sizeof(float));
     const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb), vo, so, 0));
   }
@@ -283,9 +292,9 @@ MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt
 #if defined(MI_TDEC_DIAG_Q16SB)   // timing diagnostic only: int16-wide softbuffer reads (wrong values)
   if constexpr (Q16)
     return __builtin_bit_cast(float, (uint32_t)(uint16_t)row_ld(reinterpret_cast<const int16_t*>(a.sb),
-                                                                  on ? a.pos[t0 + dt] : a.zrow, lane));
+                                                                  on ? MI_POS(a, t0 + dt) : a.zrow, lane));
 #endif
-  return row_ld(a.sb, on ? a.pos[t0 + dt] : a.zrow, lane);
+  return row_ld(a.sb, on ? MI_POS(a, t0 + dt) : a.zrow, lane);
 }
 
 // raw decoder input t (= 3k + i): softbuffer float at position pos[t], or the int16 q row t
@@ -312,7 +321,7 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
       }
       r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
     } else {
-      const uint32_t pk = a.pi[k];
+      const uint32_t pk = MI_PI(a, k);
       if constexpr (Q16 && !SQ) r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
       else r.s0[i] = dec_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
       r.r0[i] = scr_raw<Q16>(llr1, pk, lane);
@@ -426,13 +435,13 @@ MI_HD inline void tdec_emit(const TdecArgs& a, int lane, uint32_t base, int i, f
   if (!DEC2) {
     scr_st<Q16>(scr_at<Q16>(a.scr, a.K), base, lane, llr, i);           // llr1
   } else {
-    const uint32_t pk = a.pi[k];
+    const uint32_t pk = MI_PI(a, k);
     scr_st<Q16>(a.scr, pk, lane,                                         // w update
                 Q16 ? clampf(llr - xs, I16_CW)
                     : scr_cvt<Q16>(w.r1[i]) + (llr - scr_cvt<Q16>(w.r0[i])));
     const bool bit = llr > 0.0f;
     row_st(a.dec, pk, lane, (uint8_t)(bit ? 1 : 0));                    // decision
-    const uint32_t tt = a.crc24a ? a.crc_a[pk] : a.crc_b[pk];
+    const uint32_t tt = MI_CRC(a, pk);
     crc.cb ^= bit ? tt : 0u;                                            // CB CRC by linearity
   }
 }
