@@ -32,6 +32,11 @@
 
 namespace mi {
 
+// workgroup shape: RM_NW wavefronts per chunk, each owning RM_CHUNK / RM_NW = 32 consecutive positions
+// in the combine and 64 / RM_NW code-block rows (2 row-segments each) in the staging
+constexpr int RM_NW = RM_CHUNK / 32, RM_NT = 64 * RM_NW, RM_NSEG = 2 * LANES / RM_NW;
+static_assert(RM_CHUNK == 128 || RM_CHUNK == 256, "rm.hip: 128- or 256-position chunks");
+
 // Fused demap -> rate de-matching (MI_DL_FLAG_KEEP_LLR off): instead of reading the LLR stream e, the
 // staging computes each LLR from the grid and channel estimates (demap_body.h, the arithmetic of
 // demap_kernel): the 90,000 LLRs of a 20 MHz subframe are never written to or read from HBM.
@@ -158,7 +163,7 @@ __device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src
 
 // FQ / FT: the batch's common modulation order and transmission mode (FQ = 0: mixed, per-unit switch)
 template <bool FUSED, int FQ = 0, bool FT = false>
-__global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
+__global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
@@ -167,10 +172,10 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
   __shared__ uint32_t s_comb, s_new;
-  // fused staging: per-lane sources, and per wavefront 32 (row, segment) LLR runs -> demap units
+  // fused staging: per-lane sources, and per wavefront RM_NSEG (row, segment) LLR runs -> demap units
   __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
-  __shared__ uint32_t rs_ga[FUSED ? 4 : 1][32], rs_gb[FUSED ? 4 : 1][32], rs_ta[FUSED ? 4 : 1][32],
-      rs_u0[FUSED ? 4 : 1][32], rs_pre[FUSED ? 4 : 1][33];
+  __shared__ uint32_t rs_ga[FUSED ? RM_NW : 1][RM_NSEG], rs_gb[FUSED ? RM_NW : 1][RM_NSEG],
+      rs_ta[FUSED ? RM_NW : 1][RM_NSEG], rs_u0[FUSED ? RM_NW : 1][RM_NSEG], rs_pre[FUSED ? RM_NW : 1][RM_NSEG + 1];
   // the work item: (group, chunk) from the planner's list of chunks with received LLRs, or the 2-D grid
   uint32_t gi = blockIdx.y, ci = blockIdx.x;
   if (items) {
@@ -213,20 +218,20 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
   if (!__syncthreads_or(busy)) return;
   // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
   // all of a wavefront's loads issued before its LDS writes
-  constexpr int ROWS = LANES / 4, PER = RM_CHUNK / 64;
+  constexpr int ROWS = LANES / RM_NW, PER = RM_CHUNK / 64;
   if constexpr (FUSED) {
     // Every LLR computed from grid + ce, one demap unit (an RE, or an SFBC RE pair: all its Qm or 2 Qm
     // LLRs, as demap_kernel computes them) per thread and step.  Wavefront w owns code-block rows
-    // l = w + 4 r; each row's LLR run (j0 + t) mod Nv, t < nr, clipped to [0, E), is at most two
-    // contiguous runs (row-segments); the units of the wavefront's 32 row-segments are dealt to its 64
+    // l = w + RM_NW r; each row's LLR run (j0 + t) mod Nv, t < nr, clipped to [0, E), is at most two
+    // contiguous runs (row-segments); the units of the wavefront's RM_NSEG row-segments are dealt to its 64
     // threads flat, so all threads work and their loads are independent.
     const uint32_t w = tid >> 6, q = tid & 63;
 #pragma unroll
     for (int r = 0; r < ROWS; r++)
-      for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + 4 * r][t] = 0.0f;
+      for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + RM_NW * r][t] = 0.0f;
     uint32_t nu = 0;
-    if (q < 32) {
-      const uint32_t l = w + 4 * (q >> 1), seg = q & 1;
+    if (q < RM_NSEG) {
+      const uint32_t l = w + RM_NW * (q >> 1), seg = q & 1;
       const uint32_t j0 = s_j0[l], nr = s_nr[l], nv = s_nv[l], E = s_E[l];
       const uint32_t ta = seg ? nv - j0 : 0, tb = seg ? nr : (nr < nv - j0 ? nr : nv - j0);
       uint32_t ga = 0, gb = 0, u0 = 0;
@@ -242,19 +247,19 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       }
       rs_ga[w][q] = ga; rs_gb[w][q] = gb; rs_ta[w][q] = ta; rs_u0[w][q] = u0;
     }
-    // units before each row-segment: inclusive wavefront scan of nu (lanes >= 32 contribute 0)
+    // units before each row-segment: inclusive wavefront scan of nu (lanes >= RM_NSEG contribute 0)
     uint32_t incl = nu;
 #pragma unroll
-    for (int d = 1; d < 32; d <<= 1) {
+    for (int d = 1; d < RM_NSEG; d <<= 1) {
       const uint32_t t = __shfl_up(incl, d, 64);
       if (q >= (uint32_t)d) incl += t;
     }
-    if (q < 32) rs_pre[w][q + 1] = incl;
+    if (q < RM_NSEG) rs_pre[w][q + 1] = incl;
     if (q == 0) rs_pre[w][0] = 0;
-    const uint32_t total = __shfl(incl, 31, 64);
+    const uint32_t total = __shfl(incl, RM_NSEG - 1, 64);
     __syncthreads();
     auto locate = [&](uint32_t fi) {   // row-segment rs with rs_pre[rs] <= fi < rs_pre[rs + 1]
-      uint32_t lo = 0, hi = 32;
+      uint32_t lo = 0, hi = RM_NSEG;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (rs_pre[w][mid] <= fi) lo = mid; else hi = mid;
@@ -268,27 +273,27 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       uint32_t fi = q;
       if (fi < total) {
         uint32_t loA = locate(fi), uA = rs_u0[w][loA] + (fi - rs_pre[w][loA]);
-        UnitIn dA = fused_data<FT>(fz, s_src[w + 4 * (loA >> 1)], fused_idx<FQ, FT>(fz, s_src[w + 4 * (loA >> 1)], uA));
+        UnitIn dA = fused_data<FT>(fz, s_src[w + RM_NW * (loA >> 1)], fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loA >> 1)], uA));
         uint32_t loB = 0, uB = 0;
         UnitIdx iB{};
         if (fi + 64 < total) {
           loB = locate(fi + 64);
           uB = rs_u0[w][loB] + (fi + 64 - rs_pre[w][loB]);
-          iB = fused_idx<FQ, FT>(fz, s_src[w + 4 * (loB >> 1)], uB);
+          iB = fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loB >> 1)], uB);
         }
         for (;; fi += 64) {
           const bool hasB = fi + 64 < total, hasC = fi + 128 < total;
           UnitIn dB{};
-          if (hasB) dB = fused_data<FT>(fz, s_src[w + 4 * (loB >> 1)], iB);
+          if (hasB) dB = fused_data<FT>(fz, s_src[w + RM_NW * (loB >> 1)], iB);
           uint32_t loC = 0, uC = 0;
           UnitIdx iC{};
           if (hasC) {
             loC = locate(fi + 128);
             uC = rs_u0[w][loC] + (fi + 128 - rs_pre[w][loC]);
-            iC = fused_idx<FQ, FT>(fz, s_src[w + 4 * (loC >> 1)], uC);
+            iC = fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loC >> 1)], uC);
           }
 #if !MI_RM_SKIP_UNITS   // diagnostic A/B only: staging without the demap arithmetic (wrong LLRs)
-          fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + 4 * (loA >> 1)]);
+          fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + RM_NW * (loA >> 1)]);
 #endif
           if (!hasB) break;
           loA = loB; uA = uB; dA = dB;
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
       }
     } else {
       for (uint32_t fi = q; fi < total; fi += 64) {
-        const uint32_t lo = locate(fi), l = w + 4 * (lo >> 1);
+        const uint32_t lo = locate(fi), l = w + RM_NW * (lo >> 1);
         fused_unit_any(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo],
                        tile[l]);
       }
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
     const uint32_t w = tid >> 6, q = tid & 63;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
-      const uint32_t l = w + 4 * r;
+      const uint32_t l = w + RM_NW * r;
       const uint32_t nr = s_nr[l], nv = s_nv[l], E = s_E[l];
       const float* el = e + s_eoff[l];
 #pragma unroll
@@ -322,12 +327,12 @@ __global__ __launch_bounds__(256) void rm_combine_kernel(const float* __restrict
 #pragma unroll
     for (int r = 0; r < ROWS; r++)
 #pragma unroll
-      for (int c = 0; c < PER; c++) tile[w + 4 * r][q + 64 * c] = v[r][c];
+      for (int c = 0; c < PER; c++) tile[w + RM_NW * r][q + 64 * c] = v[r][c];
   }
   }
   __syncthreads();
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
-  constexpr int NP = RM_CHUNK / 4;
+  constexpr int NP = RM_CHUNK / RM_NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
   const uint32_t pw = pa + NP * (uint32_t)wave, np = g.Ncb > pw ? min(g.Ncb - pw, (uint32_t)NP) : 0u;
   const MiLaneDesc ld = lanes[g.lane0 + lane];
@@ -441,7 +446,7 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
-  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(256), 0, st, e, sb,
+  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(RM_NT), 0, st, e, sb,
                      groups, lanes, ktab_data, RmFuse{}, items);
 }
 
@@ -455,7 +460,7 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
   const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise};
 #define MI_RM_LAUNCH(...) \
-  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(256), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items)
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items)
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
