@@ -223,7 +223,7 @@ struct TdecWin {
   using R = typename std::conditional<Q16, int32_t, float>::type;
   R s0[BETA_W], s1[BETA_W];
   R r0[BETA_W], r1[BETA_W];
-  uint32_t ck[Q16 ? 4 : 8];   // raw checkpoint record (ck_state unpacks state s at use)
+  uint32_t ck[8];   // raw checkpoint (row layout: states 1..7 as loaded; record layout: the packed record)
   float f0[BETA_W], f1[BETA_W], f2[BETA_W];
 };
 
@@ -346,14 +346,24 @@ MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base
 }
 
 // Checkpoint c (beta, or in the crossed schedule's first half alpha, at step c * BETA_W) holds states
-// 1..7 (state 0 is 0 after normalisation) as ONE record per lane, [c][lane][8] elements (int16 in
-// int16 mode: 16 B, fp32 in float mode: 32 B; element 7 unused), so a checkpoint costs one 128-bit
-// access per lane (two in float mode) instead of seven row accesses: the decoder issues ~6 fewer
-// memory instructions per trellis step.  ck0 = row of checkpoint 0 in the scratch stream (a record is
-// 8 rows' worth of elements).  Checkpoints are taken where every state is reachable (k <= K for
-// beta, k >= 4 for alpha), so no -inf is ever stored.
-template <bool Q16>
+// 1..7 (state 0 is 0 after normalisation) in a slot of 8 rows' worth of elements at row ck0 + 8 c.
+// Two layouts (REC):
+//  * rows (single-wave kernel): state s in row ck0 + 8 c + s - 1, seven 128-B (int16) / 256-B row
+//    accesses per checkpoint, 14 / 28 B per lane;
+//  * record (crossed kernel): [c][lane][8] elements, one 128-bit access per lane (two in float mode),
+//    16 / 32 B per lane.  Same-box A/B (`profiles/r1/ab_ck/`): the record saves ~6 memory instructions
+//    per trellis step and is 5.6 % faster on configs[2] (0.4 groups per SIMD), but moves 1/7 more
+//    checkpoint bytes and was 0.8 % slower at the headline's 2.5 groups per SIMD -- so each kernel
+//    keeps the layout that suits the occupancy it is chosen for.
+// Checkpoints are taken where every state is reachable (k <= K for beta, k >= 4 for alpha), so no
+// -inf is ever stored.
+template <bool Q16, bool REC>
 MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const float (&b)[8]) {
+  if constexpr (!REC) {
+#pragma unroll
+    for (int s = 1; s < 8; s++) scr_st<Q16>(scr, ck0 + (size_t)c * 8, lane, b[s], s - 1);
+    return;
+  }
   constexpr uint32_t NW = Q16 ? 4 : 8, ESZ = Q16 ? 2 : 4;
   uint32_t w[NW];
   if constexpr (Q16) {
@@ -379,8 +389,16 @@ MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const f
   memcpy(reinterpret_cast<char*>(scr) + so + vo, w, sizeof(w));
 #endif
 }
-template <bool Q16>
+template <bool Q16, bool REC>
 MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane, TdecWin<Q16>& r) {
+  if constexpr (!REC) {
+#pragma unroll
+    for (int s = 1; s < 8; s++) {
+      const auto v = scr_raw<Q16>(scr, ck0 + (size_t)c * 8, lane, s - 1);
+      r.ck[s - 1] = __builtin_bit_cast(uint32_t, v);
+    }
+    return;
+  }
   constexpr uint32_t NW = Q16 ? 4 : 8, ESZ = Q16 ? 2 : 4;
   const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * ESZ), vo = (uint32_t)lane * 8 * ESZ;
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
@@ -395,10 +413,11 @@ MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane
   memcpy(r.ck, reinterpret_cast<const char*>(scr) + so + vo, NW * 4);
 #endif
 }
-// state s (1..7) of a raw checkpoint record
-template <bool Q16>
+// state s (1..7) of a raw checkpoint
+template <bool Q16, bool REC>
 MI_HD inline float ck_state(const uint32_t* ck, int s) {
-  if constexpr (Q16) return (float)(int16_t)(uint16_t)(ck[(s - 1) >> 1] >> (16 * ((s - 1) & 1)));
+  if constexpr (!REC) return Q16 ? (float)(int32_t)ck[s - 1] : __builtin_bit_cast(float, ck[s - 1]);
+  else if constexpr (Q16) return (float)(int16_t)(uint16_t)(ck[(s - 1) >> 1] >> (16 * ((s - 1) & 1)));
   else return __builtin_bit_cast(float, ck[s - 1]);
 }
 
@@ -483,7 +502,7 @@ MI_HD inline void tdec_beta_window_mkq(const TdecArgs& a, int lane, const TdecWi
 
 // forward steps of one window: beta_{base+1..base+W} recomputed in registers from the window's
 // closing checkpoint, then alpha and the LLRs
-template <bool DEC2, bool Q16, bool SQ>
+template <bool DEC2, bool Q16, bool SQ, bool REC = false>
 MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base, float (&al)[8],
                                     TdecCrc& crc) {
   float xs[BETA_W], xp[BETA_W];
@@ -492,7 +511,7 @@ MI_HD inline void tdec_alpha_window(const TdecArgs& a, int lane, const TdecWin<Q
   float bw[BETA_W][8];
   bw[BETA_W - 1][0] = 0.0f;
 #pragma unroll
-  for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = ck_state<Q16>(w.ck, s);
+  for (int s = 1; s < 8; s++) bw[BETA_W - 1][s] = ck_state<Q16, REC>(w.ck, s);
 #pragma unroll
   for (int i = BETA_W - 2; i >= 0; i--) beta_step<!Q16>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
@@ -554,7 +573,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     }
     norm8<Q16>(b);
   }
-  ck_store<Q16>(a.scr, ck, nw, lane, b);
+  ck_store<Q16, false>(a.scr, ck, nw, lane, b);
   // ---- backward pass (window j closes with checkpoint j; window 0's betas are not stored)
   auto load = [&](uint32_t w, TdecWin<Q16>& r) {
     if constexpr (MKQ) tdec_load_window_sb<FIRST, Q16>(a, lane, w * BETA_W, r);
@@ -566,7 +585,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   };
   auto fload = [&](uint32_t w, TdecWin<Q16>& r) {
     tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
-    ck_load_raw<Q16>(a.scr, ck, w + 1, lane, r);
+    ck_load_raw<Q16, false>(a.scr, ck, w + 1, lane, r);
   };
   float al[8];
 #pragma unroll
@@ -585,15 +604,15 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
       load(lo(j - 2), C);
       beta(A, j);
       if (j == 0) break;
-      ck_store<Q16>(a.scr, ck, j, lane, b);
+      ck_store<Q16, false>(a.scr, ck, j, lane, b);
       load(lo(j - 3), A);
       beta(B, j - 1);
       if (j == 1) break;
-      ck_store<Q16>(a.scr, ck, j - 1, lane, b);
+      ck_store<Q16, false>(a.scr, ck, j - 1, lane, b);
       load(lo(j - 4), B);
       beta(C, j - 2);
       if (j == 2) break;
-      ck_store<Q16>(a.scr, ck, j - 2, lane, b);
+      ck_store<Q16, false>(a.scr, ck, j - 2, lane, b);
     }
     // ---- forward pass: window j closes with checkpoint j + 1
     fload(0, A);
@@ -615,11 +634,11 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     for (uint32_t j = nw - 1;; j -= 2) {
       load(j - 1, B);
       beta(A, j);
-      ck_store<Q16>(a.scr, ck, j, lane, b);
+      ck_store<Q16, false>(a.scr, ck, j, lane, b);
       load(j >= 3 ? j - 2 : 1, A);   // last round: a harmless reload
       beta(B, j - 1);
       if (j == 1) break;
-      ck_store<Q16>(a.scr, ck, j - 1, lane, b);
+      ck_store<Q16, false>(a.scr, ck, j - 1, lane, b);
     }
     // ---- forward pass: windows 0 (A), 1 (B), ...; window j closes with checkpoint j + 1
     fload(0, A);
@@ -716,7 +735,7 @@ MI_HD inline void tdec_alpha_only_window_mkq(const TdecArgs& a, int lane, const 
 
 // phase-2 window of wave B: alpha of the window recomputed from its opening checkpoint (window 0:
 // the known start state), then backward steps emitting the LLRs (beta carried in b)
-template <bool DEC2, bool Q16, bool SQ>
+template <bool DEC2, bool Q16, bool SQ, bool REC = true>
 MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                         float (&b)[8], TdecCrc& crc) {
   float xs[BETA_W], xp[BETA_W];
@@ -725,7 +744,7 @@ MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecW
   float aw[BETA_W][8];
   aw[0][0] = 0.0f;
 #pragma unroll
-  for (int s = 1; s < 8; s++) aw[0][s] = base ? ck_state<Q16>(w.ck, s) : -INFINITY;
+  for (int s = 1; s < 8; s++) aw[0][s] = base ? ck_state<Q16, REC>(w.ck, s) : -INFINITY;
 #pragma unroll
   for (int i = 0; i < BETA_W - 1; i++) {
 #pragma unroll
@@ -806,7 +825,7 @@ struct TdecX {
     pipe_windows<PF, Win>(
         (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
-          if (w) ck_store<Q16>(a.scr, ck, w, lane, al);
+          if (w) ck_store<Q16, true>(a.scr, ck, w, lane, al);
           if constexpr (MKQ) tdec_alpha_only_window_mkq<Q16>(a, lane, r, w * BETA_W, al);
           else tdec_alpha_only_window<DEC2, Q16, SQB>(r, w * BETA_W, a.F, al);
         });
@@ -819,9 +838,9 @@ struct TdecX {
         (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
         [&](uint32_t w, Win& r) {
           tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
-          ck_load_raw<Q16>(a.scr, ck, w + 1, lane, r);
+          ck_load_raw<Q16, true>(a.scr, ck, w + 1, lane, r);
         },
-        [&](const Win& r, uint32_t w) { tdec_alpha_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, al, crc); });
+        [&](const Win& r, uint32_t w) { tdec_alpha_window<DEC2, Q16, SQF, true>(a, lane, r, w * BETA_W, al, crc); });
   }
   // wave B, phase 1: tail, then beta_{K} .. beta_{K/2}
   MI_HD static void b1(const TdecArgs& a, int lane, float (&b)[8]) {
@@ -862,13 +881,13 @@ struct TdecX {
       }
       norm8<Q16>(b);
     }
-    ck_store<Q16>(a.scr, ck, nw, lane, b);
+    ck_store<Q16, true>(a.scr, ck, nw, lane, b);
     pipe_windows<PF, Win>(
         (int)(nw - h), [nw](int i) { return nw - 1 - (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
           if constexpr (MKQ) tdec_beta_window_mkq<Q16>(a, lane, r, w * BETA_W, b);
           else tdec_beta_window<DEC2, Q16, SQB>(r, w * BETA_W, a.F, b);
-          if (w > h) ck_store<Q16>(a.scr, ck, w, lane, b);
+          if (w > h) ck_store<Q16, true>(a.scr, ck, w, lane, b);
         });
   }
   // wave B, phase 2: windows h-1 .. 0 backward (LLRs of steps 0 .. K/2-1)
@@ -879,7 +898,7 @@ struct TdecX {
         (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
         [&](uint32_t w, Win& r) {
           tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
-          ck_load_raw<Q16>(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
+          ck_load_raw<Q16, true>(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
         },
         [&](const Win& r, uint32_t w) { tdec_beta_emit_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, b, crc); });
   }
