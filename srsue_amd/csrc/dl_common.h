@@ -165,4 +165,5 @@ struct MiTbDesc {            // one per transport block
   uint32_t tbs, C, Kp, Km, Cm, F;
   uint32_t cb_list;          // offset into the lane-index list: C entries, CB r -> MiLaneDesc index
   uint32_t pay_off;          // byte offset into payload buffer
+  uint32_t crc_mul;          // kdata offset of C multipliers x^(8 bytes after CB r) mod g24A (tb_kernel)
 };

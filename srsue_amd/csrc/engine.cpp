@@ -173,7 +173,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
                 d_cbits.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(),
-                d_cblist.as<uint32_t>(), st);
+                d_cblist.as<uint32_t>(), d_kdata.as<uint32_t>(), st);
     mark(6);
   } else {
     for (int i = 3; i <= 6; i++) mark(i);

@@ -46,6 +46,6 @@ void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, con
 // TB assembly + CRC24A + payload packing
 void launch_tb(const uint8_t* cb_bytes, uint8_t* payload, uint32_t* tb_crc_ok, uint32_t* tb_its,
                const uint32_t* cb_its, const uint32_t* cb_tbp, const MiTbDesc* tbs, uint32_t n_tb,
-               const uint32_t* cb_list, hipStream_t st);
+               const uint32_t* cb_list, const uint32_t* kdata, hipStream_t st);
 
 }  // namespace mi

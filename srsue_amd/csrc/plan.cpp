@@ -1,6 +1,7 @@
 // plan.cpp -- batch planner (see engine.cpp header): RE lists, scrambling words, CRS tables,
 // code-block segmentation, rate-matching splits and 64-lane grouping of equal-K code blocks.
 #include "plan.h"
+#include "tb_body.h"
 
 #include <math.h>
 #include <string.h>
@@ -305,6 +306,24 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     // order by CB index r: CBs with K- precede K+ ones (36.212 5.1.2), K runs are sorted ascending
     tbs[s].cb_list = (uint32_t)cb_list.size();
     cb_list.insert(cb_list.end(), v.begin(), v.end());
+  }
+  // TB-CRC multipliers per segmentation: CB r's partial CRC register is shifted over the payload bytes
+  // that follow it (tb_body.h tb_crc_term), precomputed once per distinct TB shape
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> mul_off;
+  for (uint32_t s = 0; s < n; s++) {
+    MiTbDesc& t = tbs[s];
+    const auto key = std::make_tuple(t.tbs, t.C, t.Kp, t.Km, t.Cm, t.F);
+    auto it = mul_off.find(key);
+    if (it == mul_off.end()) {
+      const uint32_t off = (uint32_t)kdata.size();
+      for (uint32_t r = 0; r < t.C; r++) {
+        uint32_t after = 0;
+        for (uint32_t j = r + 1; j < t.C; j++) after += tb_cb_nbytes(t, j);
+        kdata.push_back(gf24_xpow8(after, CRC24A_POLY));
+      }
+      it = mul_off.emplace(key, off).first;
+    }
+    t.crc_mul = it->second;
   }
   return 0;
 }
