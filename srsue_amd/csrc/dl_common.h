@@ -130,6 +130,8 @@ struct MiKTab {              // per K, device resident
   uint32_t pi_off;           // uint32 offset: pi[K]
   uint32_t crca_off;         // uint32 offset: CRC24A contribution of a single 1 at bit i, [K]
   uint32_t crcb_off;         // uint32 offset: same for CRC24B
+  uint32_t ipos_off;         // uint32 offset: ipos[Ncb] decoder input index of circular-buffer position p
+                             // (the inverse of pos; 0xFFFFFFFF at dummy / null positions)
 };
 
 namespace mi {

@@ -73,8 +73,11 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
   std::vector<uint8_t> dec(K), pk(K / 8);
   c.q = q.data(); c.pi = pi.data(); c.d = d.data(); c.w = w.data(); c.dec = dec.data();
   c.bck = bck.data(); c.ack = ack.data(); c.bend = bend.data(); c.aend = aend.data();
+  std::vector<uint8_t> lmap((g.Ncb + 15) / 16 * 16);
+  c.lmap = lmap.data();
+  for (uint32_t t = 0; t < P; t++) mi::win_load_map(c, t, P, sbg, g.Ncb);
   for (uint32_t t = 0; t < P; t++)
-    mi::win_load(c, t, P, sbg, g.Ncb, kdata + kt.pos_off, kdata + kt.pi_off, lane, ld.F);
+    mi::win_load(c, t, P, sbg, g.Ncb, kdata + kt.ipos_off, kdata + kt.pi_off, lane, ld.F);
   const uint32_t* tab = kdata + (ld.crc24a ? kt.crca_off : kt.crcb_off);
   mi::TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < max_its; it++) {

@@ -21,15 +21,17 @@ static size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 void Plan::add_ktab(uint32_t K) {
   auto& kp = kpos_cache[K];
   if (kp.empty()) {
-    kp.resize(4);
+    kp.resize(5);
     cb_pos_table(K, kp[0]);
     qpp_table(K, kp[1]);
     crc_bit_table(K, 0x864CFBu, kp[2]);
     crc_bit_table(K, 0x800063u, kp[3]);
+    kp[4].assign(ncb_of(K), 0xFFFFFFFFu);   // inverse of pos (tdec_win_body.h win_load)
+    for (uint32_t i = 0; i < (uint32_t)kp[0].size(); i++) kp[4][kp[0][i]] = i;
   }
-  MiKTab t{K, ncb_of(K), 0, 0, 0, 0};
-  uint32_t* offs[4] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off};
-  for (int q = 0; q < 4; q++) {
+  MiKTab t{K, ncb_of(K), 0, 0, 0, 0, 0};
+  uint32_t* offs[5] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off, &t.ipos_off};
+  for (int q = 0; q < 5; q++) {
     *offs[q] = (uint32_t)kdata.size();
     kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
   }

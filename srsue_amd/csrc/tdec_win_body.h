@@ -52,6 +52,8 @@ struct WinCb {
   int16_t* ack;      // [(K/4 + 1) * 8] alpha checkpoints: alpha at step 4v
   int16_t* bend;     // [nseg * 8] beta at each segment's first step (its left boundary)
   int16_t* aend;     // [nseg * 8] alpha after each segment's last step (its right boundary)
+  uint8_t* lmap;     // [Ncb, rounded to 16] the group's softbuffer row map, staged for win_load only (on
+                     // the GPU it borrows the checkpoint arrays, unused until the first half-iteration)
   uint32_t K, S, nseg;
 };
 
@@ -242,30 +244,42 @@ MI_HD inline bool win_fwd_fix(const WinCb& c, uint32_t j, const float (&na)[8]) 
 // ---- load / CRC / packing (cooperative loops over the code block, thread t of P) ----------------------
 // decoder inputs of the lane `lane` of a group softbuffer (rate de-matching's layout, dl_common.h):
 // q(x) of the materialised rows, 0 for the others; filler steps k < F: DEC1 systematic/parity = -511
-MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb, const uint32_t* pos,
-                           const uint32_t* pi32, uint32_t lane, uint32_t F) {
-  // batches of B independent position -> row-map -> value chains per thread, all of a batch's loads of
-  // one kind issued before the next kind (each chain is three dependent global loads)
-  constexpr uint32_t B = 8;
+// load, step 1: the group's row map (one byte per circular-buffer position) into c.lmap, 16-byte
+// pieces (the map region is 256-byte aligned and rounded up to 256 bytes, dl_common.h)
+MI_HD inline void win_load_map(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb) {
   const uint8_t* map = reinterpret_cast<const uint8_t*>(sbg + sb_map_off(Ncb));
-  const uint32_t n = 3 * c.K + 12;
-  for (uint32_t i0 = t; i0 < n; i0 += B * P) {
-    uint32_t pp[B];
-    uint8_t mm[B];
+  for (uint32_t i = 16 * t; i < Ncb; i += 16 * P) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *reinterpret_cast<uint4*>(c.lmap + i) = *reinterpret_cast<const uint4*>(map + i);
+#else
+    memcpy(c.lmap + i, map + i, 16);
+#endif
+  }
+}
+// load, step 2 (after a barrier): walk the circular buffer in position order -- row p of this lane
+// (0 when the row is not materialised, c.lmap) goes, quantised, to decoder input ipos[p] in LDS.  The
+// position-table and softbuffer loads of a batch are independent (one round trip per batch of B per
+// thread) and consecutive threads read consecutive rows.  (Gathering in decoder order -- position,
+// then map, then value: three dependent loads, B = 8 -- was 53 us of a 174 us single-subframe decode.)
+MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb,
+                           const uint32_t* ipos, const uint32_t* pi32, uint32_t lane, uint32_t F) {
+#ifndef MI_WIN_LOAD_B
+#define MI_WIN_LOAD_B 24
+#endif
+  constexpr uint32_t B = MI_WIN_LOAD_B;
+  for (uint32_t p0 = t; p0 < Ncb; p0 += B * P) {
+    uint32_t ii[B];
     float xx[B];
 #pragma unroll
     for (uint32_t b = 0; b < B; b++) {
-      const uint32_t i = i0 + b * P;
-      pp[b] = i < n ? pos[i] : 0u;
+      const uint32_t p = p0 + b * P;
+      ii[b] = p < Ncb ? ipos[p] : 0xFFFFFFFFu;
+      xx[b] = (p < Ncb && c.lmap[p]) ? sbg[(size_t)p * LANES + lane] : 0.0f;
     }
 #pragma unroll
-    for (uint32_t b = 0; b < B; b++) mm[b] = i0 + b * P < n ? map[pp[b]] : 0;
-#pragma unroll
-    for (uint32_t b = 0; b < B; b++) xx[b] = mm[b] ? sbg[(size_t)pp[b] * LANES + lane] : 0.0f;
-#pragma unroll
     for (uint32_t b = 0; b < B; b++) {
-      const uint32_t i = i0 + b * P;
-      if (i >= n) break;
+      const uint32_t i = ii[b];
+      if (i == 0xFFFFFFFFu) continue;
       float x = q16f(xx[b]);
       if (i < 3 * F && i % 3 != 2) x = -I16_CI;
       c.q[i] = (int16_t)x;
