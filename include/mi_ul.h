@@ -9,7 +9,7 @@
  * Chain (gfx950 kernels, srsue_amd/csrc/ul.hip): TB CRC24A -> segmentation + CRC24B -> turbo encoder
  * (36.212 5.1.3.2, chunk-parallel recursive encoders) -> rate matching (5.1.4.1, full circular buffer)
  * -> channel interleaver (5.2.2.8, no UCI) -> scrambling (36.211 5.3.1) -> modulation (7.1) ->
- * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, no hopping) +
+ * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, per-slot PRBs) +
  * DMRS (5.5.2.1, L_prb >= 3) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
  * HARQ-ACK bits (1 or 2) are multiplexed as 36.212 5.2.2.6 / 5.2.2.8 prescribe (Q'_ACK coded symbols
  * puncturing the data next to the DMRS); CQI / RI on PUSCH are not supported.
@@ -31,6 +31,8 @@ typedef struct {
   uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI format 0 cyclic-shift field (0..7) */
   uint32_t ack_len, ack, I_offset_ack;                 /* HARQ-ACK on PUSCH (36.212 5.2.2.6): 0, 1 or 2 bits
                                                           (bit 0 = first), beta_offset index (36.213 8.6.3-1) */
+  uint32_t hop, n_prb1;                                /* hop = 1: slot 1 starts at PRB n_prb1 (frequency hopping,
+                                                          36.213 8.4 -- the per-TTI API computes it from the DCI) */
 } mi_ul_cfg_t;
 
 enum { MI_UL_STAGE_CRC = 0, MI_UL_STAGE_ENCODE, MI_UL_STAGE_MOD, MI_UL_NSTAGES };

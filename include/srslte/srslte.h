@@ -265,7 +265,9 @@ SRSLTE_API void srslte_vec_free(void *ptr);
  * -> channel interleaver -> scrambling -> modulation -> transform precoding + DMRS -> SC-FDMA and copies
  * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  HARQ-ACK in uci_data (1 or 2 bits) is
  * multiplexed into the PUSCH (36.212 5.2.2.6, beta_offset from set_cfg's uci_cfg.I_offset_ack).  Limits:
- * no CQI / RI on PUSCH (returns SRSLTE_ERROR), no frequency hopping, L_prb >= 3; PUCCH, SRS and UL
+ * no CQI / RI on PUSCH (returns SRSLTE_ERROR), PUSCH hopping type 1 only (36.213 8.4.1: DCI format 0 hopping
+ * bits through srslte_dci_msg_to_ul_grant's n_rb_ho, intra- or inter-subframe mode from set_cfg's hopping
+ * configuration; type 2 returns SRSLTE_ERROR), L_prb >= 3; PUCCH, SRS and UL
  * power control stay in srsLTE.  set_cfg uses the DMRS and hopping configurations, the others are
  * accepted.  set_normalization(true) scales by nof_prb / (15 sqrt(L_prb)) (srsLTE's factor as recorded
  * in DESIGN.md, unverified: srsLTE is not in the container); set_cfo(cfo) shifts the output by cfo

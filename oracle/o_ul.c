@@ -17,7 +17,8 @@
  *          does not carry): ZC root q of N_ZC = largest prime < M_sc, group hopping f_gh, sequence
  *          hopping v (M_sc >= 72), f_ss = (N_ID + delta_ss) mod 30, alpha = 2 pi n_cs / 12 with
  *          n_cs = (n1_DMRS[cyclic_shift] + n2_DMRS[dci field] + n_PRS(n_s)) mod 12, symbol 3 of each slot;
- *   mapping (5.3.4): PRBs n_prb .. n_prb + L - 1 of symbols 0-2, 4-6 of each slot (no hopping);
+ *   mapping (5.3.4): PRBs n_prb .. n_prb + L - 1 of symbols 0-2, 4-6 of slot 0, and of slot 1 unless
+ *          frequency hopping moves slot 1 to n_prb1 .. n_prb1 + L - 1 (36.213 8.4, computed by the caller);
  *   SC-FDMA (5.6): s[n] = (1/sqrt N) sum_k a_k exp(j 2 pi (k - 6 N_RB + 1/2) n / N), n = -N_CP .. N-1.
  */
 #include "oracle.h"
@@ -176,6 +177,7 @@ int or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r) {
 int or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid) {
   const uint32_t W = 12 * c->nof_prb, M = 12 * c->L_prb, G = or_pusch_G(c);
   if (c->n_prb + c->L_prb > c->nof_prb || M < 36) return -1;
+  if (c->hop && c->n_prb1 + c->L_prb > c->nof_prb) return -1;
   uint8_t *f = (uint8_t *)malloc(G);
   float *x = (float *)malloc(sizeof(float) * 2 * 12 * M), *z = (float *)malloc(sizeof(float) * 2 * M);
   if (or_ulsch_encode(c, tb, f) < 0) { free(f); free(x); free(z); return -1; }
@@ -183,7 +185,8 @@ int or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid) {
   memset(grid, 0, sizeof(float) * 2 * OR_NSYMB * W);
   uint32_t ds = 0;
   for (uint32_t l = 0; l < OR_NSYMB; l++) {
-    float *g = grid + 2 * ((size_t)l * W + 12 * c->n_prb);
+    const uint32_t n0 = (c->hop && l >= 7) ? c->n_prb1 : c->n_prb;
+    float *g = grid + 2 * ((size_t)l * W + 12 * n0);
     if (l % 7 == 3) {
       or_dmrs_pusch(c, 2 * c->sf_idx + l / 7, z);
     } else {

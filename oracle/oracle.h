@@ -231,6 +231,7 @@ typedef struct {
   uint32_t group_hopping, sequence_hopping, delta_ss;  /* DMRS cell configuration */
   uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI 0 cyclic-shift field (0..7) */
   uint32_t ack_len, ack, I_offset_ack;                 /* HARQ-ACK on PUSCH: 0..2 bits (bit 0 = o0), beta index */
+  uint32_t hop, n_prb1;                                /* hop = 1: slot 1 starts at PRB n_prb1 (36.213 8.4) */
 } or_ul_cfg_t;
 double   or_pam_level(const uint8_t *b, uint32_t Qm);
 uint32_t or_pusch_G(const or_ul_cfg_t *c);

@@ -558,12 +558,15 @@ UL_STAGES = ("crc", "encode", "mod")
 class UlCfg(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "sf_idx", "rnti", "n_prb", "L_prb", "tbs", "Qm", "rv",
                                           "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2",
-                                          "ack_len", "ack", "I_offset_ack")]
+                                          "ack_len", "ack", "I_offset_ack", "hop", "n_prb1")]
 
 
 def ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=0, Qm=4, rv=0, gh=0, sh=0, dss=0,
-           cs=0, n2=0, ack_len=0, ack=0, ioff=0):
-    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2, ack_len, ack, ioff)
+           cs=0, n2=0, ack_len=0, ack=0, ioff=0, n_prb1=None):
+    """n_prb1: start PRB of slot 1 (frequency hopping), None = no hopping"""
+    hop, n1 = (0, 0) if n_prb1 is None else (1, n_prb1)
+    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2, ack_len, ack, ioff,
+                 hop, n1)
 
 
 class UlBatch:

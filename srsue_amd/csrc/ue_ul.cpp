@@ -38,6 +38,9 @@ int ul_mcs(uint32_t mcs, uint32_t* qm, uint32_t* itbs) {
   return -1;
 }
 
+// 36.213 8.4: N~_HO = N_HO rounded up to even (pusch-HoppingOffset)
+uint32_t ul_nho_tilde(uint32_t n_rb_ho) { return n_rb_ho + (n_rb_ho & 1u); }
+
 // fill the grant of a contiguous allocation (type 2 RIV, 36.213 8.1.1 / 36.212 5.3.3.1.1)
 int grant_from_riv(uint32_t riv, uint32_t nof_prb, uint32_t mcs, uint32_t n_dmrs, srslte_ra_ul_dci_t* dci,
                    srslte_ra_ul_grant_t* g) {
@@ -126,7 +129,7 @@ void srslte_ue_ul_set_cfg(srslte_ue_ul_t* q, srslte_refsignal_dmrs_pusch_cfg_t* 
 int srslte_ue_ul_cfg_grant(srslte_ue_ul_t* q, srslte_ra_ul_grant_t* grant, uint32_t tti, uint32_t rvidx,
                            uint32_t current_tx_nb) {
   if (!q || !q->ctx || !grant) return SRSLTE_ERROR_INVALID_INPUTS;
-  if (grant->freq_hopping) { mi::set_error("PUSCH frequency hopping is not supported"); return SRSLTE_ERROR; }
+  if (grant->freq_hopping > 1) { mi::set_error("PUSCH hopping type 2 is not supported"); return SRSLTE_ERROR; }
   mi::CbSegm sg;
   if (grant->mcs.tbs <= 0 || mi::cbsegm((uint32_t)grant->mcs.tbs, &sg)) return SRSLTE_ERROR;
   q->pusch_cfg.grant = *grant;
@@ -146,6 +149,22 @@ int srslte_ue_ul_cfg_grant(srslte_ue_ul_t* q, srslte_ra_ul_grant_t* grant, uint3
   c.nof_prb = q->cell.nof_prb;
   c.sf_idx = tti % 10;
   c.n_prb = grant->n_prb[0];
+  c.hop = 0;
+  c.n_prb1 = 0;
+  if (grant->freq_hopping == 1) {
+    // 36.213 8.4.1, type 1: n_PRB = n~_PRB + N~_HO / 2; slot 1 hops (intra-subframe mode), or the whole
+    // subframe takes the hopped position when CURRENT_TX_NB is odd (inter-subframe mode)
+    const uint32_t ho = ul_nho_tilde(q->hopping_cfg.hopping_offset) / 2;
+    const uint32_t a = grant->n_prb_tilde[0] + ho, b = grant->n_prb_tilde[1] + ho;
+    const bool intra = q->hopping_cfg.hop_mode == srslte_pusch_hopping_cfg_t::SRSLTE_PUSCH_HOP_MODE_INTRA_SF;
+    const uint32_t s0 = intra ? a : (current_tx_nb & 1u) ? b : a, s1 = intra ? b : s0;
+    if (s0 + grant->L_prb > q->cell.nof_prb || s1 + grant->L_prb > q->cell.nof_prb) return SRSLTE_ERROR;
+    c.n_prb = s0;
+    c.hop = s1 != s0;
+    c.n_prb1 = s1;
+    q->pusch_cfg.grant.n_prb[0] = s0;
+    q->pusch_cfg.grant.n_prb[1] = s1;
+  }
   c.L_prb = grant->L_prb;
   c.tbs = (uint32_t)grant->mcs.tbs;
   c.Qm = grant->Qm;
@@ -218,7 +237,7 @@ void srslte_softbuffer_tx_free(srslte_softbuffer_tx_t* q) {
   memset(q, 0, sizeof(*q));
 }
 
-int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t* msg, uint32_t nof_prb, uint32_t /*n_rb_ho*/, srslte_ra_ul_dci_t* dci,
+int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t* msg, uint32_t nof_prb, uint32_t n_rb_ho, srslte_ra_ul_dci_t* dci,
                                srslte_ra_ul_grant_t* grant, uint32_t /*tti*/) {
   if (!msg || !dci || !grant || mi::symbol_sz(nof_prb) < 0) return SRSLTE_ERROR_INVALID_INPUTS;
   memset(dci, 0, sizeof(*dci));
@@ -226,15 +245,31 @@ int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t* msg, uint32_t nof_prb, uint32_t
   // 36.212 5.3.3.1.1: flag, hopping flag, RIV, MCS/RV, NDI, TPC, cyclic shift DM RS, CQI request
   uint32_t pos = 1;
   dci->freq_hop_fl = take_bits(msg->data, &pos, 1);
-  if (dci->freq_hop_fl) { mi::set_error("PUSCH frequency hopping is not supported"); return SRSLTE_ERROR; }
-  const uint32_t riv = take_bits(msg->data, &pos, rba_bits(nof_prb));
+  // with hopping the resource-allocation field's N_UL_hop MSBs are the hopping bits (36.213 8.4,
+  // Table 8.4-1), the rest is the RIV
+  const uint32_t nh = dci->freq_hop_fl ? (nof_prb < 50 ? 1u : 2u) : 0u;
+  const uint32_t hbits = take_bits(msg->data, &pos, nh);
+  const uint32_t riv = take_bits(msg->data, &pos, rba_bits(nof_prb) - nh);
   const uint32_t mcs = take_bits(msg->data, &pos, 5);
   dci->ndi = take_bits(msg->data, &pos, 1) != 0;
   dci->tpc_pusch = take_bits(msg->data, &pos, 2);
   const uint32_t ncs = take_bits(msg->data, &pos, 3);
   dci->cqi_request = take_bits(msg->data, &pos, 1) != 0;
   dci->rv_idx = mcs > 28 ? mcs - 28 : 0;
-  return grant_from_riv(riv, nof_prb, mcs, ncs, dci, grant);
+  if (grant_from_riv(riv, nof_prb, mcs, ncs, dci, grant)) return SRSLTE_ERROR;
+  if (dci->freq_hop_fl) {
+    // Table 8.4-2: type 1 offsets of the hopped allocation in the PUSCH hopping band of N_RB^PUSCH PRBs;
+    // '1' (N_UL_hop = 1) / '11' (N_UL_hop = 2) select type 2 (subband hopping), not supported
+    if (hbits == (nh == 1 ? 1u : 3u)) { mi::set_error("PUSCH hopping type 2 is not supported"); return SRSLTE_ERROR; }
+    const uint32_t N = nof_prb - ul_nho_tilde(n_rb_ho) - (nof_prb & 1u), s1 = grant->n_prb_tilde[0];
+    if (N == 0 || N > nof_prb || s1 + grant->L_prb > N) return SRSLTE_ERROR;
+    const uint32_t d = nh == 1 ? N / 2 : hbits == 0 ? N / 4 : hbits == 1 ? N - N / 4 : N / 2;
+    const uint32_t s2 = (s1 + d) % N;
+    if (s2 + grant->L_prb > N) return SRSLTE_ERROR;
+    grant->freq_hopping = 1;
+    grant->n_prb_tilde[1] = s2;
+  }
+  return SRSLTE_SUCCESS;
 }
 
 int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t* rar, uint32_t nof_prb, uint32_t /*n_rb_ho*/,

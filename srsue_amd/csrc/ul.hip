@@ -287,7 +287,8 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
   for (uint32_t i = t; i < M; i += UL_THREADS) twm[i] = twg[x.twm_off + i];
   const float sM = rsqrtf((float)M), gN = rsqrtf((float)N) * x.scale;
   constexpr int PM = (UL_MMAX + UL_THREADS - 1) / UL_THREADS;
-  const int off = (int)(12 * x.n_prb) - (int)(x.W / 2);   // allocation's first subcarrier relative to W/2
+  // allocation's first subcarrier relative to W/2 (slot 1 may hop: 36.213 8.4)
+  const int off = (int)(12 * (slot ? x.n_prb1 : x.n_prb)) - (int)(x.W / 2);
   uint32_t pos = (uint32_t)(symbol_offset((int)N, (int)l0) - cp_len((int)N, (int)(l0 % 7)));   // first sample of l0
   __syncthreads();
   for (uint32_t ls = l0 % 7; ls < l0 % 7 + per; ls++) {

@@ -11,6 +11,7 @@ struct MiUlTx {
   uint64_t iq_off;       // float2 offset of its output subframe (15 N samples)
   uint32_t N, W;         // FFT size, 12 N_RB^UL
   uint32_t n_prb, M, Qm; // first PRB, M = 12 L_prb subcarriers, bits per symbol
+  uint32_t n_prb1;       // first PRB of slot 1 (= n_prb without frequency hopping)
   uint32_t sym_off;      // byte offset of its 12 M coded symbols (Qm bits each, first bit = MSB)
   uint32_t scr_off;      // uint32 offset of its scrambling words (36.211 5.3.1, G bits)
   uint32_t pay_off;      // byte offset of its TB payload

@@ -78,7 +78,7 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) {
     const mi_ul_cfg_t& c = cfgs[i];
     const int N = symbol_sz(c.nof_prb);
-    if (N < 0 || c.nof_prb == 0 || c.sf_idx > 9 || c.L_prb < 3 || c.n_prb + c.L_prb > c.nof_prb ||
+    if (N < 0 || c.nof_prb == 0 || c.sf_idx > 9 || c.L_prb < 3 || c.n_prb + c.L_prb > c.nof_prb || (c.hop && c.n_prb1 + c.L_prb > c.nof_prb) ||
         (c.Qm != 2 && c.Qm != 4 && c.Qm != 6) || c.tbs == 0 || c.tbs % 8 || c.rv > 3) {
       set_error("invalid UL configuration (L_prb >= 3, allocation inside the cell, Qm 2/4/6, byte-aligned TBS)");
       return -1;
@@ -87,6 +87,7 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     t.N = (uint32_t)N;
     t.W = 12 * c.nof_prb;
     t.n_prb = c.n_prb;
+    t.n_prb1 = c.hop ? c.n_prb1 : c.n_prb;
     t.M = 12 * c.L_prb;
     t.Qm = c.Qm;
     t.scale = 1.0f;

@@ -8,11 +8,14 @@
  *              srslte_ue_ul_cfg_grant(&ue_ul, grant, tti + 4, rv, tx_nb) (:551),
  *              srslte_ue_ul_pusch_encode_rnti_softbuffer(.., payload, uci_data, softbuffer, rnti, signal) (:555)
  * Input file : int32 hdr[8] = {cell_id, nof_prb, ntx, group_hopping, sequence_hopping, delta_ss, cyclic_shift,
- *              flags (1 = normalisation, 2 = CFO, bits 8-11 = I_offset_ack)} + float cfo; per transmission int32
- *              p[12] = {tti, rnti, rv, use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len, ack} + int32 dci_nof_bits + 64 DCI bit bytes +
+ *              flags (1 = normalisation, 2 = CFO, bits 8-11 = I_offset_ack, bits 12-19 = pusch-HoppingOffset,
+ *              bit 20 = intra-subframe hopping)} + float cfo; per transmission int32
+ *              p[12] = {tti, rnti, rv | CURRENT_TX_NB << 8, use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len,
+ *              ack} + int32 dci_nof_bits + 64 DCI bit bytes +
  *              tbs/8 payload bytes (pass_data = 0: the payload pointer is NULL -- a retransmission from the
  *              softbuffer).
- * Output file: per transmission int32 r[6] = {ret, n_prb, L_prb, tbs, Qm, ncs_dmrs} + SF_LEN cf32 samples.
+ * Output file: per transmission int32 r[7] = {ret, n_prb slot 0, L_prb, tbs, Qm, ncs_dmrs, n_prb slot 1} + SF_LEN
+ *              cf32 samples (the slot PRBs as cfg_grant set them in ue_ul.pusch_cfg.grant).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -53,7 +56,8 @@ int main(int argc, char **argv) {
   dmrs_cfg.sequence_hopping_en = hdr[4] != 0;
   dmrs_cfg.delta_ss = (uint32_t)hdr[5];
   dmrs_cfg.cyclic_shift = (uint32_t)hdr[6];
-  pusch_hopping.hop_mode = SRSLTE_PUSCH_HOP_MODE_INTER_SF;
+  pusch_hopping.hop_mode = (hdr[7] >> 20) & 1 ? SRSLTE_PUSCH_HOP_MODE_INTRA_SF : SRSLTE_PUSCH_HOP_MODE_INTER_SF;
+  pusch_hopping.hopping_offset = (uint32_t)(hdr[7] >> 12) & 255u;
   srslte_ue_ul_set_cfg(&ue_ul, &dmrs_cfg, &srs_cfg, &pucch_cfg, &pucch_sched, &uci_cfg, &pusch_hopping, &power_ctrl);
   srslte_softbuffer_tx_t softbuffer;
   if (srslte_softbuffer_tx_init(&softbuffer, 100)) { fprintf(stderr, "softbuffer_tx\n"); return 3; }
@@ -83,7 +87,8 @@ int main(int argc, char **argv) {
       grant.Qm = (uint32_t)p[7];
       grant.ncs_dmrs = (uint32_t)p[8];
     }
-    if (!ret) ret = srslte_ue_ul_cfg_grant(&ue_ul, &grant, (uint32_t)p[0], (uint32_t)p[2], 0) ? -2 : 0;
+    if (!ret)
+      ret = srslte_ue_ul_cfg_grant(&ue_ul, &grant, (uint32_t)p[0], (uint32_t)p[2] & 255u, (uint32_t)p[2] >> 8) ? -2 : 0;
     srslte_uci_data_t uci_data;
     memset(&uci_data, 0, sizeof(uci_data));
     uci_data.uci_ack_len = (uint32_t)p[10];   /* phch_worker.cc:486-487 */
@@ -92,9 +97,10 @@ int main(int argc, char **argv) {
     if (!ret)
       ret = srslte_ue_ul_pusch_encode_rnti_softbuffer(&ue_ul, p[9] ? payload : NULL, uci_data, &softbuffer,
                                                       (uint16_t)p[1], signal) ? -3 : 0;
-    int32_t r[6] = {ret, (int32_t)grant.n_prb[0], (int32_t)grant.L_prb, grant.mcs.tbs, (int32_t)grant.Qm,
-                    (int32_t)grant.ncs_dmrs};
-    fwrite(r, 4, 6, fo);
+    const srslte_ra_ul_grant_t* gs = ret ? &grant : &ue_ul.pusch_cfg.grant;
+    int32_t r[7] = {ret, (int32_t)gs->n_prb[0], (int32_t)grant.L_prb, grant.mcs.tbs, (int32_t)grant.Qm,
+                    (int32_t)grant.ncs_dmrs, (int32_t)gs->n_prb[1]};
+    fwrite(r, 4, 7, fo);
     fwrite(signal, 8, sflen, fo);
   }
   srslte_softbuffer_tx_free(&softbuffer);

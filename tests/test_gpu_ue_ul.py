@@ -32,7 +32,8 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
             f.write(struct.pack("f", cfo))
             for t in txs:
                 dci = t.get("dci")
-                f.write(struct.pack("12i", t["tti"], t["rnti"], t["rv"], int(dci is not None), t.get("n_prb", 0),
+                f.write(struct.pack("12i", t["tti"], t["rnti"], t["rv"] | (t.get("tx_nb", 0) << 8), int(dci is not None),
+                                    t.get("n_prb", 0),
                                     t.get("L_prb", 0), t["tbs"], t.get("Qm", 0), t.get("ncs", 0),
                                     int(t.get("pass_data", True)), t.get("ack_len", 0), t.get("ack", 0)))
                 f.write(struct.pack("i", dci.nof_bits if dci else 0))
@@ -42,16 +43,16 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
         raw = open(fout, "rb").read()
     out, pos = [], 0
     for _ in txs:
-        r = struct.unpack_from("6i", raw, pos)
-        pos += 24
+        r = struct.unpack_from("7i", raw, pos)[:6] + (struct.unpack_from("7i", raw, pos)[6],)
+        pos += 28
         iq = np.frombuffer(raw[pos:pos + 15 * N * 8], np.float32)
         pos += 15 * N * 8
         out.append((r, iq))
     return out
 
 
-def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None, ioff=0):
-    c = O.ul_cfg(cell_id=cell_id, nof_prb=nof_prb, sf_idx=sf, rnti=t["rnti"], n_prb=t.get("n_prb", 0) if n_prb is None else n_prb,
+def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None, ioff=0, n_prb1=None):
+    c = O.ul_cfg(n_prb1=n_prb1, cell_id=cell_id, nof_prb=nof_prb, sf_idx=sf, rnti=t["rnti"], n_prb=t.get("n_prb", 0) if n_prb is None else n_prb,
                  L_prb=t.get("L_prb") if L is None else L, tbs=t["tbs"], Qm=t.get("Qm") if Qm is None else Qm,
                  rv=t["rv"], gh=dmrs[0], sh=dmrs[1], dss=dmrs[2], cs=dmrs[3], n2=t.get("ncs", 0) if ncs is None else ncs,
                  ack_len=t.get("ack_len", 0), ack=t.get("ack", 0), ioff=ioff)
@@ -94,7 +95,7 @@ def test_dci_format0_grant_and_harq_retransmission():
            dict(tti=41, rnti=0x46, rv=2, dci=m, tbs=T, tb=np.zeros(T // 8, np.uint8), pass_data=False)]
     res = run(1, 100, txs)
     for t, (r, iq) in zip(txs, res):
-        assert r[0] == 0 and r[1:] == (0, 100, T, 4, 3)
+        assert r[0] == 0 and r[1:6] == (0, 100, T, 4, 3) and r[6] == 0
         ref = oracle_iq(1, 100, dict(t, tb=data), t["tti"] % 10, n_prb=0, L=100, Qm=4, ncs=3)
         assert rel_err(iq, ref) < TOL
 
@@ -130,3 +131,28 @@ def test_harq_ack_on_pusch_srsue_call_order(ack):
     for t, (r, iq) in zip(txs, res):
         assert r[0] == 0
         assert rel_err(iq, oracle_iq(9, 50, t, t["tti"] % 10, ioff=6)) < TOL
+
+
+@pytest.mark.parametrize("intra", [True, False])
+def test_type1_frequency_hopping_srsue_call_order(intra):
+    """DCI format 0 with the hopping flag (type 1, 36.213 8.4.1 / Table 8.4-2) through
+    srslte_dci_msg_to_ul_grant(.., n_rb_ho = pusch-HoppingOffset, ..) and cfg_grant: intra-subframe mode
+    moves slot 1; inter-subframe mode moves the whole subframe when CURRENT_TX_NB is odd."""
+    from test_ul_grant import hop_expect
+    n_ho, start, L = 6, 4, 6                          # N_RB^PUSCH = 94, '10': hop by N / 2
+    from srsue_amd import abi
+    T = abi.lib().srslte_ra_tbs_from_idx(19, L)      # MCS 20: 16QAM, I_TBS 19
+    m = format0(100, start, L, 20, ncs=1, hop=1, hbits=2)
+    data = tb(31, T)
+    flags = (n_ho << 12) | ((1 << 20) if intra else 0)
+    txs = [dict(tti=12 + 8 * k, rnti=0x46, rv=0 if k == 0 else 2, tx_nb=k, dci=m, tbs=T, tb=data if k == 0 else
+                np.zeros(T // 8, np.uint8), pass_data=k == 0) for k in range(2)]
+    res = run(3, 100, txs, flags=flags)
+    a = start + n_ho // 2
+    b = hop_expect(100, n_ho, start, 2) + n_ho // 2
+    for k, (t, (r, iq)) in enumerate(zip(txs, res)):
+        s0, s1 = (a, b) if intra else ((b, b) if k % 2 else (a, a))
+        assert r[0] == 0 and (r[1], r[6]) == (s0, s1), (k, r)
+        ref = oracle_iq(3, 100, dict(t, tb=data), t["tti"] % 10, n_prb=s0, L=L, Qm=4, ncs=1,
+                        n_prb1=s1 if s1 != s0 else None)
+        assert rel_err(iq, ref) < TOL

@@ -15,7 +15,7 @@ from srsue_amd import abi
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
-CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [, ack_len, ack, I_offset_ack]
+CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [, ack_len, ack, I_offset_ack [, n_prb1]]
     (100, 0, 100, 39232, 4, 0, 1, 1, 0, 0, 0, 0, 0),     # 20 MHz full band, 16QAM (MCS 20)
     (100, 10, 75, 25456, 6, 2, 4, 7, 0, 1, 3, 2, 5),     # 64QAM, rv 2, sequence hopping
     (50, 5, 24, 5736, 2, 1, 7, 33, 1, 0, 0, 7, 3),       # group hopping, rv 1
@@ -27,14 +27,17 @@ CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [
     (25, 2, 20, 3000, 2, 1, 8, 4, 1, 0, 0, 2, 1, 2, 2, 12),      # 2 ACK bits, QPSK, rv 1, hopping
     (50, 0, 45, 9000, 6, 0, 6, 5, 0, 1, 0, 0, 4, 1, 0, 14),      # NACK, 64QAM, largest beta_offset
     (25, 0, 3, 104, 2, 0, 2, 9, 0, 0, 0, 0, 0, 2, 3, 14),        # Q'_ACK capped at 4 M (tiny TB), filler bits
+    (100, 2, 48, 12216, 4, 0, 5, 3, 0, 0, 0, 1, 0, 0, 0, 0, 50),  # frequency hopping: slot 1 at PRB 50
+    (50, 30, 20, 5736, 6, 1, 7, 8, 1, 0, 0, 2, 6, 1, 1, 9, 4),   # hopping down to PRB 4, ACK, group hopping
 ]
 
 
 def mk(c):
     nof_prb, n_prb, L, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 = c[:13]
-    ack_len, ack, ioff = c[13:] if len(c) > 13 else (0, 0, 0)
+    ack_len, ack, ioff = c[13:16] if len(c) > 13 else (0, 0, 0)
+    n1 = c[16] if len(c) > 16 else None      # slot-1 start PRB (frequency hopping)
     return dict(cell_id=cell, nof_prb=nof_prb, sf_idx=sf, rnti=0x46 + sf, n_prb=n_prb, L_prb=L, tbs=tbs, Qm=Qm, rv=rv,
-                gh=gh, sh=sh, dss=dss, cs=cs, n2=n2, ack_len=ack_len, ack=ack, ioff=ioff)
+                gh=gh, sh=sh, dss=dss, cs=cs, n2=n2, ack_len=ack_len, ack=ack, ioff=ioff, n_prb1=n1)
 
 
 def tb_of(i, tbs):

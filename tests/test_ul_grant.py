@@ -48,10 +48,13 @@ def rba_bits(N):
     return b
 
 
-def format0(N, start, L, mcs, ndi=1, tpc=1, ncs=0, cqi=0, hop=0):
+def format0(N, start, L, mcs, ndi=1, tpc=1, ncs=0, cqi=0, hop=0, hbits=0):
+    """hop = 1: the resource-allocation field starts with the N_UL_hop hopping bits hbits (36.213 8.4)"""
     bits = [0, hop]
     put = lambda v, n: bits.extend((v >> (n - 1 - i)) & 1 for i in range(n))
-    put(riv(N, start, L), rba_bits(N))
+    nh = (1 if N < 50 else 2) if hop else 0
+    put(hbits, nh)
+    put(riv(N, start, L), rba_bits(N) - nh)
     put(mcs, 5); put(ndi, 1); put(tpc, 2); put(ncs, 3); put(cqi, 1)
     n = O.lib().or_dci_size(O.DCI_0, N)
     bits += [0] * (n - len(bits))
@@ -94,10 +97,37 @@ def test_format0_to_grant(built, N, start, L, mcs, ncs):
         (start, L, mcs, ncs, 2, True, True)
 
 
+def hop_expect(N_ul, n_ho, start, hbits):
+    """36.213 8.4.1 / Table 8.4-2 (type 1): the hopped n~_PRB in the PUSCH hopping band"""
+    nho = n_ho + (n_ho & 1)
+    N = N_ul - nho - (N_ul & 1)
+    if N_ul < 50:
+        d = N // 2
+    else:
+        d = {0: N // 4, 1: N - N // 4, 2: N // 2}[hbits]
+    return (start + d) % N
+
+
+# with hopping the RIV has N_UL_hop bits fewer (36.213 8.4): allocations are limited to RIVs that fit
+@pytest.mark.parametrize("N,n_ho,start,L,hbits", [(100, 4, 2, 6, 0), (100, 4, 40, 6, 1), (100, 3, 10, 6, 2),
+                                                  (25, 0, 0, 6, 0), (50, 6, 5, 6, 2), (25, 3, 2, 6, 0)])
+def test_format0_type1_hopping(built, N, n_ho, start, L, hbits):
+    mcs = 10
+    m = format0(N, start, L, mcs, hop=1, hbits=hbits)
+    g, d = UlGrant(), UlDci()
+    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), N, n_ho, C.byref(d), C.byref(g), 3) == 0
+    assert d.freq_hop_fl == 1 and g.freq_hopping == 1 and g.L_prb == L
+    assert (g.n_prb_tilde[0], g.n_prb_tilde[1]) == (start, hop_expect(N, n_ho, start, hbits))
+
+
 def test_format0_rejections(built):
     g, d = UlGrant(), UlDci()
-    m = format0(100, 0, 100, 20, hop=1)
-    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0   # hopping
+    m = format0(100, 0, 6, 20, hop=1, hbits=3)
+    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0   # type 2 hopping
+    m = format0(25, 0, 6, 20, hop=1, hbits=1)
+    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 25, 0, C.byref(d), C.byref(g), 0) != 0    # type 2 hopping
+    m = format0(100, 90, 6, 20, hop=1, hbits=0)
+    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 8, C.byref(d), C.byref(g), 0) != 0   # beyond the band
     m = format0(100, 0, 100, 20)
     m.data[0] = 1                                                                                    # a 1A
     assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0
