@@ -931,11 +931,7 @@ MI_HD inline TdecLaneResult tdec_lane_x(const TdecArgs& a, int lane, Exec& ex) {
         tdec_xhalf<false, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
         tdec_xhalf<true, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
       }
-#if MI_TDEC_X_DIAG_IT0   // register-count diagnostic only
-    } else if (true) {
-#else
     } else if (it < MK) {
-#endif
       tdec_xhalf<false, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
       tdec_xhalf<true, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
     } else if (it == MK) {
