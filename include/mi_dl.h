@@ -72,10 +72,14 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
 #define MI_DL_FLAG_KEEP_LLR  64u
 /* Lane-per-code-block turbo decoder in the crossed schedule: two wavefronts per 64-code-block group, the
  * forward and backward recursions of each half-iteration run concurrently and meet in the middle
- * (bit-identical outputs, tdec_body.h).  Without MI_DL_FLAG_TDEC_X / MI_DL_FLAG_TDEC_LANE the lane form
- * is crossed when the batch has fewer than 2 groups per SIMD; MI_DL_FLAG_TDEC_LANE alone = one
+ * (bit-identical outputs, tdec_body.h).  Without MI_DL_FLAG_TDEC_X / MI_DL_FLAG_TDEC_LANE the int16 lane
+ * form is always crossed (the float one below 2 groups per SIMD); MI_DL_FLAG_TDEC_LANE alone = one
  * wavefront per group. */
 #define MI_DL_FLAG_TDEC_X    128u
+/* with MI_DL_FLAG_TDEC_X: force the crossed kernel's recompute form (metric windows recomputed per step,
+ * 92 VGPRs, 5 waves per SIMD; int16 decoder).  Default: chosen when the batch's wavefronts fit in one
+ * round at 5 but not at 4 waves per SIMD. */
+#define MI_DL_FLAG_TDEC_XR   256u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 
@@ -109,7 +113,8 @@ void   mi_dl_batch_profile_reset(mi_dl_batch_t *b);
 double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = compulsory total */);
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
 /* turbo schedule of the batch: 1 = latency form (MI_DL_FLAG_TDEC_WIN rules), 2 = lane per code block in
- * the crossed schedule (two wavefronts per group), 0 = lane per code block, one wavefront per group */
+ * the crossed schedule (two wavefronts per group), 3 = the same in its recompute form, 0 = lane per code
+ * block, one wavefront per group */
 int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 

@@ -23,7 +23,9 @@ FLAG_IQ_SC16 = 8    # IQ input as UHD sc16 (int16 I/Q, fc32 = sc16 / 32768)
 FLAG_TDEC_WIN = 16  # int16 turbo: force the latency form (one workgroup per code block)
 FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wavefronts
 FLAG_TDEC_X = 128  # lane-per-code-block decoder, crossed schedule (two wavefronts per group)
-SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X}
+FLAG_TDEC_XR = 256  # crossed kernel, recompute form (5 waves per SIMD)
+SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X,
+               "lanexr": FLAG_TDEC_LANE | FLAG_TDEC_X | FLAG_TDEC_XR}
 FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
 
 
@@ -270,7 +272,7 @@ class Batch:
     @property
     def turbo_sched(self):
         """'win' (latency form), 'lanex' (lane per code block, two wavefronts per group) or 'lane'"""
-        return {1: "win", 2: "lanex"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
+        return {1: "win", 2: "lanex", 3: "lanexr"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
 
     @property
     def n_groups(self):
@@ -533,7 +535,7 @@ class TdecBatch:
 
     @property
     def turbo_sched(self):
-        return {1: "win", 2: "lanex"}.get(lib().mi_tdec_turbo_win(self.h), "lane")
+        return {1: "win", 2: "lanex", 3: "lanexr"}.get(lib().mi_tdec_turbo_win(self.h), "lane")
 
     def close(self):
         if self.h:

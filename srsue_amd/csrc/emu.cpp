@@ -20,13 +20,14 @@ extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 
 static uint32_t crc8[256];
 
-// crossed-schedule lane decoder (two wavefronts per group, tdec_body.h tdec_lane_x): 0 = off
+// crossed-schedule lane decoder (two wavefronts per group, tdec_body.h tdec_lane_x): 0 = off, 1 = register
+// form, 2 = recompute form
 static int g_x = 0;
 extern "C" void emu_set_tdec_x(int on) { g_x = on; }
 template <bool Q16>
 static mi::TdecLaneResult emu_lane_x(const mi::TdecArgs& a, int lane) {
   mi::TdecExecHost ex;
-  mi::TdecLaneResult r = mi::tdec_lane_x<Q16>(a, lane, ex);
+  mi::TdecLaneResult r = g_x == 2 ? mi::tdec_lane_x<Q16, true>(a, lane, ex) : mi::tdec_lane_x<Q16, false>(a, lane, ex);
   r.tb_part = mi::tdec_pack(a, lane);
   return r;
 }

@@ -216,13 +216,13 @@ bool Engine::use_win() const {
 }
 
 // lane-per-code-block decoder in the crossed schedule (two wavefronts per group, tdec_body.h)
-// Auto: when the batch has fewer than 2 groups per SIMD (a single wavefront per group leaves the SIMDs
-// latency-bound: configs[0] +29 %, configs[2] +54 %); at the headline's 2.5 groups per SIMD the memory
-// system is the limit and the single-wave form is 3 % faster (profiles/r1/ab_x).
-bool Engine::tdec_crossed() const {
-  if (flags & MI_DL_FLAG_TDEC_X) return true;
-  if (flags & MI_DL_FLAG_TDEC_LANE) return false;
-  if (const char* e = getenv("MI_TDEC_X")) return atoi(e) != 0;   // A/B
+// Lane form schedule.  Crossed (two wavefronts per group, tdec_body.h) by default: the decode time is
+// each wavefront's serial chain (profiles/r1/sfsweep).  Its register form holds 4 waves per SIMD; when
+// the batch's 2 G wavefronts do not fit at 4 but fit at 5 per SIMD (the headline: 2,540 groups), the
+// recompute form (92 VGPRs) keeps them all resident in one round (-6 % at the headline; at lower
+// occupancy its extra VALU makes it slower than the register form).  MI_DL_FLAG_TDEC_LANE alone = one
+// wavefront per group; MI_DL_FLAG_TDEC_X = crossed; MI_TDEC_X (env, A/B) = 0 / 1 / 2.
+int Engine::tdec_crossed() const {
   static uint32_t simds = 0;
   if (!simds) {
     int dev = 0, cus = 0;
@@ -230,7 +230,14 @@ bool Engine::tdec_crossed() const {
       cus = 256;
     simds = 4u * (uint32_t)cus;
   }
-  return plan.groups.size() < 2ull * simds;
+  const uint64_t waves = 2ull * plan.groups.size();
+  const int form = (q16() && waves > 4ull * simds && waves <= 5ull * simds) ? 2 : 1;
+  if (const char* e = getenv("MI_TDEC_X")) return atoi(e);   // A/B
+  if (flags & MI_DL_FLAG_TDEC_XR) return q16() ? 2 : 1;
+  if (flags & MI_DL_FLAG_TDEC_X) return form;
+  if (flags & MI_DL_FLAG_TDEC_LANE) return 0;
+  if (!q16()) return waves < 4ull * simds ? 1 : 0;   // float decoder: crossed below 2 groups per SIMD (measured)
+  return form;
 }
 
 // turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts

@@ -31,7 +31,7 @@ struct Engine {
   bool q16() const { return (flags & MI_DL_FLAG_TDEC_GEN) == 0; }   // int16 turbo arithmetic (default)
   uint32_t win_threads = 0;   // latency-form turbo: threads per code block (0 = by K)
   bool use_win() const;       // latency-form (segment-parallel) turbo decoder for this plan
-  bool tdec_crossed() const;  // lane-per-code-block decoder with two wavefronts per group
+  int tdec_crossed() const;   // lane form: 0 one wavefront per group, 1 crossed, 2 crossed (recompute form)
   void launch_turbo(float* sb, hipStream_t st);
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables

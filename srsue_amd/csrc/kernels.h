@@ -33,7 +33,7 @@ void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, co
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
                  uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                  const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
-                 uint32_t early_stop, bool q16, bool crossed, hipStream_t st);
+                 uint32_t early_stop, bool q16, int crossed /* 0 one wavefront per group, 1 crossed, 2 crossed recompute */, hipStream_t st);
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
 void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,

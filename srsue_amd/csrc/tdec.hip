@@ -30,7 +30,7 @@ struct TdecExecGpu {
   }
 };
 
-template <bool Q16, bool X>
+template <bool Q16, bool X, bool RC = false>
 __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const uint32_t* __restrict__ wm,
                                            float* __restrict__ scratch, uint8_t* __restrict__ dec, const TdecOut& out,
                                            const MiGroupDesc* __restrict__ groups,
@@ -68,7 +68,7 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const u
   a.crc24a = ld.crc24a;
   if constexpr (X) {
     TdecExecGpu ex{(int)(threadIdx.x / LANES), xcrc};
-    TdecLaneResult r = tdec_lane_x<Q16>(a, lane, ex);
+    TdecLaneResult r = tdec_lane_x<Q16, RC>(a, lane, ex);
     __syncthreads();   // wave B's decisions are visible to wave F, which packs them
     if (ex.wave) return;
     out.its[li] = r.its;
@@ -143,13 +143,26 @@ void tdec_kernel_i16x(const float* __restrict__ sb, const uint32_t* __restrict__
                       const uint32_t* __restrict__ kdata, uint32_t max_its, uint32_t early_stop) {
   tdec_group<true, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
+// crossed, metric windows recomputed per step: 92 VGPRs, 5 waves per SIMD
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(5)))
+void tdec_kernel_i16xr(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
+                       uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
+                       const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
+                       const uint32_t* __restrict__ kdata, uint32_t max_its, uint32_t early_stop) {
+  tdec_group<true, true, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,
-                 bool crossed, hipStream_t st) {
+                 int crossed, hipStream_t st) {
   if (!n_groups) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  if (crossed == 2 && q16) {
+    hipLaunchKernelGGL(tdec_kernel_i16xr, dim3(n_groups), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,
+                       ktabs, ktab_data, max_its, early_stop);
+    return;
+  }
   if (crossed) {
     if (q16)
       hipLaunchKernelGGL(tdec_kernel_i16x, dim3(n_groups), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,

@@ -733,10 +733,44 @@ MI_HD inline void tdec_alpha_only_window_mkq(const TdecArgs& a, int lane, const 
   norm8<Q16>(al);
 }
 
-// phase-2 window of wave B: alpha of the window recomputed from its opening checkpoint (window 0:
+// phase-2 window of wave B: backward steps emitting the LLRs (beta carried in b); the alpha each step
+// needs is recomputed from the window's opening checkpoint (window 0: the known start state) -- i steps
+// for step i, 6 alpha steps per window instead of 3 kept in registers: the 32 VGPRs of a stored alpha
+// window were what held the crossed kernel to 4 waves per SIMD.  Recomputation is the same
+// deterministic recursion, so the values are identical.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MI_OPAQUE8(v) do { _Pragma("unroll") for (int s_ = 0; s_ < 8; s_++) asm volatile("" : "+v"((v)[s_])); } while (0)
+#else
+#define MI_OPAQUE8(v) do { } while (0)
+#endif
+template <bool DEC2, bool Q16, bool SQ>
+MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+                                        float (&b)[8], TdecCrc& crc) {
+  float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    float ai[8];
+    ai[0] = 0.0f;
+#pragma unroll
+    for (int s = 1; s < 8; s++) ai[s] = base ? ck_state<Q16, true>(w.ck, s) : -INFINITY;
+    MI_OPAQUE8(ai);   // no common subexpressions across i: recompute instead of keeping 4 alpha vectors
+#pragma unroll
+    for (int j = 0; j < i; j++) alpha_fwd<!Q16>(ai, xs[j], xp[j]);
+    tdec_emit<DEC2, Q16>(a, lane, base, i, llr_step(ai, b, xs[i], xp[i]), xs[i], w, crc);
+    float nb[8];
+    beta_step<!Q16>(b, xs[i], xp[i], nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+  norm8<Q16>(b);
+}
+
+// phase-2 window of wave B, register form (4 waves per SIMD): alpha of the window recomputed from its opening checkpoint (window 0:
 // the known start state), then backward steps emitting the LLRs (beta carried in b)
 template <bool DEC2, bool Q16, bool SQ, bool REC = true>
-MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+MI_HD inline void tdec_beta_emit_window_reg(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                         float (&b)[8], TdecCrc& crc) {
   float xs[BETA_W], xp[BETA_W];
 #pragma unroll
@@ -760,6 +794,34 @@ MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecW
     for (int s = 0; s < 8; s++) b[s] = nb[s];
   }
   norm8<Q16>(b);
+}
+
+// the forward window of the crossed kernel: like tdec_alpha_window, but the beta each step needs is
+// recomputed from the window's closing checkpoint (3 - i steps for step i) instead of keeping the 4
+// recomputed vectors in registers (same values, 6 beta steps per window instead of 3)
+template <bool DEC2, bool Q16, bool SQ>
+MI_HD inline void tdec_alpha_window_rc(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
+                                       float (&al)[8], TdecCrc& crc) {
+  float xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    float bi[8];
+    bi[0] = 0.0f;
+#pragma unroll
+    for (int s = 1; s < 8; s++) bi[s] = ck_state<Q16, true>(w.ck, s);
+    MI_OPAQUE8(bi);
+#pragma unroll
+    for (int j = BETA_W - 1; j > i; j--) {
+      float nb[8];
+      beta_step<!Q16>(bi, xs[j], xp[j], nb);
+#pragma unroll
+      for (int s = 0; s < 8; s++) bi[s] = nb[s];
+    }
+    tdec_emit<DEC2, Q16>(a, lane, base, i, alpha_step<!Q16>(al, bi, xs[i], xp[i]), xs[i], w, crc);
+  }
+  norm8<Q16>(al);
 }
 
 // software-pipelined walk over n windows widx(0), widx(1), ...: PF = 1 ping-pong buffers (loads one
@@ -804,7 +866,7 @@ MI_HD inline void pipe_windows(int n, Idx widx, Load load, Run run) {
 #define MI_TDEC_XPF_Q 1
 #endif
 // the four phase bodies of one constituent decoder (same source modes as tdec_half)
-template <bool DEC2, bool FIRST, bool Q16, int SRC>
+template <bool DEC2, bool FIRST, bool Q16, int SRC, bool RC>
 struct TdecX {
   static constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = Q16 && SRC == SRC_Q;
@@ -840,7 +902,10 @@ struct TdecX {
           tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
           ck_load_raw<Q16, true>(a.scr, ck, w + 1, lane, r);
         },
-        [&](const Win& r, uint32_t w) { tdec_alpha_window<DEC2, Q16, SQF, true>(a, lane, r, w * BETA_W, al, crc); });
+        [&](const Win& r, uint32_t w) {
+          if constexpr (RC) tdec_alpha_window_rc<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, al, crc);
+          else tdec_alpha_window<DEC2, Q16, SQF, true>(a, lane, r, w * BETA_W, al, crc);
+        });
   }
   // wave B, phase 1: tail, then beta_{K} .. beta_{K/2}
   MI_HD static void b1(const TdecArgs& a, int lane, float (&b)[8]) {
@@ -900,15 +965,18 @@ struct TdecX {
           tdec_load_window<DEC2, FIRST, Q16, SQF>(a, lane, w * BETA_W, r);
           ck_load_raw<Q16, true>(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
         },
-        [&](const Win& r, uint32_t w) { tdec_beta_emit_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, b, crc); });
+        [&](const Win& r, uint32_t w) {
+          if constexpr (RC) tdec_beta_emit_window<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, b, crc);
+          else tdec_beta_emit_window_reg<DEC2, Q16, SQF>(a, lane, r, w * BETA_W, b, crc);
+        });
   }
 };
 
 // one half-iteration in the crossed schedule: ex.run(f, b) runs wave F's and wave B's phase body and
 // then orders them (GPU: each wave its own, then a workgroup barrier; host: both in turn)
-template <bool DEC2, bool FIRST, bool Q16, int SRC, class Exec>
+template <bool DEC2, bool FIRST, bool Q16, int SRC, bool RC, class Exec>
 MI_HD inline void tdec_xhalf(const TdecArgs& a, int lane, Exec& ex, TdecCrc& cF, TdecCrc& cB) {
-  using X = TdecX<DEC2, FIRST, Q16, SRC>;
+  using X = TdecX<DEC2, FIRST, Q16, SRC, RC>;
   float mF[8], mBs[8];
   float(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
@@ -917,7 +985,9 @@ MI_HD inline void tdec_xhalf(const TdecArgs& a, int lane, Exec& ex, TdecCrc& cF,
 
 // the iteration loop of tdec_lane in the crossed schedule (same source-mode sequence); the code-block
 // CRC is the XOR of both waves' partial registers (ex.crc_combine), so both waves stop together
-template <bool Q16, class Exec>
+// RC: metric windows recomputed per step instead of held in registers (92 VGPRs: 5 waves per SIMD, for
+// batches that fit then; more VALU per wave, so the register form is faster when fewer waves are needed)
+template <bool Q16, bool RC, class Exec>
 MI_HD inline TdecLaneResult tdec_lane_x(const TdecArgs& a, int lane, Exec& ex) {
   TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
@@ -925,21 +995,21 @@ MI_HD inline TdecLaneResult tdec_lane_x(const TdecArgs& a, int lane, Exec& ex) {
     constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;
     if (it == 0) {
       if (MK == 0) {
-        tdec_xhalf<false, true, Q16, SRC_MKQ>(a, lane, ex, cF, cB);
-        tdec_xhalf<true, true, Q16, SRC_Q>(a, lane, ex, cF, cB);
+        tdec_xhalf<false, true, Q16, SRC_MKQ, RC>(a, lane, ex, cF, cB);
+        tdec_xhalf<true, true, Q16, SRC_Q, RC>(a, lane, ex, cF, cB);
       } else {
-        tdec_xhalf<false, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
-        tdec_xhalf<true, true, Q16, SRC_SB>(a, lane, ex, cF, cB);
+        tdec_xhalf<false, true, Q16, SRC_SB, RC>(a, lane, ex, cF, cB);
+        tdec_xhalf<true, true, Q16, SRC_SB, RC>(a, lane, ex, cF, cB);
       }
     } else if (it < MK) {
-      tdec_xhalf<false, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
-      tdec_xhalf<true, false, Q16, SRC_SB>(a, lane, ex, cF, cB);
+      tdec_xhalf<false, false, Q16, SRC_SB, RC>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_SB, RC>(a, lane, ex, cF, cB);
     } else if (it == MK) {
-      tdec_xhalf<false, false, Q16, SRC_MKQ>(a, lane, ex, cF, cB);
-      tdec_xhalf<true, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_xhalf<false, false, Q16, SRC_MKQ, RC>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_Q, RC>(a, lane, ex, cF, cB);
     } else {
-      tdec_xhalf<false, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
-      tdec_xhalf<true, false, Q16, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_xhalf<false, false, Q16, SRC_Q, RC>(a, lane, ex, cF, cB);
+      tdec_xhalf<true, false, Q16, SRC_Q, RC>(a, lane, ex, cF, cB);
     }
     r.its = it + 1;
     r.crc_ok = ex.crc_combine(cF.cb ^ cB.cb, lane) == 0;

@@ -25,14 +25,14 @@ CASES = [  # nof_prb, ports, tbs, Qm, snr, sf, rv, cell
 ]
 
 
-@pytest.mark.parametrize("sched", ["lane", "x"])
+@pytest.mark.parametrize("sched", ["lane", "x", "xr"])
 @pytest.mark.parametrize("mode", ["gen", "i16"])
 @pytest.mark.parametrize("nprb,ports,tbs,qm,snr,sf,rv,cid", CASES)
 def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, sf, rv, cid, mode, sched):
     """Planner + rate de-matching + turbo (float gen or int16 SSE arithmetic) + TB assembly, emulated
     lane by lane on the host, against the oracle decoder of the same arithmetic.  sched "x": the
     crossed schedule (two wavefronts per group meeting in the middle of each half-iteration, phases
-    of both waves run in turn as the kernel's barriers order them)."""
+    of both waves run in turn as the kernel's barriers order them); "xr": its recompute form."""
     cfg = abi.sf_cfg(cell_id=cid, nof_prb=nprb, nof_ports=ports, sf_idx=sf, tbs=tbs, Qm=qm, rv=rv)
     tb = tb_bytes(sf, tbs)
     iq = abi.tx_subframe(cfg, tb, snr_db=snr, seed=sf + 7)
@@ -45,7 +45,7 @@ def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, 
     eok = np.zeros(1, np.uint32)
     eits = np.zeros(1, np.uint32)
     abi.emu().emu_set_tdec_i16(int(q16))
-    abi.emu().emu_set_tdec_x(int(sched == "x"))
+    abi.emu().emu_set_tdec_x({"lane": 0, "x": 1, "xr": 2}[sched])
     try:
         rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), 1, np.ascontiguousarray(llr).ctypes.data, 4,
                                       pe.ctypes.data, eok.ctypes.data, eits.ctypes.data, None)

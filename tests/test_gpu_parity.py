@@ -20,7 +20,7 @@ S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
 
 
 # turbo decoders: float (lane per code block), int16 lane per code block, int16 latency form
-DECODERS = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex")]
+DECODERS = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr")]
 
 
 def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None, keep_llr=False):

@@ -25,7 +25,7 @@ def llr_bpsk(d, K, ebno_db, rng):
 
 
 # turbo schedules: float decoder (lane per code block), int16 lane per code block, int16 latency form
-MODES = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex")]
+MODES = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr")]
 
 
 @pytest.mark.parametrize("i16,sched", MODES)
