@@ -799,27 +799,49 @@ MI_HD inline void tdec_beta_emit_window_reg(const TdecArgs& a, int lane, const T
 // the forward window of the crossed kernel: like tdec_alpha_window, but the beta each step needs is
 // recomputed from the window's closing checkpoint (3 - i steps for step i) instead of keeping the 4
 // recomputed vectors in registers (same values, 6 beta steps per window instead of 3)
+static_assert(BETA_W == 4, "the recompute-form windows below are written for 4-step windows");
 template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_alpha_window_rc(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                        float (&al)[8], TdecCrc& crc) {
+  // two-level: beta_{base+2} (= bw[1]) is kept, bw[0] / bw[2] are one step from bw[1] / the checkpoint,
+  // bw[3] is the checkpoint -- 4 recursion steps per window, 8 extra VGPRs
   float xs[BETA_W], xp[BETA_W];
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
+  auto ck = [&](float (&v)[8]) {
+    v[0] = 0.0f;
 #pragma unroll
-  for (int i = 0; i < BETA_W; i++) {
+    for (int s = 1; s < 8; s++) v[s] = ck_state<Q16, true>(w.ck, s);
+    MI_OPAQUE8(v);
+  };
+  auto bstep = [&](float (&v)[8], int j) {
+    float nb[8];
+    beta_step<!Q16>(v, xs[j], xp[j], nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) v[s] = nb[s];
+  };
+  float b1[8];
+  ck(b1);
+  bstep(b1, 3);
+  bstep(b1, 2);   // b1 = bw[1] = beta_{base+2}
+  {
     float bi[8];
-    bi[0] = 0.0f;
 #pragma unroll
-    for (int s = 1; s < 8; s++) bi[s] = ck_state<Q16, true>(w.ck, s);
-    MI_OPAQUE8(bi);
-#pragma unroll
-    for (int j = BETA_W - 1; j > i; j--) {
-      float nb[8];
-      beta_step<!Q16>(bi, xs[j], xp[j], nb);
-#pragma unroll
-      for (int s = 0; s < 8; s++) bi[s] = nb[s];
-    }
-    tdec_emit<DEC2, Q16>(a, lane, base, i, alpha_step<!Q16>(al, bi, xs[i], xp[i]), xs[i], w, crc);
+    for (int s = 0; s < 8; s++) bi[s] = b1[s];
+    bstep(bi, 1);   // bw[0]
+    tdec_emit<DEC2, Q16>(a, lane, base, 0, alpha_step<!Q16>(al, bi, xs[0], xp[0]), xs[0], w, crc);
+  }
+  tdec_emit<DEC2, Q16>(a, lane, base, 1, alpha_step<!Q16>(al, b1, xs[1], xp[1]), xs[1], w, crc);
+  {
+    float bi[8];
+    ck(bi);
+    bstep(bi, 3);   // bw[2]
+    tdec_emit<DEC2, Q16>(a, lane, base, 2, alpha_step<!Q16>(al, bi, xs[2], xp[2]), xs[2], w, crc);
+  }
+  {
+    float bi[8];
+    ck(bi);         // bw[3]
+    tdec_emit<DEC2, Q16>(a, lane, base, 3, alpha_step<!Q16>(al, bi, xs[3], xp[3]), xs[3], w, crc);
   }
   norm8<Q16>(al);
 }
