@@ -743,26 +743,63 @@ MI_HD inline void tdec_alpha_only_window_mkq(const TdecArgs& a, int lane, const 
 #else
 #define MI_OPAQUE8(v) do { } while (0)
 #endif
+#ifndef MI_TDEC_B2_TWO_LEVEL
+#define MI_TDEC_B2_TWO_LEVEL 1
+#endif
 template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                         float (&b)[8], TdecCrc& crc) {
   float xs[BETA_W], xp[BETA_W];
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) tdec_xs_xp<DEC2, Q16, SQ>(w, i, base + i, a.F, xs[i], xp[i]);
+  auto ck = [&](float (&v)[8]) {
+    v[0] = 0.0f;
 #pragma unroll
-  for (int i = BETA_W - 1; i >= 0; i--) {
-    float ai[8];
-    ai[0] = 0.0f;
-#pragma unroll
-    for (int s = 1; s < 8; s++) ai[s] = base ? ck_state<Q16, true>(w.ck, s) : -INFINITY;
-    MI_OPAQUE8(ai);   // no common subexpressions across i: recompute instead of keeping 4 alpha vectors
-#pragma unroll
-    for (int j = 0; j < i; j++) alpha_fwd<!Q16>(ai, xs[j], xp[j]);
+    for (int s = 1; s < 8; s++) v[s] = base ? ck_state<Q16, true>(w.ck, s) : -INFINITY;
+    MI_OPAQUE8(v);
+  };
+  auto emit_back = [&](const float (&ai)[8], int i) {
     tdec_emit<DEC2, Q16>(a, lane, base, i, llr_step(ai, b, xs[i], xp[i]), xs[i], w, crc);
     float nb[8];
     beta_step<!Q16>(b, xs[i], xp[i], nb);
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
+  };
+  if constexpr (MI_TDEC_B2_TWO_LEVEL) {
+    // two-level: alpha_{base+2} kept, 4 recursion steps per window
+    float a2[8];
+    ck(a2);
+    alpha_fwd<!Q16>(a2, xs[0], xp[0]);
+    alpha_fwd<!Q16>(a2, xs[1], xp[1]);
+    {
+      float ai[8];
+#pragma unroll
+      for (int s = 0; s < 8; s++) ai[s] = a2[s];
+      alpha_fwd<!Q16>(ai, xs[2], xp[2]);
+      emit_back(ai, 3);
+    }
+    emit_back(a2, 2);
+    {
+      float ai[8];
+      ck(ai);
+      alpha_fwd<!Q16>(ai, xs[0], xp[0]);
+      emit_back(ai, 1);
+    }
+    {
+      float ai[8];
+      ck(ai);
+      emit_back(ai, 0);
+    }
+  } else {
+    // every step's alpha from the checkpoint: 6 recursion steps per window, no alpha vector kept
+#pragma unroll
+    for (int i = BETA_W - 1; i >= 0; i--) {
+      float ai[8];
+      ck(ai);
+#pragma unroll
+      for (int j = 0; j < i; j++) alpha_fwd<!Q16>(ai, xs[j], xp[j]);
+      emit_back(ai, i);
+    }
   }
   norm8<Q16>(b);
 }
