@@ -492,6 +492,96 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
                     "stream overlapped with the previous batch's decode"}
 
 
+def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
+    """Plan the batch, stage the pool in HBM (replicated on device into the batch IQ layout), run `warmup` untimed
+    and `steps` timed passes (barrier + synchronize on both sides), then check the last step's outputs: every TB's
+    CRC verdict and, for every CRC-OK TB, its payload against the transmitted bytes."""
+    B = len(cfgs)
+    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
+    d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
+    if len(pool_iq) == B and len({len(x) for x in pool_iq}) > 1:
+        flat = np.zeros(2 * batch.iq_samples, np.float32)
+        for i, iq in enumerate(pool_iq):
+            o = 2 * batch.iq_offset(i)
+            flat[o:o + len(iq)] = iq
+        d_iq.copy_(torch.from_numpy(flat))
+    else:
+        sfl = len(pool_iq[0])   # floats per subframe (one bandwidth)
+        d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
+        idx = torch.arange(B, device=dev) % len(pool_iq)
+        d_iq.view(B, sfl).copy_(d_pool[idx])
+        del d_pool
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup):
+        batch.run(d_iq.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    batch.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        batch.run(d_iq.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stage, nprof = batch.stage_ms()
+    del d_iq
+    crc = batch.download(abi.BUF_TB_CRC, np.uint32)[:B]
+    its = batch.download(abi.BUF_TB_ITS, np.uint32)[:B]
+    pay = batch.download(abi.BUF_PAYLOAD, np.uint8)
+    bad = sum(int(not np.array_equal(batch.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(B) if crc[i])
+    return {"batch": batch, "stage": stage, "nprof": nprof, "elapsed": elapsed, "n_ok": int(crc.sum()), "its": its,
+            "bad": bad, "bits_ok": float(sum(c.tbs for c, o in zip(cfgs, crc) if o))}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N copies of this command, one rank per GPU, BEFORE this
+    process touches the GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in each child's environment, rendezvous on
+    127.0.0.1).  Only rank 0 prints the JSON line; the exit code is the first failing rank's."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the N-rank launch (tests/test_dist.py): gloo instead of RCCL, each rank decodes its
+    contiguous shard of a small synthetic batch with the TEST-ONLY host emulation of the decoder kernels, from
+    the LLR streams the test wrote to --dry-run-llr; reports n_gpus / shards / CRC-OK count exactly like the GPU
+    path.  Never a measurement (no "value")."""
+    import ctypes as C
+    d = np.load(args.dry_run_llr)
+    total = int(d["total"])
+    first, n = shard_range(total, rank, world)
+    cfgs = [abi.sf_cfg(cell_id=1, nof_prb=6, nof_ports=1, sf_idx=SF_CYCLE[g % 8], tbs=4392, Qm=6)
+            for g in range(first, first + n)]
+    llr = np.concatenate([d[f"llr{g}"] for g in range(first, first + n)]).astype(np.float32)
+    pay = np.zeros(n * 549, np.uint8)
+    ok = np.zeros(n, np.uint32)
+    its = np.zeros(n, np.uint32)
+    t0 = time.perf_counter()
+    abi.emu().emu_decode_llr(C.cast(abi.cfg_array(cfgs), C.c_void_p), n, llr.ctypes.data, 4, pay.ctypes.data,
+                             ok.ctypes.data, its.ctypes.data, None)
+    elapsed = time.perf_counter() - t0
+    good = sum(int(np.array_equal(pay[i * 549:(i + 1) * 549], tb_payload(first + i, 549))) for i in range(n))
+    shards = [None] * world
+    dist.all_gather_object(shards, [first, n, good])
+    elapsed, n_ok, n_cb = reduce_over_ranks(elapsed, int(ok.sum()), n, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "shards": shards, "crc_ok": n_ok, "subframes": n_cb,
+                          "elapsed_max_s": elapsed}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -501,6 +591,9 @@ def main():
     ap.add_argument("--pool", type=int, default=256, help="distinct synthetic subframes per rank")
     ap.add_argument("--snr", type=float, default=30.0)
     ap.add_argument("--max-its", type=int, default=4)
+    ap.add_argument("--iterating-snr", type=float, default=21.5,
+                    help="default config: also run the shard at this SNR (turbo waterfall, ~3 iterations at max_its 4) "
+                         "and report it as the `iterating` block; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
@@ -524,7 +617,10 @@ def main():
                          "one code block per lane, or auto (latency form up to 1024 code blocks)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
+    ap.add_argument("--dry-run-llr", default=None, help=argparse.SUPPRESS)   # CPU launch rehearsal (tests only)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))                     # before anything touches the GPU
     if args.config == 2:
         args.sf_per_gpu = 1
     elif args.config == 3 and args.sf_per_gpu == 12500:
@@ -533,6 +629,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run_llr:
+        dist.init_process_group("gloo")
+        dry_run(args, world, rank)
+        dist.destroy_process_group()
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -558,49 +661,33 @@ def main():
         P = B                                               # every mixed subframe is distinct
     h = [0.8 + 0.3j, -0.4 + 0.5j] if args.config == 3 else None
     pool_iq, pool_tb = make_pool(cfgs[:P], args.snr, threads, first, h)
-    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
-    # stage the pool in HBM once, replicate on device into the batch IQ layout
-    d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
-    if args.config == 5:
-        flat = np.zeros(2 * batch.iq_samples, np.float32)
-        for i, iq in enumerate(pool_iq):
-            o = 2 * batch.iq_offset(i)
-            flat[o:o + len(iq)] = iq
-        d_iq.copy_(torch.from_numpy(flat))
-    else:
-        sfl = len(pool_iq[0])   # floats per subframe (one bandwidth)
-        d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
-        idx = torch.arange(B, device=dev) % len(pool_iq)
-        d_iq.view(B, sfl).copy_(d_pool[idx])
-        del d_pool
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-
-    for _ in range(args.warmup):
-        batch.run(d_iq.data_ptr(), sptr)
-    torch.cuda.synchronize(dev)
-    batch.profile_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        batch.run(d_iq.data_ptr(), sptr)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stage, nprof = batch.stage_ms()
-
-    # correctness of the timed work (last step's outputs)
-    crc = batch.download(abi.BUF_TB_CRC, np.uint32)[:B]
-    its = batch.download(abi.BUF_TB_ITS, np.uint32)[:B]
-    pay = batch.download(abi.BUF_PAYLOAD, np.uint8)
-    n_ok = int(crc.sum())
-    bad = sum(int(not np.array_equal(batch.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(0, B, max(1, B // 64)))
-    bits_ok = float(sum(c.tbs for c, o in zip(cfgs, crc) if o))
-    ncb = batch.n_codeblocks
-    elapsed, bits_all, ncb_all = reduce_over_ranks(elapsed, bits_ok, ncb, world, dev)
+    m = measure(args, cfgs, pool_iq, pool_tb, world, dev, args.steps, args.warmup)
+    batch, stage, nprof, elapsed = m["batch"], m["stage"], m["nprof"], m["elapsed"]
+    n_ok, its, bad, bits_ok = m["n_ok"], m["its"], m["bad"], m["bits_ok"]
+    elapsed, bits_all, ncb_all = reduce_over_ranks(elapsed, bits_ok, batch.n_codeblocks, world, dev)
+    # the same shard in the turbo decoder's waterfall region (every code block iterates): reported beside value
+    itr = None
+    if args.config == 4 and args.iterating_snr > 0:
+        ipool_iq, ipool_tb = make_pool(cfgs[:P], args.iterating_snr, threads, first, h)
+        isteps = max(1, min(args.steps, 5))
+        im = measure(args, cfgs, ipool_iq, ipool_tb, world, dev, isteps, 1)
+        iel, ibits, incb = reduce_over_ranks(im["elapsed"], im["bits_ok"], im["batch"].n_codeblocks, world, dev)
+        if rank == 0:
+            ib = im["batch"]
+            ims = im["stage"]["tdec"]
+            iach = ib.algo_bytes(4) / (ims * 1e-3) / 1e9
+            itr = {"snr_db": args.iterating_snr, "steps": isteps, "ms_per_step": round(iel / isteps * 1e3, 3),
+                   "Mbps": round(ibits * isteps / iel / 1e6, 2),
+                   "turbo_codeblocks_per_s": round(incb * isteps / iel, 1),
+                   "crc_ok_rate": round(im["n_ok"] / B, 6), "mean_turbo_iterations": round(float(im["its"].mean()), 4),
+                   "payload_mismatches_crc_ok": im["bad"],
+                   "stage_ms_per_step": {k: round(v, 4) for k, v in im["stage"].items()},
+                   "tdec_roofline": {"kernel": tdec_kernel_name(ib.turbo_sched), "bound": "hbm",
+                                     "achieved": round(iach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(iach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(ims, 4)},
+                   "what": f"the same {B}-subframe shard at {args.iterating_snr:g} dB AWGN (turbo waterfall region, "
+                           f"max_its {args.max_its}): Mbps counts CRC-OK TBs only"}
+        im["batch"].close()
 
     what = {2: "configs[1] 20 MHz TM1 SISO PDSCH MCS-28 (TBS 75376, 13 x K=5824), single subframe",
             3: "configs[2] 20 MHz TM2 (2-port SFBC) 64QAM MCS-28 (TBS 75376)",
@@ -624,7 +711,7 @@ def main():
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
-            "payload_spot_mismatches": bad,
+            "payload_mismatches_crc_ok": bad,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": tdec_kernel_name(batch.turbo_sched), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -634,6 +721,8 @@ def main():
         }
         if args.h2d:
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
+        if itr:
+            out["iterating"] = itr
         if args.ctrl:
             out["ctrl"] = bench_ctrl(args, batch, dev)
         if args.ul:

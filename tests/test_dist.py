@@ -67,3 +67,46 @@ def test_shard_range_covers_everything():
             spans = [bench.shard_range(total, r, world) for r in range(world)]
             assert spans[0][0] == 0 and sum(n for _, n in spans) == total
             assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_its_own_ranks(built, tmp_path):
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (the driver's N-GPU command); the CPU
+    rehearsal decodes each rank's contiguous shard with the emulated decoder over gloo and rank 0 prints one
+    line with n_gpus == 2."""
+    import json
+    import subprocess
+    import sys
+
+    import bench
+    from helpers import oracle_front
+    from srsue_amd import abi
+    total = 6
+    llrs = {"total": np.array(total)}
+    for g in range(total):
+        c = abi.sf_cfg(cell_id=1, nof_prb=6, nof_ports=1, sf_idx=bench.SF_CYCLE[g % 8], tbs=4392, Qm=6)
+        iq = abi.tx_subframe(c, bench.tb_payload(g, c.tbs // 8), snr_db=30.0, seed=0xA5A5 + g)
+        llrs[f"llr{g}"] = oracle_front(c, iq)[3]
+    path = tmp_path / "llr.npz"
+    np.savez(path, **llrs)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run-llr", str(path)],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                                   # only rank 0 prints
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["subframes"] == total and r["crc_ok"] == total
+    assert [s[:2] for s in r["shards"]] == [[0, 3], [3, 3]]  # contiguous shards
+    assert all(s[2] == s[1] for s in r["shards"])           # every TB equals the transmitted bytes
+
+
+def test_bench_rejects_world_mismatch(built):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
