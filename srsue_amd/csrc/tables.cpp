@@ -2,6 +2,7 @@
 // 3GPP TS 36.211 / 36.212 / 36.213 Rel-8; the srsLTE entry points they back are cited in
 // include/srslte/srslte.h.
 #include "tables.h"
+#include "tbs_table.h"
 
 #include <math.h>
 #include <string.h>
@@ -115,28 +116,10 @@ int mcs_to_itbs(uint32_t mcs, uint32_t* qm) {
   return -1;
 }
 
-// 36.213 Table 7.1.7.2.1-1, columns N_PRB = 6 / 25 / 50 / 100 (the bandwidths the benchmark and
-// tests use at full allocation).  Other columns return -1: on srsUE's path the TBS arrives inside
-// the DL grant (phch_worker.cc:297 -> :355), so the table is a convenience, not on the hot path.
-static const int TBS_COL[4][27] = {
-    {152, 208, 256, 328, 408, 504, 600, 712, 808, 936, 1032, 1192, 1352, 1544, 1736, 1800, 1928, 2152, 2344,
-     2600, 2792, 2984, 3240, 3496, 3624, 3752, 4392},
-    {680, 904, 1096, 1416, 1800, 2216, 2600, 3112, 3496, 4008, 4392, 4968, 5736, 6456, 7224, 7736, 7992, 9144,
-     9912, 10680, 11448, 12576, 13536, 14112, 15264, 15840, 18336},
-    {1384, 1800, 2216, 2856, 3624, 4392, 5160, 6200, 6968, 7992, 8760, 9912, 11448, 12960, 14112, 15264, 16416,
-     18336, 19848, 21384, 22920, 25456, 27376, 28336, 30576, 31704, 36696},
-    {2792, 3624, 4584, 5736, 7224, 8760, 10296, 12216, 14112, 15840, 17568, 19848, 22920, 25456, 28336, 30576,
-     32856, 36696, 39232, 43816, 46888, 51024, 55056, 57336, 61664, 63776, 75376}};
-
+// 36.213 Table 7.1.7.2.1-1 (tbs_table.h): every I_TBS 0..26 and N_PRB 1..110
 int tbs_from_idx(uint32_t i_tbs, uint32_t nof_prb) {
-  if (i_tbs > 26) return -1;
-  switch (nof_prb) {
-    case 6: return TBS_COL[0][i_tbs];
-    case 25: return TBS_COL[1][i_tbs];
-    case 50: return TBS_COL[2][i_tbs];
-    case 100: return TBS_COL[3][i_tbs];
-    default: return -1;
-  }
+  if (i_tbs > 26 || nof_prb < 1 || nof_prb > 110) return -1;
+  return (int)TBS_TABLE[i_tbs][nof_prb - 1];
 }
 
 uint32_t rm_E(uint32_t G, uint32_t C, uint32_t Qm, uint32_t NL, uint32_t r) {

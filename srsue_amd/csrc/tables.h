@@ -10,7 +10,7 @@ struct CbSegm { uint32_t C, Cp, Cm, Kp, Km, F, B; };
 int qpp_params(uint32_t K, uint32_t* f1, uint32_t* f2);           // 36.212 Table 5.1.3-3
 bool cb_size_valid(uint32_t K);
 int cbsegm(uint32_t tbs, CbSegm* s);                                // 36.212 5.1.2
-int tbs_from_idx(uint32_t i_tbs, uint32_t nof_prb);                 // 36.213 7.1.7.2.1 (spot columns)
+int tbs_from_idx(uint32_t i_tbs, uint32_t nof_prb);                 // 36.213 Table 7.1.7.2.1-1 (N_PRB 1..110)
 int mcs_to_itbs(uint32_t mcs, uint32_t* qm);                        // 36.213 Table 7.1.7.1-1
 uint32_t rm_E(uint32_t G, uint32_t C, uint32_t Qm, uint32_t NL, uint32_t r);   // 36.212 5.1.4.1.2
 uint32_t ncb_of(uint32_t K);
