@@ -21,6 +21,11 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <time.h>
+#include <math.h>
+#include <stdio.h>
+
+#include "srslte/common/timestamp.h"
+#include "srslte/utils/debug.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -354,6 +359,9 @@ typedef struct SRSLTE_API {
   uint32_t current_tx_nb;
 } srslte_pusch_cfg_t;
 struct mi_ue_ul_ctx;
+typedef struct SRSLTE_API {         /* PUCCH state srsUE reads (phch_worker.cc:628); PUCCH itself is out of scope */
+  bool shortened;
+} srslte_pucch_t;
 typedef struct SRSLTE_API {         /* owned by value per phch_worker (phch_worker.h:116) */
   srslte_cell_t cell;
   srslte_pusch_cfg_t pusch_cfg;     /* ue_ul.pusch_cfg.grant.n_prb_tilde (phch_worker.cc:223) */
@@ -365,6 +373,7 @@ typedef struct SRSLTE_API {         /* owned by value per phch_worker (phch_work
   bool cfo_en;
   float current_cfo;
   uint32_t last_pucch_format;
+  srslte_pucch_t pucch;
   struct mi_ue_ul_ctx *ctx;         /* MI355X device context: HIP stream + HBM workspace */
 } srslte_ue_ul_t;
 
@@ -403,7 +412,6 @@ SRSLTE_API int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t *rar, uint32_t 
  * into input_buffer and returns 1.  get_cfo / set_cfo: Hz; get_sfo: mean timing drift in samples/s.
  * Cell search (srslte_ue_cellsearch_*), MIB decoding (srslte_ue_mib_*) and AGC stay in srsLTE;
  * start_agc() returns an error, set_agc_period() is accepted. */
-typedef struct SRSLTE_API { time_t full_secs; double frac_secs; } srslte_timestamp_t;
 typedef struct SRSLTE_API { float threshold; float em_alpha; } srslte_sync_t;
 typedef struct SRSLTE_API { float gain; } srslte_agc_t;
 typedef struct mi_ue_sync_ctx mi_ue_sync_ctx;
@@ -432,8 +440,63 @@ SRSLTE_API int srslte_ue_sync_start_agc(srslte_ue_sync_t *q, double(set_gain_cal
 SRSLTE_API void srslte_sync_set_threshold(srslte_sync_t *q, float threshold);
 SRSLTE_API void srslte_sync_set_em_alpha(srslte_sync_t *q, float alpha);
 SRSLTE_API int srslte_sampling_freq_hz(uint32_t nof_prb);
-SRSLTE_API void srslte_timestamp_copy(srslte_timestamp_t *dest, srslte_timestamp_t *src);
-SRSLTE_API int srslte_timestamp_add(srslte_timestamp_t *t, time_t full_secs, double frac_secs);
+
+/* ---- MAC <-> PHY grant container (reference ue/hdr/common/mac_interface.h:59,73,83) -------------- */
+typedef union SRSLTE_API {
+  srslte_ra_ul_grant_t ul;
+  srslte_ra_dl_grant_t dl;
+} srslte_phy_grant_t;
+#define SRSLTE_RAR_GRANT_LEN 20   /* 36.213 6.2: RAR UL grant bits (phy_interface.h:174) */
+
+/* ---- periodic CQI reporting (phch_worker.h:128, phch_worker.cc:495-523): 36.213 7.2.2 reporting
+ * instances (Table 7.2.2-1A), wideband / UE-selected subband CQI values packed for PUCCH format 2 or
+ * PUSCH (36.212 5.2.3.3 / 5.2.2.6.4: 4-bit wideband CQI, 4-bit subband CQI + L-bit label) -------------- */
+typedef struct SRSLTE_API {
+  bool configured;
+  uint32_t pmi_idx;
+  bool simul_cqi_ack;
+  bool format_is_subband;
+  uint32_t subband_size;
+} srslte_cqi_periodic_cfg_t;
+typedef struct SRSLTE_API { uint8_t wideband_cqi; } srslte_cqi_format2_wideband_t;
+typedef struct SRSLTE_API { uint8_t subband_cqi; uint8_t subband_label; } srslte_cqi_format2_subband_t;
+typedef enum { SRSLTE_CQI_TYPE_WIDEBAND = 0, SRSLTE_CQI_TYPE_SUBBAND } srslte_cqi_type_t;
+typedef struct SRSLTE_API {
+  union {
+    srslte_cqi_format2_wideband_t wideband;
+    srslte_cqi_format2_subband_t subband;
+  };
+  srslte_cqi_type_t type;
+} srslte_cqi_value_t;
+SRSLTE_API int srslte_cqi_value_pack(srslte_cqi_value_t *value, uint8_t buff[SRSLTE_CQI_MAX_BITS]);
+SRSLTE_API bool srslte_cqi_send(uint32_t I_cqi_pmi, uint32_t tti);
+SRSLTE_API uint8_t srslte_cqi_from_snr(float snr);
+
+/* ---- small helpers srsUE calls (phch_worker.cc:449,495,531-532,654; dl_harq.cc:195) ---------------- */
+#define SRSLTE_VEC_EMA(data, average, coeff) ((coeff) * (data) + (1 - (coeff)) * (average))
+SRSLTE_API uint32_t srslte_vec_max_fi(float *x, uint32_t len);
+SRSLTE_API void srslte_vec_fprint_hex(FILE *stream, uint8_t *x, uint32_t len);
+SRSLTE_API int srslte_tti_interval(uint32_t tti1, uint32_t tti2);
+SRSLTE_API bool srslte_ue_ul_sr_send_tti(uint32_t I_sr, uint32_t current_tti);
+SRSLTE_API int srslte_refsignal_srs_send_cs(uint32_t subframe_config, uint32_t sf_idx);
+SRSLTE_API int srslte_refsignal_srs_send_ue(uint32_t I_srs, uint32_t tti);
+SRSLTE_API void srslte_ra_pusch_fprint(FILE *f, srslte_ra_ul_dci_t *q, uint32_t nof_prb);
+
+/* ---- OUT OF SCOPE (SURVEY.md 8 / DESIGN.md 9): PUCCH, SRS, UL power control and PRACH are not on the
+ * DL decode path.  They are declared so srsUE compiles against this header unchanged; this library does
+ * not implement them: an integration links srsLTE's own modules rebuilt against this header, or stubs
+ * (INTEGRATION.md). -------- */
+SRSLTE_API void srslte_ue_ul_pregen_signals(srslte_ue_ul_t *q);
+SRSLTE_API int srslte_ue_ul_pucch_encode(srslte_ue_ul_t *q, srslte_uci_data_t uci_data, uint32_t pdcch_n_cce,
+                                         uint32_t tti, cf_t *output_signal);
+SRSLTE_API int srslte_ue_ul_srs_encode(srslte_ue_ul_t *q, uint32_t tti, cf_t *output_signal);
+SRSLTE_API float srslte_ue_ul_pusch_power(srslte_ue_ul_t *q, float PL, float p0_preamble);
+SRSLTE_API float srslte_ue_ul_pucch_power(srslte_ue_ul_t *q, float PL, uint32_t format, uint32_t n_cqi,
+                                          uint32_t n_harq);
+SRSLTE_API float srslte_ue_ul_srs_power(srslte_ue_ul_t *q, float PL);
+typedef struct SRSLTE_API { uint32_t N_seq, N_cp; void *impl; } srslte_prach_t;   /* prach.h:64 (srsLTE) */
+typedef struct SRSLTE_API { uint32_t nsamples; void *impl; } srslte_cfo_t;         /* prach.h:68 (srsLTE) */
+typedef struct SRSLTE_API { srslte_cell_t cell; void *impl; } srslte_ue_mib_t;     /* phch_recv.h:77 (srsLTE MIB) */
 
 #ifdef __cplusplus
 }

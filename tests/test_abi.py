@@ -14,7 +14,11 @@ from srsue_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", "srslte", "srslte.h"), os.path.join(ROOT, "include", "mi_dl.h"),
-           os.path.join(ROOT, "include", "mi_ul.h")]
+           os.path.join(ROOT, "include", "mi_ul.h"), os.path.join(ROOT, "include", "srslte", "common", "timestamp.h"),
+           os.path.join(ROOT, "include", "srslte", "utils", "debug.h")]
+# declared in srslte.h's OUT OF SCOPE block only so srsUE compiles unchanged (PUCCH / SRS / UL power control)
+OUT_OF_SCOPE = {"srslte_ue_ul_pregen_signals", "srslte_ue_ul_pucch_encode", "srslte_ue_ul_pucch_power",
+                "srslte_ue_ul_pusch_power", "srslte_ue_ul_srs_encode", "srslte_ue_ul_srs_power"}
 
 
 def declared_functions(path):
@@ -23,7 +27,7 @@ def declared_functions(path):
     names = set()
     for m in re.finditer(r"(?:SRSLTE_API\s+)?[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", src):
         n = m.group(1)
-        if n.startswith(("srslte_", "mi_")):
+        if n.startswith(("srslte_", "mi_", "get_time_interval")):
             names.add(n)
     return names
 
@@ -32,11 +36,14 @@ def test_library_exports_every_declared_symbol(built):
     lib = abi.lib()
     missing = []
     for h in HEADERS:
-        for n in sorted(declared_functions(h)):
+        for n in sorted(declared_functions(h) - OUT_OF_SCOPE):
             if not hasattr(lib, n):
                 missing.append(n)
     assert not missing, missing
     assert len(declared_functions(HEADERS[0])) >= 25
+    src = open(HEADERS[0]).read()
+    assert OUT_OF_SCOPE <= declared_functions(HEADERS[0])
+    assert all(src.index(n) > src.index("OUT OF SCOPE (SURVEY.md 8") for n in OUT_OF_SCOPE)
 
 
 def test_headers_compile_as_c(tmp_path):
@@ -81,3 +88,35 @@ def test_product_lib_fails_loudly_without_gpu(built):
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         abi.Batch([abi.sf_cfg()])
+
+
+def test_srslte_reporting_helpers(built):
+    """The srsLTE host helpers srsUE's worker calls (srslte_util.cpp): 36.213 reporting instants and the
+    CQI packing used for UCI (phch_worker.cc:495-532)."""
+    import ctypes as C
+    from srsue_amd import abi
+    L = abi.lib()
+    L.srslte_cqi_send.restype = C.c_bool
+    L.srslte_ue_ul_sr_send_tti.restype = C.c_bool
+    L.srslte_cqi_from_snr.restype = C.c_uint8
+    L.srslte_cqi_from_snr.argtypes = [C.c_float]
+    # CQI: I = 2..6 -> N_pd 5, offset I - 2; I = 20 -> N_pd 20, offset 3
+    assert [L.srslte_cqi_send(4, t) for t in range(10)] == [t % 5 == 2 for t in range(10)]
+    assert [t for t in range(60) if L.srslte_cqi_send(20, t)] == [3, 23, 43]
+    assert not L.srslte_cqi_send(317, 0)
+    # SR: I = 7 -> period 10, offset 2; I = 157 -> every subframe
+    assert [t for t in range(30) if L.srslte_ue_ul_sr_send_tti(7, t)] == [2, 12, 22]
+    assert all(L.srslte_ue_ul_sr_send_tti(157, t) for t in range(12))
+    # SRS: cell config 7 = subframes {0, 1} mod 5; UE I = 10 -> period 10, offset 3
+    assert [L.srslte_refsignal_srs_send_cs(7, s) for s in range(10)] == [1, 1, 0, 0, 0, 1, 1, 0, 0, 0]
+    assert [t for t in range(25) if L.srslte_refsignal_srs_send_ue(10, t) == 1] == [3, 13, 23]
+    assert L.srslte_tti_interval(5, 10230) == 15 and L.srslte_tti_interval(20, 8) == 12
+    assert L.srslte_cqi_from_snr(-3.0) == 0 and L.srslte_cqi_from_snr(30.0) == 15 and L.srslte_cqi_from_snr(10.5) == 5
+
+    class Cqi(C.Structure):
+        _fields_ = [("v0", C.c_uint8), ("v1", C.c_uint8), ("type", C.c_int)]
+    buf = (C.c_uint8 * 64)()
+    v = Cqi(11, 0, 0)
+    assert L.srslte_cqi_value_pack(C.byref(v), buf) == 4 and list(buf[:4]) == [1, 0, 1, 1]
+    v = Cqi(6, 1, 1)
+    assert L.srslte_cqi_value_pack(C.byref(v), buf) == 5 and list(buf[:5]) == [0, 1, 1, 0, 1]
