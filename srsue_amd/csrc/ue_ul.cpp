@@ -49,6 +49,10 @@ int grant_from_riv(uint32_t riv, uint32_t nof_prb, uint32_t mcs, uint32_t n_dmrs
   if (a + b < nof_prb) { L = a + 1; start = b; }
   else { L = nof_prb - a + 1; start = nof_prb - 1 - b; }
   if (start + L > nof_prb) return SRSLTE_ERROR;
+  // the DFT-spread size M = 12 L must factor as 2^a 3^b 5^c (36.211 5.3.3)
+  uint32_t r = L;
+  for (uint32_t f : {2u, 3u, 5u}) while (r % f == 0) r /= f;
+  if (r != 1) { mi::set_error("L_prb must be 2^a 3^b 5^c (36.211 5.3.3)"); return SRSLTE_ERROR; }
   uint32_t qm = 0, itbs = 0;
   if (ul_mcs(mcs, &qm, &itbs)) return SRSLTE_ERROR;
   const int tbs = mi::tbs_from_idx(itbs, L);

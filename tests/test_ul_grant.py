@@ -136,7 +136,7 @@ def test_format0_rejections(built):
     assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0
     m = format0(100, 0, 100, 30)                                                                     # rv 2 retx
     assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0
-    m = format0(100, 3, 40, 20)                                                                      # no TBS column
+    m = format0(100, 3, 7, 20)                                                                       # M = 84: not 2^a 3^b 5^c
     assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0
 
 
