@@ -37,7 +37,10 @@ typedef struct {
   uint32_t tbs;          /* transport block size, bits */
   uint32_t Qm;           /* 2, 4, 6 */
   uint32_t new_tb;       /* 1 = first transmission (softbuffer overwritten), 0 = HARQ combine */
-  uint8_t  prb_mask[MI_DL_MAX_PRB];  /* allocated PRBs (same in both slots) */
+  /* allocated PRBs.  If every entry is 0 or 1, a non-zero entry = PRB used in both slots (localized).
+   * Otherwise bit 0 / bit 1 of entry p = PRB p used in slot 0 / slot 1 (distributed VRB, 36.211 6.2.3.2:
+   * srslte_ra_dl_grant_t.prb_idx[0] / [1]); the RE gather follows 36.211 6.3.5 per slot. */
+  uint8_t  prb_mask[MI_DL_MAX_PRB];
 } mi_dl_sf_cfg_t;
 
 /* stages, for mi_dl_batch_stage_ms */
@@ -152,8 +155,10 @@ int    mi_pdsch_G(const mi_dl_sf_cfg_t *cfg);
  * left in HBM.  Per subframe the search uses that subframe's cfg.rnti and cfg.cfi; PHICH resources
  * phich_ng = 0..3 (Ng = 1/6, 1/2, 1, 2; normal duration).  run() enqueues four kernels (stage mask:
  * 1 PCFICH, 2 PDCCH soft bits, 4 blind search, 8 PHICH); result() returns the first DCI of the
- * subframe in search order (UE-specific L = 1, 2, 4, 8, then common L = 4, 8): 1 found, 0 not found,
- * -1 error.  PHICH (srslte_ue_dl_decode_phich, phch_worker.cc:381): set_phich() sets per subframe the
+ * subframe in srsLTE's search order (one DCI size over all candidates of a space at a time): `ul` 0 =
+ * DL for a C-RNTI (UE-specific L = 1, 2, 4, 8 with 1A then 1, common L = 4, 8 with 1A), 1 = UL format 0,
+ * 2 = DL for an SI/RA/P-RNTI (common space only, 1A then 1C).  format: 0 = 0, 1 = 1, 2 = 1A, 3 = 1C.
+ * Returns 1 found, 0 not found, -1 error.  PHICH (srslte_ue_dl_decode_phich, phch_worker.cc:381): set_phich() sets per subframe the
  * UL grant's lowest PRB index and DMRS cyclic shift (36.213 9.1.2; default 0, 0), phich() returns the
  * HARQ indicator (1 ACK, 0 NACK, -1 error) and its soft value (> 0 favours ACK). */
 typedef struct mi_dl_ctrl mi_dl_ctrl_t;

@@ -175,6 +175,11 @@ typedef struct SRSLTE_API {
   uint32_t rv_idx;
   uint32_t tpc_pucch;
   srslte_dci_format_t dci_format;
+  /* appended (srsUE does not read them): type-1 subset / shift / VRB bitmap (format 1, 36.213 7.1.6.2),
+   * type-2 distributed VRB flag and gap (formats 1A / 1C, 36.211 6.2.3.2: 0 = N_gap,1, 1 = N_gap,2) */
+  uint32_t type1_subset, type1_shift, type1_bitmap;
+  bool type2_distributed;
+  uint32_t type2_gap;
 } srslte_ra_dl_dci_t;
 
 /* srslte_ue_dl_t, owned by value per phch_worker (phch_worker.h:111) */
@@ -210,10 +215,15 @@ SRSLTE_API int srslte_ue_dl_cfg_grant(srslte_ue_dl_t *q, srslte_ra_dl_grant_t *g
                                       uint32_t rvidx);
 
 /* ---- PDCCH / DCI (phch_worker.cc:260, 293, 297, 314, 426) --------------------------------------
- * Blind search order: UE-specific space L = 1, 2, 4, 8 (formats 1A then 1), then the common space
- * L = 4, 8 (format 1A); SI/RA/P-RNTI search the common space only.  find_* return 1 when found.
- * dci_msg_to_dl_grant: formats 1A (localized RIV) and 1 (type-0 RBG bitmap); the TBS comes from the
- * spot columns this library carries (N_PRB = 6, 25, 50, 100), other allocations return an error. */
+ * Blind search order (srsLTE's dci_blind_search, one format over all candidates at a time): C-RNTI:
+ * UE-specific space L = 1, 2, 4, 8 with format 1A then format 1, then the common space L = 4, 8 with
+ * format 1A; SI/RA/P-RNTI: the common space only, format 1A then format 1C.  find_* return 1 when found.
+ * dci_msg_to_dl_grant (36.212 5.3.3.1, 36.213 7.1.6 / 7.1.7, 36.211 6.2.3.2): format 1 with resource
+ * allocation type 0 (RBG bitmap) or type 1 (RBG subset, shift, VRB bitmap); format 1A localized or
+ * distributed VRB (N_gap,1 / N_gap,2; with SI/RA/P-RNTI the NDI bit is the gap and the TPC LSB selects
+ * N_PRB^1A = 2 / 3 with QPSK and I_TBS = I_MCS); format 1C (distributed, N_step, Table 7.1.7.2.3-1).
+ * Distributed allocations set different PRBs in grant->prb_idx[0] (slot 0) and prb_idx[1] (slot 1);
+ * the PDSCH RE gather honours both. */
 SRSLTE_API int srslte_pdcch_extract_llr(srslte_pdcch_t *q, cf_t *sf_symbols, cf_t *ce[SRSLTE_MAX_PORTS],
                                         float noise_estimate, uint32_t nsubframe, uint32_t cfi);
 SRSLTE_API int srslte_ue_dl_find_dl_dci(srslte_ue_dl_t *q, srslte_dci_msg_t *dci_msg, uint32_t cfi, uint32_t sf_idx,

@@ -193,11 +193,12 @@ int or_is_pdsch_re(const or_cell_t *c, uint32_t cfi, uint32_t sf, uint32_t l, ui
 
 int or_pdsch_re_list(const or_cell_t *c, uint32_t cfi, uint32_t sf, const uint8_t *prb_mask,
                      uint32_t *re_idx) {
-  int n = 0;
+  int n = 0, two_slot = 0;
   uint32_t W = 12 * c->nof_prb;
+  for (uint32_t p = 0; p < c->nof_prb; p++) two_slot |= prb_mask[p] >= 2;
   for (uint32_t l = 0; l < OR_NSYMB; l++)
     for (uint32_t p = 0; p < c->nof_prb; p++) {
-      if (!prb_mask[p]) continue;
+      if (two_slot ? !((prb_mask[p] >> (l / 7)) & 1u) : !prb_mask[p]) continue;
       for (uint32_t k = 12 * p; k < 12 * p + 12; k++)
         if (or_is_pdsch_re(c, cfi, sf, l, k)) re_idx[n++] = l * W + k;
     }

@@ -240,11 +240,12 @@ uint32_t or_dci_size(uint32_t format, uint32_t nof_prb) {
   uint32_t n01a = s0 > s1a ? s0 : s1a;
   if (ambiguous(n01a)) n01a++;
   if (format == OR_DCI_0 || format == OR_DCI_1A) return n01a;
+  if (format == OR_DCI_1C) return or_dci1c_size(nof_prb);
   /* format 1: [RA header if N_RB > 10] [RBG bitmap] MCS 5, HARQ 3, NDI 1, RV 2, TPC 2 */
   const uint32_t P = nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4;
   uint32_t s1 = (nof_prb > 10 ? 1 : 0) + (nof_prb + P - 1) / P + 13;
-  if (s1 == n01a) s1++;
-  while (ambiguous(s1)) s1++;
+  /* 36.212 5.3.3.1.2: pad until neither the 0/1A size nor one of Table 5.3.3.1.2-1 */
+  while (s1 == n01a || ambiguous(s1)) s1++;
   return s1;
 }
 
@@ -344,22 +345,24 @@ int or_search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, int common, uint
   return n;
 }
 
-/* blind search (srslte_ue_dl_find_dl_dci / _find_ul_dci semantics): UE-specific space first (L = 1,
-   2, 4, 8), then the common space (L = 4, 8); per candidate the formats in order; the first CRC
-   match wins.  ul != 0: format 0 (flag bit 0) instead of the DL formats 1A (flag 1) and 1. */
-int or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int ul,
-                or_dci_found_t *out) {
+/* blind search (srslte_ue_dl_find_dl_dci_type / _find_ul_dci semantics, srsLTE's dci_blind_search: one
+   format over all candidates of a space at a time, the first CRC match wins).  mode 0 (C-RNTI, DL):
+   UE-specific space (L = 1, 2, 4, 8) with the 1A size then format 1, then the common space (L = 4, 8)
+   with the 1A size.  mode 1 (UL): the same spaces with the 0/1A size, flag 0.  mode 2 (SI/RA/P-RNTI):
+   the common space only, the 1A size then format 1C.  The 0/1A flag separates 1A (1) from 0 (0). */
+int or_find_dci_mode(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int mode,
+                     or_dci_found_t *out) {
   uint32_t Ls[32], nc[32];
-  for (int common = 0; common < 2; common++) {
+  for (int common = (mode == 2); common < 2; common++) {
     const int n = or_search_space(n_cce, sf, rnti, common, Ls, nc);
-    for (int i = 0; i < n; i++) {
-      const uint32_t fmts[2] = {ul ? OR_DCI_0 : OR_DCI_1A, OR_DCI_1};
-      const int nf = (ul || common) ? 1 : 2;
-      for (int f = 0; f < nf; f++) {
+    uint32_t fmts[2] = {mode == 1 ? OR_DCI_0 : OR_DCI_1A, mode == 2 ? OR_DCI_1C : OR_DCI_1};
+    const int nf = (mode == 1 || (common && mode == 0)) ? 1 : 2;
+    for (int f = 0; f < nf; f++)
+      for (int i = 0; i < n; i++) {
         const uint32_t A = or_dci_size(fmts[f], nof_prb);
         uint8_t a[OR_DCI_MAX_BITS];
         if (!or_dci_decode(llr + 72 * nc[i], Ls[i], A, rnti, a)) continue;
-        if (fmts[f] != OR_DCI_1 && a[0] != (ul ? 0 : 1)) continue;   /* 0 / 1A flag */
+        if ((fmts[f] == OR_DCI_0 || fmts[f] == OR_DCI_1A) && a[0] != (mode == 1 ? 0 : 1)) continue;
         out->format = fmts[f];
         out->nbits = A;
         out->L = Ls[i];
@@ -367,9 +370,12 @@ int or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf,
         memcpy(out->bits, a, A);
         return 1;
       }
-    }
   }
   return 0;
+}
+int or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int ul,
+                or_dci_found_t *out) {
+  return or_find_dci_mode(llr, n_cce, nof_prb, sf, rnti, ul ? 1 : 0, out);
 }
 
 /* ---- transmit side (ground truth): one DCI on the air, noiseless, added to iq ---- */

@@ -61,7 +61,9 @@ int      or_mcs(uint32_t mcs, uint32_t *qm, uint32_t *i_tbs);
 void     or_crs_seq(uint32_t id, uint32_t ns, uint32_t l, float *re_im /* 2*220 */);
 int      or_ctrl_symbols(const or_cell_t *c, uint32_t cfi);
 int      or_is_pdsch_re(const or_cell_t *c, uint32_t cfi, uint32_t sf, uint32_t l, uint32_t k);
-/* RE list of the PDSCH in mapping order (36.211 6.3.5): index l*12*nof_prb + k; returns count */
+/* RE list of the PDSCH in mapping order (36.211 6.3.5): index l*12*nof_prb + k; returns count.
+ * prb_mask: if any entry is >= 2, bit s of entry p = PRB p is used in slot s (distributed VRB); else
+ * a non-zero entry = PRB used in both slots. */
 int      or_pdsch_re_list(const or_cell_t *c, uint32_t cfi, uint32_t sf, const uint8_t *prb_mask,
                           uint32_t *re_idx);
 int      or_rm_E(uint32_t G, uint32_t C, uint32_t Qm, uint32_t NL, uint32_t r);
@@ -132,7 +134,7 @@ int      or_simd_decode_batch(const float *in, uint32_t stride, uint32_t n, uint
 
 /* ---- DL control channels (o_ctrl.c): PHICH/PCFICH REG allocation, PDCCH, DCI ---- */
 #define OR_DCI_MAX_BITS 64
-enum { OR_DCI_0 = 0, OR_DCI_1 = 1, OR_DCI_1A = 2 };
+enum { OR_DCI_0 = 0, OR_DCI_1 = 1, OR_DCI_1A = 2, OR_DCI_1C = 3 };
 typedef struct {
   or_cell_t cell;
   uint32_t  ng;        /* PHICH resources Ng: 0 = 1/6, 1 = 1/2, 2 = 1, 3 = 2 (srslte_phich_resources_t) */
@@ -161,7 +163,23 @@ int      or_dci_decode(const float *e, uint32_t L, uint32_t A, uint16_t rnti, ui
 int      or_search_space(uint32_t n_cce, uint32_t sf, uint16_t rnti, int common, uint32_t *L, uint32_t *ncce);
 int      or_find_dci(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int ul,
                      or_dci_found_t *out);
-/* adds one noiseless DCI (L CCEs at ncce) to iq (2 * SF_LEN floats), flat per-port channel h */
+/* mode 0 = DL C-RNTI, 1 = UL (format 0), 2 = DL SI/RA/P-RNTI (common space, formats 1A then 1C) */
+int      or_find_dci_mode(const float *llr, uint32_t n_cce, uint32_t nof_prb, uint32_t sf, uint16_t rnti, int mode,
+                          or_dci_found_t *out);
+/* ---- DL resource allocation / DCI -> grant (o_ra.c; srslte_dci_msg_to_dl_grant, phch_worker.cc:297) ---- */
+typedef struct {
+  uint8_t  prb[OR_NRB_MAX];   /* bit 0: PRB used in slot 0, bit 1: in slot 1 (or_pdsch_re_list encoding) */
+  uint32_t format, alloc_type, distributed, gap2;
+  uint32_t nof_prb;           /* PRBs (VRBs) per slot */
+  uint32_t mcs, harq, ndi, rv, tpc, Qm, i_tbs, n_prb_tbs;
+  int      tbs;               /* -1: TBS column not carried by the oracle (n_prb_tbs / i_tbs still valid) */
+} or_dl_grant_t;
+uint32_t or_rbg_size(uint32_t nof_prb);
+uint32_t or_ngap(uint32_t nof_prb, int gap2);
+uint32_t or_nvrb_dist(uint32_t nof_prb, int gap2);
+int      or_vrb_to_prb(uint32_t nof_prb, int gap2, uint32_t n_vrb, uint32_t slot);
+uint32_t or_dci1c_size(uint32_t nof_prb);
+int      or_dl_dci_to_grant(const uint8_t *bits, uint32_t nbits, uint16_t rnti, uint32_t nof_prb, or_dl_grant_t *g);
 /* PHICH (o_ctrl.c): resource of an UL grant, its 12 REs, soft HI (> 0 favours ACK), transmitter */
 void     or_phich_calc(uint32_t nof_prb, uint32_t ng, uint32_t I_lowest, uint32_t n_dmrs, uint32_t *group,
                        uint32_t *seq);

@@ -43,7 +43,8 @@ def sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=1, cfi=1, tm=None, rnti=0
     c.tm = tm if tm is not None else (2 if nof_ports == 2 else 1)
     c.nl_td, c.rnti, c.rv, c.tbs, c.Qm, c.new_tb = nl_td, rnti, rv, tbs, Qm, new_tb
     for p in range(MAX_PRB):
-        c.prb_mask[p] = 1 if (p < nof_prb and (prb is None or prb[p])) else 0
+        # 0/1 entries (both slots) or the two-slot encoding of mi_dl_sf_cfg_t (bit s = used in slot s)
+        c.prb_mask[p] = (1 if prb is None else int(prb[p])) if p < nof_prb else 0
     return c
 
 

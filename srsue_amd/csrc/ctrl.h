@@ -42,6 +42,7 @@ struct CtrlEngine {
   std::vector<MiCtrlSf> sfs;
   std::vector<uint32_t> cdata;
   std::vector<MiDciJob> jobs;
+  std::vector<uint8_t> job_fmt;      // per job: bit 2 = common space; bits 0-1: 0 = 0/1A size, DCI_1, DCI_1C
   std::vector<uint32_t> job_begin;   // per subframe: jobs [job_begin[s], job_begin[s+1]) in search order
   std::vector<uint32_t> nof_prb;     // per subframe
   DevBuf d_sfs, d_cdata, d_llr, d_jobs, d_res, d_cfi, d_phich;

@@ -19,7 +19,7 @@ int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t 
     return -1;
   }
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> phich_cache;
-  sfs.clear(); cdata.clear(); jobs.clear(); job_begin.clear(); nof_prb.clear();
+  sfs.clear(); cdata.clear(); jobs.clear(); job_fmt.clear(); job_begin.clear(); nof_prb.clear();
   llr_floats = 0; max_regs = 0;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> reg_cache;  // -> (off, M)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> scr_cache, pcf_cache;
@@ -89,15 +89,18 @@ int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t 
     max_regs = std::max(max_regs, d.M);
     sfs.push_back(d);
     nof_prb.push_back(c.nof_prb);
-    // jobs in search order: UE-specific (sizes 1A/0 then 1), then common (1A/0)
+    // jobs in srsLTE's search order (dci_blind_search: one size over all candidates of a space): UE-specific
+    // space with the 1A/0 size then format 1, common space with the 1A/0 size then format 1C (1C is only
+    // selected for SI/RA/P-RNTI searches)
     job_begin.push_back((uint32_t)jobs.size());
-    const uint32_t A1a = dci_size(DCI_1A, c.nof_prb), A1 = dci_size(DCI_1, c.nof_prb);
+    const uint32_t sizes[2][2] = {{dci_size(DCI_1A, c.nof_prb), dci_size(DCI_1, c.nof_prb)},
+                                  {dci_size(DCI_1A, c.nof_prb), dci_size(DCI_1C, c.nof_prb)}};
     for (int common = 0; common < 2; common++) {
       uint32_t Ls[16], nc[16];
       const int nk = search_space(d.n_cce, sd.sf_idx, rnti[s], common != 0, Ls, nc);
-      for (int k = 0; k < nk; k++)
-        for (int f = 0; f < (common ? 1 : 2); f++) {
-          const uint32_t A = f ? A1 : A1a, D = A + 16;
+      for (int f = 0; f < 2; f++)
+        for (int k = 0; k < nk; k++) {
+          const uint32_t A = sizes[common][f], D = A + 16;
           auto ri = rank_cache.find(D);
           if (ri == rank_cache.end()) {
             std::vector<uint32_t> rank;
@@ -106,6 +109,7 @@ int CtrlEngine::build(const Plan& P, const std::vector<uint32_t>& cfi, uint32_t 
             cdata.insert(cdata.end(), rank.begin(), rank.end());
           }
           jobs.push_back(MiDciJob{(uint32_t)s, d.llr_off, Ls[k], nc[k], A, D, ri->second, rnti[s]});
+          job_fmt.push_back((uint8_t)((common << 2) | (f == 0 ? 0 : common ? DCI_1C : DCI_1)));
         }
     }
   }
@@ -147,22 +151,15 @@ int CtrlEngine::download(hipStream_t st) {
 
 DciFound CtrlEngine::select(uint32_t s, bool ul, bool common_only) const {
   DciFound out{};
-  const uint32_t A1a = dci_size(DCI_1A, nof_prb[s]);
   for (uint32_t j = job_begin[s]; j < job_begin[s + 1]; j++) {
     const MiDciJob& jb = jobs[j];
     const MiDciRes& r = res[j];
     if (!r.found) continue;
-    const uint32_t flag = (r.bits[0] >> 31) & 1u;
-    int fmt;
-    if (jb.A == A1a) fmt = flag ? DCI_1A : DCI_0;
-    else fmt = DCI_1;
+    const bool common = (job_fmt[j] >> 2) != 0;
+    int fmt = job_fmt[j] & 3;
+    if (fmt == 0) fmt = ((r.bits[0] >> 31) & 1u) ? DCI_1A : DCI_0;   // the 0/1A flag
     if (ul ? fmt != DCI_0 : fmt == DCI_0) continue;
-    if (common_only) {
-      // common-space candidates are the last ones of the subframe's job list (L = 4 / 8, one size)
-      uint32_t Ls[16], nc[16];
-      const uint32_t ncommon = (uint32_t)search_space(sfs[s].n_cce, 0, 0, true, Ls, nc);
-      if (j < job_begin[s + 1] - ncommon) continue;
-    }
+    if (common_only ? !common : fmt == DCI_1C) continue;            // 1C: SI/RA/P-RNTI only
     out.found = 1;
     out.format = (uint32_t)fmt;
     out.nbits = jb.A;
@@ -252,7 +249,7 @@ int mi_dl_ctrl_result(mi_dl_ctrl_t* c, uint32_t sf, int ul, uint32_t* cfi, uint3
     c->have_res = true;
   }
   if (cfi) *cfi = c->cfi[sf];
-  const mi::DciFound f = c->ce.select(sf, ul != 0, false);
+  const mi::DciFound f = c->ce.select(sf, ul == 1, ul == 2);
   if (!f.found) return 0;
   if (format) *format = f.format;
   if (L) *L = f.L;

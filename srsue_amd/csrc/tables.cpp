@@ -5,6 +5,8 @@
 #include "tbs_table.h"
 
 #include <math.h>
+
+#include <algorithm>
 #include <string.h>
 
 #include "dl_common.h"
@@ -224,9 +226,17 @@ uint32_t pdsch_re_list(uint32_t id, uint32_t nof_prb, uint32_t nof_ports, uint32
                        const uint8_t* prb_mask, std::vector<uint32_t>& re) {
   re.clear();
   const uint32_t W = 12 * nof_prb;
+  uint8_t any_slot_bits = 0;
+  for (uint32_t p = 0; p < nof_prb; p++) any_slot_bits |= prb_mask[p] & ~1u;
+  // per-slot use of each PRB: bit 0 / bit 1 (distributed VRB), or "both" for 0/1 masks
+  uint8_t use[2][110];
+  for (uint32_t p = 0; p < nof_prb; p++) {
+    use[0][p] = any_slot_bits ? (prb_mask[p] & 1u) : (prb_mask[p] != 0);
+    use[1][p] = any_slot_bits ? ((prb_mask[p] >> 1) & 1u) : (prb_mask[p] != 0);
+  }
   for (uint32_t l = 0; l < (uint32_t)NSYMB; l++)
     for (uint32_t p = 0; p < nof_prb; p++) {
-      if (!prb_mask[p]) continue;
+      if (!use[l / 7][p]) continue;
       for (uint32_t k = 12 * p; k < 12 * p + 12; k++)
         if (is_pdsch_re(id, nof_prb, nof_ports, cfi, sf, l, k)) re.push_back(l * W + k);
     }
@@ -326,7 +336,7 @@ void pdcch_quad_perm(uint32_t M, uint32_t id, std::vector<uint32_t>& log_of_reg)
   for (uint32_t i = 0; i < M; i++) log_of_reg[i] = w[(i + id) % M];
 }
 
-static uint32_t ceil_log2(uint32_t x) {
+uint32_t ceil_log2(uint32_t x) {
   uint32_t n = 0;
   while ((1u << n) < x) n++;
   return n;
@@ -338,12 +348,57 @@ uint32_t dci_size(int format, uint32_t nof_prb) {
   const uint32_t rba = ceil_log2(nof_prb * (nof_prb + 1) / 2);
   uint32_t n01a = 15 + rba;   // 1A = 15 + RBA >= format 0 = 14 + RBA (FDD)
   if (dci_ambiguous(n01a)) n01a++;
+  if (format == DCI_1C) return (nof_prb >= 50 ? 1 : 0) + dci1c_rba_bits(nof_prb) + 5;   // 36.212 5.3.3.1.4
   if (format != DCI_1) return n01a;
   const uint32_t P = nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4;
   uint32_t s1 = (nof_prb > 10 ? 1 : 0) + (nof_prb + P - 1) / P + 13;
-  if (s1 == n01a) s1++;
-  while (dci_ambiguous(s1)) s1++;
+  // 36.212 5.3.3.1.2: pad until neither the 0/1A size nor one of Table 5.3.3.1.2-1
+  while (s1 == n01a || dci_ambiguous(s1)) s1++;
   return s1;
+}
+
+uint32_t rbg_size(uint32_t nof_prb) { return nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4; }
+
+uint32_t n_gap(uint32_t nof_prb, bool gap2) {
+  if (gap2) return nof_prb < 50 ? 0 : nof_prb < 64 ? 9 : 16;
+  static const struct { uint32_t max_prb, gap; } T[] = {{11, 4}, {19, 8}, {26, 12}, {44, 18}, {63, 27}, {79, 32}, {110, 48}};
+  if (nof_prb <= 10) return (nof_prb + 1) / 2;
+  for (const auto& t : T)
+    if (nof_prb <= t.max_prb) return t.gap;
+  return 0;
+}
+
+uint32_t n_vrb_dist(uint32_t nof_prb, bool gap2) {
+  const uint32_t g = n_gap(nof_prb, gap2);
+  if (!g) return 0;
+  return gap2 ? (nof_prb / (2 * g)) * (2 * g) : 2 * std::min(g, nof_prb - g);
+}
+
+// 36.211 6.2.3.2 closed form: n~'_PRB from n~''_PRB (2 N_row (n~ mod 2) + n~/2) or n~'''_PRB
+// (N_row (n~ mod 4) + n~/4) with the null-cell corrections, odd slot shifted by N~/2, gap applied
+int vrb_to_prb(uint32_t nof_prb, bool gap2, uint32_t n_vrb, uint32_t slot) {
+  const uint32_t gap = n_gap(nof_prb, gap2), Nt = gap2 ? 2 * gap : n_vrb_dist(nof_prb, false);
+  if (!Nt || n_vrb >= n_vrb_dist(nof_prb, gap2)) return -1;
+  const uint32_t P = rbg_size(nof_prb), Nrow = (Nt + 4 * P - 1) / (4 * P) * P, Nnull = 4 * Nrow - Nt;
+  const uint32_t nt = n_vrb % Nt, base = Nt * (n_vrb / Nt);
+  const uint32_t p2 = 2 * Nrow * (nt & 1u) + nt / 2 + base, p3 = Nrow * (nt & 3u) + nt / 4 + base;
+  uint32_t pp;
+  if (Nnull && nt >= Nt - Nnull) pp = (nt & 1u) ? p2 - Nrow : p2 - Nrow + Nnull / 2;
+  else if (Nnull && (nt & 3u) >= 2) pp = p3 - Nnull / 2;
+  else pp = p3;
+  const uint32_t pt = slot ? (pp + Nt / 2) % Nt + base : pp;
+  return (int)(pt < Nt / 2 ? pt : pt + gap - Nt / 2);
+}
+
+uint32_t dci1c_rba_bits(uint32_t nof_prb) {
+  const uint32_t np = n_vrb_dist(nof_prb, false) / (nof_prb < 50 ? 2u : 4u);
+  return ceil_log2(np * (np + 1) / 2);
+}
+
+int tbs_1c(uint32_t i_tbs) {
+  static const int T[32] = {40,  56,  72,  120, 136, 144, 176, 208,  224,  256,  280,  296,  328,  336,  392,  488,
+                            552, 600, 632, 696, 776, 840, 904, 1000, 1064, 1128, 1224, 1288, 1384, 1480, 1608, 1736};
+  return i_tbs < 32 ? T[i_tbs] : -1;
 }
 
 void conv_rank_table(uint32_t D, std::vector<uint32_t>& rank) {

@@ -30,6 +30,8 @@ void crs_seq(uint32_t id, uint32_t ns, uint32_t l, float* re_im);
 // PDSCH RE membership / list (36.211 6.3.5 mapping order), grid index l * 12 N_RB + k
 int ctrl_symbols(uint32_t nof_prb, uint32_t cfi);
 bool is_pdsch_re(uint32_t id, uint32_t nof_prb, uint32_t nof_ports, uint32_t cfi, uint32_t sf, uint32_t l, uint32_t k);
+// prb_mask: bit s of entry p = PRB p used in slot s when any entry is >= 2 (distributed VRB), else
+// non-zero = used in both slots
 uint32_t pdsch_re_list(uint32_t id, uint32_t nof_prb, uint32_t nof_ports, uint32_t cfi, uint32_t sf,
                        const uint8_t* prb_mask, std::vector<uint32_t>& re);
 // PCFICH REs (36.211 6.7.4) in symbol 0, and scrambling init (36.211 6.7.1)
@@ -48,8 +50,17 @@ inline uint32_t phich_cinit(uint32_t id, uint32_t sf) { return (sf + 1) * (2 * i
 uint32_t pdcch_regs(uint32_t id, uint32_t nof_prb, uint32_t ng, uint32_t cfi, std::vector<uint32_t>* re4);
 // logical quadruplet carried by each physical REG (quadruplet sub-block interleaver + shift by N_ID)
 void pdcch_quad_perm(uint32_t M, uint32_t id, std::vector<uint32_t>& log_of_reg);
-enum { DCI_0 = 0, DCI_1 = 1, DCI_1A = 2 };
+enum { DCI_0 = 0, DCI_1 = 1, DCI_1A = 2, DCI_1C = 3 };
 uint32_t dci_size(int format, uint32_t nof_prb);
+// ---- DL resource allocation (36.213 7.1.6, 36.211 6.2.3.2) -------------------------------------
+uint32_t ceil_log2(uint32_t x);
+uint32_t rbg_size(uint32_t nof_prb);                       // Table 7.1.6.1-1
+uint32_t n_gap(uint32_t nof_prb, bool gap2);               // Table 6.2.3.2-1 (0: not defined)
+uint32_t n_vrb_dist(uint32_t nof_prb, bool gap2);          // N_VRB^DL of the distributed mapping
+// PRB of distributed VRB n_vrb in slot 0 / 1; -1 outside N_VRB^DL
+int vrb_to_prb(uint32_t nof_prb, bool gap2, uint32_t n_vrb, uint32_t slot);
+uint32_t dci1c_rba_bits(uint32_t nof_prb);
+int tbs_1c(uint32_t i_tbs);                                // Table 7.1.7.2.3-1, -1 for I_TBS > 31
 // circular-buffer rank of each coded bit p of the rate-1/3 tail-biting code (d0 | d1 | d2, D each):
 // e_k lands on the position of rank k mod 3D
 void conv_rank_table(uint32_t D, std::vector<uint32_t>& rank);

@@ -216,6 +216,11 @@ int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t* q, cf_t* input, uint32_t sf
   return SRSLTE_SUCCESS;
 }
 
+// grant PRBs per slot -> the two-slot mask encoding of mi_dl_sf_cfg_t (bit s: used in slot s)
+static void slot_mask(const srslte_ra_dl_grant_t* g, uint8_t* mask) {
+  for (int p = 0; p < SRSLTE_MAX_PRB; p++) mask[p] = (uint8_t)((g->prb_idx[0][p] ? 1u : 0u) | (g->prb_idx[1][p] ? 2u : 0u));
+}
+
 int srslte_ue_dl_cfg_grant(srslte_ue_dl_t* q, srslte_ra_dl_grant_t* grant, uint32_t cfi, uint32_t sf_idx,
                            uint32_t rvidx) {
   if (!q || !grant || cfi < 1 || cfi > 3 || sf_idx > 9 || rvidx > 3) return SRSLTE_ERROR_INVALID_INPUTS;
@@ -227,7 +232,7 @@ int srslte_ue_dl_cfg_grant(srslte_ue_dl_t* q, srslte_ra_dl_grant_t* grant, uint3
   pc->mimo_type = q->cell.nof_ports == 2 ? SRSLTE_MIMO_TYPE_TX_DIVERSITY : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA;
   pc->nof_layers = q->cell.nof_ports;
   uint8_t mask[SRSLTE_MAX_PRB];
-  for (int p = 0; p < SRSLTE_MAX_PRB; p++) mask[p] = grant->prb_idx[0][p] ? 1 : 0;
+  slot_mask(grant, mask);
   std::vector<uint32_t> re;
   pc->nbits.nof_re = mi::pdsch_re_list(q->cell.id, q->cell.nof_prb, q->cell.nof_ports, cfi, sf_idx, mask, re);
   pc->nbits.nof_bits = pc->nbits.nof_re * pc->grant.Qm;
@@ -256,7 +261,7 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
   s.tbs = (uint32_t)cfg->grant.mcs.tbs;
   s.Qm = cfg->grant.Qm ? cfg->grant.Qm : mod_bits(cfg->grant.mcs.mod);
   s.new_tb = 0;   // the MAC resets the softbuffer for a new TB (srslte_softbuffer_rx_reset_tbs)
-  for (int p = 0; p < SRSLTE_MAX_PRB; p++) s.prb_mask[p] = cfg->grant.prb_idx[0][p] ? 1 : 0;
+  slot_mask(&cfg->grant, s.prb_mask);
   c->eng.noise = noise_estimate;
   c->eng.max_its = q->dl_sch.max_iterations ? q->dl_sch.max_iterations : SRSLTE_PDSCH_MAX_TDEC_ITERS;
   if (c->eng.plan.build(&s, 1, true) || c->eng.upload(c->st, false)) return SRSLTE_ERROR;
@@ -309,8 +314,10 @@ static int find_dci(srslte_ue_dl_t* q, srslte_dci_msg_t* msg, uint32_t cfi, uint
   memset(msg, 0, sizeof(*msg));
   memcpy(msg->data, f.bits, f.nbits);
   msg->nof_bits = f.nbits;
-  msg->format = f.format == mi::DCI_0 ? SRSLTE_DCI_FORMAT0 : f.format == mi::DCI_1 ? SRSLTE_DCI_FORMAT1
-                                                                                  : SRSLTE_DCI_FORMAT1A;
+  msg->format = f.format == mi::DCI_0    ? SRSLTE_DCI_FORMAT0
+                : f.format == mi::DCI_1  ? SRSLTE_DCI_FORMAT1
+                : f.format == mi::DCI_1C ? SRSLTE_DCI_FORMAT1C
+                                         : SRSLTE_DCI_FORMAT1A;
   q->last_location.L = f.L;
   q->last_location.ncce = f.ncce;
   q->last_n_cce = f.ncce;
@@ -351,55 +358,139 @@ static uint32_t take_bits(const uint8_t* b, uint32_t* pos, uint32_t n) {
   return v;
 }
 
-int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t* msg, uint16_t /*msg_rnti*/, uint32_t nof_prb, srslte_ra_dl_dci_t* dci,
+// 36.213 7.1.6.3: RIV over an N-wide space -> (start, L)
+static bool riv_decode(uint32_t riv, uint32_t N, uint32_t* start, uint32_t* L) {
+  if (!N) return false;
+  const uint32_t a = riv / N, b = riv % N;
+  if (a + b < N) { *L = a + 1; *start = b; }
+  else { *L = N - a + 1; *start = N - 1 - b; }
+  return *L >= 1 && *start + *L <= N && riv < N * (N + 1) / 2;
+}
+
+static void set_prb(srslte_ra_dl_grant_t* g, uint32_t slot, int p) {
+  if (p >= 0 && p < SRSLTE_MAX_PRB) g->prb_idx[slot][p] = true;
+}
+
+int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t* msg, uint16_t msg_rnti, uint32_t nof_prb, srslte_ra_dl_dci_t* dci,
                                srslte_ra_dl_grant_t* grant) {
   if (!msg || !dci || !grant || mi::symbol_sz(nof_prb) < 0) return SRSLTE_ERROR_INVALID_INPUTS;
   memset(dci, 0, sizeof(*dci));
   memset(grant, 0, sizeof(*grant));
-  const uint32_t n1a = mi::dci_size(mi::DCI_1A, nof_prb), n1 = mi::dci_size(mi::DCI_1, nof_prb);
-  uint32_t pos = 0;
+  const uint32_t N = nof_prb, n1a = mi::dci_size(mi::DCI_1A, N), n1 = mi::dci_size(mi::DCI_1, N);
+  const uint32_t n1c = mi::dci_size(mi::DCI_1C, N);
+  // SI-RNTI, P-RNTI and RA-RNTI (1..60) scramble common-control DCIs (36.321 7.1)
+  const bool common = msg_rnti < 0x003D || msg_rnti > 0xFFF3;
+  uint32_t pos = 0, itbs_1a_common = 0, nprb_tbs = 0;
   if (msg->nof_bits == n1a && msg->data[0] == 1) {
-    // format 1A (36.212 5.3.3.1.3): flag, localized VRB, RIV, MCS, HARQ, NDI, RV, TPC
-    uint32_t rba = 0;
-    while ((1u << rba) < nof_prb * (nof_prb + 1) / 2) rba++;
+    // format 1A (36.212 5.3.3.1.3): flag, L/D VRB flag, RBA, MCS, HARQ, NDI, RV, TPC
+    const uint32_t rba = mi::ceil_log2(N * (N + 1) / 2);
     pos = 1;
-    if (take_bits(msg->data, &pos, 1)) return SRSLTE_ERROR;   // distributed VRB: not supported
-    const uint32_t riv = take_bits(msg->data, &pos, rba), a = riv / nof_prb, b = riv % nof_prb;
-    uint32_t L, start;
-    if (a + b < nof_prb) { L = a + 1; start = b; }
-    else { L = nof_prb - a + 1; start = nof_prb - 1 - b; }
-    if (start + L > nof_prb) return SRSLTE_ERROR;
+    const bool dist = take_bits(msg->data, &pos, 1) != 0;
+    // distributed, N_RB >= 50, C-RNTI: the RBA's MSB selects the gap (N_gap,1 / N_gap,2)
+    const bool gap_in_rba = dist && N >= 50 && !common;
+    const uint32_t gap_rba = gap_in_rba ? take_bits(msg->data, &pos, 1) : 0;
+    const uint32_t riv = take_bits(msg->data, &pos, gap_in_rba ? rba - 1 : rba);
+    uint32_t start, L;
+    if (!riv_decode(riv, N, &start, &L)) return SRSLTE_ERROR;
+    dci->mcs_idx = take_bits(msg->data, &pos, 5);
+    dci->harq_process = take_bits(msg->data, &pos, 3);
+    const uint32_t ndi = take_bits(msg->data, &pos, 1);
+    dci->rv_idx = take_bits(msg->data, &pos, 2);
+    dci->tpc_pucch = take_bits(msg->data, &pos, 2);
+    // SI/RA/P-RNTI: the NDI bit carries the gap of a distributed allocation (N_RB >= 50), the TPC LSB the
+    // TBS column N_PRB^1A (36.213 7.1.7.2.1: 2 or 3 PRBs), modulation QPSK with I_TBS = I_MCS
+    dci->ndi = !common && ndi;
+    dci->type2_gap = gap_in_rba ? gap_rba : (common && dist && N >= 50) ? ndi : 0;
     dci->alloc_type = SRSLTE_RA_ALLOC_TYPE2;
     dci->type2_start = start;
     dci->type2_len = L;
+    dci->type2_distributed = dist;
     dci->dci_format = SRSLTE_DCI_FORMAT1A;
-    for (uint32_t p = start; p < start + L; p++) grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
+    if (!dist) {
+      for (uint32_t p = start; p < start + L; p++) grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
+    } else {
+      if (start + L > mi::n_vrb_dist(N, dci->type2_gap != 0)) return SRSLTE_ERROR;
+      for (uint32_t n = start; n < start + L; n++)
+        for (uint32_t s = 0; s < 2; s++) set_prb(grant, s, mi::vrb_to_prb(N, dci->type2_gap != 0, n, s));
+    }
     grant->nof_prb = L;
+    if (common) {
+      itbs_1a_common = 1;
+      nprb_tbs = (dci->tpc_pucch & 1u) ? 3 : 2;
+    } else {
+      nprb_tbs = L;
+    }
+  } else if (msg->nof_bits == n1c && common) {
+    // format 1C (36.212 5.3.3.1.4): [gap if N_RB >= 50], RBA over N'_VRB = N_VRB,gap1 / N_step, I_TBS
+    const uint32_t step = N < 50 ? 2 : 4, np = mi::n_vrb_dist(N, false) / step;
+    dci->type2_gap = N >= 50 ? take_bits(msg->data, &pos, 1) : 0;
+    const uint32_t riv = take_bits(msg->data, &pos, mi::dci1c_rba_bits(N));
+    uint32_t s1, l1;
+    if (!riv_decode(riv, np, &s1, &l1)) return SRSLTE_ERROR;
+    const uint32_t start = s1 * step, L = l1 * step;
+    if (start + L > mi::n_vrb_dist(N, dci->type2_gap != 0)) return SRSLTE_ERROR;
+    dci->mcs_idx = take_bits(msg->data, &pos, 5);
+    dci->alloc_type = SRSLTE_RA_ALLOC_TYPE2;
+    dci->type2_start = start;
+    dci->type2_len = L;
+    dci->type2_distributed = true;
+    dci->dci_format = SRSLTE_DCI_FORMAT1C;
+    for (uint32_t n = start; n < start + L; n++)
+      for (uint32_t s = 0; s < 2; s++) set_prb(grant, s, mi::vrb_to_prb(N, dci->type2_gap != 0, n, s));
+    grant->nof_prb = L;
+    grant->Qm = 2;
+    grant->mcs.idx = dci->mcs_idx;
+    grant->mcs.tbs = mi::tbs_1c(dci->mcs_idx);
+    grant->mcs.mod = SRSLTE_MOD_QPSK;
+    return SRSLTE_SUCCESS;
   } else if (msg->nof_bits == n1) {
-    // format 1 (36.212 5.3.3.1.2), type-0 allocation: [header], RBG bitmap, MCS, HARQ, NDI, RV, TPC
-    const uint32_t P = nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4, nrbg = (nof_prb + P - 1) / P;
-    if (nof_prb > 10 && take_bits(msg->data, &pos, 1)) return SRSLTE_ERROR;   // type 1: not supported
-    dci->alloc_type = SRSLTE_RA_ALLOC_TYPE0;
+    // format 1 (36.212 5.3.3.1.2): [RA header if N_RB > 10], type 0 / type 1 field, MCS, HARQ, NDI, RV, TPC
+    const uint32_t P = mi::rbg_size(N), nrbg = (N + P - 1) / P;
+    const bool type1 = N > 10 && take_bits(msg->data, &pos, 1);
     dci->dci_format = SRSLTE_DCI_FORMAT1;
-    for (uint32_t g = 0; g < nrbg; g++) {
-      const uint32_t bit = take_bits(msg->data, &pos, 1);
-      dci->type0_alloc = (dci->type0_alloc << 1) | bit;
-      for (uint32_t p = g * P; bit && p < (g + 1) * P && p < nof_prb; p++) {
+    if (!type1) {
+      dci->alloc_type = SRSLTE_RA_ALLOC_TYPE0;
+      for (uint32_t g = 0; g < nrbg; g++) {
+        const uint32_t bit = take_bits(msg->data, &pos, 1);
+        dci->type0_alloc = (dci->type0_alloc << 1) | bit;
+        for (uint32_t p = g * P; bit && p < (g + 1) * P && p < N; p++) grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
+      }
+    } else {
+      // type 1 (36.213 7.1.6.2): subset p, shift, bitmap over N_RB^TYPE1 VRBs of the subset
+      dci->alloc_type = SRSLTE_RA_ALLOC_TYPE1;
+      const uint32_t pb = mi::ceil_log2(P), nt1 = nrbg - pb - 1;
+      dci->type1_subset = take_bits(msg->data, &pos, pb);
+      dci->type1_shift = take_bits(msg->data, &pos, 1);
+      dci->type1_bitmap = take_bits(msg->data, &pos, nt1);
+      const uint32_t sp = dci->type1_subset;
+      if (sp >= P) return SRSLTE_ERROR;
+      // VRBs in subset p: full RBG rows below the last RBG's subset, the partial last one, none above
+      const uint32_t last = (N - 1) / P % P, rows = (N - 1) / (P * P);
+      const uint32_t n_sub = sp < last ? rows * P + P : sp == last ? rows * P + (N - 1) % P + 1 : rows * P;
+      const uint32_t delta = dci->type1_shift ? (n_sub > nt1 ? n_sub - nt1 : 0) : 0;
+      for (uint32_t i = 0; i < nt1; i++) {
+        if (!((dci->type1_bitmap >> (nt1 - 1 - i)) & 1u)) continue;
+        const uint32_t j = i + delta, p = (j / P) * P * P + sp * P + j % P;
+        if (j >= n_sub || p >= N) return SRSLTE_ERROR;
         grant->prb_idx[0][p] = grant->prb_idx[1][p] = true;
-        grant->nof_prb++;
       }
     }
+    for (uint32_t p = 0; p < N; p++) grant->nof_prb += grant->prb_idx[0][p] ? 1 : 0;
+    if (!grant->nof_prb) return SRSLTE_ERROR;
+    nprb_tbs = grant->nof_prb;
   } else {
     return SRSLTE_ERROR;
   }
-  dci->mcs_idx = take_bits(msg->data, &pos, 5);
-  dci->harq_process = take_bits(msg->data, &pos, 3);
-  dci->ndi = take_bits(msg->data, &pos, 1) != 0;
-  dci->rv_idx = take_bits(msg->data, &pos, 2);
-  dci->tpc_pucch = take_bits(msg->data, &pos, 2);
-  uint32_t qm = 0;
-  const int itbs = mi::mcs_to_itbs(dci->mcs_idx, &qm);
-  const int tbs = itbs < 0 ? -1 : mi::tbs_from_idx((uint32_t)itbs, grant->nof_prb);
+  if (dci->dci_format == SRSLTE_DCI_FORMAT1) {
+    dci->mcs_idx = take_bits(msg->data, &pos, 5);
+    dci->harq_process = take_bits(msg->data, &pos, 3);
+    dci->ndi = take_bits(msg->data, &pos, 1) != 0;
+    dci->rv_idx = take_bits(msg->data, &pos, 2);
+    dci->tpc_pucch = take_bits(msg->data, &pos, 2);
+  }
+  uint32_t qm = 2;
+  const int itbs = itbs_1a_common ? (dci->mcs_idx <= 26 ? (int)dci->mcs_idx : -1) : mi::mcs_to_itbs(dci->mcs_idx, &qm);
+  const int tbs = itbs < 0 ? -1 : mi::tbs_from_idx((uint32_t)itbs, nprb_tbs);
   if (tbs <= 0) return SRSLTE_ERROR;
   grant->Qm = qm;
   grant->mcs.idx = dci->mcs_idx;
@@ -411,9 +502,9 @@ int srslte_dci_msg_to_dl_grant(srslte_dci_msg_t* msg, uint16_t /*msg_rnti*/, uin
 char* srslte_ra_dl_dci_string(srslte_ra_dl_dci_t* dci) {
   static thread_local char buf[96];
   if (!dci) return buf;
-  snprintf(buf, sizeof(buf), "format=%s, mcs=%u, harq=%u, ndi=%d, rv=%u",
-           dci->dci_format == SRSLTE_DCI_FORMAT1 ? "1" : "1A", dci->mcs_idx, dci->harq_process, (int)dci->ndi,
-           dci->rv_idx);
+  const char* fmt = dci->dci_format == SRSLTE_DCI_FORMAT1 ? "1" : dci->dci_format == SRSLTE_DCI_FORMAT1C ? "1C" : "1A";
+  snprintf(buf, sizeof(buf), "format=%s, mcs=%u, harq=%u, ndi=%d, rv=%u", fmt, dci->mcs_idx, dci->harq_process,
+           (int)dci->ndi, dci->rv_idx);
   return buf;
 }
 

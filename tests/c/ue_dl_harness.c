@@ -13,7 +13,8 @@
  *              with I_lowest = hdr[7] & 0xffff, n_dmrs = hdr[7] >> 16
  * Input file : int32 hdr[8] = {cell_id, nof_prb, nof_ports, nsf, phich_ng, pdcch_mode, phich, query}; per subframe
  *              int32 p[8] = {sf_idx, tbs, Qm, rv, reset_tbs, rnti, max_its, pass_own_buffers} +
- *              2*SF_LEN floats.
+ *              2*SF_LEN floats.  p[5] = rnti | rnti_type << 16 (srslte_rnti_type_t of the PDCCH search:
+ *              SRSLTE_RNTI_USER searches the C-RNTI spaces, SI/RAR/PCH the common space with 1A and 1C).
  * Output file: per subframe int32 r[8] = {ret, cfi, noi, dci_found, ncce, grant_tbs, harq, rv} +
  *              float m[5] + int32 phich (1 ACK, 0 NACK, -1 not asked) + tbs/8 payload bytes.
  */
@@ -48,7 +49,9 @@ int main(int argc, char **argv) {
     int32_t p[8];
     if (fread(p, 4, 8, fi) != 8 || fread(buf, 8, sflen, fi) != sflen) return 4;
     if (p[6] > 0) srslte_sch_set_max_noi(&ue_dl.pdsch.dl_sch, (uint32_t)p[6]);
-    srslte_ue_dl_set_rnti(&ue_dl, (uint16_t)p[5]);
+    const uint16_t rnti = (uint16_t)(p[5] & 0xffff);
+    const srslte_rnti_type_t rtype = (srslte_rnti_type_t)(p[5] >> 16);
+    if (rtype == SRSLTE_RNTI_USER) srslte_ue_dl_set_rnti(&ue_dl, rnti);
     if (p[4]) srslte_softbuffer_rx_reset_tbs(&sb, (uint32_t)p[1]);
     int32_t r[8] = {0};
     float m[5] = {0};
@@ -63,10 +66,9 @@ int main(int argc, char **argv) {
       srslte_ra_dl_dci_t dci;
       if (srslte_pdcch_extract_llr(&ue_dl.pdcch, ue_dl.sf_symbols, ue_dl.ce, 0, (uint32_t)p[0], cfi)) {
         ret = -11;
-      } else if ((r[3] = srslte_ue_dl_find_dl_dci_type(&ue_dl, &msg, cfi, (uint32_t)p[0], (uint16_t)p[5],
-                                                        SRSLTE_RNTI_USER)) != 1) {
+      } else if ((r[3] = srslte_ue_dl_find_dl_dci_type(&ue_dl, &msg, cfi, (uint32_t)p[0], rnti, rtype)) != 1) {
         ret = -12;
-      } else if (srslte_dci_msg_to_dl_grant(&msg, (uint16_t)p[5], cell.nof_prb, &dci, &grant)) {
+      } else if (srslte_dci_msg_to_dl_grant(&msg, rnti, cell.nof_prb, &dci, &grant)) {
         ret = -13;
       } else {
         r[4] = (int32_t)srslte_ue_dl_get_ncce(&ue_dl);
@@ -100,7 +102,7 @@ int main(int argc, char **argv) {
             ce[q] = ce_copy[q];
           }
         }
-        ret = srslte_pdsch_decode_rnti(&ue_dl.pdsch, &ue_dl.pdsch_cfg, &sb, grid, ce, 0.01f, (uint16_t)p[5], payload);
+        ret = srslte_pdsch_decode_rnti(&ue_dl.pdsch, &ue_dl.pdsch_cfg, &sb, grid, ce, 0.01f, rnti, payload);
         free(copy);
         for (uint32_t q = 0; q < SRSLTE_MAX_PORTS; q++) free(ce_copy[q]);
       }

@@ -38,7 +38,13 @@ class DciFound(C.Structure):
                 ("bits", C.c_uint8 * 64)]
 
 
-DCI_0, DCI_1, DCI_1A = 0, 1, 2
+class DlGrant(C.Structure):
+    _fields_ = [("prb", C.c_uint8 * NRB_MAX)] + [(n, C.c_uint32) for n in (
+        "format", "alloc_type", "distributed", "gap2", "nof_prb", "mcs", "harq", "ndi", "rv", "tpc", "Qm", "i_tbs",
+        "n_prb_tbs")] + [("tbs", C.c_int)]
+
+
+DCI_0, DCI_1, DCI_1A, DCI_1C = 0, 1, 2, 3
 
 
 class TxCfg(C.Structure):
@@ -123,6 +129,14 @@ def lib():
             "or_search_space": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_int, u32, u32]),
             "or_find_dci": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint16, C.c_int,
                                       C.POINTER(DciFound)]),
+            "or_find_dci_mode": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint16, C.c_int,
+                                           C.POINTER(DciFound)]),
+            "or_rbg_size": (C.c_uint32, [C.c_uint32]),
+            "or_ngap": (C.c_uint32, [C.c_uint32, C.c_int]),
+            "or_nvrb_dist": (C.c_uint32, [C.c_uint32, C.c_int]),
+            "or_vrb_to_prb": (C.c_int, [C.c_uint32, C.c_int, C.c_uint32, C.c_uint32]),
+            "or_dci1c_size": (C.c_uint32, [C.c_uint32]),
+            "or_dl_dci_to_grant": (C.c_int, [u8, C.c_uint32, C.c_uint16, C.c_uint32, C.POINTER(DlGrant)]),
             "or_tx_pdcch": (C.c_int, [C.POINTER(CtrlCfg), C.c_uint16, C.c_uint32, C.c_uint32, u8, C.c_uint32,
                                       C.c_void_p, f32]),
             "or_phich_calc": (None, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
@@ -273,10 +287,19 @@ def phich_soft(q, grid, ce, group, seq):
                                np.ascontiguousarray(ce, np.float32), group, seq)
 
 
-def find_dci(llr, n_cce, nof_prb, sf, rnti, ul=False):
+def find_dci(llr, n_cce, nof_prb, sf, rnti, ul=False, mode=None):
+    """mode: 0 = DL C-RNTI, 1 = UL, 2 = DL SI/RA/P-RNTI (common space, 1A then 1C); default from ul"""
     out = DciFound()
-    ok = lib().or_find_dci(np.ascontiguousarray(llr, np.float32), n_cce, nof_prb, sf, rnti, int(ul), C.byref(out))
+    m = (1 if ul else 0) if mode is None else mode
+    ok = lib().or_find_dci_mode(np.ascontiguousarray(llr, np.float32), n_cce, nof_prb, sf, rnti, m, C.byref(out))
     return (out.format, np.array(out.bits[:out.nbits], np.uint8), out.L, out.ncce) if ok else None
+
+
+def dl_grant(bits, rnti, nof_prb):
+    """or_dl_dci_to_grant: DlGrant or None"""
+    g = DlGrant()
+    b = np.ascontiguousarray(bits, np.uint8)
+    return g if lib().or_dl_dci_to_grant(b, len(b), rnti, nof_prb, C.byref(g)) == 0 else None
 
 
 def cbsegm(tbs):
@@ -296,7 +319,8 @@ def tx_cfg(cell, sf_idx=1, cfi=1, mcs=28, rv=0, rnti=0x46, tm=1, tbs=0, qm=0, pr
     cfg.sf_idx, cfg.cfi, cfg.mcs, cfg.rv, cfg.rnti, cfg.tm = sf_idx, cfi, mcs, rv, rnti, tm
     cfg.tbs, cfg.qm = tbs, qm
     for p in range(NRB_MAX):
-        cfg.prb_mask[p] = 1 if (p < cell.nof_prb and (prb is None or prb[p])) else 0
+        # prb entries are kept as given: 0/1 (both slots) or the two-slot encoding (bit s = slot s)
+        cfg.prb_mask[p] = (1 if prb is None else int(prb[p])) if p < cell.nof_prb else 0
     cfg.snr_db = snr_db
     h = h if h is not None else [1.0 + 0j, 0.0 + 0j] if cell.nof_ports == 1 else [0.8 + 0.3j, -0.4 + 0.5j]
     for p in range(2):

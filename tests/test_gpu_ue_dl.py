@@ -27,9 +27,10 @@ def run_harness(cell_id, nof_prb, nof_ports, subframes, phich_ng=0, pdcch=False,
             q = 0 if phich is None else phich[0] | (phich[1] << 16)
             f.write(struct.pack("8i", cell_id, nof_prb, nof_ports, len(subframes), phich_ng, int(pdcch),
                                 int(phich is not None), q))
-            for cfg, iq, reset, max_its, own in subframes:
-                f.write(struct.pack("8i", cfg.sf_idx, cfg.tbs, cfg.Qm, cfg.rv, int(reset), cfg.rnti, max_its,
-                                    int(own)))
+            for cfg, iq, reset, max_its, own, *rtype in subframes:
+                rt = rtype[0] if rtype else 0      # srslte_rnti_type_t of the PDCCH search (0 = C-RNTI)
+                f.write(struct.pack("8i", cfg.sf_idx, cfg.tbs, cfg.Qm, cfg.rv, int(reset), cfg.rnti | (rt << 16),
+                                    max_its, int(own)))
                 f.write(np.ascontiguousarray(iq, np.float32).tobytes())
         subprocess.check_call([HARNESS, fin, fout], timeout=300)
         out, raw = [], open(fout, "rb").read()
@@ -169,3 +170,117 @@ def test_ue_dl_decode_phich_srsue_call_order():
     for (ret, cf, noi, met, pay, extra), (tb, ack) in zip(res, tbs):
         assert ret == 0 and np.array_equal(pay, tb)
         assert extra[-1] == ack
+
+
+RNTI_USER, RNTI_SI, RNTI_RAR, RNTI_PCH = 0, 1, 2, 5
+
+
+def _clog2(x):
+    n = 0
+    while (1 << n) < x:
+        n += 1
+    return n
+
+
+def _riv(N, start, L):
+    return N * (L - 1) + start if L - 1 <= N // 2 else N * (N - L + 1) + (N - 1 - start)
+
+
+def _put(bits, v, n):
+    bits.extend((v >> (n - 1 - i)) & 1 for i in range(n))
+
+
+def _dci_bits(N, kind, **f):
+    """36.212 5.3.3.1 field layouts (see tests/test_dl_grant.py for the field-by-field checks)"""
+    b = []
+    if kind == "1a":
+        common, dist, gap = f.get("common", False), f.get("dist", 0), f.get("gap", 0)
+        b += [1, dist]
+        rba = _clog2(N * (N + 1) // 2)
+        if dist and N >= 50 and not common:
+            _put(b, gap, 1); _put(b, _riv(N, f["start"], f["L"]), rba - 1)
+        else:
+            _put(b, _riv(N, f["start"], f["L"]), rba)
+        _put(b, f["mcs"], 5); _put(b, f.get("harq", 0), 3)
+        _put(b, gap if (common and dist and N >= 50) else f.get("ndi", 1), 1)
+        _put(b, f.get("rv", 0), 2); _put(b, f.get("tpc", 0), 2)
+        n = O.lib().or_dci_size(O.DCI_1A, N)
+    elif kind == "1c":
+        step = 2 if N < 50 else 4
+        Np = O.lib().or_nvrb_dist(N, 0) // step
+        if N >= 50:
+            _put(b, f.get("gap", 0), 1)
+        _put(b, _riv(Np, f["start"] // step, f["L"] // step), _clog2(Np * (Np + 1) // 2)); _put(b, f["itbs"], 5)
+        n = O.lib().or_dci1c_size(N)
+    else:   # format 1, type 1
+        P = O.lib().or_rbg_size(N)
+        nrbg = -(-N // P)
+        pb = _clog2(P)
+        b += [1]
+        _put(b, f["subset"], pb); _put(b, f["shift"], 1); _put(b, f["bitmap"], nrbg - pb - 1)
+        _put(b, f["mcs"], 5); _put(b, f.get("harq", 0), 3); _put(b, 1, 1); _put(b, f.get("rv", 0), 2); _put(b, 0, 2)
+        n = O.lib().or_dci_size(O.DCI_1, N)
+    return np.array(b + [0] * (n - len(b)), np.uint8)
+
+
+def _tx_grant_subframe(cell_id, N, ng, cfi, sf, rnti, common, bits, tb_seed, seed, snr_db=30.0):
+    """The ORACLE transmitter (o_tx.c) puts the PDSCH on the grant's per-slot PRBs (oracle/o_ra.c decode of
+    the same DCI) and the DCI on a PDCCH candidate of the right search space; then AWGN."""
+    import ctypes as C
+    g = O.dl_grant(bits, rnti, N)
+    assert g is not None
+    tbs = g.tbs if g.tbs > 0 else abi.lib().srslte_ra_tbs_from_idx(g.i_tbs, g.n_prb_tbs)
+    tb = tb_bytes(tb_seed, tbs)
+    cell = O.make_cell(cell_id, N, 1)
+    tc = O.tx_cfg(cell, sf_idx=sf, cfi=cfi, rnti=rnti, tbs=tbs, qm=g.Qm, prb=np.array(g.prb, np.uint8),
+                  snr_db=300.0, seed=seed)
+    iq, _ = O.tx_subframe(tc, tb)
+    q = O.ctrl_cfg(cell_id, N, 1, ng, cfi, sf)
+    n = C.c_uint32()
+    O.lib().or_pdcch_regs(C.byref(q), None, C.byref(n))
+    Ls, nc = np.zeros(32, np.uint32), np.zeros(32, np.uint32)
+    k = O.lib().or_search_space(n.value, sf, 0 if common else rnti, int(common), Ls, nc)
+    assert k > 0
+    assert O.lib().or_tx_pdcch(C.byref(q), rnti, int(Ls[k - 1]), int(nc[k - 1]), bits, len(bits), None, iq) == 0
+    iq = (iq + np.random.default_rng(seed).normal(0, np.sqrt(10 ** (-snr_db / 10) / 2), iq.shape)).astype(np.float32)
+    cfg = abi.sf_cfg(cell_id=cell_id, nof_prb=N, nof_ports=1, sf_idx=sf, cfi=cfi, tbs=tbs, Qm=g.Qm, rnti=rnti,
+                     rv=g.rv, prb=np.array(g.prb, np.uint8))
+    return cfg, iq, tb, g, int(nc[k - 1])
+
+
+@pytest.mark.parametrize("N", [100, 25])
+def test_ue_dl_common_and_partial_grants_srsue_call_order(N):
+    """SURVEY 8a a5.1 / 8f-1 through the per-TTI ABI in srsUE's order (phch_worker.cc:286-305, :337-348):
+    the harness blind-decodes each DCI with srslte_ue_dl_find_dl_dci_type for the RNTI type srsUE asks
+    for, converts it with srslte_dci_msg_to_dl_grant and decodes the PDSCH on the grant's per-slot PRBs:
+    a format-1C SI grant (distributed VRB, sf 5 with PSS/SSS holes), a 13-PRB localized 1A, a distributed
+    1A (gap in the RBA for N_RB >= 50), an RA-RNTI 1A (N_PRB^1A = 3, the NDI bit as gap), a P-RNTI 1C and
+    a format-1 type-1 allocation.  The oracle transmitter puts PDSCH and PDCCH on the air; checked: the
+    decoded grant (TBS, PRB count) against the oracle's DCI decode, payload == transmitted TB (bit-exact)
+    and == the oracle's decode of the same IQ, iterations == the oracle's."""
+    step = 2 if N < 50 else 4
+    big = N >= 50
+    cases = [   # (rnti, rnti type, sf, cfi, dci)
+        (0xFFFF, RNTI_SI, 5, 2, _dci_bits(N, "1c", start=2 * step, L=2 * step, itbs=12, gap=int(big))),
+        (0x4601, RNTI_USER, 2, 1, _dci_bits(N, "1a", start=3, L=13, mcs=17, harq=5, rv=0)),
+        (0x4601, RNTI_USER, 3, 3, _dci_bits(N, "1a", start=4, L=10, mcs=12, harq=2, dist=1, gap=0)),
+        (0x0002, RNTI_RAR, 6, 3, _dci_bits(N, "1a", start=1, L=4, mcs=6, tpc=1, common=True, dist=1,
+                                            gap=int(big))),
+        (0xFFFE, RNTI_PCH, 7, 2, _dci_bits(N, "1c", start=0, L=3 * step, itbs=20)),
+        (0x4601, RNTI_USER, 8, 1, _dci_bits(N, "t1", subset=1, shift=1, bitmap=0b1011011, mcs=20, harq=1)),
+    ]
+    subs, truth = [], []
+    for i, (rnti, rt, sf, cfi, bits) in enumerate(cases):
+        common = rt != RNTI_USER
+        cfg, iq, tb, g, ncce = _tx_grant_subframe(21, N, 2, cfi, sf, rnti, common, bits, 300 + i, 40 + i)
+        subs.append((cfg, iq, True, 4, True, rt))
+        truth.append((tb, g, ncce))
+    res = run_harness(21, N, 1, subs, phich_ng=2, pdcch=True, full=True)
+    for (cfg, iq, *_), (ret, cf, noi, met, pay, extra), (tb, g, ncce) in zip(subs, res, truth):
+        found, gncce, gtbs, gharq, grv, _ = extra
+        assert cf == cfg.cfi and found == 1 and gncce == ncce
+        assert gtbs == cfg.tbs and (gharq, grv) == ((g.harq, g.rv) if g.format != O.DCI_1C else (0, 0))
+        _, _, _, ollr = oracle_front(cfg, iq)
+        ok, opay, onoi, _ = oracle_dlsch(cfg, ollr, i16=True)
+        assert ok and ret == 0, f"rnti {cfg.rnti:#x}: GPU ret {ret}"
+        assert np.array_equal(pay, tb) and np.array_equal(pay, opay) and noi == onoi
