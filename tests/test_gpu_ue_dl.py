@@ -114,7 +114,7 @@ def test_ue_dl_pdcch_to_pdsch_srsue_call_order():
     import ctypes as C
     import oracle_lib as O
     from test_oracle_ctrl import tx_with_dci
-    rnti, ng = 0x3C, 2
+    rnti, ng = 0x3D, 2      # the first C-RNTI (36.321 7.1: 0x0001-0x003C are RA-RNTIs)
     subs, truth = [], []
     for i, (ports, cfi, sf, mcs) in enumerate([(1, 1, 1, 28), (2, 2, 3, 20), (1, 3, 6, 9)]):
         qm, itbs = (2, mcs) if mcs <= 9 else (4, mcs - 1) if mcs <= 16 else (6, mcs - 2)
