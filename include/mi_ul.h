@@ -11,8 +11,10 @@
  * -> channel interleaver (5.2.2.8, no UCI) -> scrambling (36.211 5.3.1) -> modulation (7.1) ->
  * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, per-slot PRBs) +
  * DMRS (5.5.2.1, L_prb >= 3) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
- * HARQ-ACK bits (1 or 2) are multiplexed as 36.212 5.2.2.6 / 5.2.2.8 prescribe (Q'_ACK coded symbols
- * puncturing the data next to the DMRS); CQI / RI on PUSCH are not supported.
+ * Uplink control information is multiplexed as 36.212 5.2.2.6-5.2.2.8 prescribe: CQI (O <= 11 bits: the
+ * (32, O) block code; O > 11: CRC8 + tail-biting convolutional code) ahead of the data in the multiplexed
+ * sequence, RI (1 or 2 bits) in the interleaver columns next to the HARQ-ACK ones (rate matching of the
+ * data around both), HARQ-ACK (1 or 2 bits) puncturing the data next to the DMRS.
  * Normalisation: unit average power per used subcarrier (1/sqrt(M) DFT, 1/sqrt(N) IDFT).
  */
 #ifndef MI_UL_H
@@ -33,6 +35,10 @@ typedef struct {
                                                           (bit 0 = first), beta_offset index (36.213 8.6.3-1) */
   uint32_t hop, n_prb1;                                /* hop = 1: slot 1 starts at PRB n_prb1 (frequency hopping,
                                                           36.213 8.4 -- the per-TTI API computes it from the DCI) */
+  uint32_t cqi_len, I_offset_cqi;                      /* CQI on PUSCH (36.212 5.2.2.6.4): 0..64 bits, beta_offset
+                                                          index 2..15 (36.213 Table 8.6.3-3) */
+  uint8_t  cqi[64];                                    /* CQI bits o_0 .. o_{O-1}, one per byte (srslte_uci_data_t) */
+  uint32_t ri_len, ri, I_offset_ri;                    /* RI on PUSCH: 0..2 bits (bit 0 = o0), index 0..12 (8.6.3-2) */
 } mi_ul_cfg_t;
 
 enum { MI_UL_STAGE_CRC = 0, MI_UL_STAGE_ENCODE, MI_UL_STAGE_MOD, MI_UL_NSTAGES };
@@ -51,8 +57,9 @@ size_t mi_ul_batch_iq_samples(const mi_ul_batch_t *b);
 uint32_t mi_ul_batch_n_codeblocks(const mi_ul_batch_t *b);
 /* enqueue the chain on `stream` (hipStream_t, NULL = default): d_payload -> d_iq (both device) */
 int    mi_ul_batch_run(mi_ul_batch_t *b, const void *d_payload, void *d_iq, void *stream);
-/* parity hooks: the 12 M coded symbols of transmission i after the last run (rate-matching output
- * in channel-interleaver input order, Qm bits per byte, first bit = MSB) */
+/* parity hooks: the coded symbols of transmission i after the last run in channel-interleaver input order
+ * (36.212 5.2.2.7 g: Q'_CQI CQI symbols, then the rate-matched data), Qm bits per byte, first bit = MSB;
+ * 12 M bytes are written, of which the last Q'_RI (the RI cells) are zero */
 int    mi_ul_batch_symbols(mi_ul_batch_t *b, uint32_t i, uint8_t *host);
 int    mi_ul_batch_stage_ms(mi_ul_batch_t *b, float *ms /* MI_UL_NSTAGES */, uint32_t *nruns);
 void   mi_ul_batch_profile_reset(mi_ul_batch_t *b);

@@ -278,9 +278,10 @@ SRSLTE_API void srslte_vec_free(void *ptr);
  * srslte_ue_ul on the GPU (srsue_amd/csrc/ul.hip, ue_ul.cpp): cfg_grant plans the transmission,
  * pusch_encode_rnti_softbuffer copies the payload to HBM, runs TB CRC -> turbo encoder -> rate matching
  * -> channel interleaver -> scrambling -> modulation -> transform precoding + DMRS -> SC-FDMA and copies
- * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  HARQ-ACK in uci_data (1 or 2 bits) is
- * multiplexed into the PUSCH (36.212 5.2.2.6, beta_offset from set_cfg's uci_cfg.I_offset_ack).  Limits:
- * no CQI / RI on PUSCH (returns SRSLTE_ERROR), PUSCH hopping type 1 only (36.213 8.4.1: DCI format 0 hopping
+ * the subframe (SRSLTE_SF_LEN_PRB samples) to output_signal.  The UCI in uci_data is multiplexed into the
+ * PUSCH (36.212 5.2.2.6-5.2.2.8, beta_offsets from set_cfg's uci_cfg): HARQ-ACK (1 or 2 bits), periodic
+ * CQI (uci_cqi / uci_cqi_len, up to 64 bits: the (32, O) block code up to 11 bits, CRC8 + tail-biting
+ * convolutional code above) and RI (uci_ri / uci_ri_len, 1 or 2 bits).  Limits: PUSCH hopping type 1 only (36.213 8.4.1: DCI format 0 hopping
  * bits through srslte_dci_msg_to_ul_grant's n_rb_ho, intra- or inter-subframe mode from set_cfg's hopping
  * configuration; type 2 returns SRSLTE_ERROR), L_prb >= 3; PUCCH, SRS and UL
  * power control stay in srsLTE.  set_cfg uses the DMRS and hopping configurations, the others are

@@ -7,10 +7,16 @@
  * through the DL-SCH decoder, the SC-FDMA symbols through a DFT receiver).
  *
  *   UL-SCH (36.212 5.2.2): CRC24A, segmentation, CRC24B, turbo code, rate matching with the full
- *          circular buffer (the DL-SCH chain of o_tx.c with N_L = 1), G = 12 M_sc Q_m (normal CP, no
- *          SRS, no UCI);
- *   channel interleaver (5.2.2.8, no UCI): Q_m-bit symbols written row by row into M_sc rows x 12
- *          columns, read column by column -> SC-FDMA data symbol l takes rows 0..M_sc-1 of column l;
+ *          circular buffer (the DL-SCH chain of o_tx.c with N_L = 1), G = 12 M_sc Q_m - Q_CQI - Q_RI
+ *          (normal CP, no SRS);
+ *   UCI (5.2.2.6): HARQ-ACK and RI blocks of Tables 5.2.2.6-1..-4 with placeholders, Q'_ACK / Q'_RI /
+ *          Q'_CQI from the beta_offsets of 36.213 Tables 8.6.3-1..-3; CQI O <= 11 bits by the (32, O)
+ *          block code of Table 5.2.2.6.4-1, O > 11 by CRC8 + the tail-biting convolutional code + 5.1.4.2;
+ *   multiplexing (5.2.2.7): g = CQI symbols then data symbols;
+ *   channel interleaver (5.2.2.8): a matrix of M_sc rows x 12 columns of Q_m-bit cells; RI cells first,
+ *          from the last row up in ColumnSet {1, 4, 7, 10} (j = 0, 3, 2, 1, ...), then g row by row over
+ *          the remaining cells, then HARQ-ACK overwriting from the last row up in {2, 3, 8, 9}; read
+ *          column by column -> SC-FDMA data symbol l takes the rows of column l;
  *   scrambling (36.211 5.3.1): c_init = n_RNTI 2^14 + sf 2^9 + N_ID; modulation as the DL (7.1);
  *   transform precoding (5.3.3): z = (1/sqrt M) DFT_M per data symbol;
  *   DMRS (5.5.2.1, M_sc >= 36 only -- the L_prb = 1, 2 base sequences are tables this restatement
@@ -44,10 +50,82 @@ uint32_t or_ack_qprime(const or_ul_cfg_t *c) {
   return (uint32_t)(q < 4 * M ? q : 4 * M);
 }
 
-/* 36.212 Tables 5.2.2.6-1 / -2 (placeholders: 2 = x, 3 = y) */
-uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk) {
-  const uint32_t Qm = c->Qm, o0 = c->ack & 1, o1 = (c->ack >> 1) & 1, o2 = o0 ^ o1;
-  if (c->ack_len == 1) {
+/* 36.213 Table 8.6.3-2 (RI, I 0..12) and Table 8.6.3-3 (CQI, I 2..15; 0, 1 reserved), x 8 */
+static const uint32_t BETA8_RI[13] = {10, 13, 16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160};
+static const uint32_t BETA8_CQI[16] = {0, 0, 9, 10, 11, 13, 14, 16, 18, 20, 23, 25, 28, 32, 40, 50};
+
+static uint64_t ul_sum_k(const or_ul_cfg_t *c) {
+  or_cbsegm_t sg;
+  if (or_cbsegm(c->tbs, &sg)) return 0;
+  return (uint64_t)sg.Cm * sg.Km + (uint64_t)(sg.C - sg.Cm) * sg.Kp;
+}
+
+uint32_t or_ri_qprime(const or_ul_cfg_t *c) {
+  if (!c->ri_len) return 0;
+  const uint64_t sk = ul_sum_k(c), M = 12 * c->L_prb;
+  if (!sk || c->ri_len > 2 || c->I_offset_ri > 12) return (uint32_t)-1;
+  const uint64_t q = ((uint64_t)c->ri_len * M * 12 * BETA8_RI[c->I_offset_ri] + 8 * sk - 1) / (8 * sk);
+  return (uint32_t)(q < 4 * M ? q : 4 * M);
+}
+
+uint32_t or_cqi_qprime(const or_ul_cfg_t *c) {
+  if (!c->cqi_len) return 0;
+  const uint64_t sk = ul_sum_k(c), M = 12 * c->L_prb, L = c->cqi_len > 11 ? 8 : 0;
+  const uint32_t qri = or_ri_qprime(c);
+  if (!sk || c->cqi_len > 64 || c->I_offset_cqi < 2 || c->I_offset_cqi > 15 || qri == (uint32_t)-1)
+    return (uint32_t)-1;
+  const uint64_t q = ((c->cqi_len + L) * M * 12 * BETA8_CQI[c->I_offset_cqi] + 8 * sk - 1) / (8 * sk);
+  const uint64_t cap = 12 * M - qri;
+  return (uint32_t)(q < cap ? q : cap);
+}
+
+/* 36.212 Table 5.2.2.6.4-1: basis sequences M_{i,n} of the (32, O) code, row i, column n = 0..10 */
+static const uint8_t RM32[32][11] = {
+  {1,1,0,0,0,0,0,0,0,0,1}, {1,1,1,0,0,0,0,0,0,1,1}, {1,0,0,1,0,0,1,0,1,1,1}, {1,0,1,1,0,0,0,0,1,0,1},
+  {1,1,1,1,0,0,0,1,0,0,1}, {1,1,0,0,1,0,1,1,1,0,1}, {1,0,1,0,1,0,1,0,1,1,1}, {1,0,0,1,1,0,0,1,1,0,1},
+  {1,1,0,1,1,0,0,1,0,1,1}, {1,0,1,1,1,0,1,0,0,1,1}, {1,0,1,0,0,1,1,1,0,1,1}, {1,1,1,0,0,1,1,0,1,0,1},
+  {1,0,0,1,0,1,0,1,1,1,1}, {1,1,0,1,0,1,0,1,0,1,1}, {1,0,0,0,1,1,0,1,0,0,1}, {1,1,0,0,1,1,1,1,0,1,1},
+  {1,1,1,0,1,1,1,0,0,1,0}, {1,0,0,1,1,1,0,0,1,0,0}, {1,1,0,1,1,1,1,1,0,0,0}, {1,0,0,0,0,1,1,0,0,0,0},
+  {1,0,1,0,0,0,1,0,0,0,1}, {1,1,0,1,0,0,0,0,0,1,1}, {1,0,0,0,1,0,0,1,1,0,1}, {1,1,1,0,1,0,0,0,1,1,1},
+  {1,1,1,1,1,0,1,1,1,1,0}, {1,1,0,0,0,1,1,1,0,0,1}, {1,0,1,1,0,1,0,0,1,1,0}, {1,1,1,1,0,1,0,1,1,1,0},
+  {1,0,1,0,1,1,1,0,1,0,0}, {1,0,1,1,1,1,1,1,1,0,0}, {1,1,1,1,1,1,1,1,1,1,1}, {1,0,0,0,0,0,0,0,0,0,0}};
+
+uint32_t or_cqi_rm32(const uint8_t *o, uint32_t O) {
+  uint32_t w = 0;
+  for (uint32_t i = 0; i < 32; i++) {
+    uint32_t b = 0;
+    for (uint32_t n = 0; n < O && n < 11; n++) b ^= (uint32_t)(o[n] & RM32[i][n]);
+    w = (w << 1) | b;
+  }
+  return w;
+}
+
+int or_cqi_encode(const or_ul_cfg_t *c, uint8_t *q) {
+  const uint32_t qp = or_cqi_qprime(c);
+  if (qp == (uint32_t)-1) return -1;
+  const uint32_t Q = qp * c->Qm, O = c->cqi_len;
+  if (!Q) return 0;
+  if (O <= 11) {   /* q_i = b_(i mod 32) */
+    const uint32_t w = or_cqi_rm32(c->cqi, O);
+    for (uint32_t i = 0; i < Q; i++) q[i] = (uint8_t)((w >> (31 - i % 32)) & 1u);
+    return (int)Q;
+  }
+  /* 36.212 5.2.2.6.4 O > 11: CRC8 (g_CRC8 = D^8 + D^7 + D^4 + D^3 + D + 1), tail-biting convolutional
+     code (5.1.3.1), rate matching to Q bits (5.1.4.2) */
+  const uint32_t D = O + 8;
+  uint8_t a[72], d[3 * 72];
+  memcpy(a, c->cqi, O);
+  const uint32_t crc = or_crc(c->cqi, O, 0x9Bu, 8);
+  for (uint32_t i = 0; i < 8; i++) a[O + i] = (uint8_t)((crc >> (7 - i)) & 1u);
+  or_conv_encode_tb(a, D, d);
+  or_conv_rm_tx(d, D, Q, q);
+  return (int)Q;
+}
+
+/* Tables 5.2.2.6-1..-4: the HARQ-ACK / RI block of `len` bits `v` (placeholders: 2 = x, 3 = y) */
+static uint32_t uci_block(uint32_t len, uint32_t v, uint32_t Qm, uint8_t *blk) {
+  const uint32_t o0 = v & 1, o1 = (v >> 1) & 1, o2 = o0 ^ o1;
+  if (len == 1) {
     blk[0] = (uint8_t)o0;
     blk[1] = 3;
     for (uint32_t b = 2; b < Qm; b++) blk[b] = 2;
@@ -62,9 +140,16 @@ uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk) {
   return 3 * Qm;
 }
 
-int or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *f) {
-  const uint32_t A = c->tbs, G = or_pusch_G(c);
+uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk) { return uci_block(c->ack_len, c->ack, c->Qm, blk); }
+uint32_t or_ri_block(const or_ul_cfg_t *c, uint8_t *blk) { return uci_block(c->ri_len, c->ri, c->Qm, blk); }
+
+int or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *g) {
+  const uint32_t A = c->tbs, qri = or_ri_qprime(c), qcqi = or_cqi_qprime(c);
   if (A == 0 || (c->Qm != 2 && c->Qm != 4 && c->Qm != 6)) return -1;
+  if (qri == (uint32_t)-1 || qcqi == (uint32_t)-1) return -1;
+  const uint32_t Qcqi = qcqi * c->Qm, G = or_pusch_G(c) - Qcqi - qri * c->Qm;
+  if (or_cqi_encode(c, g) != (int)Qcqi) return -1;
+  uint8_t *f = g + Qcqi;
   uint8_t *b = (uint8_t *)malloc(A + 24);
   for (uint32_t i = 0; i < A; i++) b[i] = (tb[i / 8] >> (7 - i % 8)) & 1;
   const uint32_t crc = or_crc24a(b, A);
@@ -86,33 +171,52 @@ int or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *f) {
     pos_f += E;
   }
   free(b); free(cb); free(d);
-  return (int)G;
+  return (int)(Qcqi + G);
 }
 
-int or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *f, float *x) {
-  const uint32_t M = 12 * c->L_prb, Qm = c->Qm, G = or_pusch_G(c);
+int or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *g, float *x) {
+  const uint32_t M = 12 * c->L_prb, Qm = c->Qm, G = or_pusch_G(c), R = M, NC = 12;
+  const uint32_t qri = or_ri_qprime(c), qack = or_ack_qprime(c);
+  if (qri == (uint32_t)-1 || qri > 4 * M) return -1;
+  /* the interleaver matrix: R rows x 12 columns of Qm-bit cells (codes 0/1, 2 = x, 3 = y); ri[] marks RI */
+  uint8_t *y = (uint8_t *)malloc((size_t)R * NC * Qm), *ri = (uint8_t *)calloc((size_t)R * NC, 1);
   uint8_t *cs = (uint8_t *)malloc(G), *h = (uint8_t *)malloc(G);
-  for (uint32_t l = 0; l < 12; l++)          /* interleaver: output symbol l M + m <- input m 12 + l */
-    for (uint32_t m = 0; m < M; m++)
-      memcpy(h + (size_t)(l * M + m) * Qm, f + (size_t)(m * 12 + l) * Qm, Qm);
-  /* HARQ-ACK symbols overwrite the matrix from the last row up, columns ColumnSet(j), j = 0, 3, 2, 1, ... */
-  static const uint32_t COLSET[4] = {2, 3, 8, 9};
+  static const uint32_t RI_COLS[4] = {1, 4, 7, 10}, ACK_COLS[4] = {2, 3, 8, 9};
   uint8_t blk[18];
-  const uint32_t nq = or_ack_qprime(c), nb = c->ack_len ? or_ack_block(c, blk) : Qm;
-  for (uint32_t i = 0, j = 0; i < nq; i++, j = (j + 3) % 4) {
-    const uint32_t r = M - 1 - i / 4, col = COLSET[j];
-    for (uint32_t b = 0; b < Qm; b++) h[(size_t)(col * M + r) * Qm + b] = blk[(i * Qm + b) % nb];
+  /* 1. RI from the last row up */
+  uint32_t nb = c->ri_len ? or_ri_block(c, blk) : Qm;
+  for (uint32_t i = 0, j = 0; i < qri; i++, j = (j + 3) % 4) {
+    const uint32_t r = R - 1 - i / 4, col = RI_COLS[j];
+    ri[r * NC + col] = 1;
+    for (uint32_t b = 0; b < Qm; b++) y[(size_t)(r * NC + col) * Qm + b] = blk[(i * Qm + b) % nb];
   }
+  /* 2. g (CQI then data) row by row over the cells RI left free */
+  uint32_t k = 0;
+  for (uint32_t r = 0; r < R; r++)
+    for (uint32_t col = 0; col < NC; col++) {
+      if (ri[r * NC + col]) continue;
+      memcpy(y + (size_t)(r * NC + col) * Qm, g + (size_t)k * Qm, Qm);
+      k++;
+    }
+  /* 3. HARQ-ACK overwrites from the last row up */
+  nb = c->ack_len ? or_ack_block(c, blk) : Qm;
+  for (uint32_t i = 0, j = 0; i < qack; i++, j = (j + 3) % 4) {
+    const uint32_t r = R - 1 - i / 4, col = ACK_COLS[j];
+    for (uint32_t b = 0; b < Qm; b++) y[(size_t)(r * NC + col) * Qm + b] = blk[(i * Qm + b) % nb];
+  }
+  /* 4. read column by column: SC-FDMA data symbol l = column l */
+  for (uint32_t col = 0; col < NC; col++)
+    for (uint32_t r = 0; r < R; r++) memcpy(h + (size_t)(col * R + r) * Qm, y + (size_t)(r * NC + col) * Qm, Qm);
   or_gold((c->rnti << 14) | (c->sf_idx << 9) | c->cell_id, cs, G);
   for (uint32_t i = 0; i < G; i++)            /* 36.211 5.3.1 with the UCI placeholders */
     h[i] = h[i] == 2 ? 1 : h[i] == 3 ? h[i - 1] : (uint8_t)(h[i] ^ cs[i]);
   for (uint32_t s = 0; s < 12 * M; s++) {
     uint8_t bi[3], bq[3];
-    for (uint32_t j = 0; j < Qm / 2; j++) { bi[j] = h[s * Qm + 2 * j]; bq[j] = h[s * Qm + 2 * j + 1]; }
+    for (uint32_t jj = 0; jj < Qm / 2; jj++) { bi[jj] = h[s * Qm + 2 * jj]; bq[jj] = h[s * Qm + 2 * jj + 1]; }
     x[2 * s] = (float)or_pam_level(bi, Qm);
     x[2 * s + 1] = (float)or_pam_level(bq, Qm);
   }
-  free(cs); free(h);
+  free(y); free(ri); free(cs); free(h);
   return 0;
 }
 
@@ -180,8 +284,7 @@ int or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid) {
   if (c->hop && c->n_prb1 + c->L_prb > c->nof_prb) return -1;
   uint8_t *f = (uint8_t *)malloc(G);
   float *x = (float *)malloc(sizeof(float) * 2 * 12 * M), *z = (float *)malloc(sizeof(float) * 2 * M);
-  if (or_ulsch_encode(c, tb, f) < 0) { free(f); free(x); free(z); return -1; }
-  or_pusch_mod(c, f, x);
+  if (or_ulsch_encode(c, tb, f) < 0 || or_pusch_mod(c, f, x)) { free(f); free(x); free(z); return -1; }
   memset(grid, 0, sizeof(float) * 2 * OR_NSYMB * W);
   uint32_t ds = 0;
   for (uint32_t l = 0; l < OR_NSYMB; l++) {

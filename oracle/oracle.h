@@ -250,11 +250,17 @@ typedef struct {
   uint32_t cyclic_shift, n_dmrs2;                      /* RRC cyclicShift, DCI 0 cyclic-shift field (0..7) */
   uint32_t ack_len, ack, I_offset_ack;                 /* HARQ-ACK on PUSCH: 0..2 bits (bit 0 = o0), beta index */
   uint32_t hop, n_prb1;                                /* hop = 1: slot 1 starts at PRB n_prb1 (36.213 8.4) */
+  uint32_t cqi_len, I_offset_cqi;                      /* CQI on PUSCH (36.212 5.2.2.6.4): 0..64 bits, beta index */
+  uint8_t  cqi[64];                                    /* o_0 .. o_{O-1}, one bit per byte */
+  uint32_t ri_len, ri, I_offset_ri;                    /* RI on PUSCH (5.2.2.6): 0..2 bits (bit 0 = o0), beta index */
 } or_ul_cfg_t;
 double   or_pam_level(const uint8_t *b, uint32_t Qm);
-uint32_t or_pusch_G(const or_ul_cfg_t *c);
-int      or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *f);
-int      or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *f, float *x /* 12 M complex, symbol-major */);
+uint32_t or_pusch_G(const or_ul_cfg_t *c);                /* all coded bits: 12 M Qm (normal CP, no SRS) */
+/* UL-SCH data + CQI: the multiplexed sequence g (36.212 5.2.2.7) = Q_CQI CQI bits then the G data bits
+ * (G = 12 M Qm - Q_CQI - Q_RI); returns its length H = Q_CQI + G, -1 on error */
+int      or_ulsch_encode(const or_ul_cfg_t *c, const uint8_t *tb, uint8_t *g);
+/* channel interleaver (5.2.2.8) with RI / HARQ-ACK insertion, scrambling, modulation: g -> 12 M symbols */
+int      or_pusch_mod(const or_ul_cfg_t *c, const uint8_t *g, float *x /* 12 M complex, symbol-major */);
 void     or_dft_m(const float *in, uint32_t M, float *out, int inverse);
 int      or_dmrs_params(const or_ul_cfg_t *c, uint32_t ns, uint32_t *u, uint32_t *v, uint32_t *ncs);
 int      or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r);
@@ -265,6 +271,15 @@ int      or_pusch_encode(const or_ul_cfg_t *c, const uint8_t *tb, float *iq);
  * block (codes 0 / 1 = bit, 2 = placeholder x, 3 = placeholder y), returns its length in bits */
 uint32_t or_ack_qprime(const or_ul_cfg_t *c);
 uint32_t or_ack_block(const or_ul_cfg_t *c, uint8_t *blk /* <= 18 */);
+/* RI / CQI on PUSCH (36.212 5.2.2.6, beta_offset 36.213 Tables 8.6.3-2 / -3): Q'_RI, Q'_CQI (symbols; 0 if
+ * absent, (uint32_t)-1 for an invalid configuration), the RI block (as or_ack_block) and the Q_CQI CQI coded
+ * bits (O <= 11: the (32, O) block code of Table 5.2.2.6.4-1 repeated; O > 11: CRC8, tail-biting
+ * convolutional code, rate matching 5.1.4.2) */
+uint32_t or_ri_qprime(const or_ul_cfg_t *c);
+uint32_t or_cqi_qprime(const or_ul_cfg_t *c);
+uint32_t or_ri_block(const or_ul_cfg_t *c, uint8_t *blk /* <= 18 */);
+int      or_cqi_encode(const or_ul_cfg_t *c, uint8_t *q);
+uint32_t or_cqi_rm32(const uint8_t *o, uint32_t O);    /* the 32 RM code bits b_0..b_31, b_0 = MSB of the result */
 
 #ifdef __cplusplus
 }

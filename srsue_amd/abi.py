@@ -561,15 +561,22 @@ UL_STAGES = ("crc", "encode", "mod")
 class UlCfg(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("cell_id", "nof_prb", "sf_idx", "rnti", "n_prb", "L_prb", "tbs", "Qm", "rv",
                                           "group_hopping", "sequence_hopping", "delta_ss", "cyclic_shift", "n_dmrs2",
-                                          "ack_len", "ack", "I_offset_ack", "hop", "n_prb1")]
+                                          "ack_len", "ack", "I_offset_ack", "hop", "n_prb1", "cqi_len",
+                                          "I_offset_cqi")] + [("cqi", C.c_uint8 * 64)] + \
+        [(n, C.c_uint32) for n in ("ri_len", "ri", "I_offset_ri")]
 
 
 def ul_cfg(cell_id=1, nof_prb=100, sf_idx=1, rnti=0x46, n_prb=0, L_prb=100, tbs=0, Qm=4, rv=0, gh=0, sh=0, dss=0,
-           cs=0, n2=0, ack_len=0, ack=0, ioff=0, n_prb1=None):
-    """n_prb1: start PRB of slot 1 (frequency hopping), None = no hopping"""
+           cs=0, n2=0, ack_len=0, ack=0, ioff=0, n_prb1=None, cqi=(), cqi_ioff=2, ri_len=0, ri=0, ri_ioff=0):
+    """n_prb1: start PRB of slot 1 (frequency hopping), None = no hopping; cqi: CQI bits o_0.. (36.212
+    5.2.2.6.4) with beta_offset index cqi_ioff; ri_len / ri / ri_ioff: RI on PUSCH"""
     hop, n1 = (0, 0) if n_prb1 is None else (1, n_prb1)
-    return UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2, ack_len, ack, ioff,
-                 hop, n1)
+    c = UlCfg(cell_id, nof_prb, sf_idx, rnti, n_prb, L_prb, tbs, Qm, rv, gh, sh, dss, cs, n2, ack_len, ack, ioff,
+              hop, n1, len(cqi), cqi_ioff)
+    for i, b in enumerate(cqi):
+        c.cqi[i] = b
+    c.ri_len, c.ri, c.I_offset_ri = ri_len, ri, ri_ioff
+    return c
 
 
 class UlBatch:

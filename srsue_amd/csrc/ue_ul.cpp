@@ -186,14 +186,21 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
                                               srslte_softbuffer_tx_t* sb, uint16_t rnti, cf_t* output_signal) {
   if (!q || !q->ctx || !output_signal) return SRSLTE_ERROR_INVALID_INPUTS;
   mi_ue_ul_ctx* c = q->ctx;
-  if (uci.uci_cqi_len || uci.uci_ri_len || uci.uci_ack_len > 2) {
-    mi::set_error("CQI / RI on PUSCH are not supported");
+  if (uci.uci_cqi_len > SRSLTE_CQI_MAX_BITS || uci.uci_ri_len > 2 || uci.uci_ack_len > 2) {
+    mi::set_error("UCI on PUSCH: up to 64 CQI bits, 2 RI bits, 2 HARQ-ACK bits");
     return SRSLTE_ERROR;
   }
   c->cfg.rnti = rnti;
   c->cfg.ack_len = uci.uci_ack_len;   // HARQ-ACK on PUSCH (srsUE: 1 bit, phch_worker.cc:486-487)
   c->cfg.ack = uci.uci_ack & 3u;
   c->cfg.I_offset_ack = q->uci_cfg.I_offset_ack;
+  // periodic CQI (srsUE packs it at phch_worker.cc:507-523 before this call, :555) and RI, 36.212 5.2.2.6
+  c->cfg.cqi_len = uci.uci_cqi_len;
+  memcpy(c->cfg.cqi, uci.uci_cqi, uci.uci_cqi_len);
+  c->cfg.I_offset_cqi = q->uci_cfg.I_offset_cqi;
+  c->cfg.ri_len = uci.uci_ri_len;
+  c->cfg.ri = uci.uci_ri & 3u;
+  c->cfg.I_offset_ri = q->uci_cfg.I_offset_ri;
   const uint32_t nbytes = c->cfg.tbs / 8;
   if (nbytes > TX_MAX_BYTES) return SRSLTE_ERROR;
   // the TB: new data from `data`; a retransmission without data re-encodes the softbuffer's copy

@@ -307,18 +307,22 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
     } else {
       const uint32_t ld = l - (l > 3 ? 1 : 0) - (l > 10 ? 1 : 0);   // data symbol 0..11
       for (uint32_t m = t; m < M; m += UL_THREADS) {
-        // channel interleaver: data symbol ld, subcarrier m takes coded symbol m * 12 + ld, unless a HARQ-ACK
-        // symbol overwrote that matrix entry: ACK symbol i sits in row M - 1 - i / 4 of column
-        // {2, 9, 8, 3}[i % 4] (36.212 5.2.2.8, ColumnSet {2, 3, 8, 9} walked with j = (j + 3) mod 4)
+        // channel interleaver (36.212 5.2.2.8): matrix row m, column ld.  RI symbol i sits in row M - 1 - i / 4
+        // of column {1, 10, 7, 4}[i % 4], HARQ-ACK symbol i in row M - 1 - i / 4 of column {2, 9, 8, 3}[i % 4]
+        // (ColumnSets {1, 4, 7, 10} / {2, 3, 8, 9} walked with j = (j + 3) mod 4); the multiplexed sequence g
+        // (CQI then data) fills the other cells row by row, skipping the RI cells; HARQ-ACK overwrites g.
         const uint32_t i0 = (ld * M + m) * Qm;
-        int ta = -1;
-        if (x.q_ack) ta = ld == 2 ? 0 : ld == 9 ? 1 : ld == 8 ? 2 : ld == 3 ? 3 : -1;
-        const uint32_t ia = 4 * (M - 1 - m) + (uint32_t)ta;
+        const int ta = x.q_ack ? (ld == 2 ? 0 : ld == 9 ? 1 : ld == 8 ? 2 : ld == 3 ? 3 : -1) : -1;
+        const int tr = x.q_ri ? (ld == 1 ? 0 : ld == 10 ? 1 : ld == 7 ? 2 : ld == 4 ? 3 : -1) : -1;
+        const uint32_t ia = 4 * (M - 1 - m) + (uint32_t)ta, ir = 4 * (M - 1 - m) + (uint32_t)tr;
+        const bool is_ack = ta >= 0 && ia < x.q_ack, is_ri = tr >= 0 && ir < x.q_ri;
         uint32_t bits = 0;
-        if (ta >= 0 && ia < x.q_ack) {
+        if (is_ack || is_ri) {
           // 36.211 5.3.1 placeholders: x -> 1, y -> the previous scrambled bit
-          const uint32_t ks = x.ack_nblk == 1 ? 0u : ia % 3;   // selects, no dynamic index into x
-          const uint32_t cw = ks == 0 ? x.ack_sym[0] : ks == 1 ? x.ack_sym[1] : x.ack_sym[2];
+          const uint32_t nb = is_ack ? x.ack_nblk : x.ri_nblk, ks = nb == 1 ? 0u : (is_ack ? ia : ir) % 3;
+          const uint32_t w0 = is_ack ? x.ack_sym[0] : x.ri_sym[0], w1 = is_ack ? x.ack_sym[1] : x.ri_sym[1];
+          const uint32_t w2 = is_ack ? x.ack_sym[2] : x.ri_sym[2];
+          const uint32_t cw = ks == 0 ? w0 : ks == 1 ? w1 : w2;   // selects, no dynamic index into x
           uint32_t prev = 0;
           for (uint32_t b = 0; b < Qm; b++) {
             const uint32_t i = i0 + b, code = (cw >> (2 * b)) & 3u;
@@ -327,7 +331,15 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
             prev = bit;
           }
         } else {
-          const uint32_t v = syms[x.sym_off + m * 12 + ld];
+          // g index of cell (m, ld): cells of the rows above less their RI cells, plus the free cells left of
+          // ld in row m (RI cells of rows >= r: min(Q'_RI, 4 (M - r)); row m's fill {1, 10, 7, 4} in order)
+          uint32_t k = 12 * m + ld;
+          if (x.q_ri) {
+            const uint32_t below = min(x.q_ri, 4 * (M - 1 - m)), from = min(x.q_ri, 4 * (M - m)), nrow = from - below;
+            const uint32_t left = (nrow > 0 && ld > 1) + (nrow > 3 && ld > 4) + (nrow > 2 && ld > 7) + (nrow > 1 && ld > 10);
+            k -= (x.q_ri - from) + left;
+          }
+          const uint32_t v = syms[x.sym_off + k];
           for (uint32_t b = 0; b < Qm; b++) {
             const uint32_t i = i0 + b;
             bits = (bits << 1) | (((v >> (Qm - 1 - b)) ^ (scr[x.scr_off + (i >> 5)] >> (i & 31))) & 1u);

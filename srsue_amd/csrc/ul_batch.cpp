@@ -41,7 +41,9 @@ int mi_ul_batch_symbols(mi_ul_batch_t* b, uint32_t i, uint8_t* host) {
   if (i >= b->eng.plan.txs.size()) { mi::set_error("transmission index"); return -1; }
   const MiUlTx& t = b->eng.plan.txs[i];
   if (!mi::hip_ok(hipDeviceSynchronize(), "sync")) return -1;
-  return mi::hip_ok(hipMemcpy(host, b->eng.d_syms.as<uint8_t>() + t.sym_off, 12 * (size_t)t.M, hipMemcpyDeviceToHost),
+  const size_t h = 12 * (size_t)t.M - t.q_ri;   // the multiplexed sequence g; the RI cells follow as zeros
+  memset(host + h, 0, t.q_ri);
+  return mi::hip_ok(hipMemcpy(host, b->eng.d_syms.as<uint8_t>() + t.sym_off, h, hipMemcpyDeviceToHost),
                     "symbols D2H") ? 0 : -1;
 }
 int mi_ul_batch_stage_ms(mi_ul_batch_t* b, float* ms, uint32_t* nruns) { return b->eng.stage_ms(ms, nruns); }

@@ -26,6 +26,10 @@ struct MiUlTx {
   uint32_t q_ack;        // HARQ-ACK coded symbols Q'_ACK (0 = none)
   uint32_t ack_nblk;     // symbols in the encoded ACK block (1 or 3), repeated over the Q'_ACK symbols
   uint32_t ack_sym[3];   // the block's symbols: 2 bits per coded bit, bit b at bits 2b (0/1, 2 = x, 3 = y)
+  uint32_t q_ri;         // RI coded symbols Q'_RI (0 = none), placed like HARQ-ACK in columns {1, 4, 7, 10}
+  uint32_t ri_nblk;      // symbols in the encoded RI block (1 or 3)
+  uint32_t ri_sym[3];    // as ack_sym
+  uint32_t q_cqi;        // CQI coded symbols Q'_CQI at the head of the multiplexed sequence (uploaded with the plan)
 };
 
 // one UL-SCH code block

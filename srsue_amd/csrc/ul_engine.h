@@ -36,6 +36,11 @@ struct UlEngine {
     const UlPlan& P = plan;
     bool ok = up(d_txs, P.txs, st) && up(d_cbs, P.cbs, st) && up(d_scr, P.scr, st) &&
               d_tbcrc.ensure(P.txs.size() * 4) && d_syms.ensure(P.sym_bytes);
+    // CQI symbols head each transmission's multiplexed sequence (the encoder writes the data after them)
+    for (size_t i = 0; ok && i < P.txs.size(); i++)
+      if (P.txs[i].q_cqi)
+        ok = hip_ok(hipMemcpyAsync(d_syms.as<uint8_t>() + P.txs[i].sym_off, P.cqi_syms.data() + P.cqi_off[i],
+                                   P.txs[i].q_cqi, hipMemcpyHostToDevice, st), "cqi upload");
     if (ok && P.kdata != up_kdata) {
       ok = up(d_kdata, P.kdata, st);
       up_kdata = P.kdata;

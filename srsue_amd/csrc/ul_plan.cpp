@@ -59,8 +59,67 @@ uint32_t ul_radix_plan(uint32_t n) {
   return n == 1 ? plan : 0;
 }
 
+// 36.212 Table 5.2.2.6.4-1 by columns: bit 31 - i of RM32_COL[n] = M_{i,n}
+static const uint32_t RM32_COL[11] = {0xFFFFFFFFu, 0xCC95A5D2u, 0x5A7089BEu, 0x39CC64B6u, 0x07C3E38Eu, 0x003FF07Eu,
+                                      0x2671B8CEu, 0x0DAF22D6u, 0x371843BEu, 0x62ED85B2u, 0xFFFF0F42u};
+// 36.213 Table 8.6.3-2 (RI, I 0..12) and Table 8.6.3-3 (CQI, I 2..15), x 8
+static const uint32_t BETA8_RI[13] = {10, 13, 16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160};
+static const uint32_t BETA8_CQI[16] = {0, 0, 9, 10, 11, 13, 14, 16, 18, 20, 23, 25, 28, 32, 40, 50};
+
+void ul_cqi_code(const uint8_t* o, uint32_t O, uint32_t Q, std::vector<uint8_t>& q) {
+  q.assign(Q, 0);
+  if (O <= 11) {   // b = sum_n o_n M_{., n}, q_i = b_(i mod 32)
+    uint32_t w = 0;
+    for (uint32_t n = 0; n < O; n++)
+      if (o[n] & 1u) w ^= RM32_COL[n];
+    for (uint32_t i = 0; i < Q; i++) q[i] = (uint8_t)((w >> (31 - (i & 31))) & 1u);
+    return;
+  }
+  // CRC8 g = D^8 + D^7 + D^4 + D^3 + D + 1, then the rate-1/3 tail-biting code (5.1.3.1: generators 133,
+  // 171, 165 octal, register preloaded with the last six bits) and its rate matching (5.1.4.2)
+  const uint32_t D = O + 8;
+  std::vector<uint8_t> c(o, o + O);
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < O; i++) {
+    const uint32_t fb = ((r >> 7) ^ o[i]) & 1u;
+    r = ((r << 1) & 0xFFu) ^ (fb ? 0x9Bu : 0u);
+  }
+  for (int i = 7; i >= 0; i--) c.push_back((uint8_t)((r >> i) & 1u));
+  static const uint32_t G[3] = {0133, 0171, 0165};
+  std::vector<uint8_t> d(3 * D);
+  uint32_t win = 0;   // bit 6 - j = c_{k-j} (the generators' MSB taps the current bit); preload c_{D-1} .. c_{D-6}
+  for (uint32_t j = 1; j <= 6; j++) win |= (uint32_t)c[D - j] << (7 - j);
+  for (uint32_t k = 0; k < D; k++) {
+    win = (win >> 1) | ((uint32_t)c[k] << 6);
+    for (int i = 0; i < 3; i++) d[i * D + k] = (uint8_t)(__builtin_popcount(win & G[i]) & 1);
+  }
+  std::vector<uint32_t> rank, inv(3 * D);
+  conv_rank_table(D, rank);   // rank of each coded bit in the circular buffer
+  for (uint32_t p = 0; p < 3 * D; p++) inv[rank[p]] = p;
+  for (uint32_t k = 0; k < Q; k++) q[k] = d[inv[k % (3 * D)]];
+}
+
+// HARQ-ACK / RI block of Tables 5.2.2.6-1..-4 as modulation symbols (2 bits per coded bit: 0/1, 2 = x, 3 = y):
+// 1 bit [o0 y x ..], 2 bits [o0 o1 x ..][o2 o0 x ..][o1 o2 x ..]; returns the symbol count
+static uint32_t uci_block(uint32_t len, uint32_t v, uint32_t Qm, uint32_t* out) {
+  const uint32_t o0 = v & 1u, o1 = (v >> 1) & 1u, o2 = o0 ^ o1, X = 2, Y = 3;
+  auto sym = [&](uint32_t a, uint32_t b) {   // [a b x x ...]
+    uint32_t w = a | (b << 2);
+    for (uint32_t k = 2; k < Qm; k++) w |= X << (2 * k);
+    return w;
+  };
+  if (len == 1) {
+    out[0] = sym(o0, Y);
+    return 1;
+  }
+  out[0] = sym(o0, o1);
+  out[1] = sym(o2, o0);
+  out[2] = sym(o1, o2);
+  return 3;
+}
+
 int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
-  txs.clear(); cbs.clear(); kdata.clear(); scr.clear(); tw.clear(); tb_cb0.clear();
+  txs.clear(); cbs.clear(); kdata.clear(); scr.clear(); tw.clear(); tb_cb0.clear(); cqi_syms.clear(); cqi_off.clear();
   pi_off.clear(); tw_off.clear(); sel_off.clear();
   payload_bytes = sym_bytes = iq_samples = 0;
   algo_bytes = 0;
@@ -105,7 +164,38 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
       }
     t.twm_off = twiddles(t.M);
     t.twn_off = twiddles(t.N);
-    const uint32_t G = 12 * t.M * c.Qm;   // normal CP, no SRS, no UCI: 12 data symbols
+    CbSegm sg;
+    if (cbsegm(c.tbs, &sg)) {
+      set_error("segmentation");
+      return -1;
+    }
+    uint64_t sumK = 0;
+    for (uint32_t r = 0; r < sg.C; r++) sumK += r < sg.Cm ? sg.Km : sg.Kp;
+    // RI and CQI on PUSCH (36.212 5.2.2.6): Q'_RI = min(ceil(O M 12 beta / sum K_r), 4 M); Q'_CQI =
+    // min(ceil((O + L) M 12 beta / sum K_r), 12 M - Q'_RI), L = 8 (CRC) for O > 11
+    if (c.ri_len > 2 || (c.ri_len && c.I_offset_ri > 12) || c.cqi_len > 64 ||
+        (c.cqi_len && (c.I_offset_cqi < 2 || c.I_offset_cqi > 15))) {
+      set_error("UCI on PUSCH: RI 0..2 bits (beta index 0..12), CQI 0..64 bits (beta index 2..15)");
+      return -1;
+    }
+    auto qprime = [&](uint64_t bits, uint32_t beta8, uint64_t cap) {
+      const uint64_t q = (bits * t.M * 12 * beta8 + 8 * sumK - 1) / (8 * sumK);
+      return (uint32_t)(q < cap ? q : cap);
+    };
+    t.q_ri = c.ri_len ? qprime(c.ri_len, BETA8_RI[c.I_offset_ri], 4ull * t.M) : 0;
+    t.q_cqi = c.cqi_len ? qprime(c.cqi_len + (c.cqi_len > 11 ? 8 : 0), BETA8_CQI[c.I_offset_cqi], 12ull * t.M - t.q_ri) : 0;
+    cqi_off.push_back((uint32_t)cqi_syms.size());
+    if (t.q_cqi) {
+      std::vector<uint8_t> qb;
+      ul_cqi_code(c.cqi, c.cqi_len, t.q_cqi * c.Qm, qb);
+      for (uint32_t k = 0; k < t.q_cqi; k++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < c.Qm; b++) v = (v << 1) | qb[k * c.Qm + b];
+        cqi_syms.push_back((uint8_t)v);
+      }
+    }
+    // UL-SCH data bits: the 12 data symbols' cells less the CQI and RI ones (normal CP, no SRS)
+    const uint32_t G = (12 * t.M - t.q_cqi - t.q_ri) * c.Qm;
     t.iq_off = iq_samples;
     iq_samples += 15 * (size_t)N;
     t.pay_off = (uint32_t)payload_bytes;
@@ -116,14 +206,9 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     t.scr_off = (uint32_t)scr.size();
     scr.resize(scr.size() + (G + 31) / 32 + 1);
     gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, G, &scr[t.scr_off]);
-    // segmentation of (TB || CRC24A), 36.212 5.1.2
-    CbSegm sg;
-    if (cbsegm(c.tbs, &sg)) {
-      set_error("segmentation");
-      return -1;
-    }
+    // segmentation of (TB || CRC24A), 36.212 5.1.2 (sg above); the data follow the CQI symbols in g (5.2.2.7)
     tb_cb0.push_back((uint32_t)cbs.size());
-    uint32_t byte0 = 0, sym = 0;
+    uint32_t byte0 = 0, sym = t.q_cqi;
     for (uint32_t r = 0; r < sg.C; r++) {
       MiUlCb b{};
       b.tx = i;
@@ -178,28 +263,13 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
         set_error("HARQ-ACK on PUSCH: 1 or 2 bits");
         return -1;
       }
-      uint64_t sumK = 0;
-      for (uint32_t r = 0; r < sg.C; r++) sumK += r < sg.Cm ? sg.Km : sg.Kp;
       const uint64_t num = (uint64_t)c.ack_len * t.M * 12 * BETA8_ACK[c.I_offset_ack > 14 ? 14 : c.I_offset_ack];
       const uint64_t qp = (num + 8 * sumK - 1) / (8 * sumK);
       t.q_ack = (uint32_t)(qp < 4ull * t.M ? qp : 4ull * t.M);
-      const uint32_t o0 = c.ack & 1u, o1 = (c.ack >> 1) & 1u, o2 = o0 ^ o1, X = 2, Y = 3;
-      auto sym = [&](uint32_t a, uint32_t b) {   // [a b x x ...]
-        uint32_t w = a | (b << 2);
-        for (uint32_t k = 2; k < c.Qm; k++) w |= X << (2 * k);
-        return w;
-      };
-      if (c.ack_len == 1) {
-        t.ack_nblk = 1;
-        t.ack_sym[0] = sym(o0, Y);
-      } else {
-        t.ack_nblk = 3;
-        t.ack_sym[0] = sym(o0, o1);
-        t.ack_sym[1] = sym(o2, o0);
-        t.ack_sym[2] = sym(o1, o2);
-      }
+      t.ack_nblk = uci_block(c.ack_len, c.ack, c.Qm, t.ack_sym);
     }
-    if (byte0 != c.tbs / 8 + 3 || sym != 12 * t.M) {
+    if (c.ri_len) t.ri_nblk = uci_block(c.ri_len, c.ri, c.Qm, t.ri_sym);   // Tables 5.2.2.6-3 / -4
+    if (byte0 != c.tbs / 8 + 3 || sym != 12 * t.M - t.q_ri) {
       set_error("UL planner: segmentation / rate-matching bookkeeping");
       return -1;
     }

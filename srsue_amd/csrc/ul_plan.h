@@ -16,6 +16,9 @@ namespace mi {
 int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc, uint32_t* ncs);
 // radix list (8, 4, 2, 3, 5; 4 bits per stage) of an n-point transform, 0 if n has another factor
 uint32_t ul_radix_plan(uint32_t n);
+// CQI channel coding on PUSCH (36.212 5.2.2.6.4): the Q coded bits of the O-bit report o (O <= 11: the
+// (32, O) block code repeated; O > 11: CRC8, tail-biting convolutional code, 5.1.4.2 rate matching)
+void ul_cqi_code(const uint8_t* o, uint32_t O, uint32_t Q, std::vector<uint8_t>& q);
 
 struct UlPlan {
   std::vector<MiUlTx> txs;
@@ -24,6 +27,8 @@ struct UlPlan {
   std::vector<uint32_t> scr;        // scrambling words
   std::vector<float> tw;            // float2 twiddle tables
   std::vector<uint32_t> tb_cb0;     // first code block of each transmission (n + 1 entries)
+  std::vector<uint8_t> cqi_syms;    // CQI coded symbols of every transmission (Qm bits per byte, MSB first)
+  std::vector<uint32_t> cqi_off;    // per transmission: offset of its Q'_CQI symbols in cqi_syms
   size_t payload_bytes = 0, sym_bytes = 0, iq_samples = 0;
   double algo_bytes = 0;
 

@@ -9,10 +9,13 @@
  *              srslte_ue_ul_pusch_encode_rnti_softbuffer(.., payload, uci_data, softbuffer, rnti, signal) (:555)
  * Input file : int32 hdr[8] = {cell_id, nof_prb, ntx, group_hopping, sequence_hopping, delta_ss, cyclic_shift,
  *              flags (1 = normalisation, 2 = CFO, bits 8-11 = I_offset_ack, bits 12-19 = pusch-HoppingOffset,
- *              bit 20 = intra-subframe hopping)} + float cfo; per transmission int32
+ *              bit 20 = intra-subframe hopping, bits 21-24 = I_offset_cqi, bits 25-28 = I_offset_ri)} + float cfo;
+ *              per transmission int32
  *              p[12] = {tti, rnti, rv | CURRENT_TX_NB << 8, use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len,
- *              ack} + int32 dci_nof_bits + 64 DCI bit bytes +
- *              tbs/8 payload bytes (pass_data = 0: the payload pointer is NULL -- a retransmission from the
+ *              ack} + int32 dci_nof_bits + 64 DCI bit bytes + int32 u[3] = {cqi, ri_len, ri} + 64 CQI bit bytes +
+ *              tbs/8 payload bytes.  cqi > 0: a wideband CQI report of value cqi - 1 packed with
+ *              srslte_cqi_value_pack as srsUE does (phch_worker.cc:517-521); cqi < 0: -cqi raw CQI bits from the
+ *              64 bytes; 0: no CQI.  Payload bytes (pass_data = 0: the payload pointer is NULL -- a retransmission from the
  *              softbuffer).
  * Output file: per transmission int32 r[7] = {ret, n_prb slot 0, L_prb, tbs, Qm, ncs_dmrs, n_prb slot 1} + SF_LEN
  *              cf32 samples (the slot PRBs as cfg_grant set them in ue_ul.pusch_cfg.grant).
@@ -52,6 +55,8 @@ int main(int argc, char **argv) {
   memset(&pucch_sched, 0, sizeof(pucch_sched)); memset(&uci_cfg, 0, sizeof(uci_cfg));
   memset(&power_ctrl, 0, sizeof(power_ctrl));
   uci_cfg.I_offset_ack = (uint32_t)(hdr[7] >> 8) & 15u;
+  uci_cfg.I_offset_cqi = (uint32_t)(hdr[7] >> 21) & 15u;
+  uci_cfg.I_offset_ri = (uint32_t)(hdr[7] >> 25) & 15u;
   dmrs_cfg.group_hopping_en = hdr[3] != 0;
   dmrs_cfg.sequence_hopping_en = hdr[4] != 0;
   dmrs_cfg.delta_ss = (uint32_t)hdr[5];
@@ -68,7 +73,10 @@ int main(int argc, char **argv) {
     int32_t p[12], nbits;
     srslte_dci_msg_t dci_msg;
     memset(&dci_msg, 0, sizeof(dci_msg));
+    int32_t u[3];
+    uint8_t cqi_bits[64];
     if (fread(p, 4, 12, fi) != 12 || fread(&nbits, 4, 1, fi) != 1 || fread(dci_msg.data, 1, 64, fi) != 64) return 4;
+    if (fread(u, 4, 3, fi) != 3 || fread(cqi_bits, 1, 64, fi) != 64) return 4;
     if (fread(payload, 1, (size_t)p[6] / 8, fi) != (size_t)p[6] / 8) return 4;
     dci_msg.nof_bits = (uint32_t)nbits;
     srslte_ue_ul_set_rnti(&ue_ul, (uint16_t)p[1]);
@@ -93,6 +101,18 @@ int main(int argc, char **argv) {
     memset(&uci_data, 0, sizeof(uci_data));
     uci_data.uci_ack_len = (uint32_t)p[10];   /* phch_worker.cc:486-487 */
     uci_data.uci_ack = (uint8_t)p[11];
+    if (u[0] > 0) {   /* periodic wideband CQI, phch_worker.cc:517-521 */
+      srslte_cqi_value_t cqi_report;
+      memset(&cqi_report, 0, sizeof(cqi_report));
+      cqi_report.type = SRSLTE_CQI_TYPE_WIDEBAND;
+      cqi_report.wideband.wideband_cqi = (uint8_t)(u[0] - 1);
+      uci_data.uci_cqi_len = (uint32_t)srslte_cqi_value_pack(&cqi_report, uci_data.uci_cqi);
+    } else if (u[0] < 0) {
+      uci_data.uci_cqi_len = (uint32_t)(-u[0]);
+      memcpy(uci_data.uci_cqi, cqi_bits, uci_data.uci_cqi_len);
+    }
+    uci_data.uci_ri_len = (uint32_t)u[1];
+    uci_data.uci_ri = (uint8_t)u[2];
     memset(signal, 0, sflen * sizeof(cf_t));
     if (!ret)
       ret = srslte_ue_ul_pusch_encode_rnti_softbuffer(&ue_ul, p[9] ? payload : NULL, uci_data, &softbuffer,

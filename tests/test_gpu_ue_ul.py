@@ -38,6 +38,10 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
                                     int(t.get("pass_data", True)), t.get("ack_len", 0), t.get("ack", 0)))
                 f.write(struct.pack("i", dci.nof_bits if dci else 0))
                 f.write(bytes(dci.data) if dci else bytes(64))
+                raw_cqi = list(t.get("cqi_bits", []))
+                f.write(struct.pack("3i", t["cqi_wb"] + 1 if "cqi_wb" in t else -len(raw_cqi), t.get("ri_len", 0),
+                                    t.get("ri", 0)))
+                f.write(bytes(raw_cqi + [0] * (64 - len(raw_cqi))))
                 f.write(np.ascontiguousarray(t["tb"], np.uint8).tobytes())
         subprocess.check_call([HARNESS, fin, fout], timeout=300)
         raw = open(fout, "rb").read()
@@ -51,11 +55,15 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
     return out
 
 
-def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None, ioff=0, n_prb1=None):
+def oracle_iq(cell_id, nof_prb, t, sf, dmrs=(0, 0, 0, 0), n_prb=None, L=None, Qm=None, ncs=None, ioff=0, n_prb1=None,
+              cqi_ioff=2, ri_ioff=0):
+    # srsUE's wideband CQI: 4 bits, MSB first (36.212 Table 5.2.2.6.2-1 wideband CQI field)
+    cqi = [(t["cqi_wb"] >> (3 - i)) & 1 for i in range(4)] if "cqi_wb" in t else list(t.get("cqi_bits", []))
     c = O.ul_cfg(n_prb1=n_prb1, cell_id=cell_id, nof_prb=nof_prb, sf_idx=sf, rnti=t["rnti"], n_prb=t.get("n_prb", 0) if n_prb is None else n_prb,
                  L_prb=t.get("L_prb") if L is None else L, tbs=t["tbs"], Qm=t.get("Qm") if Qm is None else Qm,
                  rv=t["rv"], gh=dmrs[0], sh=dmrs[1], dss=dmrs[2], cs=dmrs[3], n2=t.get("ncs", 0) if ncs is None else ncs,
-                 ack_len=t.get("ack_len", 0), ack=t.get("ack", 0), ioff=ioff)
+                 ack_len=t.get("ack_len", 0), ack=t.get("ack", 0), ioff=ioff, cqi=cqi, cqi_ioff=cqi_ioff,
+                 ri_len=t.get("ri_len", 0), ri=t.get("ri", 0), ri_ioff=ri_ioff)
     iq = np.zeros(2 * 15 * NFFT[nof_prb], np.float32)
     assert O.lib().or_pusch_encode(ctypes.byref(c), t["tb"], iq) == 0
     return iq
@@ -156,3 +164,23 @@ def test_type1_frequency_hopping_srsue_call_order(intra):
         ref = oracle_iq(3, 100, dict(t, tb=data), t["tti"] % 10, n_prb=s0, L=L, Qm=4, ncs=1,
                         n_prb1=s1 if s1 != s0 else None)
         assert rel_err(iq, ref) < TOL
+
+
+def test_periodic_cqi_and_ri_on_pusch_srsue_call_order():
+    """srsUE packs a periodic wideband CQI into uci_data (srslte_cqi_value_pack, phch_worker.cc:507-523) before
+    srslte_ue_ul_pusch_encode_rnti_softbuffer (:555): the PUSCH carries it (36.212 5.2.2.6.4 (32, O) code,
+    multiplexed ahead of the data), with and without the HARQ-ACK bit; RI (1 / 2 bits) and a long raw CQI
+    report (CRC8 + convolutional code) through the same call.  beta_offset indices from set_cfg's uci_cfg
+    (I_offset_cqi 9, I_offset_ri 6, I_offset_ack 6); every subframe matches the oracle within 1e-4."""
+    long_cqi = list(np.random.default_rng(5).integers(0, 2, 30).astype(int))
+    txs = [dict(tti=12, rnti=0x46, rv=0, n_prb=0, L_prb=25, tbs=5736, Qm=2, ncs=0, tb=tb(16, 5736), cqi_wb=11),
+           dict(tti=16, rnti=0x46, rv=0, n_prb=5, L_prb=40, tbs=12216, Qm=4, ncs=1, tb=tb(17, 12216), cqi_wb=7,
+                ack_len=1, ack=1),
+           dict(tti=23, rnti=0x46, rv=0, n_prb=0, L_prb=50, tbs=21384, Qm=6, ncs=2, tb=tb(18, 21384), ri_len=1, ri=1,
+                ack_len=1, ack=0),
+           dict(tti=27, rnti=0x46, rv=0, n_prb=10, L_prb=30, tbs=7992, Qm=4, ncs=3, tb=tb(19, 7992),
+                cqi_bits=long_cqi, ri_len=2, ri=2)]
+    res = run(9, 50, txs, flags=(6 << 8) | (9 << 21) | (6 << 25))
+    for t, (r, iq) in zip(txs, res):
+        assert r[0] == 0
+        assert rel_err(iq, oracle_iq(9, 50, t, t["tti"] % 10, ioff=6, cqi_ioff=9, ri_ioff=6)) < TOL

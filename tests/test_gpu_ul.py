@@ -1,5 +1,6 @@
 """GPU: the UL PUSCH transmitter (include/mi_ul.h, srsue_amd/csrc/ul.hip) against the
-oracle's UL chain (oracle/o_ul.c): the rate-matched coded symbols bit-exact with or_ulsch_encode, and the
+oracle's UL chain (oracle/o_ul.c): the multiplexed coded symbols (CQI + rate-matched data) bit-exact with
+or_ulsch_encode, HARQ-ACK / RI / CQI on PUSCH (36.212 5.2.2.6-5.2.2.8) through the IQ check, and the
 SC-FDMA IQ within 1e-4 (RMS-relative) of or_pusch_encode (double precision) -- over QPSK/16QAM/64QAM,
 every redundancy version, K-/K+ segmentation with filler bits, single code blocks (CRC24A only), partial
 allocations, group / sequence hopping, cyclic shifts, and 1.4-20 MHz cells in one batch."""
@@ -29,15 +30,31 @@ CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [
     (25, 0, 3, 104, 2, 0, 2, 9, 0, 0, 0, 0, 0, 2, 3, 14),        # Q'_ACK capped at 4 M (tiny TB), filler bits
     (100, 2, 48, 12216, 4, 0, 5, 3, 0, 0, 0, 1, 0, 0, 0, 0, 50),  # frequency hopping: slot 1 at PRB 50
     (50, 30, 20, 5736, 6, 1, 7, 8, 1, 0, 0, 2, 6, 1, 1, 9, 4),   # hopping down to PRB 4, ACK, group hopping
+    # UCI on PUSCH (36.212 5.2.2.6): srsUE's 4-bit wideband CQI (phch_worker.cc:507-523) with and without ACK,
+    # RI 1 / 2 bits, a long CQI report (CRC8 + convolutional code), CQI capped by the allocation, hopping
+    (100, 0, 100, 39232, 4, 0, 1, 1, 0, 0, 0, 0, 0, dict(cqi=[1, 0, 1, 1], cqi_ioff=9)),
+    (25, 2, 20, 3000, 2, 1, 8, 4, 1, 0, 0, 2, 1, 1, 1, 7, dict(cqi=[0, 1, 1, 0], cqi_ioff=15, ri_len=1, ri=1,
+                                                                ri_ioff=12)),
+    (50, 0, 45, 9000, 6, 0, 6, 5, 0, 1, 0, 0, 4, 2, 2, 14, dict(ri_len=2, ri=3, ri_ioff=6)),
+    (100, 4, 90, 25456, 6, 2, 4, 7, 0, 1, 3, 2, 5, dict(cqi=[1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 0, 1, 1, 0,
+                                                            1, 0, 0, 1, 1, 1, 0], cqi_ioff=12, ri_len=1, ri=0)),
+    (6, 0, 6, 1000, 4, 0, 3, 2, 0, 0, 0, 1, 2, 1, 0, 3, dict(cqi=[1] * 11, cqi_ioff=15, ri_len=2, ri=2,
+                                                               ri_ioff=12)),
+    (15, 0, 15, 328, 2, 0, 2, 12, 0, 0, 0, 0, 2, 0, 0, 0, dict(cqi=[1, 0, 0, 1, 1, 0, 1, 0, 0, 0, 1, 1, 1, 0] * 3,
+                                                                 cqi_ioff=15)),   # Q'_CQI at its cap
+    (100, 2, 48, 12216, 4, 0, 5, 3, 0, 0, 0, 1, 0, 1, 1, 5, 50, dict(cqi=[0, 0, 1, 1], cqi_ioff=7, ri_len=1, ri=1,
+                                                                     ri_ioff=3)),
 ]
 
 
 def mk(c):
+    extra = c[-1] if isinstance(c[-1], dict) else {}
+    c = c[:-1] if extra else c
     nof_prb, n_prb, L, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 = c[:13]
     ack_len, ack, ioff = c[13:16] if len(c) > 13 else (0, 0, 0)
     n1 = c[16] if len(c) > 16 else None      # slot-1 start PRB (frequency hopping)
     return dict(cell_id=cell, nof_prb=nof_prb, sf_idx=sf, rnti=0x46 + sf, n_prb=n_prb, L_prb=L, tbs=tbs, Qm=Qm, rv=rv,
-                gh=gh, sh=sh, dss=dss, cs=cs, n2=n2, ack_len=ack_len, ack=ack, ioff=ioff, n_prb1=n1)
+                gh=gh, sh=sh, dss=dss, cs=cs, n2=n2, ack_len=ack_len, ack=ack, ioff=ioff, n_prb1=n1, **extra)
 
 
 def tb_of(i, tbs):
@@ -45,9 +62,12 @@ def tb_of(i, tbs):
 
 
 def oracle_symbols(oc, tb):
+    """the multiplexed sequence g (CQI then data, 36.212 5.2.2.7) as Qm-bit symbols, then zeros for the
+    Q'_RI cells (the layout of mi_ul_batch_symbols)"""
     G = O.lib().or_pusch_G(C.byref(oc))
     f = np.zeros(G, np.uint8)
-    assert O.lib().or_ulsch_encode(C.byref(oc), tb, f) == G
+    H = O.lib().or_ulsch_encode(C.byref(oc), tb, f)
+    assert H == G - O.lib().or_ri_qprime(C.byref(oc)) * oc.Qm
     Qm = oc.Qm
     w = (1 << np.arange(Qm - 1, -1, -1)).astype(np.uint32)
     return (f.reshape(-1, Qm).astype(np.uint32) @ w).astype(np.uint8)

@@ -207,3 +207,133 @@ def test_harq_ack_on_pusch_independent(L, Qm, tbs, alen, ack, ioff):
     noi, cbok = C.c_uint32(), C.c_uint32()
     rc = O.lib().or_dlsch_decode(llr, G, tbs, Qm, 1, 0, 1, sb, ncb, 4, pay, C.byref(noi), C.byref(cbok))
     assert rc == 0 and np.array_equal(pay, tb)
+
+
+BETA8_RI = [10, 13, 16, 20, 25, 32, 40, 50, 64, 80, 101, 127, 160]                  # Table 8.6.3-2 x 8
+BETA8_CQI = [0, 0, 9, 10, 11, 13, 14, 16, 18, 20, 23, 25, 28, 32, 40, 50]           # Table 8.6.3-3 x 8
+
+
+def test_cqi_rm32_code_properties():
+    """Table 5.2.2.6.4-1 pinned by structure: column 0 is all ones, columns 1-5 enumerate all 32 five-bit
+    patterns (the first-order Reed-Muller code RM(1,5) inside), and the (32, O) codes have minimum distance
+    16 for O <= 6, 12 for O = 7..10 and 10 for O = 11 (every non-zero message enumerated)."""
+    rm = O.lib().or_cqi_rm32
+    cols = [rm(np.eye(11, dtype=np.uint8)[n], 11) for n in range(11)]
+    assert cols[0] == 0xFFFFFFFF
+    pats = {tuple((cols[n] >> (31 - i)) & 1 for n in range(1, 6)) for i in range(32)}
+    assert len(pats) == 32
+    for O_, dmin in [(1, 32), (4, 16), (6, 16), (7, 12), (10, 12), (11, 10)]:
+        best = 32
+        for m in range(1, 1 << O_):
+            o = np.array([(m >> n) & 1 for n in range(O_)], np.uint8)
+            best = min(best, bin(rm(o, O_)).count("1"))
+        assert best == dmin, O_
+
+
+def _ml_rm32(r, O_):
+    """maximum-likelihood decode of the (32, O) code from the first len(r) <= 32 received bits"""
+    best, arg = 99, None
+    for m in range(1 << O_):
+        o = np.array([(m >> n) & 1 for n in range(O_)], np.uint8)
+        w = O.lib().or_cqi_rm32(o, O_)
+        d = sum(((w >> (31 - i)) & 1) != r[i] for i in range(len(r)))
+        if d < best:
+            best, arg = d, o
+    return arg
+
+
+@pytest.mark.parametrize("O_,L,Qm,tbs,ioff", [(4, 25, 4, 8000, 9), (4, 6, 2, 1000, 15), (11, 10, 6, 3000, 12),
+                                               (4, 50, 6, 2000, 15),
+                                               (20, 50, 4, 20000, 15), (40, 100, 6, 50000, 14), (64, 25, 2, 4000, 15)])
+def test_cqi_on_pusch_encoding(O_, L, Qm, tbs, ioff):
+    """36.212 5.2.2.6.4: Q'_CQI = min(ceil((O + L) M 12 beta / sum K_r), 12 M - Q'_RI) restated, and the coded
+    bits decode back: O <= 11 by maximum likelihood over the (32, O) code with 3 bit errors injected (below
+    half the minimum distance), O > 11 through the convolutional-code rate de-matcher, the tail-biting
+    Viterbi decoder and CRC8 (g = D^8 + D^7 + D^4 + D^3 + D + 1)."""
+    o = np.random.default_rng(O_).integers(0, 2, O_).astype(np.uint8)
+    c = cfg(L_prb=L, Qm=Qm, tbs=tbs, cqi=list(o), cqi_ioff=ioff, ri_len=1, ri=1, ri_ioff=4)
+    M = 12 * L
+    s = O.cbsegm(tbs)
+    sumK = s.Cm * s.Km + (s.C - s.Cm) * s.Kp
+    qri = min(-(-1 * M * 12 * BETA8_RI[4] // (8 * sumK)), 4 * M)
+    crc = 8 if O_ > 11 else 0
+    qp = min(-(-(O_ + crc) * M * 12 * BETA8_CQI[ioff] // (8 * sumK)), 12 * M - qri)
+    assert O.lib().or_ri_qprime(C.byref(c)) == qri and O.lib().or_cqi_qprime(C.byref(c)) == qp
+    q = np.zeros(qp * Qm, np.uint8)
+    assert O.lib().or_cqi_encode(C.byref(c), q) == qp * Qm
+    if O_ <= 11:
+        assert all(q[i] == q[i % 32] for i in range(len(q)))
+        r = q[:32].copy()
+        if len(r) == 32:
+            r[[3, 17, 29]] ^= 1
+        assert np.array_equal(_ml_rm32(r, O_), o)
+    else:
+        D = O_ + 8
+        llr = (2.0 * q.astype(np.float32) - 1.0)
+        d = np.zeros(3 * D, np.float32)
+        O.lib().or_conv_rm_rx(llr, len(llr), D, d)
+        dec = np.zeros(D, np.uint8)
+        O.lib().or_viterbi_tb(d, D, dec)
+        assert np.array_equal(dec[:O_], o)
+        assert O.lib().or_crc(np.ascontiguousarray(dec), D, 0x9B, 8) == 0      # CRC8 over payload || parity
+
+
+@pytest.mark.parametrize("L,Qm,tbs,ri_len,ri,rioff,ncqi", [(6, 2, 1000, 1, 1, 12, 4), (3, 6, 1800, 2, 2, 9, 0),
+                                                          (25, 4, 8000, 2, 3, 12, 11), (10, 2, 600, 1, 0, 6, 20)])
+def test_ri_and_cqi_multiplexing_independent(L, Qm, tbs, ri_len, ri, rioff, ncqi):
+    """5.2.2.7 / 5.2.2.8 with RI and CQI restated in numpy from the specification text against
+    or_ulsch_encode + or_pusch_mod: g = CQI bits then data bits; RI cells from the last row up in columns
+    1, 10, 7, 4 (ColumnSet {1, 4, 7, 10}, j = (j + 3) mod 4); g row by row over the other cells; read out
+    column by column; RI placeholders scrambled like HARQ-ACK's.  The data decodes through the DL-SCH
+    decoder from the cells g occupies."""
+    cq = list(np.random.default_rng(L).integers(0, 2, ncqi).astype(np.uint8))
+    c = cfg(L_prb=L, Qm=Qm, tbs=tbs, cell_id=91, sf_idx=6, rnti=0x2C4, cqi=cq, cqi_ioff=15, ri_len=ri_len, ri=ri,
+            ri_ioff=rioff)
+    M, Gt = 12 * L, O.lib().or_pusch_G(C.byref(c))
+    qri, qcqi = O.lib().or_ri_qprime(C.byref(c)), O.lib().or_cqi_qprime(C.byref(c))
+    assert qri > 0 and (qcqi > 0) == (ncqi > 0)
+    tb = tb_of(L + 1, tbs)
+    g = np.zeros(Gt, np.uint8)
+    H = O.lib().or_ulsch_encode(C.byref(c), tb, g)
+    assert H == Gt - qri * Qm
+    cqb = np.zeros(max(1, qcqi * Qm), np.uint8)
+    O.lib().or_cqi_encode(C.byref(c), cqb)
+    assert np.array_equal(g[:qcqi * Qm], cqb[:qcqi * Qm])
+    X, Y = 2, 3
+    o0, o1 = ri & 1, (ri >> 1) & 1
+    if ri_len == 1:
+        blk = [o0, Y] + [X] * (Qm - 2)
+    else:
+        o2 = o0 ^ o1
+        blk = sum(([a, b] + [X] * (Qm - 2) for a, b in ((o0, o1), (o2, o0), (o1, o2))), [])
+    q = [blk[k % len(blk)] for k in range(qri * Qm)]
+    mat = np.full((M, 12, Qm), -1, np.int64)
+    j = 0
+    for i in range(qri):
+        mat[M - 1 - i // 4, [1, 4, 7, 10][j]] = q[i * Qm:(i + 1) * Qm]
+        j = (j + 3) % 4
+    k = 0
+    for r in range(M):
+        for col in range(12):
+            if mat[r, col, 0] < 0:
+                mat[r, col] = g[k * Qm:(k + 1) * Qm]
+                k += 1
+    assert k * Qm == H
+    h = mat.transpose(1, 0, 2).reshape(-1)
+    cs = gold((0x2C4 << 14) | (6 << 9) | 91, Gt)
+    for i in range(Gt):
+        h[i] = 1 if h[i] == X else h[i - 1] if h[i] == Y else h[i] ^ cs[i]
+    want = np.array([pam(h[t * Qm:(t + 1) * Qm:2], Qm) + 1j * pam(h[t * Qm + 1:(t + 1) * Qm:2], Qm)
+                     for t in range(Gt // Qm)])
+    x = np.zeros(2 * Gt // Qm, np.float32)
+    assert O.lib().or_pusch_mod(C.byref(c), g, x) == 0
+    assert np.max(np.abs((x[0::2] + 1j * x[1::2]) - want)) < 1e-6
+    G = H - qcqi * Qm
+    llr = (2.0 * g[qcqi * Qm:H].astype(np.float32) - 1.0) * 8.0
+    s = O.cbsegm(tbs)
+    ncb = O.lib().or_ncb(s.Kp)
+    sb = np.zeros(s.C * ncb, np.float32)
+    pay = np.zeros(tbs // 8, np.uint8)
+    noi, cbok = C.c_uint32(), C.c_uint32()
+    rc = O.lib().or_dlsch_decode(llr, G, tbs, Qm, 1, 0, 1, sb, ncb, 4, pay, C.byref(noi), C.byref(cbok))
+    assert rc == 0 and np.array_equal(pay, tb)
