@@ -204,8 +204,9 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     sym_bytes += 12 * (size_t)t.M;
     t.tbs = c.tbs;
     t.scr_off = (uint32_t)scr.size();
-    scr.resize(scr.size() + (G + 31) / 32 + 1);
-    gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, G, &scr[t.scr_off]);
+    const uint32_t n_scr = 12 * t.M * c.Qm;   // 36.211 5.3.1 scrambles every coded bit of the subframe (UCI too)
+    scr.resize(scr.size() + (n_scr + 31) / 32 + 1);
+    gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, n_scr, &scr[t.scr_off]);
     // segmentation of (TB || CRC24A), 36.212 5.1.2 (sg above); the data follow the CQI symbols in g (5.2.2.7)
     tb_cb0.push_back((uint32_t)cbs.size());
     uint32_t byte0 = 0, sym = t.q_cqi;
