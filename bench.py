@@ -218,13 +218,15 @@ def config_cfgs(config, B, first):
 
 SCHED_DESC = {"win": "latency form", "lanex": "lane per code block, crossed (2 wavefronts per group)",
               "lanexr": "lane per code block, crossed, recompute form (2 wavefronts per group, 5 per SIMD)",
-              "lane": "lane per code block"}
+              "lane": "lane per code block",
+              "p2": "two code blocks per lane (packed int16), crossed (2 wavefronts per group pair, 3 per SIMD)"}
 
 
 def tdec_kernel_name(sched):
     return {"win": "tdec_win_kernel (max-log-MAP turbo, one workgroup per code block)",
             "lanex": "tdec_kernel_*x (max-log-MAP turbo, one code block per lane, crossed schedule)",
-            "lanexr": "tdec_kernel_i16xr (max-log-MAP turbo, one code block per lane, crossed, recompute form)"}.get(
+            "lanexr": "tdec_kernel_i16xr (max-log-MAP turbo, one code block per lane, crossed, recompute form)",
+            "p2": "tdec_kernel_p2x (max-log-MAP turbo, two code blocks per lane in packed int16, crossed)"}.get(
         sched, "tdec_kernel (max-log-MAP turbo, one code block per lane)")
 
 
@@ -612,7 +614,7 @@ def main():
                     help="also time the UL PUSCH transmitter (SURVEY 8f-4) on as many subframes; reported beside value")
     ap.add_argument("--iq", choices=("fc32", "sc16"), default="fc32",
                     help="wire format of the host IQ in the --h2d measurement (sc16 = UHD int16, half the bytes)")
-    ap.add_argument("--sched", choices=("auto", "win", "lane", "lanex", "lanexr"), default="auto",
+    ap.add_argument("--sched", choices=("auto", "win", "lane", "lanex", "lanexr", "p2"), default="auto",
                     help="int16 turbo schedule: latency form (one workgroup per code block, exact trellis segments), "
                          "one code block per lane, or auto (latency form up to 1024 code blocks)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",

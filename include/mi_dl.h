@@ -83,6 +83,11 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * 92 VGPRs, 5 waves per SIMD; int16 decoder).  Default: chosen when the batch's wavefronts fit in one
  * round at 5 but not at 4 waves per SIMD. */
 #define MI_DL_FLAG_TDEC_XR   256u
+/* int16 decoder, lane form with TWO code blocks per lane: the trellis metrics of a code block of group A
+ * (low 16 bits) and of the same lane of an equal-K group B (high 16 bits) in one register, advanced by
+ * packed int16 instructions (half the VALU instructions per code block), crossed schedule; bit-identical
+ * outputs (tdec_p2_body.h) */
+#define MI_DL_FLAG_TDEC_P2   512u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 
@@ -116,8 +121,8 @@ void   mi_dl_batch_profile_reset(mi_dl_batch_t *b);
 double mi_dl_batch_algo_bytes(const mi_dl_batch_t *b, int which_stage /* -1 = compulsory total */);
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
 /* turbo schedule of the batch: 1 = latency form (MI_DL_FLAG_TDEC_WIN rules), 2 = lane per code block in
- * the crossed schedule (two wavefronts per group), 3 = the same in its recompute form, 0 = lane per code
- * block, one wavefront per group */
+ * the crossed schedule (two wavefronts per group), 3 = the same in its recompute form, 4 = two code blocks
+ * per lane (packed int16, crossed), 0 = lane per code block, one wavefront per group */
 int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 

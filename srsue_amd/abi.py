@@ -24,8 +24,9 @@ FLAG_TDEC_WIN = 16  # int16 turbo: force the latency form (one workgroup per cod
 FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wavefronts
 FLAG_TDEC_X = 128  # lane-per-code-block decoder, crossed schedule (two wavefronts per group)
 FLAG_TDEC_XR = 256  # crossed kernel, recompute form (5 waves per SIMD)
+FLAG_TDEC_P2 = 512   # two code blocks per lane (packed int16), crossed
 SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X,
-               "lanexr": FLAG_TDEC_LANE | FLAG_TDEC_X | FLAG_TDEC_XR}
+               "lanexr": FLAG_TDEC_LANE | FLAG_TDEC_X | FLAG_TDEC_XR, "p2": FLAG_TDEC_LANE | FLAG_TDEC_P2}
 FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
 
 
@@ -273,7 +274,7 @@ class Batch:
     @property
     def turbo_sched(self):
         """'win' (latency form), 'lanex' (lane per code block, two wavefronts per group) or 'lane'"""
-        return {1: "win", 2: "lanex", 3: "lanexr"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
+        return {1: "win", 2: "lanex", 3: "lanexr", 4: "p2"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
 
     @property
     def n_groups(self):
@@ -536,7 +537,7 @@ class TdecBatch:
 
     @property
     def turbo_sched(self):
-        return {1: "win", 2: "lanex", 3: "lanexr"}.get(lib().mi_tdec_turbo_win(self.h), "lane")
+        return {1: "win", 2: "lanex", 3: "lanexr", 4: "p2"}.get(lib().mi_tdec_turbo_win(self.h), "lane")
 
     def close(self):
         if self.h:

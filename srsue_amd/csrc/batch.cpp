@@ -114,7 +114,12 @@ double mi_dl_batch_algo_bytes(const mi_dl_batch_t* b, int which_stage) {
 }
 
 uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t* b) { return b->eng.plan.n_cb; }
-int mi_dl_batch_turbo_win(const mi_dl_batch_t* b) { return b->eng.use_win() ? 1 : b->eng.tdec_crossed() == 2 ? 3 : b->eng.tdec_crossed() ? 2 : 0; }
+static int turbo_sched(const mi::Engine& e) {
+  if (e.use_win()) return 1;
+  const int x = e.tdec_crossed();
+  return x == 3 ? 4 : x == 2 ? 3 : x ? 2 : 0;
+}
+int mi_dl_batch_turbo_win(const mi_dl_batch_t* b) { return turbo_sched(b->eng); }
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
 
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */
@@ -159,7 +164,7 @@ int mi_tdec_download(mi_tdec_batch_t* b, uint8_t* bits, uint32_t* its, uint32_t*
 int mi_tdec_stage_ms(mi_tdec_batch_t* b, float* ms, uint32_t* nruns) { return b->eng.stage_ms(ms, nruns); }
 void mi_tdec_profile_reset(mi_tdec_batch_t* b) { b->eng.profile_reset(); }
 double mi_tdec_algo_bytes(const mi_tdec_batch_t* b) { return b->eng.plan.stage_bytes[MI_DL_STAGE_TDEC]; }
-int mi_tdec_turbo_win(const mi_tdec_batch_t* b) { return b->eng.use_win() ? 1 : b->eng.tdec_crossed() == 2 ? 3 : b->eng.tdec_crossed() ? 2 : 0; }
+int mi_tdec_turbo_win(const mi_tdec_batch_t* b) { return turbo_sched(b->eng); }
 
 // ---- host-IQ pipeline (double buffering) ---------------------------------------
 }  // extern "C"

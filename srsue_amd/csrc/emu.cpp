@@ -13,6 +13,7 @@
 #include "rm_body.h"
 #include "tb_body.h"
 #include "tdec_body.h"
+#include "tdec_p2_body.h"
 #include "tdec_win_body.h"
 
 static int g_q16 = 0;   // turbo arithmetic of the emulated decoder (MI_DL_FLAG_TDEC_I16)
@@ -21,7 +22,7 @@ extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 static uint32_t crc8[256];
 
 // crossed-schedule lane decoder (two wavefronts per group, tdec_body.h tdec_lane_x): 0 = off, 1 = register
-// form, 2 = recompute form
+// form, 2 = recompute form, 3 = two code blocks per lane (int16 only, tdec_p2_body.h)
 static int g_x = 0;
 extern "C" void emu_set_tdec_x(int on) { g_x = on; }
 template <bool Q16>
@@ -111,7 +112,58 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
     memcpy(&e[P.sfs[s].e_off], llr_concat + src, G * sizeof(float));
     src += G;
   }
+  if (g_x == 3 && g_q16) {
+    // two code blocks per lane (tdec_p2_body.h): rate de-matching of every group, then the group pairs
+    std::vector<std::vector<uint32_t>> wms(P.groups.size());
+    for (size_t gi = 0; gi < P.groups.size(); gi++) {
+      const MiGroupDesc& g = P.groups[gi];
+      float* sbg = &sb[g.sb_off];
+      uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
+      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p);
+      const MiKTab& kt = P.ktabs[g.ktab];
+      wms[gi].resize(g.K / mi::BETA_W + 1);
+      for (uint32_t w = 0; w < wms[gi].size(); w++) wms[gi][w] = mi::tdec_window_mask(map, &P.kdata[kt.pos_off], w);
+    }
+    for (size_t pp = 0; pp < P.pairs.size(); pp += 2) {
+      const uint32_t ga = P.pairs[pp], gbi = P.pairs[pp + 1];
+      const bool paired = gbi != 0xFFFFFFFFu;
+      const uint32_t gb = paired ? gbi : ga;
+      const MiGroupDesc &gA = P.groups[ga], &gB = P.groups[gb];
+      const MiKTab& kt = P.ktabs[gA.ktab];
+      for (int lane = 0; lane < mi::LANES; lane++) {
+        const uint32_t li[2] = {gA.lane0 + lane, gB.lane0 + lane};
+        const MiLaneDesc &l0 = P.lanes[li[0]], &l1 = P.lanes[li[1]];
+        mi::TdecArgsP2 a;
+        a.live = (l0.valid ? 1u : 0u) | (paired && l1.valid ? 2u : 0u);
+        if (!a.live) continue;
+        a.sb[0] = &sb[gA.sb_off]; a.sb[1] = &sb[gB.sb_off];
+        a.wm[0] = wms[ga].data(); a.wm[1] = wms[gb].data();
+        a.zrow[0] = gA.Ncb; a.zrow[1] = gB.Ncb;
+        a.scr = reinterpret_cast<uint32_t*>(&scr[gA.scratch_off]);
+        a.q = a.scr + (size_t)(4 * gA.K + 8) * mi::LANES;
+        a.pos = &P.kdata[kt.pos_off]; a.pi = &P.kdata[kt.pi_off];
+        a.crc_a = &P.kdata[kt.crca_off]; a.crc_b = &P.kdata[kt.crcb_off];
+        a.crc8 = crc8;
+        a.dec = &dec[gA.dec_off];
+        a.cb_bytes[0] = &cbb[(size_t)li[0] * mi::CB_BYTES_STRIDE];
+        a.cb_bytes[1] = &cbb[(size_t)li[(a.live >> 1) & 1u] * mi::CB_BYTES_STRIDE];
+        a.K = gA.K;
+        a.F[0] = l0.F; a.F[1] = paired ? l1.F : l0.F;
+        a.crc24a[0] = l0.crc24a; a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
+        a.max_its = max_its; a.early_stop = 1;
+        mi::TdecP2ExecHost ex;
+        const mi::TdecP2Result r = mi::tdec_p2_lane(a, lane, ex);
+        for (int h = 0; h < 2; h++) {
+          if (!((a.live >> h) & 1u)) continue;
+          cits[li[h]] = r.its[h];
+          ccrc[li[h]] = r.crc_ok[h];
+          ctbp[li[h]] = r.tb_part[h];
+        }
+      }
+    }
+  }
   for (const MiGroupDesc& g : P.groups) {
+    if (g_x == 3 && g_q16) break;
     float* sbg = &sb[g.sb_off];
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
     for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p);

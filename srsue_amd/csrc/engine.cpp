@@ -60,7 +60,8 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   const Tab tabs[] = {tab(d_cells, P.cells), tab(d_crs, P.crs), tab(d_pds, P.pds), tab(d_re, P.re_tab),
                       tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),
                       tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),
-                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items)};
+                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items),
+                      tab(d_pairs, P.pairs)};
   size_t total = 0;
   for (const Tab& t : tabs) total += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
   if (total > h_stage_bytes) {
@@ -233,6 +234,7 @@ int Engine::tdec_crossed() const {
   const uint64_t waves = 2ull * plan.groups.size();
   const int form = (q16() && waves > 4ull * simds && waves <= 5ull * simds) ? 2 : 1;
   if (const char* e = getenv("MI_TDEC_X")) return atoi(e);   // A/B
+  if (flags & MI_DL_FLAG_TDEC_P2) return q16() ? 3 : 1;
   if (flags & MI_DL_FLAG_TDEC_XR) return q16() ? 2 : 1;
   if (flags & MI_DL_FLAG_TDEC_X) return form;
   if (flags & MI_DL_FLAG_TDEC_LANE) return 0;
@@ -257,6 +259,13 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
   }
   launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                  (uint32_t)P.groups.size(), st);
+  if (tdec_crossed() == 3 && q16()) {
+    launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
+                   d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
+                   d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), d_pairs.as<uint32_t>(),
+                   (uint32_t)(P.pairs.size() / 2), max_its, early_stop, st);
+    return;
+  }
   launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
               d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(),

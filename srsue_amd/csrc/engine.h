@@ -31,12 +31,14 @@ struct Engine {
   bool q16() const { return (flags & MI_DL_FLAG_TDEC_GEN) == 0; }   // int16 turbo arithmetic (default)
   uint32_t win_threads = 0;   // latency-form turbo: threads per code block (0 = by K)
   bool use_win() const;       // latency-form (segment-parallel) turbo decoder for this plan
-  int tdec_crossed() const;   // lane form: 0 one wavefront per group, 1 crossed, 2 crossed (recompute form)
+  // lane form: 0 one wavefront per group, 1 crossed, 2 crossed (recompute form), 3 crossed with two code
+  // blocks per lane (packed int16, tdec_p2_body.h)
+  int tdec_crossed() const;
   void launch_turbo(float* sb, hipStream_t st);
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,
-      d_fftlist, d_tw;
+      d_fftlist, d_tw, d_pairs;
   // data buffers
   DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_wm, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,
       d_tbits;

@@ -34,6 +34,12 @@ void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* d
                  uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                  const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
                  uint32_t early_stop, bool q16, int crossed /* 0 one wavefront per group, 1 crossed, 2 crossed recompute */, hipStream_t st);
+// packed int16 decoder, two code blocks per lane: one workgroup (crossed wavefronts F and B) per group pair
+// (Plan::pairs)
+void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes,
+                    uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
+                    const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
+                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, hipStream_t st);
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
 void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,

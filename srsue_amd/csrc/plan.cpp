@@ -43,6 +43,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   cb_K = cb_n = 0;
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  pairs.clear();
   rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
@@ -222,8 +223,11 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         }
       }
     }
+    if (((j - i + LANES - 1) / LANES) & 1)   // odd group count: padding for the unpaired group's pair scratch
+      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
     i = j;
   }
+  build_pairs();
   // fused demap sources of every lane
   lane_src.assign(lanes.size(), MiLaneSrc{0, 0, 0, 0, 0, 2, 0, 0, 0});
   for (size_t li = 0; li < lanes.size(); li++) {
@@ -330,10 +334,21 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   return 0;
 }
 
+void Plan::build_pairs() {
+  pairs.clear();
+  for (size_t g = 0; g < groups.size();) {
+    const bool two = g + 1 < groups.size() && groups[g + 1].K == groups[g].K;
+    pairs.push_back((uint32_t)g);
+    pairs.push_back(two ? (uint32_t)(g + 1) : 0xFFFFFFFFu);
+    g += two ? 2 : 1;
+  }
+}
+
 int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   if (!cb_size_valid(K) || ncb_req == 0) { set_error("invalid code block size"); return -1; }
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  pairs.clear();
   rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
@@ -366,6 +381,8 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
       lanes.push_back(ld);
     }
   }
+  if (groups.size() & 1) scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));   // pair padding
+  build_pairs();
   n_cb = ncb_req;
   stage_bytes[MI_DL_STAGE_RM] = (double)ncb_req * (3 * K + 12) * 4 * 2;        // scatter: read + write
   stage_bytes[MI_DL_STAGE_TDEC] = (double)ncb_req * ((3 * K + 12) * 4 + K / 8);  // SURVEY 8d per CB

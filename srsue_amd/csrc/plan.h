@@ -29,6 +29,11 @@ struct Plan {
   std::vector<uint32_t> rm_items;
   uint32_t rm_busy = 0;
   std::vector<MiGroupDesc> groups;
+  // pairs of equal-K groups for the packed two-code-blocks-per-lane turbo decoder (tdec_p2_body.h):
+  // [2p] = group A, [2p + 1] = group B or 0xFFFFFFFF; a pair's decoder scratch spans both groups' regions
+  // (consecutive), an unpaired group is followed by one group's worth of padding
+  std::vector<uint32_t> pairs;
+  void build_pairs();
   std::vector<MiKTab> ktabs;
   std::vector<uint32_t> kdata;
   std::vector<MiTbDesc> tbs;

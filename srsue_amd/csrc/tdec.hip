@@ -3,6 +3,7 @@
 #include "kernels.h"
 #include "tb_body.h"
 #include "tdec_body.h"
+#include "tdec_p2_body.h"
 
 namespace mi {
 
@@ -150,6 +151,97 @@ void tdec_kernel_i16xr(const float* __restrict__ sb, const uint32_t* __restrict_
                        const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                        const uint32_t* __restrict__ kdata, uint32_t max_its, uint32_t early_stop) {
   tdec_group<true, true, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
+}
+
+// ---- two code blocks per lane (packed int16, tdec_p2_body.h): one workgroup of two wavefronts (the
+// crossed schedule) per PAIR of equal-K groups; pairs[2p] = group A, pairs[2p + 1] = group B or
+// 0xFFFFFFFF (an unpaired group: the high halves carry no code block)
+struct TdecP2ExecGpu {
+  static constexpr bool SHARED = true;
+  int wave;
+  uint32_t* xcrc;   // LDS [2 waves][64 lanes][2 halves] partial CB-CRC registers
+  template <class F, class B>
+  __device__ void run(F f, B b) {
+    if (wave == 0) f(); else b();
+    __syncthreads();
+  }
+  __device__ void crc_combine2(uint32_t (&c)[2], int lane) {
+    xcrc[(wave * LANES + lane) * 2] = c[0];
+    xcrc[(wave * LANES + lane) * 2 + 1] = c[1];
+    __syncthreads();
+    c[0] ^= xcrc[((wave ^ 1) * LANES + lane) * 2];
+    c[1] ^= xcrc[((wave ^ 1) * LANES + lane) * 2 + 1];
+  }
+  __device__ bool pack_wave() const { return wave == 0; }
+};
+
+#ifndef MI_TDEC_P2_WAVES
+#define MI_TDEC_P2_WAVES 3
+#endif
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
+void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
+                     uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
+                     const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
+                     const uint32_t* __restrict__ kdata, const uint32_t* __restrict__ pairs, uint32_t max_its,
+                     uint32_t early_stop) {
+  __shared__ uint32_t crc8[256];
+  __shared__ uint32_t xcrc[2 * LANES * 2];
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+  __syncthreads();
+  const uint32_t ga = pairs[2 * blockIdx.x], gbi = pairs[2 * blockIdx.x + 1];
+  const bool paired = gbi != 0xFFFFFFFFu;
+  const uint32_t gb = paired ? gbi : ga;
+  const MiGroupDesc gA = groups[ga], gB = groups[gb];
+  const MiKTab kt = ktabs[gA.ktab];
+  const int lane = threadIdx.x % LANES;
+  const uint32_t li[2] = {gA.lane0 + lane, gB.lane0 + lane};
+  const MiLaneDesc l0 = lanes[li[0]], l1 = lanes[li[1]];
+  TdecArgsP2 a;
+  a.live = (l0.valid ? 1u : 0u) | (paired && l1.valid ? 2u : 0u);
+  if (!a.live) return;   // the same on both wavefronts: no barrier is left waiting
+  a.sb[0] = sb + gA.sb_off;
+  a.sb[1] = sb + gB.sb_off;
+  a.wm[0] = wm + (size_t)ga * WM_STRIDE;
+  a.wm[1] = wm + (size_t)gb * WM_STRIDE;
+  a.zrow[0] = gA.Ncb;
+  a.zrow[1] = gB.Ncb;
+  const uint32_t K = gA.K;
+  a.scr = reinterpret_cast<uint32_t*>(scratch + gA.scratch_off);   // spans both groups' scratch (plan.cpp)
+  a.q = a.scr + (size_t)(4 * K + 8) * LANES;
+  a.pos = kdata + kt.pos_off;
+  a.pi = kdata + kt.pi_off;
+  a.crc_a = kdata + kt.crca_off;
+  a.crc_b = kdata + kt.crcb_off;
+  a.crc8 = crc8;
+  a.dec = dec + gA.dec_off;
+  a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
+  a.cb_bytes[1] = out.cb_bytes + (size_t)li[(a.live >> 1) & 1u] * CB_BYTES_STRIDE;
+  a.K = K;
+  a.F[0] = l0.F;
+  a.F[1] = paired ? l1.F : l0.F;
+  a.crc24a[0] = l0.crc24a;
+  a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
+  a.max_its = max_its;
+  a.early_stop = early_stop;
+  TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xcrc};
+  const TdecP2Result r = tdec_p2_lane(a, lane, ex);
+  if (ex.wave) return;
+  for (int h = 0; h < 2; h++) {
+    if (!((a.live >> h) & 1u)) continue;
+    out.its[li[h]] = r.its[h];
+    out.crc_ok[li[h]] = r.crc_ok[h];
+    out.tb_part[li[h]] = r.tb_part[h];
+  }
+}
+
+void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes,
+                    uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
+                    const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
+                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, hipStream_t st) {
+  if (!n_pairs) return;
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
+                     ktab_data, pairs, max_its, early_stop);
 }
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,

@@ -35,6 +35,7 @@
 #ifndef MI_HD
 #define MI_HD __host__ __device__
 #endif
+#include "p2.h"
 
 namespace mi {
 
@@ -70,8 +71,12 @@ struct TdecCrc { uint32_t cb; };
 struct TdecLaneResult { uint32_t its; uint32_t crc_ok; uint32_t tb_part; };
 
 
-MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
-  return u ? (z ? luz : lu) : (z ? lp : 0.0f);
+// The trellis steps below are generic over the metric type T: float (both scalar decoders: the float
+// srsLTE-gen one and the int16 one computing on integer-valued fp32) or P2 (p2.h: two code blocks' int16
+// metrics in one register, tdec_p2_body.h).  gam(0, 0, ...) is the additive identity (no add is emitted).
+template <class T>
+MI_HD inline T gam(int u, int z, T lu, T lp, T luz) {
+  return u ? (z ? luz : lu) : (z ? lp : Metric<T>::zero());
 }
 
 // State-metric normalisation (subtract state 0).  The float decoder normalises every step, as the
@@ -81,24 +86,25 @@ MI_HD inline float gam(int u, int z, float lu, float lp, float luz) {
 // normalises once per window (before a checkpoint is stored, at the end of each forward window) --
 // values then grow by at most 4 x (1535 + 1023 + 511) within a window, far inside fp32's exact range
 // -- and its LLRs, extrinsics and decisions stay bit-identical to the per-step oracle.
-template <bool NORM>
-MI_HD inline void norm8(float (&v)[8]) {
+template <bool NORM, class T>
+MI_HD inline void norm8(T (&v)[8]) {
   if constexpr (NORM) {
-    const float v0 = v[0];
+    const T v0 = v[0];
 #pragma unroll
     for (int s = 0; s < 8; s++) v[s] = v[s] - v0;
   }
 }
 
 // one backward step: beta_k from beta_{k+1} (NORM: normalised)
-template <bool NORM = true>
-MI_HD inline void beta_step(const float (&bn)[8], float xs, float xp, float (&bk)[8]) {
-  const float luz = xs + xp;
-  float m[8];
+template <bool NORM = true, class T>
+MI_HD inline void beta_step(const T (&bn)[8], T xs, T xp, T (&bk)[8]) {
+  const T luz = xs + xp;
+  T m[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) {
-    float b0 = bn[tr_next(s, 0)] + gam(0, tr_par(s, 0), xs, xp, luz);
-    float b1 = bn[tr_next(s, 1)] + gam(1, tr_par(s, 1), xs, xp, luz);
+    const int z0 = tr_par(s, 0), z1 = tr_par(s, 1);
+    T b0 = z0 ? bn[tr_next(s, 0)] + gam(0, z0, xs, xp, luz) : bn[tr_next(s, 0)];
+    T b1 = bn[tr_next(s, 1)] + gam(1, z1, xs, xp, luz);
     m[s] = fmaxf(b0, b1);
   }
   if constexpr (NORM) {
@@ -111,22 +117,23 @@ MI_HD inline void beta_step(const float (&bn)[8], float xs, float xp, float (&bk
 }
 
 // one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1} (NORM: alpha normalised)
-template <bool NORM = true>
-MI_HD inline float alpha_step(float (&al)[8], const float (&bn)[8], float xs, float xp) {
-  const float luz = xs + xp;
-  const float NINF = -INFINITY;
-  float c[8][2], m0 = NINF, m1 = NINF;
+// (max(-inf, t) = t exactly, so the maxima start from the first term)
+template <bool NORM = true, class T>
+MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
+  const T luz = xs + xp;
+  T c[8][2], m0 = T{}, m1 = T{};
 #pragma unroll
   for (int s = 0; s < 8; s++) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-      c[s][u] = al[s] + gam(u, tr_par(s, u), xs, xp, luz);
-      float t = c[s][u] + bn[tr_next(s, u)];
-      if (u) m1 = fmaxf(m1, t); else m0 = fmaxf(m0, t);
+      const int z = tr_par(s, u);
+      c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
+      T t = c[s][u] + bn[tr_next(s, u)];
+      if (u) m1 = s ? fmaxf(m1, t) : t; else m0 = s ? fmaxf(m0, t) : t;
     }
   }
-  float llr = m1 - m0;
-  float na[8];
+  T llr = m1 - m0;
+  T na[8];
 #pragma unroll
   for (int sp = 0; sp < 8; sp++)
     na[sp] = fmaxf(c[tr_prev_s(sp, 0)][tr_prev_u(sp, 0)], c[tr_prev_s(sp, 1)][tr_prev_u(sp, 1)]);
@@ -671,15 +678,18 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
 // permutation for the DEC2 rows).  The host emulation runs the phases of both waves in turn.
 
 // the alpha update of alpha_step without the LLR (identical operations)
-template <bool NORM = true>
-MI_HD inline void alpha_fwd(float (&al)[8], float xs, float xp) {
-  const float luz = xs + xp;
-  float c[8][2];
+template <bool NORM = true, class T>
+MI_HD inline void alpha_fwd(T (&al)[8], T xs, T xp) {
+  const T luz = xs + xp;
+  T c[8][2];
 #pragma unroll
   for (int s = 0; s < 8; s++)
 #pragma unroll
-    for (int u = 0; u < 2; u++) c[s][u] = al[s] + gam(u, tr_par(s, u), xs, xp, luz);
-  float na[8];
+    for (int u = 0; u < 2; u++) {
+      const int z = tr_par(s, u);
+      c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
+    }
+  T na[8];
 #pragma unroll
   for (int sp = 0; sp < 8; sp++)
     na[sp] = fmaxf(c[tr_prev_s(sp, 0)][tr_prev_u(sp, 0)], c[tr_prev_s(sp, 1)][tr_prev_u(sp, 1)]);
@@ -692,15 +702,22 @@ MI_HD inline void alpha_fwd(float (&al)[8], float xs, float xp) {
   }
 }
 // the LLR of alpha_step without the alpha update (identical operations)
-MI_HD inline float llr_step(const float (&al)[8], const float (&bn)[8], float xs, float xp) {
-  const float luz = xs + xp;
-  float m0 = -INFINITY, m1 = -INFINITY;
+// REACH: the alpha states that are reachable (bit s); the others are left out of the maxima (for the
+// packed int16 decoder's first trellis steps, where "-inf" is a finite stand-in, tdec_p2_body.h)
+template <uint32_t REACH = 0xFFu, class T>
+MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
+  const T luz = xs + xp;
+  T m0 = T{}, m1 = T{};
+  bool f0 = true, f1 = true;
 #pragma unroll
   for (int s = 0; s < 8; s++) {
+    if (!((REACH >> s) & 1u)) continue;
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-      const float t = (al[s] + gam(u, tr_par(s, u), xs, xp, luz)) + bn[tr_next(s, u)];
-      if (u) m1 = fmaxf(m1, t); else m0 = fmaxf(m0, t);
+      const int z = tr_par(s, u);
+      const T t = ((u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s]) + bn[tr_next(s, u)];
+      if (u) { m1 = f1 ? t : fmaxf(m1, t); f1 = false; }
+      else { m0 = f0 ? t : fmaxf(m0, t); f0 = false; }
     }
   }
   return m1 - m0;

@@ -1,0 +1,550 @@
+// tdec_p2_body.h -- the int16 max-log-MAP turbo decoder with TWO code blocks per lane (packed int16).
+//
+// Same algorithm, schedule and bit-exactness contract as the crossed lane decoder of tdec_body.h
+// (tdec_lane_x, register form), with the trellis metrics of two code blocks in one 32-bit register
+// (p2.h): lane l of a pair of 64-lane groups A and B of equal K carries code block (A, l) in the low
+// and (B, l) in the high 16 bits, so every add / subtract / maximum of the recursions is one
+// v_pk_*_16 instruction for two code blocks -- half the VALU instructions per code block -- and every
+// scratch / q-row / checkpoint access moves both code blocks' values in one memory instruction.  Two
+// wavefronts (F and B, the crossed schedule) run each pair: 2,540 wavefronts for the headline's 2,540
+// groups instead of 5,080.
+//
+// Exactness: every value the int16 decoder forms is an integer inside the int16 range (bounds in
+// oracle/o_fec.c: normalised metrics +-3R, R = 2046; with the once-per-window normalisation of
+// tdec_body.h a candidate alpha + gamma + beta stays inside +-14R = +-28644 and an LLR inside +-13R),
+// so the wrapping packed adds are exact.  The one exception is the "-inf" of the unreachable start
+// states: the packed decoder uses the finite -16384 (p2.h Metric<P2>::ninf), which loses every maximum
+// of the alpha / beta recursions against a reachable state, but could win or wrap in an LLR term whose
+// beta side is large -- so the LLRs of steps 0, 1 and 2 (the only ones with unreachable alpha states)
+// leave those states out of their maxima (llr_step<REACH>), exactly as -inf would.
+//
+// Per-code-block early stop: a lane iterates while either of its code blocks is undecided; a code block
+// that stops (CRC pass, or the iteration cap) has its decisions packed at once, so later iterations of
+// its partner never touch its outputs; iteration counts are per code block.  Outputs (packed bytes,
+// iterations, CRC verdict, partial TB-CRC register) are identical to the one-code-block-per-lane kernels
+// and to the oracle's int16 decoder (or_decode_cb16).
+#pragma once
+#include "tdec_body.h"
+
+namespace mi {
+
+struct TdecArgsP2 {
+  const float* sb[2];     // the two groups' softbuffers (dl_common.h sb_group_floats layout)
+  const uint32_t* wm[2];  // their window masks (rowmask_kernel)
+  uint32_t zrow[2];       // their all-zero rows
+  uint32_t* q;            // packed q rows [3 (K + 4)][64] (lo = group A, hi = group B)
+  const uint32_t* pos;    // [3 (K + 4)]
+  const uint32_t* pi;     // [K]
+  const uint32_t* crc_a;  // [K] CRC24A / CRC24B single-bit contributions
+  const uint32_t* crc_b;
+  const uint32_t* crc8;   // [256] CRC24A byte table
+  uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][8]
+  uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
+  uint8_t* cb_bytes[2];   // each half's packed output row
+  uint32_t K, F[2], crc24a[2], max_its, early_stop;
+  uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
+};
+struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
+
+// decoder-input quantiser q(x) = clamp(rint(32 x), +-511) of two floats, packed.  Device: fma(x, 32,
+// 1.5 * 2^23) rounds 32 x to the nearest (even) integer in the low mantissa bits (|32 x| < 2^22; beyond,
+// the clamp gives +-511 either way), med3 clamps in that domain, and the low 16 bits of the two results
+// are the two's-complement int16 values, packed by one byte permute.
+MI_HD inline P2 q16_pair(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float M = 12582912.0f;
+  const float ya = __builtin_amdgcn_fmed3f(__builtin_fmaf(a, 32.0f, M), M - I16_CI, M + I16_CI);
+  const float yb = __builtin_amdgcn_fmed3f(__builtin_fmaf(b, 32.0f, M), M - I16_CI, M + I16_CI);
+  return p2_from_bits(__builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, yb), __builtin_bit_cast(uint32_t, ya),
+                                            0x05040100u));
+#else
+  return p2_make((int)q16f(a), (int)q16f(b));
+#endif
+}
+
+// raw loads of one window (BETA_W steps), converted only at use (software pipelining, tdec_body.h):
+//   q-row passes: s0 / s1 = packed q rows;  softbuffer passes: a0/b0, a1/b1 = groups A / B floats
+//   DEC1: s0 = systematic, s1 = parity 1, r0 = w;   DEC2: s0 = parity 2, r0 = llr1[pi], r1 = w[pi]
+//   MKQ (DEC1, the q-creating pass): a0..a2 / b0..b2 = the three streams of both groups
+struct TdecWinP2 {
+  uint32_t s0[BETA_W], s1[BETA_W];
+  float a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
+  uint32_t r0[BETA_W], r1[BETA_W];
+  uint32_t ck[8];
+};
+
+MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
+MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
+  const bool on = (m >> dt) & 1u;
+  return row_ld(a.sb[h], on ? MI_POS(a, t0 + dt) : a.zrow[h], lane);
+}
+
+template <bool DEC2, bool FIRST, bool SQ>
+MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
+  const uint32_t* llr1 = a.scr + (size_t)a.K * LANES;
+  const uint32_t ma = SQ ? 0u : p2_wmask(a, 0, base / BETA_W), mb = SQ ? 0u : p2_wmask(a, 1, base / BETA_W);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    const uint32_t k = base + i;
+    if (!DEC2) {
+      if constexpr (SQ) {
+        r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i);
+        r.s1[i] = row_ld(a.q, 3 * base, lane, 3 * i + 1);
+      } else {
+        r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i, lane);
+        r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i, lane);
+        r.a1[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 1, lane);
+        r.b1[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 1, lane);
+      }
+      r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
+    } else {
+      const uint32_t pk = MI_PI(a, k);
+      if constexpr (SQ) {
+        r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i + 2);
+      } else {
+        r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 2, lane);
+        r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 2, lane);
+      }
+      r.r0[i] = row_ld(llr1, pk, lane);
+      r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
+    }
+  }
+}
+template <bool FIRST>
+MI_HD inline void p2_load_window_mkq(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
+  const uint32_t ma = p2_wmask(a, 0, base / BETA_W), mb = p2_wmask(a, 1, base / BETA_W);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i, lane);
+    r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i, lane);
+    r.a1[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 1, lane);
+    r.b1[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 1, lane);
+    r.a2[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 2, lane);
+    r.b2[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 2, lane);
+    r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
+  }
+}
+
+// checkpoint record c: states 1..7 of both code blocks (state 0 is 0), [c][lane][8] u32, two 128-bit
+// accesses per lane
+MI_HD inline void p2_ck_store(uint32_t* scr, size_t ck0, uint32_t c, int lane, const P2 (&b)[8]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 7; k++) w[k] = p2_bits(b[k + 1]);
+  w[7] = 0u;
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * 4), vo = (uint32_t)lane * 32u;
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
+  __builtin_amdgcn_raw_buffer_store_b128(u4{w[0], w[1], w[2], w[3]}, rs, vo, so, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(u4{w[4], w[5], w[6], w[7]}, rs, vo + 16, so, 0);
+#else
+  memcpy(reinterpret_cast<char*>(scr) + so + vo, w, sizeof(w));
+#endif
+}
+MI_HD inline void p2_ck_load(const uint32_t* scr, size_t ck0, uint32_t c, int lane, TdecWinP2& r) {
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * 4), vo = (uint32_t)lane * 32u;
+#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
+  const u4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
+  const u4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16, so, 0);
+  r.ck[0] = v0.x; r.ck[1] = v0.y; r.ck[2] = v0.z; r.ck[3] = v0.w;
+  r.ck[4] = v1.x; r.ck[5] = v1.y; r.ck[6] = v1.z; r.ck[7] = v1.w;
+#else
+  memcpy(r.ck, reinterpret_cast<const char*>(scr) + so + vo, sizeof(r.ck));
+#endif
+}
+MI_HD inline void p2_ck_vec(const TdecWinP2& r, P2 (&v)[8]) {
+  v[0] = Metric<P2>::zero();
+#pragma unroll
+  for (int s = 1; s < 8; s++) v[s] = p2_from_bits(r.ck[s - 1]);
+}
+
+// decoder inputs (xs, xp) of step base + i; filler bits (k < F, known zeros; F < 64) of each half get
+// q(FILLER_LLR) = -511 in the systematic and parity-1 inputs
+template <bool SQ>
+MI_HD inline P2 p2_chan0(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s0[i]) : q16_pair(r.a0[i], r.b0[i]); }
+template <bool SQ>
+MI_HD inline P2 p2_chan1(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s1[i]) : q16_pair(r.a1[i], r.b1[i]); }
+MI_HD inline P2 p2_fill(P2 x, uint32_t k, const TdecArgsP2& a) {
+  const int FILL = -(int)I16_CI;
+  return p2_make(k < a.F[0] ? FILL : p2_lo(x), k < a.F[1] ? FILL : p2_hi(x));
+}
+template <bool DEC2, bool SQ>
+MI_HD inline void p2_xs_xp(const TdecArgsP2& a, const TdecWinP2& r, int i, uint32_t base, P2& xs, P2& xp) {
+  if (!DEC2) {
+    P2 c0 = p2_chan0<SQ>(r, i), c1 = p2_chan1<SQ>(r, i);
+    if (base < 64) {   // wave-uniform: only the first 16 windows can hold filler bits
+      c0 = p2_fill(c0, base + i, a);
+      c1 = p2_fill(c1, base + i, a);
+    }
+    xs = c0 + p2_from_bits(r.r0[i]);
+    xp = c1;
+  } else {
+    xs = p2_clamp(p2_from_bits(r.r0[i]) - p2_from_bits(r.r1[i]), (int)I16_CX);
+    xp = p2_chan0<SQ>(r, i);
+  }
+}
+
+// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1; DEC2 updates w, stores the two decision
+// bits and folds them into each half's code-block CRC
+template <bool DEC2>
+MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, P2 llr, P2 xs, uint32_t (&crc)[2]) {
+  const uint32_t k = base + i;
+  if (!DEC2) {
+    row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(llr), i);
+  } else {
+    const uint32_t pk = MI_PI(a, k);
+    row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
+    const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
+    const uint32_t b0 = (ng >> 15) & 1u, b1 = ng >> 31;
+    row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 1)));
+    const uint32_t ta = a.crc_a[pk], tb = a.crc_b[pk];
+    crc[0] ^= b0 ? (a.crc24a[0] ? ta : tb) : 0u;
+    crc[1] ^= b1 ? (a.crc24a[1] ? ta : tb) : 0u;
+  }
+}
+
+// ---- window bodies (the register form of tdec_body.h's crossed schedule) --------------------------
+// wave F, phase 1: alpha only
+template <bool DEC2, bool SQ>
+MI_HD inline void p2_alpha_only_window(const TdecArgsP2& a, const TdecWinP2& w, uint32_t base, P2 (&al)[8]) {
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    P2 xs, xp;
+    p2_xs_xp<DEC2, SQ>(a, w, i, base, xs, xp);
+    alpha_fwd<false>(al, xs, xp);
+  }
+  norm8<true>(al);
+}
+// the q-creating first pass (DEC1): quantise the window's three streams of both groups, store the packed
+// q rows, then the steps
+MI_HD inline void p2_store_q(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, int i, P2& q0, P2& q1) {
+  q0 = q16_pair(w.a0[i], w.b0[i]);
+  q1 = q16_pair(w.a1[i], w.b1[i]);
+  const P2 q2 = q16_pair(w.a2[i], w.b2[i]);
+  row_st(a.q, 3 * base, lane, p2_bits(q0), 3 * i);
+  row_st(a.q, 3 * base, lane, p2_bits(q1), 3 * i + 1);
+  row_st(a.q, 3 * base, lane, p2_bits(q2), 3 * i + 2);
+}
+MI_HD inline void p2_mkq_xs_xp(const TdecArgsP2& a, const TdecWinP2& w, uint32_t base, int i, P2 q0, P2 q1, P2& xs,
+                               P2& xp) {
+  if (base < 64) {
+    q0 = p2_fill(q0, base + i, a);
+    q1 = p2_fill(q1, base + i, a);
+  }
+  xs = q0 + p2_from_bits(w.r0[i]);
+  xp = q1;
+}
+MI_HD inline void p2_alpha_only_window_mkq(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base,
+                                           P2 (&al)[8]) {
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) {
+    P2 q0, q1, xs, xp;
+    p2_store_q(a, lane, w, base, i, q0, q1);
+    p2_mkq_xs_xp(a, w, base, i, q0, q1, xs, xp);
+    alpha_fwd<false>(al, xs, xp);
+  }
+  norm8<true>(al);
+}
+// wave B, phase 1: beta only
+template <bool DEC2, bool SQ>
+MI_HD inline void p2_beta_window(const TdecArgsP2& a, const TdecWinP2& w, uint32_t base, P2 (&b)[8]) {
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    P2 xs, xp, nb[8];
+    p2_xs_xp<DEC2, SQ>(a, w, i, base, xs, xp);
+    beta_step<false>(b, xs, xp, nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+  norm8<true>(b);
+}
+MI_HD inline void p2_beta_window_mkq(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&b)[8]) {
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    P2 q0, q1, xs, xp, nb[8];
+    p2_store_q(a, lane, w, base, i, q0, q1);
+    p2_mkq_xs_xp(a, w, base, i, q0, q1, xs, xp);
+    beta_step<false>(b, xs, xp, nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+  norm8<true>(b);
+}
+// wave F, phase 2: beta_{base+1..base+4} recomputed from the closing checkpoint, then alpha + LLRs
+template <bool DEC2, bool SQ>
+MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&al)[8],
+                                  uint32_t (&crc)[2]) {
+  P2 xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, w, i, base, xs[i], xp[i]);
+  P2 bw[BETA_W][8];
+  p2_ck_vec(w, bw[BETA_W - 1]);
+#pragma unroll
+  for (int i = BETA_W - 2; i >= 0; i--) beta_step<false>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) p2_emit<DEC2>(a, lane, base, i, alpha_step<false>(al, bw[i], xs[i], xp[i]), xs[i], crc);
+  norm8<true>(al);
+}
+// wave B, phase 2: alpha of the window recomputed from its opening checkpoint (window 0: the start
+// state), then backward steps emitting the LLRs.  FIRST_WIN (window 0): steps 0..2 have unreachable
+// alpha states, left out of their LLR maxima.
+template <bool DEC2, bool SQ, bool FIRST_WIN>
+MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&b)[8],
+                                      uint32_t (&crc)[2]) {
+  P2 xs[BETA_W], xp[BETA_W];
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, w, i, base, xs[i], xp[i]);
+  P2 aw[BETA_W][8];
+  if constexpr (FIRST_WIN) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) aw[0][s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+  } else {
+    p2_ck_vec(w, aw[0]);
+  }
+#pragma unroll
+  for (int i = 0; i < BETA_W - 1; i++) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) aw[i + 1][s] = aw[i][s];
+    alpha_fwd<false>(aw[i + 1], xs[i], xp[i]);
+  }
+#pragma unroll
+  for (int i = BETA_W - 1; i >= 0; i--) {
+    P2 llr;
+    // reachable alpha states at steps 0, 1, 2 from state 0 (tr_next: 0 -> {0, 4} -> {0, 2, 4, 6})
+    if (FIRST_WIN && i == 0) llr = llr_step<0x01u>(aw[i], b, xs[i], xp[i]);
+    else if (FIRST_WIN && i == 1) llr = llr_step<0x11u>(aw[i], b, xs[i], xp[i]);
+    else if (FIRST_WIN && i == 2) llr = llr_step<0x55u>(aw[i], b, xs[i], xp[i]);
+    else llr = llr_step(aw[i], b, xs[i], xp[i]);
+    p2_emit<DEC2>(a, lane, base, i, llr, xs[i], crc);
+    P2 nb[8];
+    beta_step<false>(b, xs[i], xp[i], nb);
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = nb[s];
+  }
+  norm8<true>(b);
+}
+
+#ifndef MI_TDEC_P2_PF_Q
+#define MI_TDEC_P2_PF_Q 1
+#endif
+// the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
+template <bool DEC2, bool FIRST, int SRC>
+struct TdecP2X {
+  static constexpr bool MKQ = !DEC2 && SRC == SRC_MKQ;
+  static constexpr bool SQB = SRC == SRC_Q;    // backward-side passes read q rows
+  static constexpr bool SQF = SRC != SRC_SB;   // forward-side passes read q rows
+  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_P2_PF_Q;
+  using Win = TdecWinP2;
+
+  MI_HD static void load1(const TdecArgsP2& a, int lane, uint32_t w, Win& r) {
+    if constexpr (MKQ) p2_load_window_mkq<FIRST>(a, lane, w * BETA_W, r);
+    else p2_load_window<DEC2, FIRST, SQB>(a, lane, w * BETA_W, r);
+  }
+  // wave F, phase 1: alpha_0 .. alpha_{K/2}, alpha checkpoints 1 .. h - 1
+  MI_HD static void f1(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
+    const uint32_t h = a.K / (2 * BETA_W);
+    const size_t ck = (size_t)2 * a.K;
+#pragma unroll
+    for (int s = 0; s < 8; s++) al[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    pipe_windows<PF, Win>(
+        (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
+        [&](const Win& r, uint32_t w) {
+          if (w) p2_ck_store(a.scr, ck, w, lane, al);
+          if constexpr (MKQ) p2_alpha_only_window_mkq(a, lane, r, w * BETA_W, al);
+          else p2_alpha_only_window<DEC2, SQB>(a, r, w * BETA_W, al);
+        });
+  }
+  // wave F, phase 2: windows h .. nw - 1, LLRs of steps K/2 .. K - 1
+  MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8], uint32_t (&crc)[2]) {
+    const uint32_t nw = a.K / BETA_W, h = nw / 2;
+    const size_t ck = (size_t)2 * a.K;
+    pipe_windows<PF, Win>(
+        (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
+        [&](uint32_t w, Win& r) {
+          p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
+          p2_ck_load(a.scr, ck, w + 1, lane, r);
+        },
+        [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al, crc); });
+  }
+  // wave B, phase 1: tail, then beta_K .. beta_{K/2}, beta checkpoints h + 1 .. nw
+  MI_HD static void b1(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
+    const uint32_t K = a.K, nw = K / BETA_W, h = nw / 2;
+    const size_t ck = (size_t)2 * K;
+#pragma unroll
+    for (int s = 0; s < 8; s++) b[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    {
+      const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
+      P2 tx[3], tp[3];
+      if constexpr (MKQ) {
+        // all 12 tail inputs (both constituent codes) quantised into their q rows
+        const uint32_t ma = p2_wmask(a, 0, nw), mb = p2_wmask(a, 1, nw);
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+          const P2 q = q16_pair(p2_sb_in(a, 0, ma, 3 * K, j, lane), p2_sb_in(a, 1, mb, 3 * K, j, lane));
+          row_st(a.q, 3 * K, lane, p2_bits(q), j);
+          if (j < 6) { if (j & 1) tp[j / 2] = q; else tx[j / 2] = q; }
+        }
+      } else if constexpr (!SQB) {
+        const uint32_t ma = p2_wmask(a, 0, nw), mb = p2_wmask(a, 1, nw);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          const uint32_t d = t0 - 3 * K + 2 * j;
+          tx[j] = q16_pair(p2_sb_in(a, 0, ma, 3 * K, d, lane), p2_sb_in(a, 1, mb, 3 * K, d, lane));
+          tp[j] = q16_pair(p2_sb_in(a, 0, ma, 3 * K, d + 1, lane), p2_sb_in(a, 1, mb, 3 * K, d + 1, lane));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          tx[j] = p2_from_bits(row_ld(a.q, t0, lane, 2 * j));
+          tp[j] = p2_from_bits(row_ld(a.q, t0, lane, 2 * j + 1));
+        }
+      }
+#pragma unroll
+      for (int j = 2; j >= 0; j--) {
+        P2 nb[8];
+        beta_step<false>(b, tx[j], tp[j], nb);
+#pragma unroll
+        for (int s = 0; s < 8; s++) b[s] = nb[s];
+      }
+      norm8<true>(b);
+    }
+    p2_ck_store(a.scr, ck, nw, lane, b);
+    pipe_windows<PF, Win>(
+        (int)(nw - h), [nw](int i) { return nw - 1 - (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
+        [&](const Win& r, uint32_t w) {
+          if constexpr (MKQ) p2_beta_window_mkq(a, lane, r, w * BETA_W, b);
+          else p2_beta_window<DEC2, SQB>(a, r, w * BETA_W, b);
+          if (w > h) p2_ck_store(a.scr, ck, w, lane, b);
+        });
+  }
+  // wave B, phase 2: windows h - 1 .. 0 backward, LLRs of steps 0 .. K/2 - 1
+  MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8], uint32_t (&crc)[2]) {
+    const uint32_t h = a.K / (2 * BETA_W);
+    const size_t ck = (size_t)2 * a.K;
+    pipe_windows<PF, Win>(
+        (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
+        [&](uint32_t w, Win& r) {
+          p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
+          p2_ck_load(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
+        },
+        [&](const Win& r, uint32_t w) {
+          if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b, crc);
+          else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b, crc);
+        });
+  }
+};
+
+template <bool DEC2, bool FIRST, int SRC, class Exec>
+MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex, uint32_t (&cF)[2], uint32_t (&cB)[2]) {
+  using X = TdecP2X<DEC2, FIRST, SRC>;
+  P2 mF[8], mBs[8];
+  P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
+  ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
+  ex.run([&] { X::f2(a, lane, mF, cF); }, [&] { X::b2(a, lane, mB, cB); });
+}
+
+// pack half h's decisions MSB first and run its TB-payload bytes through the byte-wise CRC24A (the partial
+// TB-CRC register tb_kernel combines, tdec_body.h tdec_pack)
+MI_HD inline uint32_t tdec_p2_pack(const TdecArgsP2& a, int lane, int h) {
+  const uint32_t b0 = a.F[h] / 8, b1 = a.K / 8 - (a.crc24a[h] ? 0 : 3);
+  uint32_t tb = 0;
+  for (uint32_t j = 0; j < a.K / 8; j++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) v |= (uint32_t)((row_ld(a.dec, 8 * j + q, lane) >> h) & 1u) << (7 - q);
+    a.cb_bytes[h][j] = (uint8_t)v;
+    if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
+  }
+  return tb;
+}
+// both halves at once (one pass over the decision rows)
+MI_HD inline void tdec_p2_pack2(const TdecArgsP2& a, int lane, uint32_t (&tbp)[2]) {
+  uint32_t bl[2], bh[2], tb[2] = {0u, 0u};
+  for (int h = 0; h < 2; h++) { bl[h] = a.F[h] / 8; bh[h] = a.K / 8 - (a.crc24a[h] ? 0 : 3); }
+  for (uint32_t j = 0; j < a.K / 8; j++) {
+    uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t d = row_ld(a.dec, 8 * j + q, lane);
+      v0 |= (d & 1u) << (7 - q);
+      v1 |= ((d >> 1) & 1u) << (7 - q);
+    }
+    a.cb_bytes[0][j] = (uint8_t)v0;
+    a.cb_bytes[1][j] = (uint8_t)v1;
+    if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];
+    if (j >= bl[1] && j < bh[1]) tb[1] = ((tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[1] >> 16) ^ v1) & 0xFFu];
+  }
+  tbp[0] = tb[0];
+  tbp[1] = tb[1];
+}
+
+// the iteration loop (tdec_body.h tdec_lane_x's source-mode sequence) with per-code-block stopping.
+// ex.crc_combine2 XORs both waves' partial CRC registers of both halves; ex.pack_wave is true on the wave
+// that packs outputs (GPU: wave F after the iteration's barrier; host: always).
+template <class Exec>
+MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
+  TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
+  uint32_t active = a.live & 3u, packed = 0u;
+  for (uint32_t it = 0; it < a.max_its && active; it++) {
+    uint32_t cF[2] = {0u, 0u}, cB[2] = {0u, 0u};
+    constexpr uint32_t MK = MI_TDEC_MKQ_IT;
+    if (it == 0) {
+      if (MK == 0) {
+        tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex, cF, cB);
+        tdec_p2_xhalf<true, true, SRC_Q>(a, lane, ex, cF, cB);
+      } else {
+        tdec_p2_xhalf<false, true, SRC_SB>(a, lane, ex, cF, cB);
+        tdec_p2_xhalf<true, true, SRC_SB>(a, lane, ex, cF, cB);
+      }
+    } else if (it < MK) {
+      tdec_p2_xhalf<false, false, SRC_SB>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<true, false, SRC_SB>(a, lane, ex, cF, cB);
+    } else if (it == MK) {
+      tdec_p2_xhalf<false, false, SRC_MKQ>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex, cF, cB);
+    } else {
+      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex, cF, cB);
+    }
+    uint32_t c[2] = {cF[0] ^ cB[0], cF[1] ^ cB[1]};
+    ex.crc_combine2(c, lane);
+    uint32_t stop = 0u;
+    for (int h = 0; h < 2; h++) {
+      if (!((active >> h) & 1u)) continue;
+      r.its[h] = it + 1;
+      r.crc_ok[h] = c[h] == 0;
+      if ((a.early_stop && r.crc_ok[h]) || it + 1 == a.max_its) stop |= 1u << h;
+    }
+    active &= ~stop;
+    // a half that stops while its partner goes on is packed now (its partner's iterations rewrite the
+    // decision rows); halves that stop together are packed after the loop in one pass
+    if (stop && active && ex.pack_wave()) {
+      const int h = stop & 1u ? 0 : 1;
+      r.tb_part[h] = tdec_p2_pack(a, lane, h);
+      packed |= 1u << h;
+    }
+  }
+  if (ex.pack_wave()) {
+    const uint32_t rest = (a.live & 3u) & ~packed;
+    if (rest == 3u) {
+      tdec_p2_pack2(a, lane, r.tb_part);
+    } else {
+      for (int h = 0; h < 2; h++)
+        if ((rest >> h) & 1u) r.tb_part[h] = tdec_p2_pack(a, lane, h);
+    }
+  }
+  return r;
+}
+
+struct TdecP2ExecHost {
+  static constexpr bool SHARED = false;
+  template <class F, class B>
+  void run(F f, B b) { f(); b(); }
+  void crc_combine2(uint32_t (&)[2], int) {}
+  bool pack_wave() const { return true; }
+};
+
+}  // namespace mi

@@ -25,14 +25,17 @@ CASES = [  # nof_prb, ports, tbs, Qm, snr, sf, rv, cell
 ]
 
 
-@pytest.mark.parametrize("sched", ["lane", "x", "xr"])
+@pytest.mark.parametrize("sched", ["lane", "x", "xr", "p2"])
 @pytest.mark.parametrize("mode", ["gen", "i16"])
 @pytest.mark.parametrize("nprb,ports,tbs,qm,snr,sf,rv,cid", CASES)
 def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, sf, rv, cid, mode, sched):
     """Planner + rate de-matching + turbo (float gen or int16 SSE arithmetic) + TB assembly, emulated
     lane by lane on the host, against the oracle decoder of the same arithmetic.  sched "x": the
     crossed schedule (two wavefronts per group meeting in the middle of each half-iteration, phases
-    of both waves run in turn as the kernel's barriers order them); "xr": its recompute form."""
+    of both waves run in turn as the kernel's barriers order them); "xr": its recompute form; "p2": two code
+    blocks per lane in packed int16 (int16 arithmetic only; a single subframe leaves its groups unpaired)."""
+    if sched == "p2" and mode == "gen":
+        pytest.skip("the packed decoder is the int16 arithmetic")
     cfg = abi.sf_cfg(cell_id=cid, nof_prb=nprb, nof_ports=ports, sf_idx=sf, tbs=tbs, Qm=qm, rv=rv)
     tb = tb_bytes(sf, tbs)
     iq = abi.tx_subframe(cfg, tb, snr_db=snr, seed=sf + 7)
@@ -45,7 +48,7 @@ def test_emulated_kernels_bit_exact_vs_oracle(built, nprb, ports, tbs, qm, snr, 
     eok = np.zeros(1, np.uint32)
     eits = np.zeros(1, np.uint32)
     abi.emu().emu_set_tdec_i16(int(q16))
-    abi.emu().emu_set_tdec_x({"lane": 0, "x": 1, "xr": 2}[sched])
+    abi.emu().emu_set_tdec_x({"lane": 0, "x": 1, "xr": 2, "p2": 3}[sched])
     try:
         rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), 1, np.ascontiguousarray(llr).ctypes.data, 4,
                                       pe.ctypes.data, eok.ctypes.data, eits.ctypes.data, None)
@@ -115,3 +118,42 @@ def test_emulated_segment_parallel_turbo_bit_exact(built, nprb, ports, tbs, qm, 
     assert bool(eok[0]) == ok
     assert eits[0] == onoi
     assert np.array_equal(pe, opay)
+
+
+@pytest.mark.parametrize("snr0", [18.6, 30.0])
+def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0):
+    """The packed decoder (two code blocks per lane, tdec_p2_body.h) on a batch whose code blocks fill
+    PAIRED groups: 11 subframes of 20 MHz MCS-28 (143 code blocks of K = 5824: one pair + one unpaired
+    group) at per-subframe SNRs across the waterfall (code blocks of one lane stop at different
+    iterations, some never), plus a 1.4 MHz subframe (another K, unpaired); every TB against the
+    oracle's int16 decoder: payload, CRC verdict, iterations."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(11)]
+    cfgs.append(abi.sf_cfg(cell_id=301, nof_prb=6, sf_idx=2, tbs=4392, Qm=6))
+    snrs = [snr0 + 0.35 * (i % 5) for i in range(len(cfgs))]
+    iqs = [abi.tx_subframe(c, tb_bytes(60 + i, c.tbs), snr_db=snrs[i], seed=90 + i) for i, c in enumerate(cfgs)]
+    llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
+    arr = abi.cfg_array(cfgs)
+    n = len(cfgs)
+    offs = [abi.emu().emu_payload_offset(C.cast(arr, C.c_void_p), n, i) for i in range(n)]
+    pe = np.zeros(offs[-1] + cfgs[-1].tbs // 8, np.uint8)
+    eok = np.zeros(n, np.uint32)
+    eits = np.zeros(n, np.uint32)
+    cbits = np.zeros(64 * 4, np.uint32)
+    flat = np.concatenate(llrs).astype(np.float32)
+    abi.emu().emu_set_tdec_i16(1)
+    abi.emu().emu_set_tdec_x(3)
+    try:
+        rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
+                                      eok.ctypes.data, eits.ctypes.data, cbits.ctypes.data)
+    finally:
+        abi.emu().emu_set_tdec_i16(0)
+        abi.emu().emu_set_tdec_x(0)
+    assert rc == 0
+    for i, c in enumerate(cfgs):
+        with O.tdec_mode(O.TDEC_I16):
+            ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
+        assert bool(eok[i]) == ok, i
+        assert eits[i] == onoi, i
+        assert np.array_equal(pe[offs[i]:offs[i] + c.tbs // 8], opay), i
+    if snr0 < 20:
+        assert len(set(cbits[:143].tolist())) >= 3   # code blocks of one lane stopped at different iterations

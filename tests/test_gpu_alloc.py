@@ -101,7 +101,7 @@ def _run(cfgs, iqs, **kw):
     return b
 
 
-@pytest.mark.parametrize("sched", [None, "win"])
+@pytest.mark.parametrize("sched", [None, "win", "p2"])
 def test_partial_allocations_mixed_cells_match_oracle(sched):
     cfgs = _mix(4, 42)
     tbs = [tb_bytes(700 + i, c.tbs) for i, c in enumerate(cfgs)]
@@ -128,14 +128,15 @@ def test_partial_allocations_mixed_cells_match_oracle(sched):
     b.close()
 
 
-def test_headline_shape_at_scale_every_tb():
+@pytest.mark.parametrize("sched", [None, "p2"])
+def test_headline_shape_at_scale_every_tb(sched):
     """12,500 x (20 MHz TM1 MCS-28) in one batch: the schedule the bench times (5,080 wavefronts)."""
     n, pool = 12500, 64
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=(1, 2, 3, 4, 6, 7, 8, 9)[i % 8], tbs=75376, Qm=6, rnti=0x46)
             for i in range(n)]
-    b = abi.Batch(cfgs, max_its=4, tdec_i16=True)
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=True, sched=sched)
     assert abi.lib().mi_dl_batch_n_codeblocks(b.h) == 13 * n
-    assert abi.lib().mi_dl_batch_turbo_win(b.h) in (2, 3)           # the crossed lane schedule
+    assert b.turbo_sched == (sched or b.turbo_sched) and b.turbo_sched in ("lanex", "lanexr", "p2")
     L = 2 * abi.lib().mi_sf_len(100)
     assert b.iq_offset(1) * 2 == L and b.iq_samples * 2 == n * L
     # pool entry j is transmitted with sf_idx of subframe j (pool divides the 8-cycle)

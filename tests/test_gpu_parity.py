@@ -20,7 +20,8 @@ S_RM_TDEC_TB = (1 << 3) | (1 << 4) | (1 << 5)
 
 
 # turbo decoders: float (lane per code block), int16 lane per code block, int16 latency form
-DECODERS = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr")]
+DECODERS = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr"),
+            (True, "p2")]
 
 
 def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None, keep_llr=False):
@@ -124,6 +125,38 @@ def test_turbo_bit_exact_on_identical_llrs(snr, i16, sched):
         assert bool(crc[i]) == ok
         assert its[i] == onoi
         assert np.array_equal(b.payload(i, pay), opay)
+
+
+@pytest.mark.parametrize("sched", ["p2", "lanexr"])
+def test_turbo_bit_exact_paired_groups_waterfall(sched):
+    """Identical LLRs through a batch whose code blocks fill PAIRED groups (11 subframes of 20 MHz MCS-28:
+    143 code blocks of K = 5824 = one pair + one unpaired group for the two-code-blocks-per-lane decoder),
+    per-subframe SNRs across the waterfall so the two code blocks of a lane stop at different iterations:
+    payload, TB CRC and iterations == the oracle's int16 decoder, per code block iterations as well."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + (i % 4), tbs=75376, Qm=6, rnti=0x46 + i) for i in range(11)]
+    snrs = [18.4 + 0.4 * (i % 6) for i in range(11)]
+    iqs = [abi.tx_subframe(c, tb_bytes(i, c.tbs), snr_db=snrs[i], seed=300 + i) for i, c in enumerate(cfgs)]
+    b = abi.Batch(cfgs, max_its=6, tdec_i16=True, sched=sched)
+    assert b.turbo_sched == sched
+    llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
+    flat = np.zeros(b.download(abi.BUF_LLR, np.float32).shape, np.float32)
+    for i, l in enumerate(llrs):
+        o = b.offset(abi.BUF_LLR, i)
+        flat[o:o + len(l)] = l
+    b.upload(abi.BUF_LLR, flat)
+    b.run_stages(S_RM_TDEC_TB)
+    pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+    crc = b.download(abi.BUF_TB_CRC, np.uint32)
+    its = b.download(abi.BUF_TB_ITS, np.uint32)
+    cbits = b.download(abi.BUF_CB_ITS, np.uint32)
+    for i, c in enumerate(cfgs):
+        with O.tdec_mode(O.TDEC_I16):
+            ok, opay, onoi, _ = oracle_dlsch(c, llrs[i], max_its=6)
+        assert bool(crc[i]) == ok, i
+        assert its[i] == onoi, i
+        assert np.array_equal(b.payload(i, pay), opay), i
+    assert len(set(cbits[cbits > 0].tolist())) >= 3
+    b.close()
 
 
 def test_host_iq_pipeline_matches_batch():

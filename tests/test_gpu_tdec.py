@@ -25,7 +25,8 @@ def llr_bpsk(d, K, ebno_db, rng):
 
 
 # turbo schedules: float decoder (lane per code block), int16 lane per code block, int16 latency form
-MODES = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr")]
+MODES = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (True, "lanex"), (True, "lanexr"),
+         (True, "p2")]   # p2: two code blocks per lane (the 70 code blocks fill one group pair)
 
 
 @pytest.mark.parametrize("i16,sched", MODES)
