@@ -239,6 +239,11 @@ int Engine::tdec_crossed() const {
   if (flags & MI_DL_FLAG_TDEC_X) return form;
   if (flags & MI_DL_FLAG_TDEC_LANE) return 0;
   if (!q16()) return waves < 4ull * simds ? 1 : 0;   // float decoder: crossed below 2 groups per SIMD (measured)
+  // packed int16, two code blocks per lane: half the VALU per code block but half the wavefronts, so it
+  // pays once its wavefronts (2 per group pair) still cover every SIMD -- the headline (2.5 per SIMD:
+  // 7.68 vs 7.95 ms) and configs[0] (1 per SIMD, 8 iterations: 35.2 vs 36.6 ms); below that the per-wave
+  // chain dominates (configs[2], 0.2 per SIMD: 8.5 vs 6.1 ms; profiles/r2/ab_p2)
+  if (2ull * (plan.pairs.size() / 2) >= simds) return 3;
   return form;
 }
 

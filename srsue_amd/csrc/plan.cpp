@@ -32,6 +32,7 @@ void Plan::add_ktab(uint32_t K) {
   MiKTab t{K, ncb_of(K), 0, 0, 0, 0, 0};
   uint32_t* offs[5] = {&t.pos_off, &t.pi_off, &t.crca_off, &t.crcb_off, &t.ipos_off};
   for (int q = 0; q < 5; q++) {
+    while (kdata.size() % 4) kdata.push_back(0u);   // 16-B aligned tables (tdec_body.h pos_window)
     *offs[q] = (uint32_t)kdata.size();
     kdata.insert(kdata.end(), kp[q].begin(), kp[q].end());
   }

@@ -215,7 +215,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.crc8 = crc8;
   a.dec = dec + gA.dec_off;
   a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
-  a.cb_bytes[1] = out.cb_bytes + (size_t)li[(a.live >> 1) & 1u] * CB_BYTES_STRIDE;
+  a.cb_bytes[1] = out.cb_bytes + (size_t)((a.live & 2u) ? li[1] : li[0]) * CB_BYTES_STRIDE;
   a.K = K;
   a.F[0] = l0.F;
   a.F[1] = paired ? l1.F : l0.F;
@@ -226,6 +226,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xcrc};
   const TdecP2Result r = tdec_p2_lane(a, lane, ex);
   if (ex.wave) return;
+#pragma unroll
   for (int h = 0; h < 2; h++) {
     if (!((a.live >> h) & 1u)) continue;
     out.its[li[h]] = r.its[h];

@@ -286,12 +286,40 @@ MI_HD inline uint32_t wmask(const TdecArgs& a, uint32_t w) { return a.wm[w]; }
 #ifndef MI_SB_ZROW_I16
 #define MI_SB_ZROW_I16 1
 #endif
+// The 12 position-table entries of window inputs t0 .. t0 + 11 (t0 = 12 w; the tail's 12 inputs start at
+// 3 K = 12 (K / 4)), loaded together as three 128-bit scalar loads (Plan::add_ktab aligns every table to 16
+// B).  Loaded one by one, each entry feeds only a select and the backend turns the select into a scalar
+// branch around a lone scalar load and a full wait -- 12 serialised table loads per window and group.
+struct PosW { uint32_t v[12]; };
+MI_HD inline PosW pos_window(const uint32_t* pos, uint32_t t0) {
+  PosW P;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MI_TDEC_DIAG_NOTAB)
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(4))) u4 cu4;
+  cu4* q = (cu4*)(pos + t0);
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const u4 x = q[j];
+    P.v[4 * j] = x.x; P.v[4 * j + 1] = x.y; P.v[4 * j + 2] = x.z; P.v[4 * j + 3] = x.w;
+  }
+#else
+  for (int j = 0; j < 12; j++) P.v[j] = pos[t0 + j];
+#endif
+  return P;
+}
+#if defined(MI_TDEC_DIAG_NOTAB)
+#define MI_POSW(a, t0) PosW{{MI_POS(a, t0), MI_POS(a, t0 + 1), MI_POS(a, t0 + 2), MI_POS(a, t0 + 3), MI_POS(a, t0 + 4), \
+                             MI_POS(a, t0 + 5), MI_POS(a, t0 + 6), MI_POS(a, t0 + 7), MI_POS(a, t0 + 8), MI_POS(a, t0 + 9), \
+                             MI_POS(a, t0 + 10), MI_POS(a, t0 + 11)}}
+#else
+#define MI_POSW(a, t0) pos_window((a).pos, t0)
+#endif
 template <bool Q16>
-MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
+MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, const PosW& P, uint32_t dt, int lane) {
   const bool on = (m >> dt) & 1u;
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
   if constexpr (!(Q16 ? MI_SB_ZROW_I16 : MI_SB_ZROW_GEN)) {
-    const uint32_t so = MI_POS(a, t0 + dt) * (uint32_t)(LANES * sizeof(float));
+    const uint32_t so = P.v[dt] * (uint32_t)(LANES * sizeof(float));
     const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb), vo, so, 0));
   }
@@ -299,38 +327,41 @@ MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt
 #if defined(MI_TDEC_DIAG_Q16SB)   // timing diagnostic only: int16-wide softbuffer reads (wrong values)
   if constexpr (Q16)
     return __builtin_bit_cast(float, (uint32_t)(uint16_t)row_ld(reinterpret_cast<const int16_t*>(a.sb),
-                                                                  on ? MI_POS(a, t0 + dt) : a.zrow, lane));
+                                                                  on ? P.v[dt] : a.zrow, lane));
 #endif
-  return row_ld(a.sb, on ? MI_POS(a, t0 + dt) : a.zrow, lane);
+  return row_ld(a.sb, on ? P.v[dt] : a.zrow, lane);
 }
 
 // raw decoder input t (= 3k + i): softbuffer float at position pos[t], or the int16 q row t
 template <bool Q16>
-MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
+MI_HD inline typename TdecWin<Q16>::R dec_in(const TdecArgs& a, uint32_t m, const PosW& P, uint32_t t0, uint32_t dt,
+                                             int lane) {
   if constexpr (Q16) return (int32_t)row_ld(a.q16, t0, lane, dt);
-  else return sb_in<Q16>(a, m, t0, dt, lane);
+  else return sb_in<Q16>(a, m, P, dt, lane);
 }
 
 template <bool DEC2, bool FIRST, bool Q16, bool SQ>
 MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
   const float* llr1 = scr_at<Q16>(a.scr, a.K);
   const uint32_t m = (Q16 && SQ) ? 0u : wmask(a, base / BETA_W);
+  PosW P{};
+  if constexpr (!(Q16 && SQ)) P = MI_POSW(a, 3 * base);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
     if (!DEC2) {
       if constexpr (Q16 && !SQ) {
-        r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i, lane);
-        r.f1[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
+        r.f0[i] = sb_in<Q16>(a, m, P, 3 * i, lane);
+        r.f1[i] = sb_in<Q16>(a, m, P, 3 * i + 1, lane);
       } else {
-        r.s0[i] = dec_in<Q16>(a, m, 3 * base, 3 * i, lane);
-        r.s1[i] = dec_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
+        r.s0[i] = dec_in<Q16>(a, m, P, 3 * base, 3 * i, lane);
+        r.s1[i] = dec_in<Q16>(a, m, P, 3 * base, 3 * i + 1, lane);
       }
       r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
     } else {
       const uint32_t pk = MI_PI(a, k);
-      if constexpr (Q16 && !SQ) r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
-      else r.s0[i] = dec_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
+      if constexpr (Q16 && !SQ) r.f0[i] = sb_in<Q16>(a, m, P, 3 * i + 2, lane);
+      else r.s0[i] = dec_in<Q16>(a, m, P, 3 * base, 3 * i + 2, lane);
       r.r0[i] = scr_raw<Q16>(llr1, pk, lane);
       r.r1[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, pk, lane);
     }
@@ -343,11 +374,12 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
 template <bool FIRST, bool Q16>
 MI_HD inline void tdec_load_window_sb(const TdecArgs& a, int lane, uint32_t base, TdecWin<Q16>& r) {
   const uint32_t m = wmask(a, base / BETA_W);
+  const PosW P = MI_POSW(a, 3 * base);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
-    r.f0[i] = sb_in<Q16>(a, m, 3 * base, 3 * i, lane);
-    r.f1[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 1, lane);
-    r.f2[i] = sb_in<Q16>(a, m, 3 * base, 3 * i + 2, lane);
+    r.f0[i] = sb_in<Q16>(a, m, P, 3 * i, lane);
+    r.f1[i] = sb_in<Q16>(a, m, P, 3 * i + 1, lane);
+    r.f2[i] = sb_in<Q16>(a, m, P, 3 * i + 2, lane);
     r.r0[i] = FIRST ? 0 : scr_raw<Q16>(a.scr, base, lane, i);
   }
 }
@@ -548,12 +580,13 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   for (int s = 0; s < 8; s++) b[s] = s ? NINF : 0.0f;
   {
     const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0), tm = (Q16 && SQB) ? 0u : wmask(a, nw);
+    const PosW PT = MI_POSW(a, 3 * K);   // unused (and not loaded) when the tail comes from q rows
     float tx[3], tp[3];
     if constexpr (MKQ) {
       // all 12 tail inputs (both constituent codes) quantised into their q rows
       float tq[12];
 #pragma unroll
-      for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, 3 * K, j, lane));
+      for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, PT, j, lane));
 #pragma unroll
       for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
 #pragma unroll
@@ -561,14 +594,14 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
     } else if constexpr (Q16 && !SQB) {
 #pragma unroll
       for (int j = 0; j < 3; j++) {
-        tx[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
-        tp[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+        tx[j] = q16f(sb_in<Q16>(a, tm, PT, t0 - 3 * K + 2 * j, lane));
+        tp[j] = q16f(sb_in<Q16>(a, tm, PT, t0 - 3 * K + 2 * j + 1, lane));
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 3; j++) {
-        tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
-        tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+        tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, PT, 3 * K, t0 - 3 * K + 2 * j, lane));
+        tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, PT, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
       }
     }
 #pragma unroll
@@ -991,11 +1024,12 @@ struct TdecX {
     for (int s = 0; s < 8; s++) b[s] = s ? -INFINITY : 0.0f;
     {
       const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0), tm = SQB ? 0u : wmask(a, nw);
+      const PosW PT = MI_POSW(a, 3 * K);
       float tx[3], tp[3];
       if constexpr (MKQ) {
         float tq[12];
 #pragma unroll
-        for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, 3 * K, j, lane));
+        for (int j = 0; j < 12; j++) tq[j] = q16f(sb_in<Q16>(a, tm, PT, j, lane));
 #pragma unroll
         for (int j = 0; j < 12; j++) row_st(a.q16, 3 * K, lane, (int16_t)tq[j], j);
 #pragma unroll
@@ -1003,14 +1037,14 @@ struct TdecX {
       } else if constexpr (Q16 && !SQB) {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-          tx[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
-          tp[j] = q16f(sb_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+          tx[j] = q16f(sb_in<Q16>(a, tm, PT, t0 - 3 * K + 2 * j, lane));
+          tp[j] = q16f(sb_in<Q16>(a, tm, PT, t0 - 3 * K + 2 * j + 1, lane));
         }
       } else {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-          tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j, lane));
-          tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
+          tx[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, PT, 3 * K, t0 - 3 * K + 2 * j, lane));
+          tp[j] = scr_cvt<Q16>(dec_in<Q16>(a, tm, PT, 3 * K, t0 - 3 * K + 2 * j + 1, lane));
         }
       }
 #pragma unroll

@@ -74,15 +74,17 @@ struct TdecWinP2 {
 };
 
 MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
-MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, uint32_t t0, uint32_t dt, int lane) {
+MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
   const bool on = (m >> dt) & 1u;
-  return row_ld(a.sb[h], on ? MI_POS(a, t0 + dt) : a.zrow[h], lane);
+  return row_ld(a.sb[h], on ? P.v[dt] : a.zrow[h], lane);   // tdec_body.h sb_in
 }
 
 template <bool DEC2, bool FIRST, bool SQ>
 MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
   const uint32_t* llr1 = a.scr + (size_t)a.K * LANES;
   const uint32_t ma = SQ ? 0u : p2_wmask(a, 0, base / BETA_W), mb = SQ ? 0u : p2_wmask(a, 1, base / BETA_W);
+  PosW P{};
+  if constexpr (!SQ) P = MI_POSW(a, 3 * base);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
     const uint32_t k = base + i;
@@ -91,10 +93,10 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
         r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i);
         r.s1[i] = row_ld(a.q, 3 * base, lane, 3 * i + 1);
       } else {
-        r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i, lane);
-        r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i, lane);
-        r.a1[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 1, lane);
-        r.b1[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 1, lane);
+        r.a0[i] = p2_sb_in(a, 0, ma, P, 3 * i, lane);
+        r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i, lane);
+        r.a1[i] = p2_sb_in(a, 0, ma, P, 3 * i + 1, lane);
+        r.b1[i] = p2_sb_in(a, 1, mb, P, 3 * i + 1, lane);
       }
       r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
     } else {
@@ -102,8 +104,8 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
       if constexpr (SQ) {
         r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i + 2);
       } else {
-        r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 2, lane);
-        r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 2, lane);
+        r.a0[i] = p2_sb_in(a, 0, ma, P, 3 * i + 2, lane);
+        r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i + 2, lane);
       }
       r.r0[i] = row_ld(llr1, pk, lane);
       r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
@@ -113,14 +115,15 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
 template <bool FIRST>
 MI_HD inline void p2_load_window_mkq(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
   const uint32_t ma = p2_wmask(a, 0, base / BETA_W), mb = p2_wmask(a, 1, base / BETA_W);
+  const PosW P = MI_POSW(a, 3 * base);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) {
-    r.a0[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i, lane);
-    r.b0[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i, lane);
-    r.a1[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 1, lane);
-    r.b1[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 1, lane);
-    r.a2[i] = p2_sb_in(a, 0, ma, 3 * base, 3 * i + 2, lane);
-    r.b2[i] = p2_sb_in(a, 1, mb, 3 * base, 3 * i + 2, lane);
+    r.a0[i] = p2_sb_in(a, 0, ma, P, 3 * i, lane);
+    r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i, lane);
+    r.a1[i] = p2_sb_in(a, 0, ma, P, 3 * i + 1, lane);
+    r.b1[i] = p2_sb_in(a, 1, mb, P, 3 * i + 1, lane);
+    r.a2[i] = p2_sb_in(a, 0, ma, P, 3 * i + 2, lane);
+    r.b2[i] = p2_sb_in(a, 1, mb, P, 3 * i + 2, lane);
     r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
   }
 }
@@ -330,13 +333,16 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
 #ifndef MI_TDEC_P2_PF_Q
 #define MI_TDEC_P2_PF_Q 1
 #endif
+#ifndef MI_TDEC_P2_PF_SB
+#define MI_TDEC_P2_PF_SB MI_TDEC_PF_SB
+#endif
 // the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
 template <bool DEC2, bool FIRST, int SRC>
 struct TdecP2X {
   static constexpr bool MKQ = !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = SRC == SRC_Q;    // backward-side passes read q rows
   static constexpr bool SQF = SRC != SRC_SB;   // forward-side passes read q rows
-  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_P2_PF_Q;
+  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_P2_PF_SB : MI_TDEC_P2_PF_Q;
   using Win = TdecWinP2;
 
   MI_HD static void load1(const TdecArgsP2& a, int lane, uint32_t w, Win& r) {
@@ -381,19 +387,21 @@ struct TdecP2X {
       if constexpr (MKQ) {
         // all 12 tail inputs (both constituent codes) quantised into their q rows
         const uint32_t ma = p2_wmask(a, 0, nw), mb = p2_wmask(a, 1, nw);
+        const PosW PT = MI_POSW(a, 3 * K);
 #pragma unroll
         for (int j = 0; j < 12; j++) {
-          const P2 q = q16_pair(p2_sb_in(a, 0, ma, 3 * K, j, lane), p2_sb_in(a, 1, mb, 3 * K, j, lane));
+          const P2 q = q16_pair(p2_sb_in(a, 0, ma, PT, j, lane), p2_sb_in(a, 1, mb, PT, j, lane));
           row_st(a.q, 3 * K, lane, p2_bits(q), j);
           if (j < 6) { if (j & 1) tp[j / 2] = q; else tx[j / 2] = q; }
         }
       } else if constexpr (!SQB) {
         const uint32_t ma = p2_wmask(a, 0, nw), mb = p2_wmask(a, 1, nw);
+        const PosW PT = MI_POSW(a, 3 * K);
 #pragma unroll
         for (int j = 0; j < 3; j++) {
           const uint32_t d = t0 - 3 * K + 2 * j;
-          tx[j] = q16_pair(p2_sb_in(a, 0, ma, 3 * K, d, lane), p2_sb_in(a, 1, mb, 3 * K, d, lane));
-          tp[j] = q16_pair(p2_sb_in(a, 0, ma, 3 * K, d + 1, lane), p2_sb_in(a, 1, mb, 3 * K, d + 1, lane));
+          tx[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d, lane), p2_sb_in(a, 1, mb, PT, d, lane));
+          tp[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d + 1, lane), p2_sb_in(a, 1, mb, PT, d + 1, lane));
         }
       } else {
 #pragma unroll
@@ -446,16 +454,19 @@ MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex, uint32_
   ex.run([&] { X::f2(a, lane, mF, cF); }, [&] { X::b2(a, lane, mB, cB); });
 }
 
-// pack half h's decisions MSB first and run its TB-payload bytes through the byte-wise CRC24A (the partial
-// TB-CRC register tb_kernel combines, tdec_body.h tdec_pack)
-MI_HD inline uint32_t tdec_p2_pack(const TdecArgsP2& a, int lane, int h) {
-  const uint32_t b0 = a.F[h] / 8, b1 = a.K / 8 - (a.crc24a[h] ? 0 : 3);
+// pack half H's decisions MSB first and run its TB-payload bytes through the byte-wise CRC24A (the partial
+// TB-CRC register tb_kernel combines, tdec_body.h tdec_pack).  H is a template parameter: a run-time index
+// into the argument struct's arrays would force the struct into private memory on the GPU.
+template <int H>
+MI_HD inline uint32_t tdec_p2_pack(const TdecArgsP2& a, int lane) {
+  const uint32_t b0 = a.F[H] / 8, b1 = a.K / 8 - (a.crc24a[H] ? 0 : 3);
+  uint8_t* out = a.cb_bytes[H];
   uint32_t tb = 0;
   for (uint32_t j = 0; j < a.K / 8; j++) {
     uint32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) v |= (uint32_t)((row_ld(a.dec, 8 * j + q, lane) >> h) & 1u) << (7 - q);
-    a.cb_bytes[h][j] = (uint8_t)v;
+    for (int q = 0; q < 8; q++) v |= (uint32_t)((row_ld(a.dec, 8 * j + q, lane) >> H) & 1u) << (7 - q);
+    out[j] = (uint8_t)v;
     if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
   }
   return tb;
@@ -463,6 +474,7 @@ MI_HD inline uint32_t tdec_p2_pack(const TdecArgsP2& a, int lane, int h) {
 // both halves at once (one pass over the decision rows)
 MI_HD inline void tdec_p2_pack2(const TdecArgsP2& a, int lane, uint32_t (&tbp)[2]) {
   uint32_t bl[2], bh[2], tb[2] = {0u, 0u};
+#pragma unroll
   for (int h = 0; h < 2; h++) { bl[h] = a.F[h] / 8; bh[h] = a.K / 8 - (a.crc24a[h] ? 0 : 3); }
   for (uint32_t j = 0; j < a.K / 8; j++) {
     uint32_t v0 = 0, v1 = 0;
@@ -512,6 +524,7 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     uint32_t c[2] = {cF[0] ^ cB[0], cF[1] ^ cB[1]};
     ex.crc_combine2(c, lane);
     uint32_t stop = 0u;
+#pragma unroll
     for (int h = 0; h < 2; h++) {
       if (!((active >> h) & 1u)) continue;
       r.its[h] = it + 1;
@@ -522,9 +535,9 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     // a half that stops while its partner goes on is packed now (its partner's iterations rewrite the
     // decision rows); halves that stop together are packed after the loop in one pass
     if (stop && active && ex.pack_wave()) {
-      const int h = stop & 1u ? 0 : 1;
-      r.tb_part[h] = tdec_p2_pack(a, lane, h);
-      packed |= 1u << h;
+      if (stop & 1u) r.tb_part[0] = tdec_p2_pack<0>(a, lane);
+      else r.tb_part[1] = tdec_p2_pack<1>(a, lane);
+      packed |= stop;
     }
   }
   if (ex.pack_wave()) {
@@ -532,8 +545,8 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     if (rest == 3u) {
       tdec_p2_pack2(a, lane, r.tb_part);
     } else {
-      for (int h = 0; h < 2; h++)
-        if ((rest >> h) & 1u) r.tb_part[h] = tdec_p2_pack(a, lane, h);
+      if (rest & 1u) r.tb_part[0] = tdec_p2_pack<0>(a, lane);
+      if (rest & 2u) r.tb_part[1] = tdec_p2_pack<1>(a, lane);
     }
   }
   return r;

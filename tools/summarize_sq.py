@@ -18,8 +18,8 @@ def main(d):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mi::", "").split("<")[0]
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print("| kernel | waves | VALU instr / wave | SALU / wave | VMEM rd / wave | VMEM wr / wave | "
-          "active % | issue-stall % | parked (s_waitcnt) % | VALU busy % |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+          "active % | issue-stall % | parked (s_waitcnt) % | VALU busy % | VMEM LEVEL / instr | SMEM LEVEL / instr |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for k, v in acc.items():
         if not k.startswith(("tdec", "rm_", "demap", "ofdm", "chest", "tb_")):
             continue
@@ -30,9 +30,12 @@ def main(d):
         park = wc - act - stall
         cyc = m.get("GRBM_GUI_ACTIVE", 0) / 8 or 1
         busy = 100 * m.get("SQ_INSTS_VALU", 0) * 2 / (1024 * cyc)
+        # SQ_INST_LEVEL_* accumulate in-flight instructions per sample: / instructions ~ mean latency (counter units)
+        vlat = m["SQ_INST_LEVEL_VMEM"] / m["SQ_INSTS_VMEM"] if m.get("SQ_INSTS_VMEM") else float("nan")
+        slat = m["SQ_INST_LEVEL_SMEM"] / m["SQ_INSTS_SMEM"] if m.get("SQ_INSTS_SMEM") else float("nan")
         print(f"| {k} | {w:.0f} | {m.get('SQ_INSTS_VALU', 0) / w:.0f} | {m.get('SQ_INSTS_SALU', 0) / w:.0f} | "
               f"{m.get('SQ_INSTS_VMEM_RD', 0) / w:.0f} | {m.get('SQ_INSTS_VMEM_WR', 0) / w:.0f} | "
-              f"{100 * act / wc:.1f} | {100 * stall / wc:.1f} | {100 * park / wc:.1f} | {busy:.1f} |")
+              f"{100 * act / wc:.1f} | {100 * stall / wc:.1f} | {100 * park / wc:.1f} | {busy:.1f} | {vlat:.0f} | {slat:.0f} |")
 
 
 if __name__ == "__main__":
