@@ -38,16 +38,26 @@ void launch_phich(const float2* grid, const float2* ce, const MiCtrlSf* sfs, con
 
 struct DciFound { uint32_t found, format, nbits, L, ncce; uint8_t bits[DCI_MAX_BITS]; };
 
-struct CtrlEngine {
+// the tables one build produces (a parked copy can be swapped back in: the per-TTI API's memo, ue_dl.cpp)
+struct CtrlTables {
   std::vector<MiCtrlSf> sfs;
   std::vector<uint32_t> cdata;
   std::vector<MiDciJob> jobs;
   std::vector<uint8_t> job_fmt;      // per job: bit 2 = common space; bits 0-1: 0 = 0/1A size, DCI_1, DCI_1C
   std::vector<uint32_t> job_begin;   // per subframe: jobs [job_begin[s], job_begin[s+1]) in search order
   std::vector<uint32_t> nof_prb;     // per subframe
-  DevBuf d_sfs, d_cdata, d_llr, d_jobs, d_res, d_cfi, d_phich;
+  DevBuf d_sfs, d_cdata, d_jobs;
   size_t llr_floats = 0;
   uint32_t max_regs = 0;
+  void swap_tables(CtrlTables& o) {
+    sfs.swap(o.sfs); cdata.swap(o.cdata); jobs.swap(o.jobs); job_fmt.swap(o.job_fmt); job_begin.swap(o.job_begin);
+    nof_prb.swap(o.nof_prb); d_sfs.swap(o.d_sfs); d_cdata.swap(o.d_cdata); d_jobs.swap(o.d_jobs);
+    std::swap(llr_floats, o.llr_floats); std::swap(max_regs, o.max_regs);
+  }
+};
+
+struct CtrlEngine : CtrlTables {
+  DevBuf d_llr, d_res, d_cfi, d_phich;
   std::vector<MiDciRes> res;         // host copy after download
   // plan over the subframes of P (cells, grid / ce layout) with per-subframe CFI and RNTI; phich: per
   // subframe the PHICH query I_lowest | n_dmrs << 16 (36.213 9.1.2), empty = (0, 0)

@@ -41,6 +41,10 @@ void DevBuf::release() {
 }
 
 Engine::~Engine() {
+  if (stage_done) {
+    (void)hipEventSynchronize(stage_done);
+    (void)hipEventDestroy(stage_done);
+  }
   if (h_stage) (void)hipHostFree(h_stage);
   for (auto& set : ev_sets)
     for (auto& e : set) (void)hipEventDestroy(e);
@@ -53,17 +57,27 @@ static bool up(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
   return hip_ok(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st), "upload");
 }
 
-int Engine::upload(hipStream_t st, bool alloc_sb) {
+namespace {
+struct Tab { DevBuf* dst; const void* src; size_t bytes; };
+size_t tab_span(size_t bytes) { return (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255; }
+}  // namespace
+
+// the descriptor tables of the current plan, in arena order
+#define MI_ENGINE_TABS(P)                                                                                           \
+  auto tab = [](DevBuf& d, const auto& v) { return Tab{&d, v.data(), v.size() * sizeof(v[0])}; };                   \
+  const Tab tabs[] = {tab(d_cells, P.cells), tab(d_crs, P.crs), tab(d_pds, P.pds), tab(d_re, P.re_tab),              \
+                      tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),   \
+                      tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),      \
+                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items),         \
+                      tab(d_pairs, P.pairs)}
+
+int Engine::stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t st) {
   const Plan& P = plan;
-  struct Tab { DevBuf* dst; const void* src; size_t bytes; };
-  auto tab = [](DevBuf& d, const auto& v) { return Tab{&d, v.data(), v.size() * sizeof(v[0])}; };
-  const Tab tabs[] = {tab(d_cells, P.cells), tab(d_crs, P.crs), tab(d_pds, P.pds), tab(d_re, P.re_tab),
-                      tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),
-                      tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),
-                      tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items),
-                      tab(d_pairs, P.pairs)};
+  MI_ENGINE_TABS(P);
   size_t total = 0;
-  for (const Tab& t : tabs) total += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
+  for (const Tab& t : tabs) total += tab_span(t.bytes);
+  // the previous DMA out of the staging buffer must be done before it is rewritten
+  if (stage_done && !hip_ok(hipEventSynchronize(stage_done), "stage wait")) return -1;
   if (total > h_stage_bytes) {
     if (h_stage) (void)hipHostFree(h_stage);
     h_stage = nullptr;
@@ -71,18 +85,34 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
     if (!hip_ok(hipHostMalloc(&h_stage, total, hipHostMallocDefault), "hipHostMalloc tables")) return -1;
     h_stage_bytes = total;
   }
-  if (total > d_tables.bytes) {
-    for (const Tab& t : tabs) t.dst->release();   // views into the old arena
-    if (!d_tables.ensure(total)) return -1;
+  if (total > arena.bytes || arena.view) {
+    if (&arena == &d_tables)
+      for (const Tab& t : tabs) t.dst->release();   // views into the old arena
+    if (!arena.ensure(total)) return -1;
   }
+  offs.clear();
   size_t off = 0;
   for (const Tab& t : tabs) {
     if (t.bytes) memcpy(static_cast<char*>(h_stage) + off, t.src, t.bytes);
-    t.dst->set_view(static_cast<char*>(d_tables.p) + off, std::max<size_t>(t.bytes, 1));
-    off += (std::max<size_t>(t.bytes, 1) + 255) & ~(size_t)255;
+    offs.push_back(off);
+    off += tab_span(t.bytes);
   }
-  bool ok = hip_ok(hipMemcpyAsync(d_tables.p, h_stage, total, hipMemcpyHostToDevice, st), "upload tables");
-  if (!ok) return -1;
+  if (!stage_done && !hip_ok(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "event")) return -1;
+  return hip_ok(hipMemcpyAsync(arena.p, h_stage, total, hipMemcpyHostToDevice, st), "upload tables") &&
+                 hip_ok(hipEventRecord(stage_done, st), "event")
+             ? 0
+             : -1;
+}
+
+void Engine::bind_tables(const DevBuf& arena, const std::vector<size_t>& offs) {
+  const Plan& P = plan;
+  MI_ENGINE_TABS(P);
+  for (size_t i = 0; i < sizeof(tabs) / sizeof(tabs[0]); i++)
+    tabs[i].dst->set_view(static_cast<char*>(arena.p) + offs[i], std::max<size_t>(tabs[i].bytes, 1));
+}
+
+int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
+  const Plan& P = plan;
   // twiddles per FFT size (double precision on the host)
   bool need_tw = false;
   for (auto& fl : P.fft_lists) need_tw |= !tw_off.count(fl.first);
@@ -96,10 +126,10 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
         tw.push_back((float)sin(-2.0 * M_PI * t / N));
       }
     }
-    if (!up(d_tw, tw, st)) return -1;
+    if (!up(d_tw, tw, st) || !hip_ok(hipStreamSynchronize(st), "twiddles")) return -1;
   }
   const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
-  ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
+  bool ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
   if (P.has_pdsch || P.cb_n) {
     ok = ok && d_e.ensure(P.e_floats * 4) && d_wm.ensure(P.groups.size() * WM_STRIDE * 4) &&
          d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
@@ -113,6 +143,52 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
     }
   }
   return ok ? 0 : -1;
+}
+
+int Engine::upload(hipStream_t st, bool alloc_sb) {
+  // a plain plan.build() over an active memo entry overwrote that entry's (swapped-in) plan: drop the entry
+  if (memo_active >= 0) {
+    (void)hipStreamSynchronize(st);
+    memo.erase(memo.begin() + memo_active);
+    memo_active = -1;
+  }
+  std::vector<size_t> offs;
+  if (stage_tables(d_tables, offs, st)) return -1;
+  bind_tables(d_tables, offs);
+  return ensure_work(st, alloc_sb);
+}
+
+int Engine::plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, hipStream_t st) {
+  std::string key(reinterpret_cast<const char*>(cfgs), sizeof(mi_dl_sf_cfg_t) * n);
+  key.push_back(with_pdsch ? 'P' : 'F');
+  // park the active entry's plan back in its slot
+  if (memo_active >= 0) std::swap(static_cast<PlanData&>(plan), memo[(size_t)memo_active]->plan);
+  memo_active = -1;
+  int hit = -1;
+  for (size_t i = 0; i < memo.size(); i++)
+    if (memo[i]->key == key) { hit = (int)i; break; }
+  if (hit < 0) {
+    if (plan.build(cfgs, n, with_pdsch)) return -1;
+    if (memo.size() >= MEMO_MAX) {   // evict the least recently used entry
+      size_t lru = 0;
+      for (size_t i = 1; i < memo.size(); i++)
+        if (memo[i]->used < memo[lru]->used) lru = i;
+      (void)hipStreamSynchronize(st);   // its arena may still be read by this stream's kernels
+      memo.erase(memo.begin() + (ptrdiff_t)lru);
+    }
+    memo.push_back(std::make_unique<PlanMemo>());
+    hit = (int)memo.size() - 1;
+    PlanMemo& e = *memo[(size_t)hit];
+    e.key = key;
+    if (stage_tables(e.arena, e.offs, st)) { memo.pop_back(); return -1; }
+    std::swap(static_cast<PlanData&>(plan), e.plan);   // park, then activate below
+  }
+  PlanMemo& e = *memo[(size_t)hit];
+  std::swap(static_cast<PlanData&>(plan), e.plan);
+  memo_active = hit;
+  e.used = ++memo_clock;
+  bind_tables(e.arena, e.offs);
+  return ensure_work(st, false);
 }
 
 int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_override) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <memory>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -20,6 +21,10 @@ struct DevBuf {
   bool ensure(size_t n);   // grow-only
   void release();
   void set_view(void* ptr, size_t n) { release(); p = ptr; bytes = n; view = true; }
+  void swap(DevBuf& o) { std::swap(p, o.p); std::swap(bytes, o.bytes); std::swap(view, o.view); }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
@@ -50,6 +55,25 @@ struct Engine {
   const uint32_t* rm_items() const { return plan.rm_items.empty() ? nullptr : d_rmitems.as<uint32_t>(); }
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
+  hipEvent_t stage_done = nullptr;   // the last DMA out of h_stage (waited for before h_stage is rewritten)
+  // Per-TTI plan memo (the srsLTE per-TTI API re-plans every call; srsUE cycles through the same few
+  // configurations -- one per subframe index and stage): a configuration planned before is re-activated
+  // by swapping its parked plan in and pointing the table views at its own device arena, instead of
+  // rebuilding and re-uploading the tables.  Entries hold the plan data, the arena and the table offsets.
+  struct PlanMemo {
+    std::string key;
+    PlanData plan;
+    DevBuf arena;
+    std::vector<size_t> offs;
+    uint64_t used = 0;
+  };
+  std::vector<std::unique_ptr<PlanMemo>> memo;
+  int memo_active = -1;
+  uint64_t memo_clock = 0;
+  static constexpr size_t MEMO_MAX = 32;
+  // build + upload of the plan of cfgs unless memoised (alloc_sb = false: the per-TTI API's external
+  // softbuffer); 0 on success
+  int plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, hipStream_t st);
   hipStream_t last_stream = nullptr;
   // profiling: one event set per run since the last reset (MI_DL_FLAG_PROFILE)
   std::vector<std::vector<hipEvent_t>> ev_sets;
@@ -58,6 +82,11 @@ struct Engine {
 
   ~Engine();
   int upload(hipStream_t st, bool alloc_sb);
+  // upload() in parts: the descriptor tables packed into `arena` with one DMA (offsets per table), the
+  // table views pointed into an arena, and the work buffers / twiddles sized for the current plan
+  int stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t st);
+  void bind_tables(const DevBuf& arena, const std::vector<size_t>& offs);
+  int ensure_work(hipStream_t st, bool alloc_sb);
   // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.
   int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override);
   // raw code-block decoding: scatter d into the softbuffer layout, then the turbo kernel

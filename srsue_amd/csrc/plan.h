@@ -15,7 +15,9 @@ namespace mi {
 void set_error(const std::string& s);
 const char* last_error();
 
-struct Plan {
+// Everything a build produces (what the kernels' tables and launch sizes come from).  Kept apart from the
+// planner's lookup caches so that a built plan can be parked and re-activated by a swap (Engine::plan_memo).
+struct PlanData {
   std::vector<MiCellDesc> cells;
   std::vector<float> crs;                 // float2 pairs
   std::vector<MiPdschDesc> pds;
@@ -33,7 +35,6 @@ struct Plan {
   // [2p] = group A, [2p + 1] = group B or 0xFFFFFFFF; a pair's decoder scratch spans both groups' regions
   // (consecutive), an unpaired group is followed by one group's worth of padding
   std::vector<uint32_t> pairs;
-  void build_pairs();
   std::vector<MiKTab> ktabs;
   std::vector<uint32_t> kdata;
   std::vector<MiTbDesc> tbs;
@@ -49,7 +50,11 @@ struct Plan {
   // algorithmic byte counts
   double bytes_compulsory = 0;
   double stage_bytes[MI_DL_NSTAGES] = {0};
+  uint32_t cb_K = 0, cb_n = 0;
+};
 
+struct Plan : PlanData {
+  void build_pairs();
   // cached per-key tables (kept across rebuilds)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<float>> crs_cache;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::vector<uint32_t>> scr_cache;
@@ -61,7 +66,6 @@ struct Plan {
   int build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool has_pdsch);
   // raw code-block mode (srslte_tdec_* contract): n_cb blocks of size K, no PHY front end
   int build_codeblocks(uint32_t K, uint32_t n_cb, bool crc24a);
-  uint32_t cb_K = 0, cb_n = 0;
 };
 
 }  // namespace mi

@@ -9,6 +9,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+#include <memory>
+#include <tuple>
+#include <vector>
 
 #include "../../include/srslte/srslte.h"
 #include "ctrl.h"
@@ -19,23 +24,92 @@ struct mi_ue_dl_ctx {
   mi::Engine eng;
   hipStream_t st = nullptr;
   mi::DevBuf d_iq;
+  // page-locked staging: the subframe's IQ (srsUE's buffer is pageable; a pageable H2D costs ~70 us
+  // through HIP's own staging), the small per-call results and the payload
+  cf_t* h_iq = nullptr;
+  struct Small { float met[5]; uint32_t cfi, tb_ok, its; float phich; };
+  Small* h_small = nullptr;
+  uint8_t* h_pay = nullptr;
+  static constexpr size_t MAX_TB_BYTES = 16384;   // > 75,376 bits, the largest single-layer TBS
   mi_dl_sf_cfg_t cfg{};    // current subframe configuration
   uint32_t cfi = 1, sf_idx = 0;
   bool fft_done = false;
   cf_t* host_grid = nullptr;
   cf_t* host_ce[SRSLTE_MAX_PORTS] = {};
   mi::CtrlEngine ctrl;     // PCFICH / PDCCH / DCI blind search over eng's grid and ce (ctrl.hip)
+  // control-plan memo: (sf_idx, cfi, rnti, PHICH query) -> parked tables (ctrl_plan); -1 = none active
+  struct CtrlMemo {
+    std::tuple<uint32_t, uint32_t, uint32_t, uint32_t> key;
+    mi::CtrlTables t;
+    uint64_t used = 0;
+  };
+  std::vector<std::unique_ptr<CtrlMemo>> ctrl_memo;
+  int ctrl_active = -1;
+  uint64_t ctrl_clock = 0;
   uint32_t phich_ng = 0;
   bool llr_done = false;
+  // per-phase host-clock breakdown of the per-TTI calls (MI_UE_DL_PROF=1: the stream is synchronised at
+  // every mark so GPU work is attributed to its phase; printed to stderr by srslte_ue_dl_free)
+  struct Prof {
+    bool on = getenv("MI_UE_DL_PROF") != nullptr;
+    double acc[12] = {}, last = 0;
+    uint64_t n[12] = {};
+    static double now() {
+      timespec t;
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+    }
+    void start() { if (on) last = now(); }
+    void mark(int i, hipStream_t st) {
+      if (!on) return;
+      (void)hipStreamSynchronize(st);
+      const double t = now();
+      acc[i] += t - last; n[i]++; last = t;
+    }
+  } prof;
+  ~mi_ue_dl_ctx() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (void* p : {(void*)h_iq, (void*)h_small, (void*)h_pay})
+      if (p) (void)hipHostFree(p);
+    if (st) (void)hipStreamDestroy(st);
+  }
 };
 
 namespace {
 
-// plan the control stage for the instance's single subframe (cheap: tables of one cell / sf / cfi)
+// plan the control stage for the instance's single subframe.  srsUE asks for the same few plans every
+// frame (per subframe index: PCFICH, PDCCH soft bits, the blind search of each RNTI, PHICH), so built
+// plans are memoised: a repeat swaps its parked tables (device copies included) back in.
 bool ctrl_plan(mi_ue_dl_ctx* c, uint32_t cfi, uint16_t rnti, uint32_t phich_q = 0) {
-  return c->ctrl.build(c->eng.plan, std::vector<uint32_t>{cfi}, c->phich_ng, std::vector<uint16_t>{rnti},
-                       std::vector<uint32_t>{phich_q}) == 0 &&
-         c->ctrl.upload(c->st) == 0;
+  const auto key = std::make_tuple(c->sf_idx, cfi, (uint32_t)rnti, phich_q);
+  if (c->ctrl_active >= 0) {
+    if (c->ctrl_memo[(size_t)c->ctrl_active]->key == key) return true;
+    c->ctrl.swap_tables(c->ctrl_memo[(size_t)c->ctrl_active]->t);   // park
+    c->ctrl_active = -1;
+  }
+  int hit = -1;
+  for (size_t i = 0; i < c->ctrl_memo.size(); i++)
+    if (c->ctrl_memo[i]->key == key) { hit = (int)i; break; }
+  if (hit < 0) {
+    if (c->ctrl.build(c->eng.plan, std::vector<uint32_t>{cfi}, c->phich_ng, std::vector<uint16_t>{rnti},
+                      std::vector<uint32_t>{phich_q}) != 0 ||
+        c->ctrl.upload(c->st) != 0)
+      return false;
+    if (c->ctrl_memo.size() >= 64) {   // least recently used entry out (upload synchronised the stream)
+      size_t lru = 0;
+      for (size_t i = 1; i < c->ctrl_memo.size(); i++)
+        if (c->ctrl_memo[i]->used < c->ctrl_memo[lru]->used) lru = i;
+      c->ctrl_memo.erase(c->ctrl_memo.begin() + (ptrdiff_t)lru);
+    }
+    c->ctrl_memo.push_back(std::make_unique<mi_ue_dl_ctx::CtrlMemo>());
+    hit = (int)c->ctrl_memo.size() - 1;
+    c->ctrl_memo.back()->key = key;
+    c->ctrl.swap_tables(c->ctrl_memo.back()->t);   // park the fresh build, re-activated below
+  }
+  c->ctrl.swap_tables(c->ctrl_memo[(size_t)hit]->t);
+  c->ctrl_active = hit;
+  c->ctrl_memo[(size_t)hit]->used = ++c->ctrl_clock;
+  return true;
 }
 
 // grid / ce on the device: the copies decode_fft_estimate left are reused when the caller passes this
@@ -147,7 +221,12 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, srslte_cell_t cell) {
   q->sf_symbols = host_alloc(n * sizeof(cf_t));
   for (uint32_t p = 0; p < cell.nof_ports; p++) q->ce[p] = host_alloc(n * sizeof(cf_t));
   if (!q->sf_symbols || !q->ce[0] || (cell.nof_ports == 2 && !q->ce[1])) { delete ctx; return SRSLTE_ERROR; }
-  if (!ctx->d_iq.ensure((size_t)mi::sf_len(mi::symbol_sz(cell.nof_prb)) * 8)) { delete ctx; return SRSLTE_ERROR; }
+  const size_t sfl = (size_t)mi::sf_len(mi::symbol_sz(cell.nof_prb));
+  if (!ctx->d_iq.ensure(sfl * 8)) { delete ctx; return SRSLTE_ERROR; }
+  ctx->h_iq = host_alloc(sfl * sizeof(cf_t));
+  ctx->h_small = reinterpret_cast<mi_ue_dl_ctx::Small*>(host_alloc(sizeof(mi_ue_dl_ctx::Small)));
+  ctx->h_pay = reinterpret_cast<uint8_t*>(host_alloc(mi_ue_dl_ctx::MAX_TB_BYTES));
+  if (!ctx->h_iq || !ctx->h_small || !ctx->h_pay) { delete ctx; return SRSLTE_ERROR; }
   ctx->cfg.cell_id = cell.id;
   ctx->cfg.nof_prb = cell.nof_prb;
   ctx->cfg.nof_ports = cell.nof_ports;
@@ -165,7 +244,16 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, srslte_cell_t cell) {
 void srslte_ue_dl_free(srslte_ue_dl_t* q) {
   if (!q) return;
   if (q->ctx) {
-    if (q->ctx->st) (void)hipStreamDestroy(q->ctx->st);
+    const auto& pf = q->ctx->prof;
+    if (pf.on) {
+      static const char* names[11] = {"fft.h2d_iq", "fft.plan_upload", "fft.ofdm_chest", "fft.ctrl_plan", "fft.pcfich",
+                                      "fft.d2h_sync", "pdsch.plan_upload", "-", "pdsch.grid", "pdsch.kernels",
+                                      "pdsch.d2h_sync"};
+      fprintf(stderr, "{\"ue_dl_prof_us\": {");
+      for (int i = 0; i < 11; i++)
+        fprintf(stderr, "\"%s\": %.1f%s", names[i], pf.n[i] ? pf.acc[i] / (double)pf.n[i] : 0.0, i < 10 ? ", " : "");
+      fprintf(stderr, "}}\n");
+    }
     delete q->ctx;
   }
   if (q->sf_symbols) (void)hipHostFree(q->sf_symbols);
@@ -188,23 +276,31 @@ int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t* q, cf_t* input, uint32_t sf
   c->sf_idx = sf_idx;
   const size_t W = 12 * q->cell.nof_prb, n = (size_t)mi::NSYMB * W;
   const size_t sfl = (size_t)mi::sf_len(mi::symbol_sz(q->cell.nof_prb));
-  if (!mi::hip_ok(hipMemcpyAsync(c->d_iq.p, input, sfl * 8, hipMemcpyHostToDevice, c->st), "H2D iq"))
+  c->prof.start();
+  memcpy(c->h_iq, input, sfl * 8);   // the previous call's DMA out of h_iq ended with its stream sync
+  if (!mi::hip_ok(hipMemcpyAsync(c->d_iq.p, c->h_iq, sfl * 8, hipMemcpyHostToDevice, c->st), "H2D iq"))
     return SRSLTE_ERROR;
-  if (c->eng.plan.build(&c->cfg, 1, false) || c->eng.upload(c->st, false)) return SRSLTE_ERROR;
+  c->prof.mark(0, c->st);
+  if (c->eng.plan_memo(&c->cfg, 1, false, c->st)) return SRSLTE_ERROR;
+  c->prof.mark(1, c->st);
   if (c->eng.run(c->d_iq.p, c->st, (1u << MI_DL_STAGE_OFDM) | (1u << MI_DL_STAGE_CHEST), nullptr)) return SRSLTE_ERROR;
+  c->prof.mark(2, c->st);
   // PCFICH -> CFI on the GPU (the control plan's PCFICH tables do not depend on the CFI)
-  if (!ctrl_plan(c, 1, q->current_rnti) ||
-      c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 1u, 0.0f, c->st))
-    return SRSLTE_ERROR;
-  uint32_t cf = 0;
-  float met[5];
+  if (!ctrl_plan(c, 1, q->current_rnti)) return SRSLTE_ERROR;
+  c->prof.mark(3, c->st);
+  if (c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 1u, 0.0f, c->st)) return SRSLTE_ERROR;
+  c->prof.mark(4, c->st);
+  mi_ue_dl_ctx::Small* hs = c->h_small;
   bool ok = mi::hip_ok(hipMemcpyAsync(q->sf_symbols, c->eng.d_grid.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H");
   for (uint32_t p = 0; p < q->cell.nof_ports && ok; p++)
     ok = mi::hip_ok(hipMemcpyAsync(q->ce[p], c->eng.d_ce.as<float2>() + p * n, n * 8, hipMemcpyDeviceToHost, c->st), "D2H");
-  ok = ok && mi::hip_ok(hipMemcpyAsync(met, c->eng.d_metrics.p, sizeof(met), hipMemcpyDeviceToHost, c->st), "D2H") &&
-       mi::hip_ok(hipMemcpyAsync(&cf, c->ctrl.d_cfi.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
+  ok = ok && mi::hip_ok(hipMemcpyAsync(hs->met, c->eng.d_metrics.p, sizeof(hs->met), hipMemcpyDeviceToHost, c->st), "D2H") &&
+       mi::hip_ok(hipMemcpyAsync(&hs->cfi, c->ctrl.d_cfi.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipStreamSynchronize(c->st), "sync");
+  const float* met = hs->met;
+  const uint32_t cf = hs->cfi;
   if (!ok) return SRSLTE_ERROR;
+  c->prof.mark(5, c->st);
   q->chest.rsrp = met[0]; q->chest.rssi = met[1]; q->chest.rsrq = met[2];
   q->chest.noise_estimate = met[3]; q->chest.snr = met[4];
   if (cf < 1 || cf > 3) return SRSLTE_ERROR;
@@ -264,19 +360,27 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
   slot_mask(&cfg->grant, s.prb_mask);
   c->eng.noise = noise_estimate;
   c->eng.max_its = q->dl_sch.max_iterations ? q->dl_sch.max_iterations : SRSLTE_PDSCH_MAX_TDEC_ITERS;
-  if (c->eng.plan.build(&s, 1, true) || c->eng.upload(c->st, false)) return SRSLTE_ERROR;
+  c->prof.start();
+  if (c->eng.plan_memo(&s, 1, true, c->st)) return SRSLTE_ERROR;
+  c->prof.mark(6, c->st);
   if (c->eng.plan.sb_floats * sizeof(float) > softbuffer->dev_bytes) return SRSLTE_ERROR;
   bool ok = device_grid(c, cell, sf_symbols, ce);
   if (!ok) return SRSLTE_ERROR;
+  c->prof.mark(8, c->st);
   const uint32_t stages = (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM) | (1u << MI_DL_STAGE_TDEC) |
                           (1u << MI_DL_STAGE_TB);
   if (c->eng.run(nullptr, c->st, stages, reinterpret_cast<float*>(softbuffer->dev))) return SRSLTE_ERROR;
-  uint32_t tb_ok = 0, its = 0;
-  ok = mi::hip_ok(hipMemcpyAsync(data, c->eng.d_payload.p, s.tbs / 8, hipMemcpyDeviceToHost, c->st), "D2H") &&
-       mi::hip_ok(hipMemcpyAsync(&tb_ok, c->eng.d_tbok.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
-       mi::hip_ok(hipMemcpyAsync(&its, c->eng.d_tbits.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
+  c->prof.mark(9, c->st);
+  if (s.tbs / 8 > mi_ue_dl_ctx::MAX_TB_BYTES) return SRSLTE_ERROR;
+  mi_ue_dl_ctx::Small* hs = c->h_small;
+  ok = mi::hip_ok(hipMemcpyAsync(c->h_pay, c->eng.d_payload.p, s.tbs / 8, hipMemcpyDeviceToHost, c->st), "D2H") &&
+       mi::hip_ok(hipMemcpyAsync(&hs->tb_ok, c->eng.d_tbok.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
+       mi::hip_ok(hipMemcpyAsync(&hs->its, c->eng.d_tbits.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipStreamSynchronize(c->st), "sync");
   if (!ok) return SRSLTE_ERROR;
+  memcpy(data, c->h_pay, s.tbs / 8);
+  const uint32_t tb_ok = hs->tb_ok, its = hs->its;
+  c->prof.mark(10, c->st);
   q->dl_sch.nof_iterations = its;
   q->dl_sch.average_nof_iterations = 0.8f * q->dl_sch.average_nof_iterations + 0.2f * (float)its;
   return tb_ok ? SRSLTE_SUCCESS : SRSLTE_ERROR;
@@ -341,13 +445,13 @@ bool srslte_ue_dl_decode_phich(srslte_ue_dl_t* q, uint32_t sf_idx, uint32_t n_pr
   if (!q || !q->ctx || !q->ctx->fft_done || sf_idx != q->ctx->sf_idx || n_prb_lowest > 0xFFFFu || n_dmrs > 7)
     return false;
   mi_ue_dl_ctx* c = q->ctx;
-  float soft = 0.0f;
   // the grid / ce of the last decode_fft_estimate are still in HBM (device_grid keeps them)
   if (!ctrl_plan(c, c->cfi ? c->cfi : 1, q->current_rnti, n_prb_lowest | (n_dmrs << 16)) ||
       c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 8u, 0.0f, c->st) ||
-      !mi::hip_ok(hipMemcpyAsync(&soft, c->ctrl.d_phich.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") ||
+      !mi::hip_ok(hipMemcpyAsync(&c->h_small->phich, c->ctrl.d_phich.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") ||
       !mi::hip_ok(hipStreamSynchronize(c->st), "sync"))
     return false;
+  const float soft = c->h_small->phich;
   // the rebuilt plan has the same CFI: the PDCCH soft bits stay valid for find_ul_dci (:426)
   return soft > 0.0f;
 }
