@@ -78,15 +78,19 @@ PATH_SOURCES = ("cbscatter.hip", "chest.hip", "demap.hip", "dl_common.h", "engin
                 "tb.hip", "tb_body.h", "tdec.hip", "tdec_body.h")
 
 
-def pmc_traffic(sf_per_gpu, tdec):
+def pmc_traffic(sf_per_gpu, tdec, kernel):
+    """The turbo kernel's PMC figures of the profiled build (tools/profile.sh -> profiles/traffic.json): HBM
+    traffic per launch and VALU busy; only when the kernel sources, the shard size, the arithmetic and the
+    kernel that ran all match the profiled run."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         t = json.load(open(p))
     except (OSError, ValueError):
-        return None, None
-    if t.get("src_hash") != kernel_src_hash() or t.get("sf_per_gpu") != sf_per_gpu or t.get("tdec", "gen") != tdec:
-        return None, None
-    return t["tdec_traffic_bytes_per_launch"], "profiles/traffic.json: " + t["source"]
+        return None, None, None
+    if (t.get("src_hash") != kernel_src_hash() or t.get("sf_per_gpu") != sf_per_gpu or t.get("tdec", "gen") != tdec
+            or t.get("tdec_kernel", kernel) != kernel):
+        return None, None, None
+    return t["tdec_traffic_bytes_per_launch"], t.get("tdec_valu_busy_pct"), "profiles/traffic.json: " + t["source"]
 
 
 def make_cfg(i, new_tb=1):
@@ -702,7 +706,7 @@ def main():
         tdec_ms = stage["tdec"]
         tdec_bytes = batch.algo_bytes(4)
         achieved = tdec_bytes / (tdec_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(B, args.tdec)
+        traffic, valu_busy, traffic_src = pmc_traffic(B, args.tdec, tdec_kernel_name(batch.turbo_sched))
         out = {
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
@@ -717,7 +721,7 @@ def main():
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": tdec_kernel_name(batch.turbo_sched), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic": traffic, "valu_busy_pct": valu_busy, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": tdec_bytes,
                          "avg_launch_ms": round(tdec_ms, 4), "launches_averaged": nprof},
         }

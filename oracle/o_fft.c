@@ -6,8 +6,28 @@
  */
 #include "oracle.h"
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* Twiddles of every radix-2 stage (len = 2 .. 2048), both signs, computed once with exactly the expression
+ * the butterfly loop used to evaluate per call -- cos / sin(sgn 2 pi k / len) -- so the transform is
+ * bit-identical to the per-call form, about 4x faster (the CPU baseline runs this chain).  Entry (len, k)
+ * at index len / 2 - 1 + k. */
+#define TW_NMAX 2048
+static double tw_re[2][TW_NMAX], tw_im[2][TW_NMAX];
+static pthread_once_t tw_once = PTHREAD_ONCE_INIT;
+static void tw_init(void) {
+  for (int inv = 0; inv < 2; inv++) {
+    const double sgn = inv ? 1.0 : -1.0;
+    for (int len = 2; len <= TW_NMAX; len <<= 1)
+      for (int k = 0; k < len / 2; k++) {
+        double ang = sgn * 2.0 * M_PI * k / len;
+        tw_re[inv][len / 2 - 1 + k] = cos(ang);
+        tw_im[inv][len / 2 - 1 + k] = sin(ang);
+      }
+  }
+}
 
 static void fft_pow2(double *a, int N, int inverse) {
   /* iterative radix-2, bit reversal */
@@ -21,12 +41,12 @@ static void fft_pow2(double *a, int N, int inverse) {
       a[2 * j] = tr; a[2 * j + 1] = ti;
     }
   }
-  const double sgn = inverse ? 1.0 : -1.0;
+  pthread_once(&tw_once, tw_init);
+  const double *twr = tw_re[inverse ? 1 : 0], *twi = tw_im[inverse ? 1 : 0];
   for (int len = 2; len <= N; len <<= 1) {
     int h = len >> 1;
     for (int k = 0; k < h; k++) {
-      double ang = sgn * 2.0 * M_PI * k / len;
-      double wr = cos(ang), wi = sin(ang);
+      const double wr = twr[h - 1 + k], wi = twi[h - 1 + k];
       for (int i = k; i < N; i += len) {
         double *u = a + 2 * i, *v = a + 2 * (i + h);
         double vr = v[0] * wr - v[1] * wi, vi = v[0] * wi + v[1] * wr;
@@ -38,6 +58,7 @@ static void fft_pow2(double *a, int N, int inverse) {
 }
 
 void or_dft(const double *in, double *out, int N, int inverse) {
+  if (N > TW_NMAX) abort();   /* LTE: N <= 2048 */
   if ((N & (N - 1)) == 0) {
     memcpy(out, in, sizeof(double) * 2 * N);
     fft_pow2(out, N, inverse);

@@ -131,19 +131,32 @@ int or_chest(const or_cell_t *c, uint32_t sf, const float *grid, float *ce, floa
   return 0;
 }
 
-/* max-log soft demapper of one complex symbol into Qm LLRs */
-static void demod_symbol(double xr, double xi, uint32_t Qm, float *llr) {
+/* max-log soft demapper of one complex symbol into Qm LLRs: per bit, the smallest squared distance to a
+ * PAM level whose label has the bit 0 / 1 (exhaustive over the levels).  Each level's squared distance is
+ * formed once per dimension and shared by the nb bits' minima (the same values and comparisons as one
+ * search per bit, so the LLRs are unchanged; the CPU baseline runs this). */
+static void pam_levels(uint32_t Qm, double *lev) {
+  uint32_t nb = Qm / 2, nl = 1u << nb;
+  for (uint32_t lab = 0; lab < nl; lab++) {
+    uint8_t bits[3];
+    for (uint32_t q = 0; q < nb; q++) bits[q] = (lab >> (nb - 1 - q)) & 1;
+    lev[lab] = or_pam_level(bits, Qm);
+  }
+}
+static void demod_symbol(double xr, double xi, uint32_t Qm, const double *lev, float *llr) {
   const double inv_s2 = 1.0 / 0.5;
   uint32_t nb = Qm / 2, nl = 1u << nb;
   for (int dim = 0; dim < 2; dim++) {
     double x = dim ? xi : xr;
+    double d2[8];
+    for (uint32_t lab = 0; lab < nl; lab++) {
+      double d = x - lev[lab];
+      d2[lab] = d * d;
+    }
     for (uint32_t j = 0; j < nb; j++) {
       double m0 = 1e300, m1 = 1e300;
       for (uint32_t lab = 0; lab < nl; lab++) {
-        uint8_t bits[3];
-        for (uint32_t q = 0; q < nb; q++) bits[q] = (lab >> (nb - 1 - q)) & 1;
-        double d = x - or_pam_level(bits, Qm), d2 = d * d;
-        if (bits[j]) { if (d2 < m1) m1 = d2; } else { if (d2 < m0) m0 = d2; }
+        if ((lab >> (nb - 1 - j)) & 1) { if (d2[lab] < m1) m1 = d2[lab]; } else { if (d2[lab] < m0) m0 = d2[lab]; }
       }
       llr[2 * j + dim] = (float)((m0 - m1) * inv_s2);
     }
@@ -194,8 +207,10 @@ int or_pdsch_llr(const or_cell_t *c, uint32_t cfi, uint32_t sf, const uint8_t *p
   uint32_t G = (uint32_t)nre * Qm;
   uint8_t *cs = (uint8_t *)malloc(G + 8);
   or_gold((rnti << 14) | (sf << 9) | c->id, cs, G);
+  double lev[8];
+  pam_levels(Qm, lev);
   for (int i = 0; i < nre; i++) {
-    demod_symbol(sym[2 * i], sym[2 * i + 1], Qm, llr + (size_t)i * Qm);
+    demod_symbol(sym[2 * i], sym[2 * i + 1], Qm, lev, llr + (size_t)i * Qm);
     if (symbols_out) { symbols_out[2 * i] = (float)sym[2 * i]; symbols_out[2 * i + 1] = (float)sym[2 * i + 1]; }
   }
   for (uint32_t i = 0; i < G; i++) if (cs[i]) llr[i] = -llr[i];
@@ -211,7 +226,9 @@ int or_pcfich(const or_cell_t *c, uint32_t sf, const float *grid, const float *c
   uint32_t tm = c->nof_ports == 2 ? 2 : 1;
   equalize(grid, ce, OR_NSYMB * 12 * c->nof_prb, kk, 16, tm, 0.0, sym);
   float llr[32];
-  for (int i = 0; i < 16; i++) demod_symbol(sym[2 * i], sym[2 * i + 1], 2, llr + 2 * i);
+  double lev[8];
+  pam_levels(2, lev);
+  for (int i = 0; i < 16; i++) demod_symbol(sym[2 * i], sym[2 * i + 1], 2, lev, llr + 2 * i);
   uint8_t sc[32];
   or_gold(or_pcfich_cinit(c, sf), sc, 32);
   for (int i = 0; i < 32; i++) if (sc[i]) llr[i] = -llr[i];
