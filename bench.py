@@ -501,9 +501,17 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
 def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     """Plan the batch, stage the pool in HBM (replicated on device into the batch IQ layout), run `warmup` untimed
     and `steps` timed passes (barrier + synchronize on both sides), then check the last step's outputs: every TB's
-    CRC verdict and, for every CRC-OK TB, its payload against the transmitted bytes."""
+    CRC verdict and, for every CRC-OK TB, its payload against the transmitted bytes.
+
+    --streams S > 1: S workspaces (abi.Batch) of the same batch on S HIP streams, consecutive steps issued
+    round-robin -- a streaming receiver's double (triple) buffering: step i + 1's front end (OFDM, channel
+    estimation, rate de-matching) runs while step i's turbo decoder occupies the GPU.  Every step still decodes
+    the whole batch; the timed region covers all `steps` steps."""
     B = len(cfgs)
-    batch = abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
+    S = max(1, args.streams)
+    batches = [abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
+               for _ in range(S)]
+    batch = batches[0]
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
     if len(pool_iq) == B and len({len(x) for x in pool_iq}) > 1:
         flat = np.zeros(2 * batch.iq_samples, np.float32)
@@ -517,29 +525,42 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
         idx = torch.arange(B, device=dev) % len(pool_iq)
         d_iq.view(B, sfl).copy_(d_pool[idx])
         del d_pool
-    sptr = torch.cuda.current_stream(dev).cuda_stream
-    for _ in range(warmup):
-        batch.run(d_iq.data_ptr(), sptr)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    sptr = [st.cuda_stream for st in streams]
     torch.cuda.synchronize(dev)
-    batch.profile_reset()
+    for w in range(warmup * S):
+        batches[w % S].run(d_iq.data_ptr(), sptr[w % S])
+    torch.cuda.synchronize(dev)
+    for b in batches:
+        b.profile_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        batch.run(d_iq.data_ptr(), sptr)
+    for i in range(steps):
+        batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stage, nprof = batch.stage_ms()
+    # stage times: HIP events on each workspace's stream, averaged over every timed step
+    per = [(b.stage_ms(), b) for b in batches[:min(S, steps)]]
+    nprof = sum(n for (_, n), _ in per)
+    stage = {k: sum(st[k] * n for (st, n), _ in per) / nprof for k in per[0][0][0]}
     del d_iq
-    crc = batch.download(abi.BUF_TB_CRC, np.uint32)[:B]
-    its = batch.download(abi.BUF_TB_ITS, np.uint32)[:B]
-    pay = batch.download(abi.BUF_PAYLOAD, np.uint8)
-    bad = sum(int(not np.array_equal(batch.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(B) if crc[i])
-    return {"batch": batch, "stage": stage, "nprof": nprof, "elapsed": elapsed, "n_ok": int(crc.sum()), "its": its,
-            "bad": bad, "bits_ok": float(sum(c.tbs for c, o in zip(cfgs, crc) if o))}
+    bad, n_ok, its, bits_ok = 0, 0, None, 0.0
+    for k, b in enumerate(batches[:min(S, steps)]):
+        crc = b.download(abi.BUF_TB_CRC, np.uint32)[:B]
+        pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+        bad += sum(int(not np.array_equal(b.payload(i, pay), pool_tb[i % len(pool_tb)])) for i in range(B) if crc[i])
+        if k == 0:
+            its = b.download(abi.BUF_TB_ITS, np.uint32)[:B]
+            n_ok = int(crc.sum())
+            bits_ok = float(sum(c.tbs for c, o in zip(cfgs, crc) if o))
+    for b in batches[1:]:
+        b.close()
+    return {"batch": batch, "stage": stage, "nprof": nprof, "elapsed": elapsed, "n_ok": n_ok, "its": its,
+            "bad": bad, "bits_ok": bits_ok}
 
 
 def spawn_ranks(n):
@@ -601,6 +622,10 @@ def main():
                     help="default config: also run the shard at this SNR (turbo waterfall, ~3 iterations at max_its 4) "
                          "and report it as the `iterating` block; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="workspaces / HIP streams the steps rotate over (consecutive batches overlap); 1 = serial; "
+                         "0 = auto: 1 for the headline shard (its turbo kernel already fills the GPU: +5-8 %% with 2-4), "
+                         "4 for the low-occupancy configs[2] / configs[4] batches (2.2x / 1.7x, profiles/r2/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
@@ -627,6 +652,8 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))                     # before anything touches the GPU
+    if args.streams <= 0:
+        args.streams = 4 if args.config in (3, 5) else 1
     if args.config == 2:
         args.sf_per_gpu = 1
     elif args.config == 3 and args.sf_per_gpu == 12500:
@@ -714,6 +741,7 @@ def main():
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
+                       "streams": max(1, args.streams),
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
