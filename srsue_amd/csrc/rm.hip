@@ -331,6 +331,10 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   }
   }
   __syncthreads();
+#if MI_RM_DIAG_NOCOMBINE   // timing diagnostic only: staging without the combine (wrong results)
+  if (tile[threadIdx.x & 63][threadIdx.x >> 6] == 12345.f) sbg[threadIdx.x] = 1.f;
+  return;
+#endif
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
   constexpr int NP = RM_CHUNK / RM_NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
