@@ -940,7 +940,22 @@ template <int PF, class Win, class Idx, class Load, class Run>
 MI_HD inline void pipe_windows(int n, Idx widx, Load load, Run run) {
   if (n <= 0) return;
   auto at = [&](int i) { return widx(i < n ? i : n - 1); };
-  if constexpr (PF >= 2) {
+  if constexpr (PF >= 3) {
+    // PF + 1 buffers in a ring, the rotation unrolled so every buffer index is a compile-time constant
+    // (the windows stay in registers); the loads of window i + PF are issued before window i is computed
+    constexpr int NB = PF + 1;
+    Win buf[NB];
+#pragma unroll
+    for (int b = 0; b < PF; b++) load(at(b), buf[b]);
+    for (int i = 0;; i += NB) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        load(at(i + b + PF), buf[(b + PF) % NB]);
+        run(buf[b], at(i + b));
+        if (i + b + 1 >= n) return;
+      }
+    }
+  } else if constexpr (PF == 2) {
     Win A, B, C;
     load(at(0), A);
     load(at(1), B);

@@ -17,8 +17,16 @@ struct mi_ue_ul_ctx {
   mi::UlEngine eng;
   hipStream_t st = nullptr;
   mi::DevBuf d_pay, d_iq;
+  // page-locked staging of the TB (H2D) and of the subframe's IQ (D2H): srsUE's buffers are pageable
+  uint8_t* h_pay = nullptr;
+  cf_t* h_iq = nullptr;
   mi_ul_cfg_t cfg{};
   bool planned = false;
+  ~mi_ue_ul_ctx() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (h_pay) (void)hipHostFree(h_pay);
+    if (h_iq) (void)hipHostFree(h_iq);
+  }
 };
 
 namespace {
@@ -90,8 +98,12 @@ int srslte_ue_ul_init(srslte_ue_ul_t* q, srslte_cell_t cell) {
   memset(q, 0, sizeof(*q));
   q->cell = cell;
   auto* c = new mi_ue_ul_ctx();
+  c->eng.packed = true;
+  const size_t iq_bytes = (size_t)15 * mi::symbol_sz(cell.nof_prb) * 8;
   if (!mi::hip_ok(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "stream") || !c->d_pay.ensure(TX_MAX_BYTES) ||
-      !c->d_iq.ensure((size_t)15 * mi::symbol_sz(cell.nof_prb) * 8)) {
+      !c->d_iq.ensure(iq_bytes) ||
+      !mi::hip_ok(hipHostMalloc(reinterpret_cast<void**>(&c->h_pay), TX_MAX_BYTES, hipHostMallocDefault), "pinned") ||
+      !mi::hip_ok(hipHostMalloc(reinterpret_cast<void**>(&c->h_iq), iq_bytes, hipHostMallocDefault), "pinned")) {
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
     return SRSLTE_ERROR;
@@ -206,7 +218,9 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
   // the TB: new data from `data`; a retransmission without data re-encodes the softbuffer's copy
   const void* src = nullptr;
   if (data) {
-    if (!mi::hip_ok(hipMemcpyAsync(c->d_pay.p, data, nbytes, hipMemcpyHostToDevice, c->st), "H2D payload")) return SRSLTE_ERROR;
+    memcpy(c->h_pay, data, nbytes);   // the previous call's DMA out of h_pay ended with its stream sync
+    if (!mi::hip_ok(hipMemcpyAsync(c->d_pay.p, c->h_pay, nbytes, hipMemcpyHostToDevice, c->st), "H2D payload"))
+      return SRSLTE_ERROR;
     if (sb && sb->dev && c->cfg.rv == 0) {
       if (!mi::hip_ok(hipMemcpyAsync(sb->dev, c->d_pay.p, nbytes, hipMemcpyDeviceToDevice, c->st), "softbuffer"))
         return SRSLTE_ERROR;
@@ -225,9 +239,10 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
   if (q->cfo_en) P.txs[0].cfo = q->current_cfo;
   const size_t n = (size_t)15 * mi::symbol_sz(q->cell.nof_prb);
   if (c->eng.upload(c->st) || c->eng.run(src, c->d_iq.p, c->st) ||
-      !mi::hip_ok(hipMemcpyAsync(output_signal, c->d_iq.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H IQ") ||
+      !mi::hip_ok(hipMemcpyAsync(c->h_iq, c->d_iq.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H IQ") ||
       !mi::hip_ok(hipStreamSynchronize(c->st), "ul sync"))
     return SRSLTE_ERROR;
+  memcpy(output_signal, c->h_iq, n * 8);
   return SRSLTE_SUCCESS;
 }
 

@@ -1,6 +1,9 @@
 // ul_engine.h -- device workspace + launch sequence of one UL PUSCH plan (shared by the batched ABI,
 // ul_batch.cpp, and the per-TTI srslte_ue_ul_t, ue_ul.cpp).
 #pragma once
+#include <string.h>
+
+#include <algorithm>
 #include <vector>
 
 #include "engine.h"
@@ -22,6 +25,11 @@ struct UlEngine {
   ~UlEngine() {
     for (auto& s : ev_sets)
       for (auto& e : s) (void)hipEventDestroy(e);
+    if (stage_done) {
+      (void)hipEventSynchronize(stage_done);
+      (void)hipEventDestroy(stage_done);
+    }
+    if (h_stage) (void)hipHostFree(h_stage);
   }
   template <class T>
   static bool up(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
@@ -32,9 +40,45 @@ struct UlEngine {
   // QPP / selection tables and twiddles only change with the code-block sizes and bandwidth
   std::vector<uint32_t> up_kdata;
   std::vector<float> up_tw;
+  // packed upload (the per-TTI path): the per-grant tables (transmissions, code blocks, scrambling words)
+  // packed into one page-locked buffer and copied with a single DMA into one device arena
+  DevBuf d_tables;
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
+  hipEvent_t stage_done = nullptr;
+  bool packed = false;
+  bool up_packed(hipStream_t st) {
+    const UlPlan& P = plan;
+    const size_t b0 = P.txs.size() * sizeof(MiUlTx), b1 = P.cbs.size() * sizeof(MiUlCb), b2 = P.scr.size() * 4;
+    auto span = [](size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; };
+    const size_t o1 = span(b0), o2 = o1 + span(b1), total = o2 + span(b2);
+    if (stage_done && !hip_ok(hipEventSynchronize(stage_done), "ul stage wait")) return false;
+    if (total > h_stage_bytes) {
+      if (h_stage) (void)hipHostFree(h_stage);
+      h_stage = nullptr;
+      h_stage_bytes = 0;
+      if (!hip_ok(hipHostMalloc(&h_stage, total, hipHostMallocDefault), "ul stage")) return false;
+      h_stage_bytes = total;
+    }
+    if (total > d_tables.bytes) {
+      d_txs.release(); d_cbs.release(); d_scr.release();
+      if (!d_tables.ensure(total)) return false;
+    }
+    char* h = static_cast<char*>(h_stage);
+    if (b0) memcpy(h, P.txs.data(), b0);
+    if (b1) memcpy(h + o1, P.cbs.data(), b1);
+    if (b2) memcpy(h + o2, P.scr.data(), b2);
+    char* d = static_cast<char*>(d_tables.p);
+    d_txs.set_view(d, std::max<size_t>(b0, 1));
+    d_cbs.set_view(d + o1, std::max<size_t>(b1, 1));
+    d_scr.set_view(d + o2, std::max<size_t>(b2, 1));
+    if (!stage_done && !hip_ok(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "event")) return false;
+    return hip_ok(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, st), "ul upload") &&
+           hip_ok(hipEventRecord(stage_done, st), "event");
+  }
   int upload(hipStream_t st) {
     const UlPlan& P = plan;
-    bool ok = up(d_txs, P.txs, st) && up(d_cbs, P.cbs, st) && up(d_scr, P.scr, st) &&
+    bool ok = (packed ? up_packed(st) : (up(d_txs, P.txs, st) && up(d_cbs, P.cbs, st) && up(d_scr, P.scr, st))) &&
               d_tbcrc.ensure(P.txs.size() * 4) && d_syms.ensure(P.sym_bytes);
     // CQI symbols head each transmission's multiplexed sequence (the encoder writes the data after them)
     for (size_t i = 0; ok && i < P.txs.size(); i++)
