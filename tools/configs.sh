@@ -10,9 +10,11 @@ run() { name=$1; shift; timeout -k 10 240 python3 bench.py "$@" > $OUT/$name.jso
 run c2 --config 2 --cpu-seconds 6
 run c2_lane --config 2 --sched lane --no-cpu-baseline
 run c3 --config 3 --cpu-seconds 6
+run c3_s1 --config 3 --streams 1 --no-cpu-baseline
 run c1 --config 1 --cpu-seconds 9
-run c1_win --config 1 --sched win --cb-per-gpu 16384 --no-cpu-baseline
 run c5 --config 5 --cpu-seconds 6
-run c4_gen --tdec gen --cpu-seconds 6
-run ul --ul --cpu-seconds 6 --steps 5
+run c5_s1 --config 5 --streams 1 --no-cpu-baseline
+run c4 --cpu-seconds 9
+run c4_gen --tdec gen --cpu-seconds 6 --iterating-snr 0
+run ul --ul --cpu-seconds 6 --steps 5 --iterating-snr 0
 echo done
