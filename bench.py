@@ -248,24 +248,36 @@ def bench_codeblocks(args, world, rank, dev):
     sigma2 = 1.0 / (2 * (K / (3.0 * K + 12)) * 10 ** (args.ebno / 10))
     llr = np.stack([(-2.0 * ((1.0 - 2.0 * abi.turbo_encode(b, K)) + rng.normal(0, np.sqrt(sigma2), 3 * K + 12))
                      / sigma2).astype(np.float32) for b in bits])
-    tb = abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
+    # S workspaces on S streams, steps round-robin (measure()'s --streams): 65,536 code blocks give the packed
+    # decoder one wavefront per SIMD, so consecutive steps overlap
+    S = max(1, args.streams)
+    tbs = [abi.TdecBatch(K, n, max_its=8, early_stop=False, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
+           for _ in range(S)]
+    tb = tbs[0]
     d = torch.from_numpy(llr).to(dev)[torch.arange(n, device=dev) % pool].contiguous()
-    sptr = torch.cuda.current_stream(dev).cuda_stream
-    for _ in range(args.warmup):
-        tb.run(d.data_ptr(), sptr)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    sptr = [st.cuda_stream for st in streams]
     torch.cuda.synchronize(dev)
-    tb.profile_reset()
+    for w in range(args.warmup * S):
+        tbs[w % S].run(d.data_ptr(), sptr[w % S])
+    torch.cuda.synchronize(dev)
+    for t in tbs:
+        t.profile_reset()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tb.run(d.data_ptr(), sptr)
+    for i in range(args.steps):
+        tbs[i % S].run(d.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stage, nprof = tb.stage_ms()
+    per = [t.stage_ms() for t in tbs[:min(S, args.steps)]]
+    nprof = sum(k for _, k in per)
+    stage = {key: sum(st[key] * k for st, k in per) / nprof for key in per[0][0]}
     dec, its, _ = tb.results()
+    for k, t in enumerate(tbs[1:min(S, args.steps)], 1):
+        assert np.array_equal(t.results()[0][:pool], dec[:pool]), f"stream {k} decoded differently"
     ber = float(np.mean(dec[:pool] != bits))
     elapsed, _, n_all = reduce_over_ranks(elapsed, 0, n, world, dev)
     if rank:
@@ -278,7 +290,7 @@ def bench_codeblocks(args, world, rank, dev):
            "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
            "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
                                   f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
-                      "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec,
+                      "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec, "streams": S,
                       "turbo_schedule": SCHED_DESC[tb.turbo_sched]},
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
            "roofline": {"kernel": tdec_kernel_name(tb.turbo_sched), "bound": "hbm", "achieved": round(ach, 2),
@@ -625,7 +637,8 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="workspaces / HIP streams the steps rotate over (consecutive batches overlap); 1 = serial; "
                          "0 = auto: 1 for the headline shard (its turbo kernel already fills the GPU: +5-8 %% with 2-4), "
-                         "4 for the low-occupancy configs[2] / configs[4] batches (2.2x / 1.7x, profiles/r2/streams)")
+                         "4 for the low-occupancy configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; "
+                         "profiles/r2/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
@@ -653,7 +666,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))                     # before anything touches the GPU
     if args.streams <= 0:
-        args.streams = 4 if args.config in (3, 5) else 1
+        args.streams = 4 if args.config in (3, 5) else 3 if args.config == 1 else 1
     if args.config == 2:
         args.sf_per_gpu = 1
     elif args.config == 3 and args.sf_per_gpu == 12500:
