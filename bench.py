@@ -521,8 +521,9 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     the whole batch; the timed region covers all `steps` steps."""
     B = len(cfgs)
     S = max(1, args.streams)
-    batches = [abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched)
-               for _ in range(S)]
+    compact = args.ce == "compact" and not args.ctrl   # --ctrl reads the batch's full channel estimates
+    batches = [abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched,
+                         compact_ce=compact) for _ in range(S)]
     batch = batches[0]
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
     if len(pool_iq) == B and len({len(x) for x in pool_iq}) > 1:
@@ -634,6 +635,9 @@ def main():
                     help="default config: also run the shard at this SNR (turbo waterfall, ~3 iterations at max_its 4) "
                          "and report it as the `iterating` block; 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--ce", choices=("compact", "full"), default="compact",
+                    help="channel estimates of the batch: compact = the 4 pilot rows per port, interpolated in time "
+                         "inside the fused demap (MI_DL_FLAG_CE_COMPACT, identical LLRs); full = all 14 symbols")
     ap.add_argument("--streams", type=int, default=0,
                     help="workspaces / HIP streams the steps rotate over (consecutive batches overlap); 1 = serial; "
                          "0 = auto: 1 for the headline shard (its turbo kernel already fills the GPU: +5-8 %% with 2-4), "
@@ -755,6 +759,7 @@ def main():
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
+                       "channel_estimates": "full" if (args.ce == "full" or args.ctrl) else "compact",
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),

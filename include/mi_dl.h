@@ -49,7 +49,8 @@ enum { MI_DL_STAGE_OFDM = 0, MI_DL_STAGE_CHEST, MI_DL_STAGE_DEMAP, MI_DL_STAGE_R
 
 /* buffers that can be downloaded for parity checks */
 enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL_BUF_TB_CRC, MI_DL_BUF_TB_ITS,
-       MI_DL_BUF_METRICS, MI_DL_BUF_CB_ITS, MI_DL_BUF_CB_CRC };
+       MI_DL_BUF_METRICS, MI_DL_BUF_CB_ITS, MI_DL_BUF_CB_CRC,
+       MI_DL_BUF_SOFTBUFFER /* the batch's HARQ softbuffer arena (group layout, dl_common.h sb_group_floats) */ };
 
 #define MI_DL_FLAG_PROFILE 1u  /* record HIP events around every stage of every run */
 /* turbo decoder arithmetic.  Default (and MI_DL_FLAG_TDEC_I16): the int16 decoder of srsLTE's SSE
@@ -88,6 +89,12 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * packed int16 instructions (half the VALU instructions per code block), crossed schedule; bit-identical
  * outputs (tdec_p2_body.h) */
 #define MI_DL_FLAG_TDEC_P2   512u
+/* compact channel estimates: the channel-estimation stage writes, per port, only the 4 pilot symbols'
+ * frequency-interpolated rows ([port][4][12 N_RB] at the subframe's ce offset) and the fused demap stage
+ * interpolates each RE's estimate in time from them with the chest kernel's own expression -- identical
+ * LLRs, 10 of 14 rows of channel-estimate traffic written and read never.  Batch throughput mode: the
+ * batch's ce buffer then does not hold the full estimates (no MI_DL_FLAG_KEEP_LLR, no mi_dl_ctrl_* on it) */
+#define MI_DL_FLAG_CE_COMPACT 1024u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 

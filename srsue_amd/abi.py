@@ -15,7 +15,7 @@ EMU_PATH = os.path.join(PKG_DIR, "libsrsue_amd_emu.so")
 
 MAX_PRB = 110
 STAGES = ("ofdm", "chest", "demap", "rm", "tdec", "tb")
-BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF_CB_ITS, BUF_CB_CRC = range(9)
+BUF_GRID, BUF_CE, BUF_LLR, BUF_PAYLOAD, BUF_TB_CRC, BUF_TB_ITS, BUF_METRICS, BUF_CB_ITS, BUF_CB_CRC, BUF_SB = range(10)
 FLAG_PROFILE = 1
 FLAG_TDEC_I16 = 2   # int16 ("SSE") turbo arithmetic (the default), see include/mi_dl.h
 FLAG_TDEC_GEN = 4   # float srsLTE-gen turbo arithmetic
@@ -25,6 +25,7 @@ FLAG_TDEC_LANE = 32  # int16 turbo: force one code block per lane of 64-lane wav
 FLAG_TDEC_X = 128  # lane-per-code-block decoder, crossed schedule (two wavefronts per group)
 FLAG_TDEC_XR = 256  # crossed kernel, recompute form (5 waves per SIMD)
 FLAG_TDEC_P2 = 512   # two code blocks per lane (packed int16), crossed
+FLAG_CE_COMPACT = 1024  # compact channel estimates (4 pilot rows per port), interpolated in the fused demap
 SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X,
                "lanexr": FLAG_TDEC_LANE | FLAG_TDEC_X | FLAG_TDEC_XR, "p2": FLAG_TDEC_LANE | FLAG_TDEC_P2}
 FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
@@ -189,11 +190,13 @@ def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
 class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
-    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None, keep_llr=False):
+    def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None, keep_llr=False,
+                 compact_ce=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
         flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
-            (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched] | (FLAG_KEEP_LLR if keep_llr else 0)
+            (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched] | (FLAG_KEEP_LLR if keep_llr else 0) | \
+            (FLAG_CE_COMPACT if compact_ce else 0)
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())

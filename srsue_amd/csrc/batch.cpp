@@ -48,6 +48,7 @@ static mi::DevBuf* buf_of(mi_dl_batch_t* b, int which, size_t* bytes) {
     case MI_DL_BUF_METRICS: *bytes = nsf * 5 * 4; return &b->eng.d_metrics;
     case MI_DL_BUF_CB_ITS: *bytes = P.lanes.size() * 4; return &b->eng.d_cbits;
     case MI_DL_BUF_CB_CRC: *bytes = P.lanes.size() * 4; return &b->eng.d_cbcrc;
+    case MI_DL_BUF_SOFTBUFFER: *bytes = P.sb_floats * 4; return &b->eng.d_sb;
   }
   *bytes = 0;
   return nullptr;

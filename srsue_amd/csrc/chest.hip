@@ -27,7 +27,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 __global__ __launch_bounds__(256) void chest_kernel(const float2* __restrict__ grid, float2* __restrict__ ce,
                                                    const MiSfDesc* __restrict__ sfs,
                                                    const MiCellDesc* __restrict__ cells,
-                                                   const float2* __restrict__ crs, float* __restrict__ metrics) {
+                                                   const float2* __restrict__ crs, float* __restrict__ metrics,
+                                                   uint32_t compact) {
   constexpr int PL[4] = {0, 4, 7, 11};
   constexpr float W1 = 0.1f, W0 = 0.8f;
   __shared__ float2 hp[4][2 * NRB_MAX];
@@ -81,7 +82,8 @@ __global__ __launch_bounds__(256) void chest_kernel(const float2* __restrict__ g
     __syncthreads();
     // frequency interpolation of the 4 pilot symbols at subcarrier k (kept in registers), then the
     // time interpolation / extrapolation of all 14 symbols at k: coalesced rows of ce[port][l][k]
-    float2* cp = ce + d.ce_off + (size_t)p * NSYMB * W;
+    // compact (MI_DL_FLAG_CE_COMPACT): the 4 frequency-interpolated pilot rows [port][4][W] only
+    float2* cp = ce + d.ce_off + (size_t)p * (compact ? 4 : NSYMB) * W;
     for (int k = tid; k < W; k += 256) {
       float2 hk[4];
 #pragma unroll
@@ -94,13 +96,13 @@ __global__ __launch_bounds__(256) void chest_kernel(const float2* __restrict__ g
         const float2 a = hs[i][m], b = hs[i][m + 1];
         hk[i] = make_float2(a.x + frac * (b.x - a.x), a.y + frac * (b.y - a.y));
       }
+      if (compact) {
 #pragma unroll
-      for (int l = 0; l < NSYMB; l++) {
-        const int ia = l <= 4 ? 0 : (l <= 7 ? 1 : 2), ib = ia + 1;
-        const float tt = (float)(l - PL[ia]) / (float)(PL[ib] - PL[ia]);
-        const float2 a = hk[ia], b = hk[ib];
-        cp[l * W + k] = make_float2(a.x + tt * (b.x - a.x), a.y + tt * (b.y - a.y));
+        for (int i = 0; i < 4; i++) cp[i * W + k] = hk[i];
+        continue;
       }
+#pragma unroll
+      for (int l = 0; l < NSYMB; l++) cp[l * W + k] = ce_time_interp(hk[ce_ia(l)], hk[ce_ia(l) + 1], CE_TT[l]);
     }
     __syncthreads();
   }
@@ -122,9 +124,10 @@ __global__ __launch_bounds__(256) void chest_kernel(const float2* __restrict__ g
 }
 
 void launch_chest(const float2* grid, float2* ce, const MiSfDesc* sfs, const MiCellDesc* cells, const float2* crs,
-                  float* metrics, uint32_t n_sf, hipStream_t st) {
+                  float* metrics, uint32_t n_sf, hipStream_t st, bool compact) {
   if (!n_sf) return;
-  hipLaunchKernelGGL(chest_kernel, dim3(n_sf), dim3(256), 0, st, grid, ce, sfs, cells, crs, metrics);
+  hipLaunchKernelGGL(chest_kernel, dim3(n_sf), dim3(256), 0, st, grid, ce, sfs, cells, crs, metrics,
+                     (uint32_t)compact);
 }
 
 }  // namespace mi

@@ -25,6 +25,23 @@ constexpr int KMAX = 6144;           // largest turbo code block
 constexpr int NCB_MAX = 3 * 32 * ((KMAX + 4 + 31) / 32);   // 18528
 constexpr int LANES = 64;            // code blocks per wavefront group (one CB per lane)
 constexpr int BETA_W = 4;            // beta register window of the turbo kernel
+// channel estimation: CRS pilot symbols of a port-0/1 subframe and the linear time interpolation /
+// extrapolation of the pilot symbols' rows to symbol l (chest.hip writes it, the compact-estimate consumers
+// recompute it: one table and one expression, so both give the same floats)
+constexpr int CE_PL[4] = {0, 4, 7, 11};
+__host__ __device__ constexpr int ce_ia(int l) { return l <= 4 ? 0 : (l <= 7 ? 1 : 2); }
+__host__ __device__ constexpr float ce_tt_of(int l) {
+  return (float)(l - CE_PL[ce_ia(l)]) / (float)(CE_PL[ce_ia(l) + 1] - CE_PL[ce_ia(l)]);
+}
+constexpr float CE_TT[NSYMB] = {ce_tt_of(0), ce_tt_of(1), ce_tt_of(2), ce_tt_of(3), ce_tt_of(4), ce_tt_of(5), ce_tt_of(6),
+                                ce_tt_of(7), ce_tt_of(8), ce_tt_of(9), ce_tt_of(10), ce_tt_of(11), ce_tt_of(12), ce_tt_of(13)};
+// CE_TT[l] for a run-time l without a table load: quarters are exact, thirds are the table's constants
+__host__ __device__ inline float ce_tt(int l) {
+  return l <= 4 ? 0.25f * (float)l : l == 5 ? CE_TT[5] : l == 6 ? CE_TT[6] : l == 7 ? 1.0f : 0.25f * (float)(l - 7);
+}
+__host__ __device__ inline float2 ce_time_interp(float2 a, float2 b, float tt) {
+  return make_float2(__builtin_fmaf(tt, b.x - a.x, a.x), __builtin_fmaf(tt, b.y - a.y, a.y));
+}
 #ifndef MI_TDEC_CK
 #define MI_TDEC_CK 4
 #endif
@@ -112,7 +129,7 @@ struct MiLaneSrc {           // one per code block: where the fused demap stage 
   uint32_t re, scr;          // offsets of the PDSCH RE list and scrambling words
   uint32_t qm, tm2;          // bits per symbol, SFBC
   uint32_t eb;               // LLR index of the code block's first LLR within its subframe
-  uint32_t pad;
+  uint32_t wdiv;             // floor(2^32 / W) + 1: RE index / W = __umulhi(re, wdiv) (compact estimates)
 };
 
 struct MiGroupDesc {         // one per wavefront group of <= 64 code blocks of equal K

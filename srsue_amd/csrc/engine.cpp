@@ -209,6 +209,12 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     if (prof) (void)hipEventRecord(ev[i], st);
   };
   const uint32_t nsf = (uint32_t)P.sfs.size();
+  // compact channel estimates (MI_DL_FLAG_CE_COMPACT): only when this run both writes and consumes them
+  // (channel estimation and the fused demap in one run), nothing else reads the full estimates, and no
+  // code block repeats LLRs (the single-LLR repetition path reads full estimates)
+  const uint32_t full = (1u << MI_DL_STAGE_CHEST) | (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM);
+  const bool compact = (flags & MI_DL_FLAG_CE_COMPACT) && !(flags & MI_DL_FLAG_KEEP_LLR) && P.has_pdsch &&
+                       (mask & full) == full && !P.rm_rep;
   mark(0);
   if (mask & (1u << MI_DL_STAGE_OFDM)) {
     for (size_t i = 0; i < P.fft_lists.size(); i++) {
@@ -221,7 +227,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   mark(1);
   if (mask & (1u << MI_DL_STAGE_CHEST))
     launch_chest(d_grid.as<float2>(), d_ce.as<float2>(), d_sfs.as<MiSfDesc>(), d_cells.as<MiCellDesc>(),
-                 d_crs.as<float2>(), d_metrics.as<float>(), nsf, st);
+                 d_crs.as<float2>(), d_metrics.as<float>(), nsf, st, compact);
   mark(2);
   if (P.has_pdsch) {
     float* sb = sb_override ? sb_override : d_sb.as<float>();
@@ -237,7 +243,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                       d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind, rm_items(),
-                      P.rm_busy, (uint32_t)P.rm_items.size(), st);
+                      P.rm_busy, (uint32_t)P.rm_items.size(), compact, st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,

@@ -11,7 +11,8 @@ void launch_ofdm_rx(int N, const void* iq, bool sc16, float2* grid, const MiSfDe
                     uint32_t n, const float2* tw, uint32_t W, hipStream_t st);
 // channel estimation (srslte_chest_dl_estimate): one workgroup per subframe, all ports
 void launch_chest(const float2* grid, float2* ce, const MiSfDesc* sfs, const MiCellDesc* cells,
-                  const float2* crs, float* metrics, uint32_t n_sf, hipStream_t st);
+                  const float2* crs, float* metrics, uint32_t n_sf, hipStream_t st,
+                  bool compact = false /* MI_DL_FLAG_CE_COMPACT: only the 4 pilot rows per port */);
 // equalise + soft demap + descramble (srslte_predecoding_* / demod_soft / scrambling_f)
 void launch_demap(const float2* grid, const float2* ce, float* e, const MiSfDesc* sfs,
                   const MiPdschDesc* pd, const MiCellDesc* cells, const uint32_t* re_tab,
@@ -25,7 +26,7 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind /* Qm + 8 TM2 common to all lanes, 0 = mixed */,
                      const uint32_t* items /* Plan::rm_items, NULL = every chunk */, uint32_t n_busy, uint32_t n_items,
-                     hipStream_t st);
+                     bool compact_ce, hipStream_t st);
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
 // window masks of the sparse softbuffer rows (which decoder inputs have a materialised row)
 void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,

@@ -46,6 +46,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
   pairs.clear();
   rm_busy = 0;
+  rm_rep = false;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
   max_units = max_ncb = n_cb = 0;
@@ -236,8 +237,12 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     if (!ld.valid) continue;
     const MiSfDesc& sd = sfs[ld.tb];
     const MiPdschDesc& pd = pds[sd.pdsch];
-    lane_src[li] = MiLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * cells[sd.cell].W, pd.re_off, pd.scr_off, pd.Qm,
-                             pd.tm == 2 ? 1u : 0u, (uint32_t)(ld.e_off - sd.e_off), 0};
+    // pad: floor(2^32 / W) + 1, so that __umulhi(re, pad) = re / W exactly for every RE index (< 2^32 / W)
+    const uint32_t W = cells[sd.cell].W;
+    lane_src[li] = MiLaneSrc{sd.grid_off, sd.ce_off, (uint32_t)NSYMB * W, pd.re_off, pd.scr_off, pd.Qm,
+                             pd.tm == 2 ? 1u : 0u, (uint32_t)(ld.e_off - sd.e_off),
+                             (uint32_t)(0x100000000ull / W + 1)};
+    rm_rep |= ld.E > ld.Nv;
   }
   unit_kind = 0;
   bool mixed = false;

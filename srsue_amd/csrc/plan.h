@@ -30,6 +30,7 @@ struct PlanData {
   // of every group included: it writes the group's zero row), then the other chunks (rm_busy items first)
   std::vector<uint32_t> rm_items;
   uint32_t rm_busy = 0;
+  bool rm_rep = false;                    // some code block repeats LLRs (E > N_v): no compact estimates
   std::vector<MiGroupDesc> groups;
   // pairs of equal-K groups for the packed two-code-blocks-per-lane turbo decoder (tdec_p2_body.h):
   // [2p] = group A, [2p + 1] = group B or 0xFFFFFFFF; a pair's decoder scratch spans both groups' regions

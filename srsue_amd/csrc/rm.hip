@@ -47,7 +47,17 @@ struct RmFuse {
   const uint32_t* re_tab;
   const uint32_t* scr_tab;
   float noise;
+  uint32_t compact;          // MI_DL_FLAG_CE_COMPACT: ce holds the 4 pilot rows [port][4][W] per subframe
 };
+
+// channel estimate of port plane cp at RE index ra (= l W + k): full estimates are read; compact ones are
+// interpolated in time from the two pilot rows around symbol l with chest.hip's expression (identical floats)
+__device__ __forceinline__ float2 ce_at(const RmFuse& f, const MiLaneSrc& src, const float2* cp, uint32_t ra) {
+  if (!f.compact) return cp[ra];
+  const uint32_t W = src.c1 / NSYMB, l = __umulhi(ra, src.wdiv), k = ra - l * W;
+  const int ia = ce_ia((int)l);
+  return ce_time_interp(cp[ia * W + k], cp[(ia + 1) * W + k], ce_tt((int)l));
+}
 
 // All LLRs of one demap unit (TM1: one RE, QM LLRs; TM2: one SFBC RE pair, 2 QM LLRs), descrambled, into
 // the tile positions of [ga, gb): demap_kernel's arithmetic (demap_body.h).  Split in three so that the
@@ -80,13 +90,13 @@ __device__ __forceinline__ UnitIn fused_data(const RmFuse& f, const MiLaneSrc& s
   const float2* c0 = f.ce + src.coff;
   UnitIn d;
   d.r0 = g[x.ra];
-  d.h00 = c0[x.ra];
+  d.h00 = ce_at(f, src, c0, x.ra);
   if constexpr (TM2) {
-    const float2* c1 = c0 + src.c1;
+    const float2* c1 = c0 + (f.compact ? 4 * (src.c1 / NSYMB) : src.c1);
     d.r1 = g[x.rb];
-    d.h01 = c0[x.rb];
-    d.h10 = c1[x.ra];
-    d.h11 = c1[x.rb];
+    d.h01 = ce_at(f, src, c0, x.rb);
+    d.h10 = ce_at(f, src, c1, x.ra);
+    d.h11 = ce_at(f, src, c1, x.rb);
   }
   d.s0 = x.s0;
   d.s1 = x.s1;
@@ -457,12 +467,12 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
-                     const uint32_t* items, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
+                     const uint32_t* items, uint32_t n_busy, uint32_t n_items, bool compact_ce, hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
   const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
-  const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise};
+  const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise, (uint32_t)compact_ce};
 #define MI_RM_LAUNCH(...) \
   hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items)
   switch (unit_kind) {   // Qm + 8 * (TM2)

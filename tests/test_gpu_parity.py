@@ -24,8 +24,9 @@ DECODERS = [(False, "lane"), (True, "lane"), (True, "win"), (False, "lanex"), (T
             (True, "p2")]
 
 
-def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None, keep_llr=False):
-    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16, sched=sched, keep_llr=keep_llr)
+def run_batch(cfgs, iqs, max_its=4, profile=False, tdec_i16=False, sched=None, keep_llr=False, compact_ce=False):
+    b = abi.Batch(cfgs, max_its=max_its, profile=profile, tdec_i16=tdec_i16, sched=sched, keep_llr=keep_llr,
+                  compact_ce=compact_ce)
     flat = np.zeros(2 * b.iq_samples, np.float32)
     for i, iq in enumerate(iqs):
         o = 2 * b.iq_offset(i)
@@ -100,6 +101,26 @@ def test_fused_demap_rate_dematching_matches_unfused(snr):
         assert np.array_equal(a, f)
     if snr >= 30.0:
         assert res[1][1].all()
+
+
+@pytest.mark.parametrize("snr", [30.0, 19.0])
+def test_compact_channel_estimates_identical_softbuffer(snr):
+    """MI_DL_FLAG_CE_COMPACT: channel estimation writes only the 4 pilot rows per port and the fused demap
+    interpolates each RE's estimate in time with the chest kernel's own expression.  The rate-de-matched
+    softbuffer must be bit-identical to the full-estimate run (every float of the arena), and so payload,
+    TB CRC and per-code-block iterations, over every configuration of CASES (TM1/TM2, 1.4-20 MHz, sync
+    holes, filler bits, rv 2)."""
+    cfgs = [abi.sf_cfg(**c) for c in CASES]
+    iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=int(snr) + 7)
+    res = []
+    for compact in (False, True):
+        b = run_batch(cfgs, iqs, tdec_i16=True, compact_ce=compact)
+        res.append((b.download(abi.BUF_SB, np.uint32), b.download(abi.BUF_PAYLOAD, np.uint8),
+                    b.download(abi.BUF_TB_CRC, np.uint32), b.download(abi.BUF_CB_ITS, np.uint32)))
+        b.close()
+    for a, c in zip(res[0], res[1]):
+        assert np.array_equal(a, c)
+    assert res[0][0].any()
 
 
 @pytest.mark.parametrize("i16,sched", DECODERS)

@@ -2,6 +2,8 @@
 srslte_dci_msg_to_dl_grant at phch_worker.cc:297).  No copy of 36.213 or srsLTE is in the container, so the
 table is pinned by the invariants the specification guarantees plus the columns carried independently by
 the oracle (N_PRB 6/25/50/100) and the small-allocation columns N_PRB 1..5."""
+import os
+
 import pytest
 
 # 36.213 Table 7.1.7.2.1-1, I_TBS 0..26, for N_PRB = 1..5
@@ -63,3 +65,21 @@ def test_out_of_range(built):
     L = abi.lib()
     assert L.srslte_ra_tbs_from_idx(27, 50) == -1 and L.srslte_ra_tbs_from_idx(0, 0) == -1
     assert L.srslte_ra_tbs_from_idx(0, 111) == -1
+
+
+def test_compact_estimate_weights_match_table(tmp_path):
+    """ce_tt(l) (the table-free time-interpolation weight the compact-estimate consumers use) equals the
+    CE_TT table the chest kernel uses, bit for bit, for every symbol (dl_common.h)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("needs g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "t.cpp"
+    src.write_text('#include <string.h>\n#include "dl_common.h"\nint main() { int bad = 0;\n'
+                   '  for (int l = 0; l < mi::NSYMB; l++) { float a = mi::ce_tt(l), b = mi::CE_TT[l];\n'
+                   '    bad += memcmp(&a, &b, 4) != 0; }\n  return bad; }\n')
+    exe = tmp_path / "t"
+    subprocess.check_call(["g++", "-std=c++17", "-DMI_EMU", "-I", os.path.join(root, "srsue_amd", "csrc"), "-I",
+                           os.path.join(root, "include"), str(src), "-o", str(exe)])
+    assert subprocess.run([str(exe)]).returncode == 0
