@@ -98,27 +98,60 @@ __device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gs
   __syncthreads();
 }
 
+// The first stage (radix 8 for every size) reads the symbol's IQ straight from HBM.  Its loads are split
+// off (FirstIn / first_load) so the subframe loop can issue the NEXT symbol's loads before the current
+// symbol's LDS stages run: the HBM latency of every symbol but the first hides behind a symbol of work.
+template <int N>
+struct FirstIn {
+  static constexpr int NB = N / 8, PER = (NB + 255) / 256;
+  float2 v[PER][8];
+};
 template <int N, typename IQ>
-__device__ __forceinline__ void fft_symbol(float2* buf, const IQ* __restrict__ src, const float2* tw) {
+__device__ __forceinline__ void first_load(const IQ* __restrict__ src, FirstIn<N>& f) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < FirstIn<N>::PER; p++) {
+    const int j = tid + p * 256;
+    if (j < FirstIn<N>::NB) {
+#pragma unroll
+      for (int r = 0; r < 8; r++) f.v[p][r] = load_iq(src, j + r * FirstIn<N>::NB);
+    }
+  }
+}
+// fft_stage<N, 8, true> on loaded values (Ns = 1: no twiddles); the caller synchronised buf's readers
+template <int N>
+__device__ __forceinline__ void first_stage(float2* buf, FirstIn<N>& f) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < FirstIn<N>::PER; p++) {
+    const int j = tid + p * 256;
+    if (j < FirstIn<N>::NB) {
+      dft<8>(f.v[p]);
+#pragma unroll
+      for (int r = 0; r < 8; r++) buf[j * 8 + r] = f.v[p][r];
+    }
+  }
+  __syncthreads();
+}
+// the stages after the first
+template <int N, typename IQ>
+__device__ __forceinline__ void fft_rest(float2* buf, const float2* tw) {
   if constexpr (N == 2048) {
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 8, false, IQ>(buf, src, tw, 64); fft_stage<N, 4, false, IQ>(buf, src, tw, 512);
+    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 512);
   } else if constexpr (N == 1536) {
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 8, false, IQ>(buf, src, tw, 64); fft_stage<N, 3, false, IQ>(buf, src, tw, 512);
+    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 3, false, IQ>(buf, nullptr, tw, 512);
   } else if constexpr (N == 1024) {
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 4, false, IQ>(buf, src, tw, 64); fft_stage<N, 4, false, IQ>(buf, src, tw, 256);
+    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 256);
   } else if constexpr (N == 512) {
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 8, false, IQ>(buf, src, tw, 64);
+    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
   } else if constexpr (N == 256) {
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 8, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 4, false, IQ>(buf, src, tw, 64);
+    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
   } else {
     static_assert(N == 128, "unsupported FFT size");
-    fft_stage<N, 8, true, IQ>(buf, src, tw, 1); fft_stage<N, 4, false, IQ>(buf, src, tw, 8);
-    fft_stage<N, 4, false, IQ>(buf, src, tw, 32);
+    fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 32);
   }
 }
 
@@ -138,8 +171,13 @@ __global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq,
   const IQ* src_sf = iq + d.iq_off;
   float2* dst = grid + d.grid_off;
   const int l0 = (int)blockIdx.y * per;
+  FirstIn<N> cur, nxt;
+  first_load<N, IQ>(src_sf + symbol_offset(N, l0), nxt);
   for (int l = l0; l < l0 + per; l++) {
-    fft_symbol<N, IQ>(buf, src_sf + symbol_offset(N, l), tw);
+    cur = nxt;
+    if (l + 1 < l0 + per) first_load<N, IQ>(src_sf + symbol_offset(N, l + 1), nxt);   // in flight meanwhile
+    first_stage<N>(buf, cur);
+    fft_rest<N, IQ>(buf, tw);
     for (int k = threadIdx.x; k < (int)W; k += 256) dst[l * W + k] = buf[sc_bin(k, (int)W, N)];
     __syncthreads();
   }
