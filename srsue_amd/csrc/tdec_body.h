@@ -156,6 +156,13 @@ MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
 #ifndef MI_ROW_BUFFER
 #define MI_ROW_BUFFER 1
 #endif
+// MI_ROW_CROW_SOFF: the compile-time row delta goes into the wave-uniform soffset instead of the lane
+// offset.  In the VGPR form LICM hoists every distinct (lane + crow * 64) * size out of the window loops
+// -- one loop-invariant VGPR per row delta, live across the whole pass -- instead of leaving the
+// constant in the instruction's immediate offset.
+#ifndef MI_ROW_CROW_SOFF
+#define MI_ROW_CROW_SOFF 1
+#endif
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
 __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
@@ -164,8 +171,13 @@ __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
 // immediate offset): consecutive rows of one window share a single soffset SGPR
 template <class T>
 __device__ inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
+#if MI_ROW_CROW_SOFF
+  const uint32_t so = ((uint32_t)row + crow) * (uint32_t)(LANES * sizeof(T));
+  const uint32_t vo = (uint32_t)lane * (uint32_t)sizeof(T);
+#else
   const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
   const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
+#endif
   if constexpr (sizeof(T) == 4)
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), vo, so, 0));
   else if constexpr (sizeof(T) == 2)
@@ -175,8 +187,13 @@ __device__ inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 
 }
 template <class T>
 __device__ inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
+#if MI_ROW_CROW_SOFF
+  const uint32_t so = ((uint32_t)row + crow) * (uint32_t)(LANES * sizeof(T));
+  const uint32_t vo = (uint32_t)lane * (uint32_t)sizeof(T);
+#else
   const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
   const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
+#endif
   if constexpr (sizeof(T) == 4)
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), row_rsrc(base), vo, so, 0);
   else if constexpr (sizeof(T) == 2)

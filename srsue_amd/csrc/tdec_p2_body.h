@@ -38,7 +38,7 @@ struct TdecArgsP2 {
   const uint32_t* crc_a;  // [K] CRC24A / CRC24B single-bit contributions
   const uint32_t* crc_b;
   const uint32_t* crc8;   // [256] CRC24A byte table
-  uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][8]
+  uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][7]
   uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
   uint8_t* cb_bytes[2];   // each half's packed output row
   uint32_t K, F[2], crc24a[2], max_its, early_stop;
@@ -70,7 +70,7 @@ struct TdecWinP2 {
   uint32_t s0[BETA_W], s1[BETA_W];
   float a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
   uint32_t r0[BETA_W], r1[BETA_W];
-  uint32_t ck[8];
+  uint32_t ck[7];
 };
 
 MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
@@ -128,41 +128,48 @@ MI_HD inline void p2_load_window_mkq(const TdecArgsP2& a, int lane, uint32_t bas
   }
 }
 
-// checkpoint record c: states 1..7 of both code blocks (state 0 is 0), [c][lane][8] u32, two 128-bit
-// accesses per lane
+// checkpoint record c: states 1..7 of both code blocks (state 0 is 0), [c][lane][7] u32 -- one 128-bit and
+// one 96-bit access per lane, the 64 lanes' records one contiguous 1,792-B run (no padding word: an
+// eighth of the checkpoint traffic saved)
+constexpr uint32_t P2_CKW = 7;
 MI_HD inline void p2_ck_store(uint32_t* scr, size_t ck0, uint32_t c, int lane, const P2 (&b)[8]) {
-  uint32_t w[8];
+  uint32_t w[P2_CKW];
 #pragma unroll
   for (int k = 0; k < 7; k++) w[k] = p2_bits(b[k + 1]);
-  w[7] = 0u;
-  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * 4), vo = (uint32_t)lane * 32u;
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * P2_CKW * LANES) * 4), vo = (uint32_t)lane * (4 * P2_CKW);
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u3 __attribute__((ext_vector_type(3)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
   __builtin_amdgcn_raw_buffer_store_b128(u4{w[0], w[1], w[2], w[3]}, rs, vo, so, 0);
-  __builtin_amdgcn_raw_buffer_store_b128(u4{w[4], w[5], w[6], w[7]}, rs, vo + 16, so, 0);
+  __builtin_amdgcn_raw_buffer_store_b96(u3{w[4], w[5], w[6]}, rs, vo + 16, so, 0);
 #else
   memcpy(reinterpret_cast<char*>(scr) + so + vo, w, sizeof(w));
 #endif
 }
-MI_HD inline void p2_ck_load(const uint32_t* scr, size_t ck0, uint32_t c, int lane, TdecWinP2& r) {
-  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * 4), vo = (uint32_t)lane * 32u;
+MI_HD inline void p2_ck_load_to(const uint32_t* scr, size_t ck0, uint32_t c, int lane, uint32_t (&ck)[P2_CKW]) {
+  const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * P2_CKW * LANES) * 4), vo = (uint32_t)lane * (4 * P2_CKW);
 #if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u3 __attribute__((ext_vector_type(3)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
   const u4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
-  const u4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16, so, 0);
-  r.ck[0] = v0.x; r.ck[1] = v0.y; r.ck[2] = v0.z; r.ck[3] = v0.w;
-  r.ck[4] = v1.x; r.ck[5] = v1.y; r.ck[6] = v1.z; r.ck[7] = v1.w;
+  const u3 v1 = __builtin_amdgcn_raw_buffer_load_b96(rs, vo + 16, so, 0);
+  ck[0] = v0.x; ck[1] = v0.y; ck[2] = v0.z; ck[3] = v0.w;
+  ck[4] = v1.x; ck[5] = v1.y; ck[6] = v1.z;
 #else
-  memcpy(r.ck, reinterpret_cast<const char*>(scr) + so + vo, sizeof(r.ck));
+  memcpy(ck, reinterpret_cast<const char*>(scr) + so + vo, sizeof(ck));
 #endif
 }
-MI_HD inline void p2_ck_vec(const TdecWinP2& r, P2 (&v)[8]) {
+MI_HD inline void p2_ck_load(const uint32_t* scr, size_t ck0, uint32_t c, int lane, TdecWinP2& r) {
+  p2_ck_load_to(scr, ck0, c, lane, r.ck);
+}
+MI_HD inline void p2_ck_vec(const uint32_t (&ck)[7], P2 (&v)[8]) {
   v[0] = Metric<P2>::zero();
 #pragma unroll
-  for (int s = 1; s < 8; s++) v[s] = p2_from_bits(r.ck[s - 1]);
+  for (int s = 1; s < 8; s++) v[s] = p2_from_bits(ck[s - 1]);
 }
+MI_HD inline void p2_ck_vec(const TdecWinP2& r, P2 (&v)[8]) { p2_ck_vec(r.ck, v); }
 
 // decoder inputs (xs, xp) of step base + i; filler bits (k < F, known zeros; F < 64) of each half get
 // q(FILLER_LLR) = -511 in the systematic and parity-1 inputs
@@ -330,6 +337,168 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
   norm8<true>(b);
 }
 
+// ---- 8-step checkpoint spacing (MI_TDEC_P2_CK8, default) -------------------------------------------
+// The phase-1 passes store a checkpoint every second window (8 steps) and the phase-2 passes walk PAIRS
+// of windows between them: half the checkpoint stores and loads (8 of the ~35 B per code block and
+// step), and each pair's loads are issued once the previous pair's inputs are converted, so they are in
+// flight for 8 steps of compute with a single raw buffer.  The 8 metric vectors a pair needs are
+// recomputed by halving (the checkpoint, the vector 4 steps in, normalised, then 2 and 1 steps from
+// those): 12 recursion steps per 8 instead of 6, in the same 4 live vectors as the 4-step register
+// form.  Every LLR still takes its alpha and beta at most 3 unnormalised steps from a normalised vector
+// and the running metrics are normalised after every 4 steps exactly as before, so the int16 bounds
+// (p2.h) and every output are unchanged; only the traversal of the recomputation differs.
+#ifndef MI_TDEC_P2_CK8
+#define MI_TDEC_P2_CK8 1
+#endif
+// scheduling fences keep the pair's recomputation in program order (left alone, the scheduler interleaves
+// the independent metric chains and the next pair's loads, and the live vectors exceed the register budget)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MI_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MI_SCHED_FENCE() ((void)0)
+#endif
+struct TdecWin8P2 {
+  TdecWinP2 lo, hi;
+  uint32_t ck[P2_CKW];
+};
+struct TdecX8P2 { P2 xs[2 * BETA_W], xp[2 * BETA_W]; };
+
+template <bool DEC2, bool SQ>
+MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t base, TdecX8P2& x) {
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, r.lo, i, base, x.xs[i], x.xp[i]);
+#pragma unroll
+  for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, r.hi, i, base + BETA_W, x.xs[BETA_W + i], x.xp[BETA_W + i]);
+}
+MI_HD inline void p2_cp8(P2 (&d)[8], const P2 (&s)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) d[k] = s[k];
+}
+// the start of a recomputation chain: an opaque copy, so GVN cannot merge the recomputed chain with the
+// chain that produced the same values earlier (which would keep every intermediate vector live: the
+// register form this layout avoids)
+MI_HD inline void p2_cp8_opaque(P2 (&d)[8], const P2 (&s)[8]) {
+  p2_cp8(d, s);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+  for (int k = 0; k < 8; k++) asm volatile("" : "+v"(d[k].v));
+#endif
+}
+// v <- the backward recursion through steps hi .. lo (inputs x[hi] down to x[lo])
+template <int HI, int LO>
+MI_HD inline void p2_beta_run(P2 (&v)[8], const TdecX8P2& x) {
+#pragma unroll
+  for (int i = HI; i >= LO; i--) {
+    P2 nb[8];
+    beta_step<false>(v, x.xs[i], x.xp[i], nb);
+    p2_cp8(v, nb);
+  }
+}
+// v <- the forward recursion through steps lo .. hi
+template <int LO, int HI>
+MI_HD inline void p2_alpha_run(P2 (&v)[8], const TdecX8P2& x) {
+#pragma unroll
+  for (int i = LO; i <= HI; i++) alpha_fwd<false>(v, x.xs[i], x.xp[i]);
+}
+// wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1)
+template <bool DEC2>
+MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
+                                   P2 (&al)[8], uint32_t (&crc)[2]) {
+  P2 B4[8], Bm[8], Bt[8];
+#define emit(I, BN) p2_emit<DEC2>(a, lane, base, I, alpha_step<false>(al, BN, x.xs[I], x.xp[I]), x.xs[I], crc)
+  p2_cp8_opaque(B4, B8);
+  p2_beta_run<7, 4>(B4, x);
+  norm8<true>(B4);
+  p2_cp8_opaque(Bm, B4);
+  p2_beta_run<3, 2>(Bm, x);   // B(2)
+  p2_cp8_opaque(Bt, Bm);
+  p2_beta_run<1, 1>(Bt, x);   // B(1)
+  MI_SCHED_FENCE();
+  emit(0, Bt);
+  MI_SCHED_FENCE();
+  emit(1, Bm);
+  p2_cp8_opaque(Bt, B4);
+  p2_beta_run<3, 3>(Bt, x);   // B(3)
+  MI_SCHED_FENCE();
+  emit(2, Bt);
+  MI_SCHED_FENCE();
+  emit(3, B4);
+  norm8<true>(al);
+  p2_cp8_opaque(Bm, B8);
+  p2_beta_run<7, 6>(Bm, x);   // B(6)
+  p2_cp8_opaque(Bt, Bm);
+  p2_beta_run<5, 5>(Bt, x);   // B(5)
+  MI_SCHED_FENCE();
+  emit(4, Bt);
+  MI_SCHED_FENCE();
+  emit(5, Bm);
+  p2_cp8_opaque(Bt, B8);
+  p2_beta_run<7, 7>(Bt, x);   // B(7)
+  MI_SCHED_FENCE();
+  emit(6, Bt);
+  MI_SCHED_FENCE();
+  emit(7, B8);
+  norm8<true>(al);
+#undef emit
+}
+// LLR of step I from alpha_I (av) and the running beta_{I + 1}, then beta_I
+template <bool DEC2, bool FIRST_WIN, int I>
+MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&av)[8], uint32_t base,
+                                   P2 (&b)[8], uint32_t (&crc)[2]) {
+  P2 llr;
+  // reachable alpha states at steps 0, 1, 2 from state 0 (p2_beta_emit_window)
+  if (FIRST_WIN && I == 0) llr = llr_step<0x01u>(av, b, x.xs[I], x.xp[I]);
+  else if (FIRST_WIN && I == 1) llr = llr_step<0x11u>(av, b, x.xs[I], x.xp[I]);
+  else if (FIRST_WIN && I == 2) llr = llr_step<0x55u>(av, b, x.xs[I], x.xp[I]);
+  else llr = llr_step(av, b, x.xs[I], x.xp[I]);
+  p2_emit<DEC2>(a, lane, base, I, llr, x.xs[I], crc);
+  P2 nb[8];
+  beta_step<false>(b, x.xs[I], x.xp[I], nb);
+  p2_cp8(b, nb);
+}
+// wave B, phase 2, one pair: A(j) = alpha_{base + j}, A(0) = the checkpoint (pair 0: the start state);
+// LLR i from A(i) and beta_{base + i + 1} (the running b)
+template <bool DEC2, bool FIRST_WIN>
+MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
+                                       uint32_t base, P2 (&b)[8], uint32_t (&crc)[2]) {
+  P2 A4[8], Am[8], At[8];
+#define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b, crc)
+  p2_cp8_opaque(A4, A0);
+  p2_alpha_run<0, 3>(A4, x);
+  norm8<true>(A4);
+  p2_cp8_opaque(Am, A4);
+  p2_alpha_run<4, 5>(Am, x);   // A(6)
+  p2_cp8_opaque(At, Am);
+  p2_alpha_run<6, 6>(At, x);   // A(7)
+  MI_SCHED_FENCE();
+  emit(7, At);
+  MI_SCHED_FENCE();
+  emit(6, Am);
+  p2_cp8_opaque(At, A4);
+  p2_alpha_run<4, 4>(At, x);   // A(5)
+  MI_SCHED_FENCE();
+  emit(5, At);
+  MI_SCHED_FENCE();
+  emit(4, A4);
+  norm8<true>(b);
+  p2_cp8_opaque(Am, A0);
+  p2_alpha_run<0, 1>(Am, x);   // A(2)
+  p2_cp8_opaque(At, Am);
+  p2_alpha_run<2, 2>(At, x);   // A(3)
+  MI_SCHED_FENCE();
+  emit(3, At);
+  MI_SCHED_FENCE();
+  emit(2, Am);
+  p2_cp8_opaque(At, A0);
+  p2_alpha_run<0, 0>(At, x);   // A(1)
+  MI_SCHED_FENCE();
+  emit(1, At);
+  MI_SCHED_FENCE();
+  emit(0, A0);
+  norm8<true>(b);
+#undef emit
+}
+
 #ifndef MI_TDEC_P2_PF_Q
 #define MI_TDEC_P2_PF_Q 1
 #endif
@@ -358,7 +527,7 @@ struct TdecP2X {
     pipe_windows<PF, Win>(
         (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
-          if (w) p2_ck_store(a.scr, ck, w, lane, al);
+          if (w && (!MI_TDEC_P2_CK8 || !((h - w) & 1u))) p2_ck_store(a.scr, ck, w, lane, al);
           if constexpr (MKQ) p2_alpha_only_window_mkq(a, lane, r, w * BETA_W, al);
           else p2_alpha_only_window<DEC2, SQB>(a, r, w * BETA_W, al);
         });
@@ -367,6 +536,36 @@ struct TdecP2X {
   MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8], uint32_t (&crc)[2]) {
     const uint32_t nw = a.K / BETA_W, h = nw / 2;
     const size_t ck = (size_t)2 * a.K;
+#if MI_TDEC_P2_CK8
+    // pairs (h + 2j, h + 2j + 1), beta checkpoint h + 2j + 2; an odd count leaves window nw - 1 alone
+    const uint32_t n = nw - h, np = n / 2;
+    auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
+      p2_ck_load_to(a.scr, ck, w0 + 2, lane, r.ck);
+    };
+    if (np) {
+      TdecWin8P2 r;
+      load8(h, r);
+      for (uint32_t j = 0; j < np; j++) {
+        const uint32_t w0 = h + 2 * j;
+        TdecX8P2 x;
+        P2 B8[8];
+        p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+        p2_ck_vec(r.ck, B8);
+        MI_SCHED_FENCE();
+        load8(j + 1 < np ? w0 + 2 : w0, r);   // the last pair reloads itself (unused)
+        MI_SCHED_FENCE();
+        p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al, crc);
+      }
+    }
+    if (n & 1u) {
+      Win r;
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, (nw - 1) * BETA_W, r);
+      p2_ck_load(a.scr, ck, nw, lane, r);
+      p2_alpha_window<DEC2, SQF>(a, lane, r, (nw - 1) * BETA_W, al, crc);
+    }
+#else
     pipe_windows<PF, Win>(
         (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
         [&](uint32_t w, Win& r) {
@@ -374,6 +573,7 @@ struct TdecP2X {
           p2_ck_load(a.scr, ck, w + 1, lane, r);
         },
         [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al, crc); });
+#endif
   }
   // wave B, phase 1: tail, then beta_K .. beta_{K/2}, beta checkpoints h + 1 .. nw
   MI_HD static void b1(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
@@ -425,13 +625,49 @@ struct TdecP2X {
         [&](const Win& r, uint32_t w) {
           if constexpr (MKQ) p2_beta_window_mkq(a, lane, r, w * BETA_W, b);
           else p2_beta_window<DEC2, SQB>(a, r, w * BETA_W, b);
-          if (w > h) p2_ck_store(a.scr, ck, w, lane, b);
+          if (w > h && (!MI_TDEC_P2_CK8 || !((w - h) & 1u))) p2_ck_store(a.scr, ck, w, lane, b);
         });
   }
   // wave B, phase 2: windows h - 1 .. 0 backward, LLRs of steps 0 .. K/2 - 1
   MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8], uint32_t (&crc)[2]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
+#if MI_TDEC_P2_CK8
+    // pairs (h - 2j - 2, h - 2j - 1), alpha checkpoint h - 2j - 2 (pair 0: the start state); an odd h
+    // leaves window 0 alone
+    const uint32_t np = h / 2;
+    auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
+      p2_ck_load_to(a.scr, ck, w0, lane, r.ck);   // w0 = 0: slot 0 is loaded but not used
+    };
+    if (np) {
+      TdecWin8P2 r;
+      load8(h - 2, r);
+      for (uint32_t j = 0; j < np; j++) {
+        const uint32_t w0 = h - 2 * j - 2;
+        TdecX8P2 x;
+        P2 A0[8];
+        p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+        if (w0) {
+          p2_ck_vec(r.ck, A0);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 8; s++) A0[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+        }
+        MI_SCHED_FENCE();
+        load8(j + 1 < np ? w0 - 2 : w0, r);   // the last pair reloads itself (unused)
+        MI_SCHED_FENCE();
+        if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b, crc);
+        else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b, crc);
+      }
+    }
+    if (h & 1u) {
+      Win r;
+      p2_load_window<DEC2, FIRST, SQF>(a, lane, 0, r);
+      p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b, crc);
+    }
+#else
     pipe_windows<PF, Win>(
         (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
         [&](uint32_t w, Win& r) {
@@ -442,6 +678,7 @@ struct TdecP2X {
           if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b, crc);
           else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b, crc);
         });
+#endif
   }
 };
 
