@@ -682,13 +682,20 @@ struct TdecP2X {
   }
 };
 
+#ifndef MI_TDEC_P2_DIAG
+#define MI_TDEC_P2_DIAG 0
+#endif
 template <bool DEC2, bool FIRST, int SRC, class Exec>
 MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex, uint32_t (&cF)[2], uint32_t (&cB)[2]) {
   using X = TdecP2X<DEC2, FIRST, SRC>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
+#if MI_TDEC_P2_DIAG != 2   // timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
+#endif
+#if MI_TDEC_P2_DIAG != 1
   ex.run([&] { X::f2(a, lane, mF, cF); }, [&] { X::b2(a, lane, mB, cB); });
+#endif
 }
 
 // pack half H's decisions MSB first and run its TB-payload bytes through the byte-wise CRC24A (the partial
