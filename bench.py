@@ -73,9 +73,9 @@ def kernel_src_hash():
     return h.hexdigest()[:16]
 
 
-PATH_SOURCES = ("cbscatter.hip", "chest.hip", "demap.hip", "dl_common.h", "engine.cpp", "engine.h", "kernels.h",
-                "kernels_consts.h", "ofdm.hip", "plan.cpp", "plan.h", "rm.hip", "rm_body.h", "tables.cpp", "tables.h",
-                "tb.hip", "tb_body.h", "tdec.hip", "tdec_body.h")
+PATH_SOURCES = ("cbscatter.hip", "chest.hip", "demap.hip", "demap_body.h", "dl_common.h", "engine.cpp", "engine.h",
+                "kernels.h", "kernels_consts.h", "ofdm.hip", "p2.h", "plan.cpp", "plan.h", "rm.hip", "rm_body.h",
+                "tables.cpp", "tables.h", "tb.hip", "tb_body.h", "tdec.hip", "tdec_body.h", "tdec_p2_body.h")
 
 
 def pmc_traffic(sf_per_gpu, tdec, kernel):

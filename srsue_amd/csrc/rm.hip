@@ -226,6 +226,10 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   if (tid < RM_CHUNK / 4) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
   if (!__syncthreads_or(busy)) return;
+#if MI_RM_DIAG_PROLOGUE   // timing diagnostic only: the descriptor chain alone (wrong results)
+  if (s_j0[tid & 63] == 0xFFFFFFFFu) sbg[tid] = 1.f;
+  return;
+#endif
   // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
   // all of a wavefront's loads issued before its LDS writes
   constexpr int ROWS = LANES / RM_NW, PER = RM_CHUNK / 64;
