@@ -109,6 +109,8 @@ def reduce_over_ranks(elapsed, n_ok, n_cb, world, device="cpu"):
     """The only cross-rank traffic: max of the elapsed time, sums of CRC-OK TBs and code blocks."""
     if world == 1:
         return elapsed, float(n_ok), float(n_cb)
+    if dist.get_backend() == "gloo":   # CPU rehearsal, or --share-gpu
+        device = "cpu"
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     s = torch.tensor([float(n_ok), float(n_cb)], dtype=torch.float64, device=device)
@@ -644,6 +646,8 @@ def main():
                          "4 for the low-occupancy configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; "
                          "profiles/r2/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="N-rank rehearsal on one GPU: every rank on GPU 0, gloo collectives (not a scaling number)")
     ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
     ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
@@ -686,7 +690,13 @@ def main():
         dry_run(args, world, rank)
         dist.destroy_process_group()
         return
-    if world > 1:
+    if world > 1 and args.share_gpu:
+        # rehearsal of the N-rank path on a one-GPU box: every rank decodes its shard on GPU 0, the
+        # timing barrier and the three-scalar reduction go over gloo (the ranks' kernels share the card,
+        # so the aggregate is not a scaling measurement)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -756,6 +766,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
+                       **({"share_gpu_rehearsal": True} if args.share_gpu and world > 1 else {}),
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),

@@ -110,3 +110,28 @@ def test_bench_rejects_world_mismatch(built):
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu(built):
+    """The N-rank launch on real hardware: `bench.py --gpus 2 --share-gpu` spawns two ranks that each decode
+    their contiguous shard with the HIP kernels on GPU 0, synchronise and reduce over gloo (the one-GPU box has
+    no second card for RCCL); rank 0 prints one line with n_gpus 2, the two shards' total and every TB
+    decoded (crc_ok_rate 1.0, no payload mismatch).  The rate is not a scaling figure (the ranks share a card)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--sf-per-gpu",
+                        "256", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--iterating-snr", "0"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["share_gpu_rehearsal"] is True
+    assert d["config"]["subframes_per_gpu"] == 256
+    assert d["crc_ok_rate"] == 1.0 and d["payload_mismatches_crc_ok"] == 0
