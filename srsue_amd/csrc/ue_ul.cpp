@@ -5,6 +5,7 @@
 // UlEngine planned for the current grant (cfg_grant), a device payload buffer and a device subframe.
 // A retransmission (rv > 0) re-encodes the TB kept in the HARQ softbuffer: the circular buffer is a
 // deterministic function of the TB, so this equals srsLTE's reuse of its stored coded bits.
+#include <time.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,7 +23,34 @@ struct mi_ue_ul_ctx {
   cf_t* h_iq = nullptr;
   mi_ul_cfg_t cfg{};
   bool planned = false;
+  // per-phase host-clock breakdown of pusch_encode (MI_UE_UL_PROF=1: the stream is synchronised at every
+  // mark so GPU work is attributed to its phase; printed to stderr when the instance is freed):
+  // 0 payload H2D, 1 plan, 2 table upload, 3 kernels, 4 IQ D2H + copy out
+  struct Prof {
+    bool on = getenv("MI_UE_UL_PROF") != nullptr;
+    double acc[5] = {}, last = 0;
+    uint64_t n[5] = {};
+    static double now() {
+      timespec t;
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+    }
+    void start() { if (on) last = now(); }
+    void mark(int i, hipStream_t s) {
+      if (!on) return;
+      (void)hipStreamSynchronize(s);
+      const double t = now();
+      acc[i] += t - last; n[i]++; last = t;
+    }
+  } prof;
   ~mi_ue_ul_ctx() {
+    if (prof.on) {
+      static const char* name[5] = {"payload_h2d", "plan", "upload", "kernels", "iq_d2h"};
+      fprintf(stderr, "{\"ue_ul_prof_us\": {");
+      for (int i = 0; i < 5; i++)
+        fprintf(stderr, "%s\"%s\": %.1f", i ? ", " : "", name[i], prof.n[i] ? prof.acc[i] / prof.n[i] : 0.0);
+      fprintf(stderr, "}}\n");
+    }
     if (st) (void)hipStreamSynchronize(st);
     if (h_pay) (void)hipHostFree(h_pay);
     if (h_iq) (void)hipHostFree(h_iq);
@@ -217,6 +245,7 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
   if (nbytes > TX_MAX_BYTES) return SRSLTE_ERROR;
   // the TB: new data from `data`; a retransmission without data re-encodes the softbuffer's copy
   const void* src = nullptr;
+  c->prof.start();
   if (data) {
     memcpy(c->h_pay, data, nbytes);   // the previous call's DMA out of h_pay ended with its stream sync
     if (!mi::hip_ok(hipMemcpyAsync(c->d_pay.p, c->h_pay, nbytes, hipMemcpyHostToDevice, c->st), "H2D payload"))
@@ -233,16 +262,22 @@ int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t* q, uint8_t* data, 
     mi::set_error("no data and no stored TB of this size in the softbuffer");
     return SRSLTE_ERROR;
   }
+  c->prof.mark(0, c->st);
   mi::UlPlan& P = c->eng.plan;
   if (P.build(&c->cfg, 1)) return SRSLTE_ERROR;
   if (q->normalize_en) P.txs[0].scale = (float)q->cell.nof_prb / 15.0f / sqrtf((float)c->cfg.L_prb);
   if (q->cfo_en) P.txs[0].cfo = q->current_cfo;
+  c->prof.mark(1, c->st);
   const size_t n = (size_t)15 * mi::symbol_sz(q->cell.nof_prb);
-  if (c->eng.upload(c->st) || c->eng.run(src, c->d_iq.p, c->st) ||
-      !mi::hip_ok(hipMemcpyAsync(c->h_iq, c->d_iq.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H IQ") ||
+  if (c->eng.upload(c->st)) return SRSLTE_ERROR;
+  c->prof.mark(2, c->st);
+  if (c->eng.run(src, c->d_iq.p, c->st)) return SRSLTE_ERROR;
+  c->prof.mark(3, c->st);
+  if (!mi::hip_ok(hipMemcpyAsync(c->h_iq, c->d_iq.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H IQ") ||
       !mi::hip_ok(hipStreamSynchronize(c->st), "ul sync"))
     return SRSLTE_ERROR;
   memcpy(output_signal, c->h_iq, n * 8);
+  c->prof.mark(4, c->st);
   return SRSLTE_SUCCESS;
 }
 

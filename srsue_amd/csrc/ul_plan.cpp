@@ -127,10 +127,13 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     auto it = tw_off.find(len);
     if (it != tw_off.end()) return it->second;
     const uint32_t off = (uint32_t)(tw.size() / 2);
-    for (uint32_t t = 0; t < len; t++) {
-      tw.push_back((float)cos(-2.0 * M_PI * t / len));
-      tw.push_back((float)sin(-2.0 * M_PI * t / len));
-    }
+    auto& tc = tw_cache[len];   // computed once per length (cos / sin of 2,048 + 1,200 points: ~0.1 ms)
+    if (tc.empty())
+      for (uint32_t t = 0; t < len; t++) {
+        tc.push_back((float)cos(-2.0 * M_PI * t / len));
+        tc.push_back((float)sin(-2.0 * M_PI * t / len));
+      }
+    tw.insert(tw.end(), tc.begin(), tc.end());
     tw_off[len] = off;
     return off;
   };
@@ -205,8 +208,17 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
     t.tbs = c.tbs;
     t.scr_off = (uint32_t)scr.size();
     const uint32_t n_scr = 12 * t.M * c.Qm;   // 36.211 5.3.1 scrambles every coded bit of the subframe (UCI too)
-    scr.resize(scr.size() + (n_scr + 31) / 32 + 1);
-    gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, n_scr, &scr[t.scr_off]);
+    {
+      const auto key = std::make_pair((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, n_scr);
+      auto it = scr_cache.find(key);
+      if (it == scr_cache.end()) {
+        if (scr_cache.size() >= SCR_CACHE_MAX) scr_cache.clear();
+        std::vector<uint32_t> wv((n_scr + 31) / 32 + 1, 0u);
+        gold_words(key.first, n_scr, wv.data());
+        it = scr_cache.emplace(key, std::move(wv)).first;
+      }
+      scr.insert(scr.end(), it->second.begin(), it->second.end());
+    }
     // segmentation of (TB || CRC24A), 36.212 5.1.2 (sg above); the data follow the CQI symbols in g (5.2.2.7)
     tb_cb0.push_back((uint32_t)cbs.size());
     uint32_t byte0 = 0, sym = t.q_cqi;

@@ -38,6 +38,11 @@ struct UlPlan {
   struct SelTab { std::vector<uint32_t> sel; uint32_t r0[4]; };
   std::map<std::pair<uint32_t, uint32_t>, SelTab> sel_cache;
   std::map<uint32_t, std::vector<uint32_t>> pi_cache;
+  std::map<uint32_t, std::vector<float>> tw_cache;   // DFT length -> interleaved cos / sin twiddles
+  // scrambling words by (c_init, bits): srsUE's RNTI and cell are fixed, so a worker sees a handful of
+  // keys (10 subframes x the grant sizes); bounded, cleared when it grows past SCR_CACHE_MAX
+  std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> scr_cache;
+  static constexpr size_t SCR_CACHE_MAX = 256;
   int build(const mi_ul_cfg_t* cfgs, uint32_t n);
 };
 
