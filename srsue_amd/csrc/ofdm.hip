@@ -4,7 +4,8 @@
 // One 256-thread workgroup per subframe runs the 14 symbol FFTs back to back: the first Stockham
 // stage reads the IQ straight from HBM with consecutive lanes on consecutive samples (coalesced),
 // the remaining radix-8/4/3 stages exchange through one LDS buffer, and the twiddles
-// exp(-2 pi i t / N) are staged into LDS once per workgroup and reused by all 14 symbols.  The
+// exp(-2 pi i t / N) (a half-wave table, tw_at) are staged into LDS once per workgroup and reused by all
+// 14 symbols.  The
 // last pass writes the 12 N_RB used subcarriers (DC skipped) row-major [symbol][subcarrier].
 // Unnormalised forward DFT (oracle/o_rx.c convention).
 #include "kernels.h"
@@ -64,6 +65,17 @@ __device__ __forceinline__ float2 load_iq(const short2* __restrict__ p, int i) {
   return make_float2((float)v.x * (1.0f / 32768.0f), (float)v.y * (1.0f / 32768.0f));
 }
 
+// twiddle W_N^t from the half-wave table tw2[t mod N/2] (t < N): W_N^(t0 + N/2) = -W_N^t0.  The LDS holds N/2
+// entries instead of N: for N = 2048 the workgroup needs 24 KB instead of 32 KB of LDS (6 instead of 5
+// workgroups per CU) and stages 8 KB of twiddles instead of 16.
+template <int N>
+__device__ __forceinline__ float2 tw_at(const float2* tw2, int t) {
+  constexpr int H = N / 2;
+  const bool hi = t >= H;
+  const float2 w = tw2[hi ? t - H : t];
+  return hi ? make_float2(-w.x, -w.y) : w;
+}
+
 template <int N, int R, bool FIRST, typename IQ>
 __device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gsrc, const float2* tw, int Ns) {
   constexpr int NB = N / R;
@@ -87,7 +99,7 @@ __device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gs
       if (!FIRST) {
         const int step = k * (N / (Ns * R));
 #pragma unroll
-        for (int r = 1; r < R; r++) v[p][r] = c_mul(v[p][r], tw[step * r]);
+        for (int r = 1; r < R; r++) v[p][r] = c_mul(v[p][r], tw_at<N>(tw, step * r));
       }
       dft<R>(v[p]);
       const int base = (j / Ns) * Ns * R + k;
@@ -158,15 +170,19 @@ __device__ __forceinline__ void fft_rest(float2* buf, const float2* tw) {
 // symbols [blockIdx.y * per, (blockIdx.y + 1) * per) of a subframe: per = 14 (one workgroup per
 // subframe, twiddles staged once for 14 FFTs -- batches) or 1 (a workgroup per symbol -- small batches,
 // the per-TTI latency path)
+// 6 waves per SIMD: the VGPR budget (<= 80) that matches the 6 workgroups per CU the LDS now allows
+#ifndef MI_OFDM_WAVES
+#define MI_OFDM_WAVES 6
+#endif
 template <int N, typename IQ>
-__global__ __launch_bounds__(256) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI_OFDM_WAVES))) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
                                                       const MiSfDesc* __restrict__ sfs,
                                                       const uint32_t* __restrict__ list,
                                                       const float2* __restrict__ twg, uint32_t W, int per) {
   __shared__ float2 buf[N];
-  __shared__ float2 tw[N];
+  __shared__ float2 tw[N / 2];   // half-wave table (tw_at)
   const MiSfDesc d = sfs[list[blockIdx.x]];
-  for (int t = threadIdx.x; t < N; t += 256) tw[t] = twg[t];
+  for (int t = threadIdx.x; t < N / 2; t += 256) tw[t] = twg[t];
   __syncthreads();
   const IQ* src_sf = iq + d.iq_off;
   float2* dst = grid + d.grid_off;
