@@ -93,7 +93,9 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * frequency-interpolated rows ([port][4][12 N_RB] at the subframe's ce offset) and the fused demap stage
  * interpolates each RE's estimate in time from them with the chest kernel's own expression -- identical
  * LLRs, 10 of 14 rows of channel-estimate traffic written and read never.  Batch throughput mode: the
- * batch's ce buffer then does not hold the full estimates (no MI_DL_FLAG_KEEP_LLR, no mi_dl_ctrl_* on it) */
+ * batch's ce buffer then does not hold the full estimates (no MI_DL_FLAG_KEEP_LLR, no mi_dl_ctrl_* on it).
+ * A run whose stage mask includes DEMAP but not CHEST after a compact estimation fails (returns -1,
+ * mi_dl_last_error says why) instead of reading rows that were never written. */
 #define MI_DL_FLAG_CE_COMPACT 1024u
 
 typedef struct mi_dl_batch mi_dl_batch_t;

@@ -26,6 +26,7 @@
 
 #include "srslte/common/timestamp.h"
 #include "srslte/utils/debug.h"
+#include "srslte/utils/bit.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -406,9 +407,9 @@ SRSLTE_API int srslte_ue_ul_pusch_encode_rnti_softbuffer(srslte_ue_ul_t *q, uint
 SRSLTE_API int srslte_softbuffer_tx_init(srslte_softbuffer_tx_t *q, uint32_t nof_prb);
 SRSLTE_API void srslte_softbuffer_tx_reset(srslte_softbuffer_tx_t *q);
 SRSLTE_API void srslte_softbuffer_tx_free(srslte_softbuffer_tx_t *q);
-/* DCI format 0 (36.212 5.3.3.1.1, no hopping) / RAR grant (36.213 6.2) -> UL grant: MCS per 36.213
- * Table 8.6.1-1 (29-31: retransmission, rv 1-3, TBS of the last grant not known here: error); TBS from
- * the spot columns this library carries (N_PRB = 6, 25, 50, 100). */
+/* DCI format 0 (36.212 5.3.3.1.1) / RAR grant (36.213 6.2) -> UL grant: MCS per 36.213 Table 8.6.1-1
+ * (29-31: retransmission, rv 1-3, TBS of the last grant not known here: error); TBS from the full
+ * 36.213 Table 7.1.7.2.1-1. */
 SRSLTE_API int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t *msg, uint32_t nof_prb, uint32_t n_rb_ho,
                                           srslte_ra_ul_dci_t *ul_dci, srslte_ra_ul_grant_t *grant, uint32_t harq_pid);
 SRSLTE_API int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t *rar, uint32_t nof_prb, uint32_t n_rb_ho,
@@ -507,7 +508,84 @@ SRSLTE_API float srslte_ue_ul_pucch_power(srslte_ue_ul_t *q, float PL, uint32_t 
 SRSLTE_API float srslte_ue_ul_srs_power(srslte_ue_ul_t *q, float PL);
 typedef struct SRSLTE_API { uint32_t N_seq, N_cp; void *impl; } srslte_prach_t;   /* prach.h:64 (srsLTE) */
 typedef struct SRSLTE_API { uint32_t nsamples; void *impl; } srslte_cfo_t;         /* prach.h:68 (srsLTE) */
-typedef struct SRSLTE_API { srslte_cell_t cell; void *impl; } srslte_ue_mib_t;     /* phch_recv.h:77 (srsLTE MIB) */
+/* PRACH preamble generation and its CFO pre-correction (reference ue/src/phy/prach.cc:56-57,77-98,130,152) */
+SRSLTE_API int srslte_prach_init(srslte_prach_t *p, uint32_t N_ifft_ul, uint32_t preamble_format,
+                                 uint32_t root_seq_index, bool high_speed_flag, uint32_t zero_corr_zone_config);
+SRSLTE_API int srslte_prach_free(srslte_prach_t *p);
+SRSLTE_API uint32_t srslte_prach_get_preamble_format(uint32_t config_idx);
+SRSLTE_API int srslte_prach_gen(srslte_prach_t *p, uint32_t seq_index, uint32_t freq_offset, cf_t *signal);
+SRSLTE_API bool srslte_prach_send_tti(uint32_t config_idx, uint32_t current_tti, int allowed_subframe);
+SRSLTE_API int srslte_cfo_init(srslte_cfo_t *h, uint32_t nsamples);
+SRSLTE_API void srslte_cfo_free(srslte_cfo_t *h);
+SRSLTE_API void srslte_cfo_correct(srslte_cfo_t *h, cf_t *input, cf_t *output, float freq);
+
+/* Cell search and MIB decoding (reference ue/src/phy/phch_recv.cc:98,137-220,246-253; types held by value
+ * at ue/hdr/phy/phch_recv.h:77 and by the cell-search locals).  The types carry the members srsUE touches
+ * (cs.ue_sync.agc, ue_mib_sync.ue_sync.agc, ue_mib.pbch). */
+#define SRSLTE_BCH_PAYLOAD_LEN 24            /* MIB bits, 36.331 MasterInformationBlock */
+#define SRSLTE_UE_MIB_FOUND 1
+#define SRSLTE_UE_MIB_NOTFOUND 0
+typedef struct SRSLTE_API { uint32_t frame_idx; void *impl; } srslte_pbch_t;
+typedef struct SRSLTE_API { srslte_cell_t cell; srslte_pbch_t pbch; void *impl; } srslte_ue_mib_t;
+typedef struct SRSLTE_API { srslte_ue_mib_t ue_mib; srslte_ue_sync_t ue_sync; void *impl; } srslte_ue_mib_sync_t;
+typedef struct SRSLTE_API {
+  uint32_t cell_id;
+  srslte_cp_t cp;
+  float peak;
+  float mode;
+  float psr;
+  float cfo;
+} srslte_ue_cellsearch_result_t;
+typedef struct SRSLTE_API {
+  srslte_ue_sync_t ue_sync;
+  uint32_t max_frames;
+  uint32_t nof_valid_frames;
+  void *impl;
+} srslte_ue_cellsearch_t;
+SRSLTE_API int srslte_ue_mib_init(srslte_ue_mib_t *q, srslte_cell_t cell);
+SRSLTE_API void srslte_ue_mib_free(srslte_ue_mib_t *q);
+SRSLTE_API int srslte_ue_mib_decode(srslte_ue_mib_t *q, cf_t *input, uint8_t bch_payload[SRSLTE_BCH_PAYLOAD_LEN],
+                                    uint32_t *nof_tx_ports, uint32_t *sfn_offset);
+SRSLTE_API void srslte_pbch_decode_reset(srslte_pbch_t *q);
+SRSLTE_API int srslte_ue_mib_sync_init(srslte_ue_mib_sync_t *q, uint32_t cell_id, srslte_cp_t cp,
+                                       int(recv_callback)(void *, void *, uint32_t, srslte_timestamp_t *),
+                                       void *stream_handler);
+SRSLTE_API void srslte_ue_mib_sync_free(srslte_ue_mib_sync_t *q);
+SRSLTE_API int srslte_ue_mib_sync_decode(srslte_ue_mib_sync_t *q, uint32_t max_frames_timeout,
+                                         uint8_t bch_payload[SRSLTE_BCH_PAYLOAD_LEN], uint32_t *nof_tx_ports,
+                                         uint32_t *sfn_offset);
+SRSLTE_API int srslte_ue_cellsearch_init(srslte_ue_cellsearch_t *q,
+                                         int(recv_callback)(void *, void *, uint32_t, srslte_timestamp_t *),
+                                         void *stream_handler);
+SRSLTE_API void srslte_ue_cellsearch_free(srslte_ue_cellsearch_t *q);
+SRSLTE_API void srslte_ue_cellsearch_set_nof_frames_to_scan(srslte_ue_cellsearch_t *q, uint32_t nof_frames);
+SRSLTE_API void srslte_ue_cellsearch_set_threshold(srslte_ue_cellsearch_t *q, float threshold);
+SRSLTE_API int srslte_ue_cellsearch_scan_N_id_2(srslte_ue_cellsearch_t *q, uint32_t N_id_2,
+                                                srslte_ue_cellsearch_result_t *found_cell);
+SRSLTE_API int srslte_ue_cellsearch_scan(srslte_ue_cellsearch_t *q, srslte_ue_cellsearch_result_t found_cells[3],
+                                         uint32_t *max_N_id_2);
+
+/* ---- host utilities srsUE calls outside the worker, implemented here (srslte_util.cpp) ---------------
+ * AGC gain (phch_recv.cc:174,211), MIB unpacking (36.331: dl-Bandwidth 3 bits, phich-Config 1 + 2 bits,
+ * systemFrameNumber 8 MSBs; phch_recv.cc:216,253), cell / CP printing (:192,218), timing advance (36.213
+ * 4.2.3: N_TA = 16 T_A from a RAR, N_TA += 16 (T_A - 31) from a MAC CE; phy.cc:125-132), the RAR grant's
+ * 20 bits (36.213 6.2; phch_common.cc:122), PRACH power / scaling helpers (prach.cc:157-168) */
+#define SRSLTE_LTE_TS (1.0f / (15000.0f * 2048.0f))   /* basic time unit T_s, 36.211 4 */
+#define SRSLTE_PC_MAX 23                              /* dBm, power class 3 */
+#define SRSLTE_MIN(a, b) ((a) < (b) ? (a) : (b))
+#define SRSLTE_MAX(a, b) ((a) > (b) ? (a) : (b))
+#define SRSLTE_SIRNTI 0xFFFF
+#define SRSLTE_PRNTI 0xFFFE
+SRSLTE_API float srslte_agc_get_gain(srslte_agc_t *q);
+SRSLTE_API void srslte_pbch_mib_unpack(uint8_t *msg, srslte_cell_t *cell, uint32_t *sfn);
+SRSLTE_API void srslte_pbch_mib_pack(srslte_cell_t *cell, uint32_t sfn, uint8_t *msg);
+SRSLTE_API char *srslte_cp_string(srslte_cp_t cp);
+SRSLTE_API void srslte_cell_fprint(FILE *stream, srslte_cell_t *cell, uint32_t sfn);
+SRSLTE_API uint32_t srslte_N_ta_new_rar(uint32_t ta);
+SRSLTE_API uint32_t srslte_N_ta_new(uint32_t N_ta_old, uint32_t ta);
+SRSLTE_API void srslte_dci_rar_grant_unpack(srslte_dci_rar_grant_t *rar, uint8_t grant[SRSLTE_RAR_GRANT_LEN]);
+SRSLTE_API float srslte_vec_avg_power_cf(cf_t *x, uint32_t len);
+SRSLTE_API void srslte_vec_sc_prod_cfc(cf_t *x, float h, cf_t *z, uint32_t len);
 
 #ifdef __cplusplus
 }

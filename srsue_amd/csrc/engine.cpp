@@ -215,6 +215,12 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   const uint32_t full = (1u << MI_DL_STAGE_CHEST) | (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM);
   const bool compact = (flags & MI_DL_FLAG_CE_COMPACT) && !(flags & MI_DL_FLAG_KEEP_LLR) && P.has_pdsch &&
                        (mask & full) == full && !P.rm_rep;
+  // the demap stage (alone or fused into rate de-matching) reads the estimates; without a chest stage in
+  // this run they must be full ones
+  if (P.has_pdsch && ce_compact && !(mask & (1u << MI_DL_STAGE_CHEST)) && (mask & (1u << MI_DL_STAGE_DEMAP))) {
+    set_error("the channel estimates are in compact form (MI_DL_FLAG_CE_COMPACT): re-run with the CHEST stage");
+    return -1;
+  }
   mark(0);
   if (mask & (1u << MI_DL_STAGE_OFDM)) {
     for (size_t i = 0; i < P.fft_lists.size(); i++) {
@@ -228,6 +234,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   if (mask & (1u << MI_DL_STAGE_CHEST))
     launch_chest(d_grid.as<float2>(), d_ce.as<float2>(), d_sfs.as<MiSfDesc>(), d_cells.as<MiCellDesc>(),
                  d_crs.as<float2>(), d_metrics.as<float>(), nsf, st, compact);
+  if (mask & (1u << MI_DL_STAGE_CHEST)) ce_compact = compact;
   mark(2);
   if (P.has_pdsch) {
     float* sb = sb_override ? sb_override : d_sb.as<float>();

@@ -75,6 +75,9 @@ struct Engine {
   // softbuffer); 0 on success
   int plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, hipStream_t st);
   hipStream_t last_stream = nullptr;
+  // layout the last channel-estimation stage wrote: true = compact (4 pilot rows per port).  A run that
+  // reads the estimates without re-estimating them is rejected while they are compact
+  bool ce_compact = false;
   // profiling: one event set per run since the last reset (MI_DL_FLAG_PROFILE)
   std::vector<std::vector<hipEvent_t>> ev_sets;
   size_t ev_used = 0;

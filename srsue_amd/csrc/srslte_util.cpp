@@ -117,3 +117,111 @@ void srslte_ra_pusch_fprint(FILE* f, srslte_ra_ul_dci_t* q, uint32_t nof_prb) {
 }
 
 }  // extern "C"
+
+/* ---- bit utilities (srslte/utils/bit.h): one bit per byte, MSB first -------------------------------- */
+extern "C" {
+
+uint32_t srslte_bit_pack(uint8_t** bits, int nof_bits) {
+  uint32_t v = 0;
+  for (int i = 0; i < nof_bits; i++) v = (v << 1) | ((*bits)[i] & 1u);
+  *bits += nof_bits;
+  return v;
+}
+
+void srslte_bit_unpack(uint32_t value, uint8_t** bits, int nof_bits) {
+  for (int i = 0; i < nof_bits; i++) (*bits)[i] = (uint8_t)((value >> (nof_bits - 1 - i)) & 1u);
+  *bits += nof_bits;
+}
+
+// a trailing partial byte is left-aligned (its low bits zero)
+void srslte_bit_pack_vector(uint8_t* unpacked, uint8_t* packed, int nof_bits) {
+  for (int i = 0; i < nof_bits / 8; i++) packed[i] = (uint8_t)srslte_bit_pack(&unpacked, 8);
+  if (nof_bits % 8) packed[nof_bits / 8] = (uint8_t)(srslte_bit_pack(&unpacked, nof_bits % 8) << (8 - nof_bits % 8));
+}
+
+void srslte_bit_unpack_vector(uint8_t* packed, uint8_t* unpacked, int nof_bits) {
+  for (int i = 0; i < nof_bits / 8; i++) srslte_bit_unpack(packed[i], &unpacked, 8);
+  if (nof_bits % 8) srslte_bit_unpack((uint32_t)packed[nof_bits / 8] >> (8 - nof_bits % 8), &unpacked, nof_bits % 8);
+}
+
+/* ---- helpers around the PHY outside the worker (srslte/srslte.h "host utilities") --------------------- */
+float srslte_agc_get_gain(srslte_agc_t* q) { return q ? q->gain : 1.0f; }
+
+// 36.331 MasterInformationBlock: dl-Bandwidth (3), phich-Duration (1), phich-Resource (2), the 8 MSBs of
+// the SFN (the 2 LSBs come from the PBCH's 40 ms phase: sfn_offset, phch_recv.cc:255), 10 spare bits
+void srslte_pbch_mib_unpack(uint8_t* msg, srslte_cell_t* cell, uint32_t* sfn) {
+  static const uint32_t bw_prb[6] = {6, 15, 25, 50, 75, 100};
+  const uint32_t bw = srslte_bit_pack(&msg, 3);
+  if (cell) {
+    cell->bw_idx = bw;
+    cell->nof_prb = bw < 6 ? bw_prb[bw] : 0;
+    cell->phich_length = srslte_bit_pack(&msg, 1) ? SRSLTE_PHICH_EXT : SRSLTE_PHICH_NORM;
+    cell->phich_resources = (srslte_phich_resources_t)srslte_bit_pack(&msg, 2);
+  } else {
+    msg += 3;
+  }
+  const uint32_t s = srslte_bit_pack(&msg, 8);
+  if (sfn) *sfn = s << 2;
+}
+
+void srslte_pbch_mib_pack(srslte_cell_t* cell, uint32_t sfn, uint8_t* msg) {
+  static const uint32_t bw_prb[6] = {6, 15, 25, 50, 75, 100};
+  uint32_t bw = 0;
+  for (uint32_t i = 0; i < 6; i++)
+    if (bw_prb[i] == cell->nof_prb) bw = i;
+  memset(msg, 0, SRSLTE_BCH_PAYLOAD_LEN);
+  srslte_bit_unpack(bw, &msg, 3);
+  srslte_bit_unpack(cell->phich_length == SRSLTE_PHICH_EXT ? 1u : 0u, &msg, 1);
+  srslte_bit_unpack((uint32_t)cell->phich_resources, &msg, 2);
+  srslte_bit_unpack((sfn >> 2) & 0xFFu, &msg, 8);
+}
+
+char* srslte_cp_string(srslte_cp_t cp) {
+  return const_cast<char*>(cp == SRSLTE_CP_NORM ? "Normal  " : "Extended");
+}
+
+void srslte_cell_fprint(FILE* stream, srslte_cell_t* cell, uint32_t sfn) {
+  static const char* res[4] = {"1/6", "1/2", "1", "2"};
+  fprintf(stream, " - Cell ID:         %u\n", cell->id);
+  fprintf(stream, " - Nof ports:       %u\n", cell->nof_ports);
+  fprintf(stream, " - CP:              %s\n", srslte_cp_string(cell->cp));
+  fprintf(stream, " - PRB:             %u\n", cell->nof_prb);
+  fprintf(stream, " - PHICH Length:    %s\n", cell->phich_length == SRSLTE_PHICH_EXT ? "Extended" : "Normal");
+  fprintf(stream, " - PHICH Resources: %s\n", res[(uint32_t)cell->phich_resources & 3u]);
+  fprintf(stream, " - SFN:             %u\n", sfn);
+}
+
+// 36.213 4.2.3: a RAR's 11-bit T_A sets N_TA = 16 T_A; a MAC CE's 6-bit T_A adjusts N_TA by 16 (T_A - 31)
+uint32_t srslte_N_ta_new_rar(uint32_t ta) { return ta * 16; }
+uint32_t srslte_N_ta_new(uint32_t N_ta_old, uint32_t ta) {
+  const int n = (int)N_ta_old + ((int)ta - 31) * 16;
+  return n < 0 ? 0u : (uint32_t)n;
+}
+
+// 36.213 6.2: hopping flag (1), fixed-size RB assignment (10), truncated MCS (4), TPC for PUSCH (3),
+// UL delay (1), CSI request (1)
+void srslte_dci_rar_grant_unpack(srslte_dci_rar_grant_t* rar, uint8_t grant[SRSLTE_RAR_GRANT_LEN]) {
+  uint8_t* g = grant;
+  rar->hopping_flag = srslte_bit_pack(&g, 1) != 0;
+  rar->rba = srslte_bit_pack(&g, 10);
+  rar->trunc_mcs = srslte_bit_pack(&g, 4);
+  rar->tpc_pusch = srslte_bit_pack(&g, 3);
+  rar->ul_delay = srslte_bit_pack(&g, 1) != 0;
+  rar->cqi_request = srslte_bit_pack(&g, 1) != 0;
+}
+
+float srslte_vec_avg_power_cf(cf_t* x, uint32_t len) {
+  if (!len) return 0.0f;
+  const float* f = reinterpret_cast<const float*>(x);
+  double acc = 0.0;
+  for (uint32_t i = 0; i < 2 * len; i++) acc += (double)f[i] * f[i];
+  return (float)(acc / len);
+}
+
+void srslte_vec_sc_prod_cfc(cf_t* x, float h, cf_t* z, uint32_t len) {
+  const float* a = reinterpret_cast<const float*>(x);
+  float* b = reinterpret_cast<float*>(z);
+  for (uint32_t i = 0; i < 2 * len; i++) b[i] = a[i] * h;
+}
+
+}  // extern "C"

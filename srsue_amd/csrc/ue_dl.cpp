@@ -126,6 +126,14 @@ bool device_grid(mi_ue_dl_ctx* c, const srslte_cell_t& cell, cf_t* sf_symbols, c
   return ok;
 }
 
+// error return after work was enqueued on the instance stream: the next call rewrites the page-locked
+// staging (h_iq, h_small, h_pay) assuming the previous call's copies ended at its stream sync, so an
+// early return drains the stream first
+int fail_sync(mi_ue_dl_ctx* c) {
+  (void)hipStreamSynchronize(c->st);
+  return SRSLTE_ERROR;
+}
+
 uint32_t mod_bits(srslte_mod_t m) {
   switch (m) {
     case SRSLTE_MOD_BPSK: return 1;
@@ -279,16 +287,16 @@ int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t* q, cf_t* input, uint32_t sf
   c->prof.start();
   memcpy(c->h_iq, input, sfl * 8);   // the previous call's DMA out of h_iq ended with its stream sync
   if (!mi::hip_ok(hipMemcpyAsync(c->d_iq.p, c->h_iq, sfl * 8, hipMemcpyHostToDevice, c->st), "H2D iq"))
-    return SRSLTE_ERROR;
+    return fail_sync(c);
   c->prof.mark(0, c->st);
-  if (c->eng.plan_memo(&c->cfg, 1, false, c->st)) return SRSLTE_ERROR;
+  if (c->eng.plan_memo(&c->cfg, 1, false, c->st)) return fail_sync(c);
   c->prof.mark(1, c->st);
-  if (c->eng.run(c->d_iq.p, c->st, (1u << MI_DL_STAGE_OFDM) | (1u << MI_DL_STAGE_CHEST), nullptr)) return SRSLTE_ERROR;
+  if (c->eng.run(c->d_iq.p, c->st, (1u << MI_DL_STAGE_OFDM) | (1u << MI_DL_STAGE_CHEST), nullptr)) return fail_sync(c);
   c->prof.mark(2, c->st);
   // PCFICH -> CFI on the GPU (the control plan's PCFICH tables do not depend on the CFI)
-  if (!ctrl_plan(c, 1, q->current_rnti)) return SRSLTE_ERROR;
+  if (!ctrl_plan(c, 1, q->current_rnti)) return fail_sync(c);
   c->prof.mark(3, c->st);
-  if (c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 1u, 0.0f, c->st)) return SRSLTE_ERROR;
+  if (c->ctrl.run(c->eng.d_grid.as<float2>(), c->eng.d_ce.as<float2>(), 1u, 0.0f, c->st)) return fail_sync(c);
   c->prof.mark(4, c->st);
   mi_ue_dl_ctx::Small* hs = c->h_small;
   bool ok = mi::hip_ok(hipMemcpyAsync(q->sf_symbols, c->eng.d_grid.p, n * 8, hipMemcpyDeviceToHost, c->st), "D2H");
@@ -299,7 +307,7 @@ int srslte_ue_dl_decode_fft_estimate(srslte_ue_dl_t* q, cf_t* input, uint32_t sf
        mi::hip_ok(hipStreamSynchronize(c->st), "sync");
   const float* met = hs->met;
   const uint32_t cf = hs->cfi;
-  if (!ok) return SRSLTE_ERROR;
+  if (!ok) return fail_sync(c);
   c->prof.mark(5, c->st);
   q->chest.rsrp = met[0]; q->chest.rssi = met[1]; q->chest.rsrq = met[2];
   q->chest.noise_estimate = met[3]; q->chest.snr = met[4];
@@ -361,23 +369,23 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
   c->eng.noise = noise_estimate;
   c->eng.max_its = q->dl_sch.max_iterations ? q->dl_sch.max_iterations : SRSLTE_PDSCH_MAX_TDEC_ITERS;
   c->prof.start();
-  if (c->eng.plan_memo(&s, 1, true, c->st)) return SRSLTE_ERROR;
+  if (c->eng.plan_memo(&s, 1, true, c->st)) return fail_sync(c);
   c->prof.mark(6, c->st);
-  if (c->eng.plan.sb_floats * sizeof(float) > softbuffer->dev_bytes) return SRSLTE_ERROR;
+  if (c->eng.plan.sb_floats * sizeof(float) > softbuffer->dev_bytes) return fail_sync(c);
   bool ok = device_grid(c, cell, sf_symbols, ce);
-  if (!ok) return SRSLTE_ERROR;
+  if (!ok) return fail_sync(c);
   c->prof.mark(8, c->st);
   const uint32_t stages = (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM) | (1u << MI_DL_STAGE_TDEC) |
                           (1u << MI_DL_STAGE_TB);
-  if (c->eng.run(nullptr, c->st, stages, reinterpret_cast<float*>(softbuffer->dev))) return SRSLTE_ERROR;
+  if (c->eng.run(nullptr, c->st, stages, reinterpret_cast<float*>(softbuffer->dev))) return fail_sync(c);
   c->prof.mark(9, c->st);
-  if (s.tbs / 8 > mi_ue_dl_ctx::MAX_TB_BYTES) return SRSLTE_ERROR;
+  if (s.tbs / 8 > mi_ue_dl_ctx::MAX_TB_BYTES) return fail_sync(c);
   mi_ue_dl_ctx::Small* hs = c->h_small;
   ok = mi::hip_ok(hipMemcpyAsync(c->h_pay, c->eng.d_payload.p, s.tbs / 8, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipMemcpyAsync(&hs->tb_ok, c->eng.d_tbok.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipMemcpyAsync(&hs->its, c->eng.d_tbits.p, 4, hipMemcpyDeviceToHost, c->st), "D2H") &&
        mi::hip_ok(hipStreamSynchronize(c->st), "sync");
-  if (!ok) return SRSLTE_ERROR;
+  if (!ok) return fail_sync(c);
   memcpy(data, c->h_pay, s.tbs / 8);
   const uint32_t tb_ok = hs->tb_ok, its = hs->its;
   c->prof.mark(10, c->st);

@@ -51,9 +51,11 @@ struct mi_ue_ul_ctx {
         fprintf(stderr, "%s\"%s\": %.1f", i ? ", " : "", name[i], prof.n[i] ? prof.acc[i] / prof.n[i] : 0.0);
       fprintf(stderr, "}}\n");
     }
+    // the stream is owned here (as in ue_dl.cpp): synchronised, the staging freed, then destroyed
     if (st) (void)hipStreamSynchronize(st);
     if (h_pay) (void)hipHostFree(h_pay);
     if (h_iq) (void)hipHostFree(h_iq);
+    if (st) (void)hipStreamDestroy(st);
   }
 };
 
@@ -132,8 +134,7 @@ int srslte_ue_ul_init(srslte_ue_ul_t* q, srslte_cell_t cell) {
       !c->d_iq.ensure(iq_bytes) ||
       !mi::hip_ok(hipHostMalloc(reinterpret_cast<void**>(&c->h_pay), TX_MAX_BYTES, hipHostMallocDefault), "pinned") ||
       !mi::hip_ok(hipHostMalloc(reinterpret_cast<void**>(&c->h_iq), iq_bytes, hipHostMallocDefault), "pinned")) {
-    if (c->st) (void)hipStreamDestroy(c->st);
-    delete c;
+    delete c;   // the destructor destroys the stream
     return SRSLTE_ERROR;
   }
   q->ctx = c;
@@ -142,9 +143,7 @@ int srslte_ue_ul_init(srslte_ue_ul_t* q, srslte_cell_t cell) {
 
 void srslte_ue_ul_free(srslte_ue_ul_t* q) {
   if (!q || !q->ctx) return;
-  (void)hipStreamSynchronize(q->ctx->st);
-  (void)hipStreamDestroy(q->ctx->st);
-  delete q->ctx;
+  delete q->ctx;   // synchronises and destroys the instance's stream
   q->ctx = nullptr;
 }
 

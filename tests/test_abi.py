@@ -15,10 +15,25 @@ from srsue_amd import abi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", "srslte", "srslte.h"), os.path.join(ROOT, "include", "mi_dl.h"),
            os.path.join(ROOT, "include", "mi_ul.h"), os.path.join(ROOT, "include", "srslte", "common", "timestamp.h"),
-           os.path.join(ROOT, "include", "srslte", "utils", "debug.h")]
-# declared in srslte.h's OUT OF SCOPE block only so srsUE compiles unchanged (PUCCH / SRS / UL power control)
-OUT_OF_SCOPE = {"srslte_ue_ul_pregen_signals", "srslte_ue_ul_pucch_encode", "srslte_ue_ul_pucch_power",
-                "srslte_ue_ul_pusch_power", "srslte_ue_ul_srs_encode", "srslte_ue_ul_srs_power"}
+           os.path.join(ROOT, "include", "srslte", "utils", "debug.h"),
+           os.path.join(ROOT, "include", "srslte", "utils", "bit.h")]
+OOS_BEGIN = "OUT OF SCOPE (SURVEY.md 8"
+OOS_END = "host utilities srsUE calls outside the worker"
+
+
+def out_of_scope():
+    """functions srslte.h declares between its OUT OF SCOPE marker and the host-utilities block: declared only
+    so srsUE's PHY compiles unchanged (PUCCH / SRS / UL power control, PRACH, cell search, MIB)"""
+    src = open(HEADERS[0]).read()
+    a, b = src.index(OOS_BEGIN), src.index(OOS_END)
+    seg = src[a - 8:b]
+    names = set()
+    for m in re.finditer(r"SRSLTE_API\s+[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", re.sub(r"/\*.*?\*/", "", seg, flags=re.S)):
+        names.add(m.group(1))
+    return names
+
+
+OUT_OF_SCOPE = out_of_scope()
 
 
 def declared_functions(path):
@@ -41,9 +56,13 @@ def test_library_exports_every_declared_symbol(built):
                 missing.append(n)
     assert not missing, missing
     assert len(declared_functions(HEADERS[0])) >= 25
-    src = open(HEADERS[0]).read()
     assert OUT_OF_SCOPE <= declared_functions(HEADERS[0])
-    assert all(src.index(n) > src.index("OUT OF SCOPE (SURVEY.md 8") for n in OUT_OF_SCOPE)
+    # PUCCH / SRS / UL power control, PRACH, cell search and MIB decoding -- and nothing on the DL data path
+    assert {"srslte_ue_ul_pucch_encode", "srslte_prach_gen", "srslte_ue_cellsearch_scan",
+            "srslte_ue_mib_sync_decode"} <= OUT_OF_SCOPE
+    assert not any(n.startswith(("srslte_ue_dl", "srslte_pdsch", "srslte_softbuffer", "srslte_chest")) for n in OUT_OF_SCOPE)
+    lib = abi.lib()
+    assert not [n for n in OUT_OF_SCOPE if hasattr(lib, n)], "an out-of-scope symbol is exported"
 
 
 def test_headers_compile_as_c(tmp_path):
@@ -120,3 +139,61 @@ def test_srslte_reporting_helpers(built):
     assert L.srslte_cqi_value_pack(C.byref(v), buf) == 4 and list(buf[:4]) == [1, 0, 1, 1]
     v = Cqi(6, 1, 1)
     assert L.srslte_cqi_value_pack(C.byref(v), buf) == 5 and list(buf[:5]) == [0, 1, 1, 0, 1]
+
+
+def test_host_utilities_outside_the_worker(built):
+    """bit utilities, MIB unpacking, RAR grant unpacking and timing advance (srslte.h host-utilities block;
+    phch_recv.cc:216,220,253, phch_common.cc:122, phy.cc:125-132, pdu.cc:776,791)"""
+    lib = abi.lib()
+    rng = np.random.default_rng(7)
+    for nbits in (1, 7, 8, 13, 24, 32):
+        bits = rng.integers(0, 2, nbits, dtype=np.uint8)
+        packed = np.zeros((nbits + 7) // 8, np.uint8)
+        lib.srslte_bit_pack_vector(bits.ctypes.data_as(C.c_void_p), packed.ctypes.data_as(C.c_void_p), nbits)
+        assert np.array_equal(packed, np.packbits(bits)), nbits      # MSB first, trailing byte left-aligned
+        back = np.zeros(nbits, np.uint8)
+        lib.srslte_bit_unpack_vector(packed.ctypes.data_as(C.c_void_p), back.ctypes.data_as(C.c_void_p), nbits)
+        assert np.array_equal(back, bits)
+    # cursor form: pack / unpack advance the caller's pointer
+    buf = (C.c_uint8 * 16)()
+    cur = C.cast(buf, C.POINTER(C.c_uint8))
+    lib.srslte_bit_unpack.argtypes = [C.c_uint32, C.POINTER(C.POINTER(C.c_uint8)), C.c_int]
+    lib.srslte_bit_unpack(0x2D, C.byref(cur), 6)
+    lib.srslte_bit_unpack(0x5, C.byref(cur), 3)
+    assert list(buf[:9]) == [1, 0, 1, 1, 0, 1, 1, 0, 1]
+    cur = C.cast(buf, C.POINTER(C.c_uint8))
+    lib.srslte_bit_pack.argtypes = [C.POINTER(C.POINTER(C.c_uint8)), C.c_int]
+    lib.srslte_bit_pack.restype = C.c_uint32
+    assert lib.srslte_bit_pack(C.byref(cur), 6) == 0x2D and lib.srslte_bit_pack(C.byref(cur), 3) == 0x5
+
+    class Cell(C.Structure):
+        _fields_ = [("nof_prb", C.c_uint32), ("nof_ports", C.c_uint32), ("bw_idx", C.c_uint32), ("id", C.c_uint32),
+                    ("cp", C.c_int), ("phich_length", C.c_int), ("phich_resources", C.c_int)]
+    for bw, prb in enumerate((6, 15, 25, 50, 75, 100)):
+        for sfn in (0, 4, 517, 1020):
+            cell = Cell(prb, 2, 0, 1, 0, bw & 1, (bw + 1) & 3)
+            mib = np.zeros(24, np.uint8)
+            lib.srslte_pbch_mib_pack(C.byref(cell), sfn, mib.ctypes.data_as(C.c_void_p))
+            # 36.331 MIB: 3 bandwidth bits, phich-Duration, 2 phich-Resource bits, 8 SFN MSBs, 10 spare
+            want = [int(b) for b in f"{bw:03b}{bw & 1:01b}{(bw + 1) & 3:02b}{sfn >> 2:08b}"] + [0] * 10
+            assert mib.tolist() == want
+            out, osfn = Cell(), C.c_uint32()
+            lib.srslte_pbch_mib_unpack(mib.ctypes.data_as(C.c_void_p), C.byref(out), C.byref(osfn))
+            assert (out.nof_prb, out.phich_length, out.phich_resources, osfn.value) == (prb, bw & 1, (bw + 1) & 3,
+                                                                                         sfn & ~3)
+
+    class Rar(C.Structure):
+        _fields_ = [("hopping_flag", C.c_bool), ("rba", C.c_uint32), ("trunc_mcs", C.c_uint32),
+                    ("tpc_pusch", C.c_uint32), ("ul_delay", C.c_bool), ("cqi_request", C.c_bool)]
+    for hop, rba, mcs, tpc, dly, cqi in [(1, 0x2A5, 9, 5, 0, 1), (0, 1023, 15, 7, 1, 0), (0, 0, 0, 0, 0, 0)]:
+        g = np.array([int(b) for b in f"{hop:01b}{rba:010b}{mcs:04b}{tpc:03b}{dly:01b}{cqi:01b}"], np.uint8)
+        r = Rar()
+        lib.srslte_dci_rar_grant_unpack(C.byref(r), g.ctypes.data_as(C.c_void_p))
+        assert (r.hopping_flag, r.rba, r.trunc_mcs, r.tpc_pusch, r.ul_delay, r.cqi_request) == (
+            bool(hop), rba, mcs, tpc, bool(dly), bool(cqi))
+    # 36.213 4.2.3 timing advance
+    lib.srslte_N_ta_new_rar.restype = C.c_uint32
+    lib.srslte_N_ta_new.restype = C.c_uint32
+    assert lib.srslte_N_ta_new_rar(1282) == 20512
+    assert lib.srslte_N_ta_new(20512, 31) == 20512 and lib.srslte_N_ta_new(20512, 63) == 20512 + 512
+    assert lib.srslte_N_ta_new(100, 0) == 0

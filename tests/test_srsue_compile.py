@@ -1,9 +1,17 @@
-"""The drop-in boundary compiles srsUE unchanged: g++ -fsyntax-only of the reference's PHY worker (every DL
-call site of SURVEY.md 8b) and of the MAC's DL HARQ entity (softbuffer ownership, dl_harq.cc:169-259) against
-include/ (this repo's srslte/srslte.h, srslte/common/timestamp.h, srslte/utils/debug.h).  The only other
-srsLTE headers srsUE includes -- the UHD glue (srslte/cuhd/cuhd.h, radio_uhd.h:29) and the MAC bit utilities
-(srslte/utils/bit.h, mac/pdu.h) -- are not on the DL path and come from tests/c/srsue_stubs.  Needs the
-reference tree (this container only; the GPU box has no /root/reference)."""
+"""The drop-in boundary compiles srsUE's PHY and MAC unchanged: every `ue/src/phy/*.cc` and `ue/src/mac/*.cc` of
+the reference is compiled against include/ (this repo's srslte/srslte.h, srslte/common/timestamp.h,
+srslte/utils/debug.h, srslte/utils/bit.h).  The only other srsLTE header srsUE includes -- the UHD glue
+(srslte/cuhd/cuhd.h, radio_uhd.h:29) -- is not on the PHY path and comes from tests/c/srsue_stubs.
+
+Beyond compiling, the objects' undefined `srslte_*` symbols are resolved against libsrsue_amd.so's exports: every
+symbol srsUE's PHY and MAC need is exported by the library except the documented out-of-scope set (cell search,
+MIB / PBCH decoding, PRACH and its CFO pre-correction, PUCCH / SRS encoding and UL power control: the "OUT OF
+SCOPE" block of srslte.h), which an integration takes from srsLTE itself.
+
+`phy.cc:103` takes the address of a temporary (`&(ostringstream() << i)`, a reference-inherent error that
+older g++ accepted); that file alone is compiled with -fpermissive.
+Needs the reference tree (this container only; the GPU box has no /root/reference)."""
+import glob
 import os
 import shutil
 import subprocess
@@ -12,20 +20,73 @@ import pytest
 
 REF = "/root/reference"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "srsue_amd", "libsrsue_amd.so")
+
+SOURCES = sorted(os.path.relpath(p, REF) for p in glob.glob(os.path.join(REF, "ue/src/phy/*.cc")) +
+                 glob.glob(os.path.join(REF, "ue/src/mac/*.cc"))) if os.path.isdir(REF) else []
+
+# srsLTE modules srsUE uses that this library does not implement (srslte.h "OUT OF SCOPE" block)
+OUT_OF_SCOPE = {
+    "srslte_prach_init", "srslte_prach_free", "srslte_prach_get_preamble_format", "srslte_prach_gen",
+    "srslte_prach_send_tti", "srslte_cfo_init", "srslte_cfo_free", "srslte_cfo_correct",
+    "srslte_ue_mib_init", "srslte_ue_mib_decode", "srslte_pbch_decode_reset",
+    "srslte_ue_mib_sync_init", "srslte_ue_mib_sync_free", "srslte_ue_mib_sync_decode",
+    "srslte_ue_cellsearch_init", "srslte_ue_cellsearch_free", "srslte_ue_cellsearch_set_nof_frames_to_scan",
+    "srslte_ue_cellsearch_set_threshold", "srslte_ue_cellsearch_scan_N_id_2", "srslte_ue_cellsearch_scan",
+    "srslte_ue_ul_pregen_signals", "srslte_ue_ul_pucch_encode", "srslte_ue_ul_srs_encode",
+    "srslte_ue_ul_pusch_power", "srslte_ue_ul_pucch_power", "srslte_ue_ul_srs_power",
+}
+
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF) or shutil.which("g++") is None,
+                               reason="needs /root/reference and g++")
 
 
-@pytest.mark.skipif(not os.path.isdir(REF) or shutil.which("g++") is None, reason="needs /root/reference and g++")
-@pytest.mark.parametrize("src", ["ue/src/phy/phch_worker.cc", "ue/src/mac/dl_harq.cc"])
-def test_srsue_source_compiles_against_include(src):
-    cmd = ["g++", "-std=c++11", "-fsyntax-only", "-I" + os.path.join(ROOT, "include"),
+def _cmd(src, *extra):
+    cmd = ["g++", "-std=c++11", "-w", "-I" + os.path.join(ROOT, "include"),
            "-I" + os.path.join(ROOT, "tests", "c", "srsue_stubs"), "-I" + os.path.join(REF, "ue", "hdr"),
-           "-I" + os.path.join(REF, "liblte", "hdr"), os.path.join(REF, src)]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+           "-I" + os.path.join(REF, "liblte", "hdr")]
+    if src.endswith("phy/phy.cc"):
+        cmd.append("-fpermissive")
+    return cmd + list(extra) + [os.path.join(REF, src)]
+
+
+@needs_ref
+@pytest.mark.parametrize("src", SOURCES)
+def test_srsue_source_compiles_against_include(src):
+    out = subprocess.run(_cmd(src, "-fsyntax-only"), capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
 
 
-def test_stub_dir_holds_only_non_dl_srslte_headers():
+def _exports():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+@needs_ref
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libsrsue_amd.so not built")
+def test_srsue_phy_mac_link_against_library(tmp_path):
+    """Every srslte_* symbol the PHY + MAC objects reference is exported by libsrsue_amd.so, or is in the
+    documented out-of-scope set -- and every out-of-scope symbol is really referenced (the list is not padding)."""
+    undefined = set()
+    for i, src in enumerate(SOURCES):
+        obj = str(tmp_path / f"o{i}.o")
+        out = subprocess.run(_cmd(src, "-c", "-O0", "-o", obj), capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, src + "\n" + out.stderr[-3000:]
+        nm = subprocess.run(["nm", "-u", obj], capture_output=True, text=True, check=True).stdout
+        undefined |= {ln.split()[-1] for ln in nm.splitlines() if ln.split()[-1].startswith("srslte_")}
+    exports = _exports()
+    missing = sorted(undefined - exports - OUT_OF_SCOPE)
+    assert not missing, f"srsUE PHY/MAC symbols neither exported nor documented out of scope: {missing}"
+    assert OUT_OF_SCOPE <= undefined, f"out-of-scope list names symbols srsUE never uses: {sorted(OUT_OF_SCOPE - undefined)}"
+    assert not (OUT_OF_SCOPE & exports), "a symbol documented as out of scope is exported"
+    # the GPU-backed entry points of SURVEY.md 8b are among those srsUE uses and the library exports
+    for sym in ("srslte_ue_dl_init", "srslte_ue_dl_decode_fft_estimate", "srslte_pdsch_decode_rnti",
+                "srslte_softbuffer_rx_init", "srslte_ue_ul_pusch_encode_rnti_softbuffer", "srslte_ue_sync_zerocopy"):
+        assert sym in undefined and sym in exports, sym
+
+
+def test_stub_dir_holds_only_non_phy_srslte_headers():
     stubs = []
     for d, _, fs in os.walk(os.path.join(ROOT, "tests", "c", "srsue_stubs")):
         stubs += [os.path.relpath(os.path.join(d, f), os.path.join(ROOT, "tests", "c", "srsue_stubs")) for f in fs]
-    assert sorted(stubs) == ["srslte/cuhd/cuhd.h", "srslte/utils/bit.h"]
+    assert sorted(stubs) == ["srslte/cuhd/cuhd.h"]
