@@ -247,6 +247,13 @@ int or_pcfich(const or_cell_t *c, uint32_t sf, const float *grid, const float *c
 int or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL, uint32_t rv,
                     int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its, uint8_t *payload,
                     uint32_t *noi_out, uint32_t *cb_crc_ok_out) {
+  return or_dlsch_decode_cbits(llr, G, tbs, Qm, NL, rv, new_tb, sb, sb_stride, max_its, payload, noi_out,
+                               cb_crc_ok_out, NULL);
+}
+
+int or_dlsch_decode_cbits(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL, uint32_t rv,
+                          int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its, uint8_t *payload,
+                          uint32_t *noi_out, uint32_t *cb_crc_ok_out, uint32_t *cb_its_out) {
   or_cbsegm_t sg;
   if (or_cbsegm(tbs, &sg)) return -1;
   /* per-call decoder state: or_dlsch_decode / or_decode_subframe are called from several threads
@@ -267,6 +274,7 @@ int or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uin
               : mode == OR_TDEC_SIMD ? or_simd_decode_cb(h, din, K, max_its, 1, sg.C == 1, bits, &ok)
                                      : or_decode_cb((or_tdec_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok);
     if ((uint32_t)its > noi) noi = (uint32_t)its;
+    if (cb_its_out) cb_its_out[r] = (uint32_t)its;
     ncb_ok += ok ? 1 : 0;
     uint32_t L = sg.C > 1 ? 24 : 0;
     for (uint32_t k = F; k < K - L; k++) b[pb++] = bits[k];

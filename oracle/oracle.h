@@ -222,6 +222,10 @@ int      or_pcfich(const or_cell_t *c, uint32_t sf, const float *grid, const flo
 int      or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL,
                          uint32_t rv, int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its,
                          uint8_t *payload, uint32_t *noi_out, uint32_t *cb_crc_ok_out);
+/* same, plus each code block's iteration count (cb_its_out[C], may be NULL) */
+int      or_dlsch_decode_cbits(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL,
+                               uint32_t rv, int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its,
+                               uint8_t *payload, uint32_t *noi_out, uint32_t *cb_crc_ok_out, uint32_t *cb_its_out);
 /* End-to-end subframe decode (what srslte_ue_dl_decode_fft_estimate + srslte_pdsch_decode_rnti
  * do back to back).  Returns 0 if CRC ok. */
 int      or_decode_subframe(const or_cell_t *c, uint32_t sf, uint32_t cfi, const uint8_t *prb_mask,

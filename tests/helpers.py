@@ -46,6 +46,23 @@ def oracle_dlsch(cfg, llr, max_its=4, sb=None, new_tb=True, i16=None):
     return rc == 0, pay, noi.value, sb
 
 
+def oracle_dlsch_cbits(cfg, llr, max_its=4, i16=True):
+    """oracle_dlsch of a new TB that also returns each code block's iteration count:
+    (crc_ok, payload, tb_iterations, cb_iterations[C])"""
+    with O.tdec_mode(O.TDEC_I16 if i16 else O.TDEC_GEN):
+        L = O.lib()
+        s = O.cbsegm(cfg.tbs)
+        ncb = L.or_ncb(s.Kp)
+        sb = np.zeros(s.C * ncb, np.float32)
+        pay = np.zeros(cfg.tbs // 8, np.uint8)
+        noi, cbok = C.c_uint32(), C.c_uint32()
+        cbits = (C.c_uint32 * s.C)()
+        nl = (cfg.nl_td or 2) if cfg.tm == 2 else 1
+        rc = L.or_dlsch_decode_cbits(np.ascontiguousarray(llr, np.float32), len(llr), cfg.tbs, cfg.Qm, nl, cfg.rv,
+                                     1, sb, ncb, max_its, pay, C.byref(noi), C.byref(cbok), cbits)
+    return rc == 0, pay, noi.value, np.array(cbits[:], np.uint32)
+
+
 def tb_bytes(seed, tbs):
     return O.splitmix_bytes(0x5EED0000 + seed, tbs // 8)
 

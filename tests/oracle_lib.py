@@ -181,6 +181,9 @@ def lib():
             "or_dlsch_decode": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_int, f32, C.c_uint32, C.c_uint32, u8, C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_uint32)]),
+            "or_dlsch_decode_cbits": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                                C.c_int, f32, C.c_uint32, C.c_uint32, u8, C.POINTER(C.c_uint32),
+                                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
             "or_decode_subframe": (C.c_int, [C.POINTER(Cell), C.c_uint32, C.c_uint32, u8, C.c_uint32, C.c_uint32,
                                              C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, f32, f32, C.c_uint32,
                                              C.c_int, C.c_uint32, u8, C.POINTER(C.c_uint32)]),
