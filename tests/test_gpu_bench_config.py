@@ -12,7 +12,9 @@ iterations (the lane-pair early-stop logic of `tdec_p2_body.h`):
   `MI_DL_FLAG_KEEP_LLR`): payload, TB CRC, TB iterations and every code block's iterations must be identical in
   every copy of the subframe, wherever its code blocks land in the big batch (lane, group, pair half);
 * those GPU LLRs are within 1e-4 of the oracle front end's (`or_ofdm_rx` + `or_chest` + `or_pdsch_llr`), and the
-  oracle decode of the oracle's own LLRs gives the same TB CRC and payload (iterations: reported, see below).
+  oracle decode of the oracle's own LLRs gives the same TB CRC and payload (iterations are compared on the GPU's
+  LLRs only: the int16 quantiser q(x) = rint(32 x) can turn a 1e-7 LLR difference into a one-step input
+  difference, which may move a code block's stopping iteration without changing its decisions).
 
 Anchor: srsUE's `srslte_pdsch_decode_rnti` call (reference ue/src/phy/phch_worker.cc:347-348), iteration cap
 srslte_sch_set_max_noi (phch_worker.cc:87-89, 4 = ue.conf.example's default, the bench's max_its).
@@ -146,7 +148,8 @@ def test_bench_iterating_shape_compact_vs_oracle():
     b, cfgs = run_bench_config(n, iqs)
     assert b.turbo_sched == "p2", b.turbo_sched
     crc, CB = check_against(b, n, pool, exp_full, tbs_pool, sample)
-    assert crc.mean() > 0.8 and CB.mean() > 1.5
+    # the waterfall: a few failing TBs, most code blocks stop early while their TB's slowest one iterates on
+    assert 0.8 < crc.mean() < 1.0 and 1.1 < CB.mean() < CB.max(axis=1).mean()
     for k, j in enumerate(sample):
         assert orc[k][0] == exp[k][0] and np.array_equal(orc[k][1], exp[k][1]), f"pool entry {j}: oracle front"
     b.close()
