@@ -19,7 +19,7 @@
 static int g_q16 = 0;   // turbo arithmetic of the emulated decoder (MI_DL_FLAG_TDEC_I16)
 extern "C" void emu_set_tdec_i16(int on) { g_q16 = on; }
 
-static uint32_t crc8[256];
+static uint32_t crc8[256], crc8b[256];   // CRC24A / CRC24B byte tables
 
 // crossed-schedule lane decoder (two wavefronts per group, tdec_body.h tdec_lane_x): 0 = off, 1 = register
 // form, 2 = recompute form, 3 = two code blocks per lane (int16 only, tdec_p2_body.h)
@@ -100,7 +100,10 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
 
 extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
                               uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
-  for (uint32_t b = 0; b < 256; b++) crc8[b] = mi::crc24_byte_entry(b, mi::CRC24A_POLY);
+  for (uint32_t b = 0; b < 256; b++) {
+    crc8[b] = mi::crc24_byte_entry(b, mi::CRC24A_POLY);
+    crc8b[b] = mi::crc24_byte_entry(b, mi::CRC24B_POLY);
+  }
   mi::Plan P;
   if (P.build(cfgs, n, true)) return -1;
   std::vector<float> e(P.e_floats, 0.f), sb(P.sb_floats, 0.f), scr(P.scratch_floats, 0.f);
@@ -142,8 +145,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.scr = reinterpret_cast<uint32_t*>(&scr[gA.scratch_off]);
         a.q = a.scr + (size_t)(4 * gA.K + 8) * mi::LANES;
         a.pos = &P.kdata[kt.pos_off]; a.pi = &P.kdata[kt.pi_off];
-        a.crc_a = &P.kdata[kt.crca_off]; a.crc_b = &P.kdata[kt.crcb_off];
         a.crc8 = crc8;
+        a.crc8b = crc8b;
         a.dec = &dec[gA.dec_off];
         a.cb_bytes[0] = &cbb[(size_t)li[0] * mi::CB_BYTES_STRIDE];
         a.cb_bytes[1] = &cbb[(size_t)li[(a.live >> 1) & 1u] * mi::CB_BYTES_STRIDE];

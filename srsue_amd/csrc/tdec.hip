@@ -159,18 +159,17 @@ void tdec_kernel_i16xr(const float* __restrict__ sb, const uint32_t* __restrict_
 struct TdecP2ExecGpu {
   static constexpr bool SHARED = true;
   int wave;
-  uint32_t* xcrc;   // LDS [2 waves][64 lanes][2 halves] partial CB-CRC registers
+  uint32_t* xs;   // LDS [64]: wave F's per-lane code-block CRC verdicts
   template <class F, class B>
   __device__ void run(F f, B b) {
     if (wave == 0) f(); else b();
     __syncthreads();
   }
-  __device__ void crc_combine2(uint32_t (&c)[2], int lane) {
-    xcrc[(wave * LANES + lane) * 2] = c[0];
-    xcrc[(wave * LANES + lane) * 2 + 1] = c[1];
+  // wave F's value of this lane, on both waves
+  __device__ uint32_t share(uint32_t v, int lane) {
+    if (wave == 0) xs[lane] = v;
     __syncthreads();
-    c[0] ^= xcrc[((wave ^ 1) * LANES + lane) * 2];
-    c[1] ^= xcrc[((wave ^ 1) * LANES + lane) * 2 + 1];
+    return xs[lane];
   }
   __device__ bool pack_wave() const { return wave == 0; }
 };
@@ -184,9 +183,12 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                      const uint32_t* __restrict__ kdata, const uint32_t* __restrict__ pairs, uint32_t max_its,
                      uint32_t early_stop) {
-  __shared__ uint32_t crc8[256];
-  __shared__ uint32_t xcrc[2 * LANES * 2];
-  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+  __shared__ uint32_t crc8[256], crc8b[256];
+  __shared__ uint32_t xs[LANES];
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
+    crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+    crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
+  }
   __syncthreads();
   const uint32_t ga = pairs[2 * blockIdx.x], gbi = pairs[2 * blockIdx.x + 1];
   const bool paired = gbi != 0xFFFFFFFFu;
@@ -210,9 +212,8 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.q = a.scr + (size_t)(4 * K + 8) * LANES;
   a.pos = kdata + kt.pos_off;
   a.pi = kdata + kt.pi_off;
-  a.crc_a = kdata + kt.crca_off;
-  a.crc_b = kdata + kt.crcb_off;
   a.crc8 = crc8;
+  a.crc8b = crc8b;
   a.dec = dec + gA.dec_off;
   a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
   a.cb_bytes[1] = out.cb_bytes + (size_t)((a.live & 2u) ? li[1] : li[0]) * CB_BYTES_STRIDE;
@@ -223,7 +224,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
   a.max_its = max_its;
   a.early_stop = early_stop;
-  TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xcrc};
+  TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   const TdecP2Result r = tdec_p2_lane(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll

@@ -18,11 +18,18 @@
 // beta side is large -- so the LLRs of steps 0, 1 and 2 (the only ones with unreachable alpha states)
 // leave those states out of their maxima (llr_step<REACH>), exactly as -inf would.
 //
-// Per-code-block early stop: a lane iterates while either of its code blocks is undecided; a code block
-// that stops (CRC pass, or the iteration cap) has its decisions packed at once, so later iterations of
-// its partner never touch its outputs; iteration counts are per code block.  Outputs (packed bytes,
-// iterations, CRC verdict, partial TB-CRC register) are identical to the one-code-block-per-lane kernels
-// and to the oracle's int16 decoder (or_decode_cb16).
+// Per-code-block early stop: a lane iterates while either of its code blocks is undecided.  After each
+// iteration one pass over the decision rows (tdec_p2_check, on wave F) packs the bytes of every code block
+// still iterating and runs them through two byte-wise CRC24 registers: the code block's own CRC (CRC24B,
+// or CRC24A for a one-code-block TB: remainder 0 = pass, the early-stop test) and the partial TB CRC24A
+// of its payload bytes (tb_kernel combines them).  A code block that stops keeps the bytes of its last
+// pass; later iterations of its partner never touch its outputs; iteration counts are per code block.
+// Outputs (packed bytes, iterations, CRC verdict, partial TB-CRC register) are identical to the
+// one-code-block-per-lane kernels and to the oracle's int16 decoder (or_decode_cb16).
+//
+// The DEC2 passes carry each step's interleaver index pi(k) from the window's loads to its stores in
+// scalar registers (TdecWinP2::pk): no table load, and no wait on one, between a step's arithmetic and
+// its outputs.
 #pragma once
 #include "tdec_body.h"
 
@@ -35,9 +42,8 @@ struct TdecArgsP2 {
   uint32_t* q;            // packed q rows [3 (K + 4)][64] (lo = group A, hi = group B)
   const uint32_t* pos;    // [3 (K + 4)]
   const uint32_t* pi;     // [K]
-  const uint32_t* crc_a;  // [K] CRC24A / CRC24B single-bit contributions
-  const uint32_t* crc_b;
-  const uint32_t* crc8;   // [256] CRC24A byte table
+  const uint32_t* crc8;   // [256] CRC24A byte table (LDS on the GPU)
+  const uint32_t* crc8b;  // [256] CRC24B byte table
   uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][7]
   uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
   uint8_t* cb_bytes[2];   // each half's packed output row
@@ -70,6 +76,7 @@ struct TdecWinP2 {
   uint32_t s0[BETA_W], s1[BETA_W];
   float a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
   uint32_t r0[BETA_W], r1[BETA_W];
+  uint32_t pk[BETA_W];   // DEC2: pi(k) of the window's steps (wave-uniform: scalar registers)
   uint32_t ck[7];
 };
 
@@ -101,6 +108,7 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
       r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
     } else {
       const uint32_t pk = MI_PI(a, k);
+      r.pk[i] = pk;
       if constexpr (SQ) {
         r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i + 2);
       } else {
@@ -197,22 +205,18 @@ MI_HD inline void p2_xs_xp(const TdecArgsP2& a, const TdecWinP2& r, int i, uint3
   }
 }
 
-// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1; DEC2 updates w, stores the two decision
-// bits and folds them into each half's code-block CRC
+// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1; DEC2 updates w at row pi(k) (pk, carried
+// from the window's loads) and stores the two decision bits there (the code-block CRCs are taken from
+// the decision rows after the iteration: tdec_p2_check)
 template <bool DEC2>
-MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, P2 llr, P2 xs, uint32_t (&crc)[2]) {
-  const uint32_t k = base + i;
+MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, uint32_t pk, P2 llr, P2 xs) {
   if (!DEC2) {
     row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(llr), i);
   } else {
-    const uint32_t pk = MI_PI(a, k);
     row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
     const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
     const uint32_t b0 = (ng >> 15) & 1u, b1 = ng >> 31;
     row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 1)));
-    const uint32_t ta = a.crc_a[pk], tb = a.crc_b[pk];
-    crc[0] ^= b0 ? (a.crc24a[0] ? ta : tb) : 0u;
-    crc[1] ^= b1 ? (a.crc24a[1] ? ta : tb) : 0u;
   }
 }
 
@@ -285,8 +289,7 @@ MI_HD inline void p2_beta_window_mkq(const TdecArgsP2& a, int lane, const TdecWi
 }
 // wave F, phase 2: beta_{base+1..base+4} recomputed from the closing checkpoint, then alpha + LLRs
 template <bool DEC2, bool SQ>
-MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&al)[8],
-                                  uint32_t (&crc)[2]) {
+MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&al)[8]) {
   P2 xs[BETA_W], xp[BETA_W];
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, w, i, base, xs[i], xp[i]);
@@ -295,15 +298,14 @@ MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2
 #pragma unroll
   for (int i = BETA_W - 2; i >= 0; i--) beta_step<false>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
-  for (int i = 0; i < BETA_W; i++) p2_emit<DEC2>(a, lane, base, i, alpha_step<false>(al, bw[i], xs[i], xp[i]), xs[i], crc);
+  for (int i = 0; i < BETA_W; i++) p2_emit<DEC2>(a, lane, base, i, w.pk[i], alpha_step<false>(al, bw[i], xs[i], xp[i]), xs[i]);
   norm8<true>(al);
 }
 // wave B, phase 2: alpha of the window recomputed from its opening checkpoint (window 0: the start
 // state), then backward steps emitting the LLRs.  FIRST_WIN (window 0): steps 0..2 have unreachable
 // alpha states, left out of their LLR maxima.
 template <bool DEC2, bool SQ, bool FIRST_WIN>
-MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&b)[8],
-                                      uint32_t (&crc)[2]) {
+MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&b)[8]) {
   P2 xs[BETA_W], xp[BETA_W];
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, w, i, base, xs[i], xp[i]);
@@ -328,7 +330,7 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
     else if (FIRST_WIN && i == 1) llr = llr_step<0x11u>(aw[i], b, xs[i], xp[i]);
     else if (FIRST_WIN && i == 2) llr = llr_step<0x55u>(aw[i], b, xs[i], xp[i]);
     else llr = llr_step(aw[i], b, xs[i], xp[i]);
-    p2_emit<DEC2>(a, lane, base, i, llr, xs[i], crc);
+    p2_emit<DEC2>(a, lane, base, i, w.pk[i], llr, xs[i]);
     P2 nb[8];
     beta_step<false>(b, xs[i], xp[i], nb);
 #pragma unroll
@@ -361,7 +363,10 @@ struct TdecWin8P2 {
   TdecWinP2 lo, hi;
   uint32_t ck[P2_CKW];
 };
-struct TdecX8P2 { P2 xs[2 * BETA_W], xp[2 * BETA_W]; };
+struct TdecX8P2 {
+  P2 xs[2 * BETA_W], xp[2 * BETA_W];
+  uint32_t pk[2 * BETA_W];   // DEC2: pi(k) of the pair's steps
+};
 
 template <bool DEC2, bool SQ>
 MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t base, TdecX8P2& x) {
@@ -369,6 +374,13 @@ MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t bas
   for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, r.lo, i, base, x.xs[i], x.xp[i]);
 #pragma unroll
   for (int i = 0; i < BETA_W; i++) p2_xs_xp<DEC2, SQ>(a, r.hi, i, base + BETA_W, x.xs[BETA_W + i], x.xp[BETA_W + i]);
+  if constexpr (DEC2) {
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) {
+      x.pk[i] = r.lo.pk[i];
+      x.pk[BETA_W + i] = r.hi.pk[i];
+    }
+  }
 }
 MI_HD inline void p2_cp8(P2 (&d)[8], const P2 (&s)[8]) {
 #pragma unroll
@@ -403,9 +415,9 @@ MI_HD inline void p2_alpha_run(P2 (&v)[8], const TdecX8P2& x) {
 // wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1)
 template <bool DEC2>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
-                                   P2 (&al)[8], uint32_t (&crc)[2]) {
+                                   P2 (&al)[8]) {
   P2 B4[8], Bm[8], Bt[8];
-#define emit(I, BN) p2_emit<DEC2>(a, lane, base, I, alpha_step<false>(al, BN, x.xs[I], x.xp[I]), x.xs[I], crc)
+#define emit(I, BN) p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), x.xs[I])
   p2_cp8_opaque(B4, B8);
   p2_beta_run<7, 4>(B4, x);
   norm8<true>(B4);
@@ -444,14 +456,14 @@ MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2
 // LLR of step I from alpha_I (av) and the running beta_{I + 1}, then beta_I
 template <bool DEC2, bool FIRST_WIN, int I>
 MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&av)[8], uint32_t base,
-                                   P2 (&b)[8], uint32_t (&crc)[2]) {
+                                   P2 (&b)[8]) {
   P2 llr;
   // reachable alpha states at steps 0, 1, 2 from state 0 (p2_beta_emit_window)
   if (FIRST_WIN && I == 0) llr = llr_step<0x01u>(av, b, x.xs[I], x.xp[I]);
   else if (FIRST_WIN && I == 1) llr = llr_step<0x11u>(av, b, x.xs[I], x.xp[I]);
   else if (FIRST_WIN && I == 2) llr = llr_step<0x55u>(av, b, x.xs[I], x.xp[I]);
   else llr = llr_step(av, b, x.xs[I], x.xp[I]);
-  p2_emit<DEC2>(a, lane, base, I, llr, x.xs[I], crc);
+  p2_emit<DEC2>(a, lane, base, I, x.pk[I], llr, x.xs[I]);
   P2 nb[8];
   beta_step<false>(b, x.xs[I], x.xp[I], nb);
   p2_cp8(b, nb);
@@ -460,9 +472,9 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
 // LLR i from A(i) and beta_{base + i + 1} (the running b)
 template <bool DEC2, bool FIRST_WIN>
 MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
-                                       uint32_t base, P2 (&b)[8], uint32_t (&crc)[2]) {
+                                       uint32_t base, P2 (&b)[8]) {
   P2 A4[8], Am[8], At[8];
-#define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b, crc)
+#define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b)
   p2_cp8_opaque(A4, A0);
   p2_alpha_run<0, 3>(A4, x);
   norm8<true>(A4);
@@ -533,7 +545,7 @@ struct TdecP2X {
         });
   }
   // wave F, phase 2: windows h .. nw - 1, LLRs of steps K/2 .. K - 1
-  MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8], uint32_t (&crc)[2]) {
+  MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
     const uint32_t nw = a.K / BETA_W, h = nw / 2;
     const size_t ck = (size_t)2 * a.K;
 #if MI_TDEC_P2_CK8
@@ -556,14 +568,14 @@ struct TdecP2X {
         MI_SCHED_FENCE();
         load8(j + 1 < np ? w0 + 2 : w0, r);   // the last pair reloads itself (unused)
         MI_SCHED_FENCE();
-        p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al, crc);
+        p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
       }
     }
     if (n & 1u) {
       Win r;
       p2_load_window<DEC2, FIRST, SQF>(a, lane, (nw - 1) * BETA_W, r);
       p2_ck_load(a.scr, ck, nw, lane, r);
-      p2_alpha_window<DEC2, SQF>(a, lane, r, (nw - 1) * BETA_W, al, crc);
+      p2_alpha_window<DEC2, SQF>(a, lane, r, (nw - 1) * BETA_W, al);
     }
 #else
     pipe_windows<PF, Win>(
@@ -572,7 +584,7 @@ struct TdecP2X {
           p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
           p2_ck_load(a.scr, ck, w + 1, lane, r);
         },
-        [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al, crc); });
+        [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al); });
 #endif
   }
   // wave B, phase 1: tail, then beta_K .. beta_{K/2}, beta checkpoints h + 1 .. nw
@@ -629,7 +641,7 @@ struct TdecP2X {
         });
   }
   // wave B, phase 2: windows h - 1 .. 0 backward, LLRs of steps 0 .. K/2 - 1
-  MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8], uint32_t (&crc)[2]) {
+  MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
 #if MI_TDEC_P2_CK8
@@ -658,14 +670,14 @@ struct TdecP2X {
         MI_SCHED_FENCE();
         load8(j + 1 < np ? w0 - 2 : w0, r);   // the last pair reloads itself (unused)
         MI_SCHED_FENCE();
-        if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b, crc);
-        else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b, crc);
+        if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b);
+        else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b);
       }
     }
     if (h & 1u) {
       Win r;
       p2_load_window<DEC2, FIRST, SQF>(a, lane, 0, r);
-      p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b, crc);
+      p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
     }
 #else
     pipe_windows<PF, Win>(
@@ -675,8 +687,8 @@ struct TdecP2X {
           p2_ck_load(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
         },
         [&](const Win& r, uint32_t w) {
-          if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b, crc);
-          else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b, crc);
+          if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b);
+          else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
         });
 #endif
   }
@@ -686,7 +698,7 @@ struct TdecP2X {
 #define MI_TDEC_P2_DIAG 0
 #endif
 template <bool DEC2, bool FIRST, int SRC, class Exec>
-MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex, uint32_t (&cF)[2], uint32_t (&cB)[2]) {
+MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
   using X = TdecP2X<DEC2, FIRST, SRC>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
@@ -694,104 +706,116 @@ MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex, uint32_
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
 #endif
 #if MI_TDEC_P2_DIAG != 1
-  ex.run([&] { X::f2(a, lane, mF, cF); }, [&] { X::b2(a, lane, mB, cB); });
+  ex.run([&] { X::f2(a, lane, mF); }, [&] { X::b2(a, lane, mB); });
 #endif
 }
 
-// pack half H's decisions MSB first and run its TB-payload bytes through the byte-wise CRC24A (the partial
-// TB-CRC register tb_kernel combines, tdec_body.h tdec_pack).  H is a template parameter: a run-time index
-// into the argument struct's arrays would force the struct into private memory on the GPU.
-template <int H>
-MI_HD inline uint32_t tdec_p2_pack(const TdecArgsP2& a, int lane) {
-  const uint32_t b0 = a.F[H] / 8, b1 = a.K / 8 - (a.crc24a[H] ? 0 : 3);
-  uint8_t* out = a.cb_bytes[H];
-  uint32_t tb = 0;
-  for (uint32_t j = 0; j < a.K / 8; j++) {
-    uint32_t v = 0;
+// The pass after an iteration (wave F; tdec_body.h tdec_pack is the one-code-block form): for every half in
+// `act` (still iterating), pack its decision bits MSB first into its output row, run the bytes through the
+// code block's own CRC register -- CRC24A for a one-code-block TB, else CRC24B, the register of the whole
+// K-bit block (filler bits included, as the oracle checks it) is 0 iff the CRC passes -- and through the
+// partial TB CRC24A of its payload bytes F/8 .. K/8 - (CB CRC ? 3 : 0) that tb_kernel combines.  Returns
+// bit h = half h's code-block CRC passed.  (The byte-wise register of a K-bit block equals the XOR of the
+// per-bit contributions crc_a / crc_b[k] the one-code-block kernels accumulate: CRC is linear.)
+MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2]) {
+  uint32_t bl[2], bh[2], tb[2] = {0u, 0u}, cb[2] = {0u, 0u};
+  const uint32_t* ct[2];
 #pragma unroll
-    for (int q = 0; q < 8; q++) v |= (uint32_t)((row_ld(a.dec, 8 * j + q, lane) >> H) & 1u) << (7 - q);
-    out[j] = (uint8_t)v;
-    if (j >= b0 && j < b1) tb = ((tb << 8) & 0xFFFFFFu) ^ a.crc8[((tb >> 16) ^ v) & 0xFFu];
+  for (int h = 0; h < 2; h++) {
+    bl[h] = a.F[h] / 8;
+    bh[h] = a.K / 8 - (a.crc24a[h] ? 0 : 3);
+    ct[h] = a.crc24a[h] ? a.crc8 : a.crc8b;
   }
-  return tb;
-}
-// both halves at once (one pass over the decision rows)
-MI_HD inline void tdec_p2_pack2(const TdecArgsP2& a, int lane, uint32_t (&tbp)[2]) {
-  uint32_t bl[2], bh[2], tb[2] = {0u, 0u};
+  const bool p0 = act & 1u, p1 = (act >> 1) & 1u;
+  const uint32_t nb = a.K / 8;
+  // the decision rows of 4 bytes (32 rows) per chunk, the next chunk's loads issued before this chunk's
+  // bits are used (rows past K are clamped to row K - 1 and their bytes never used)
+  uint32_t d[2][32];
+  auto load = [&](uint32_t c, uint32_t (&dd)[32]) {
 #pragma unroll
-  for (int h = 0; h < 2; h++) { bl[h] = a.F[h] / 8; bh[h] = a.K / 8 - (a.crc24a[h] ? 0 : 3); }
-  for (uint32_t j = 0; j < a.K / 8; j++) {
-    uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t d = row_ld(a.dec, 8 * j + q, lane);
-      v0 |= (d & 1u) << (7 - q);
-      v1 |= ((d >> 1) & 1u) << (7 - q);
+    for (int q = 0; q < 32; q++) {
+      const uint32_t row = 32 * c + (uint32_t)q;
+      dd[q] = row_ld(a.dec, row < a.K ? row : a.K - 1, lane);
     }
-    a.cb_bytes[0][j] = (uint8_t)v0;
-    a.cb_bytes[1][j] = (uint8_t)v1;
-    if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];
-    if (j >= bl[1] && j < bh[1]) tb[1] = ((tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[1] >> 16) ^ v1) & 0xFFu];
+  };
+  auto run = [&](uint32_t c, const uint32_t (&dd)[32]) {
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) {
+      const uint32_t j = 4 * c + (uint32_t)jj;
+      if (j >= nb) break;   // wave-uniform
+      uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        v0 |= (dd[8 * jj + q] & 1u) << (7 - q);
+        v1 |= ((dd[8 * jj + q] >> 1) & 1u) << (7 - q);
+      }
+      if (p0) a.cb_bytes[0][j] = (uint8_t)v0;
+      if (p1) a.cb_bytes[1][j] = (uint8_t)v1;
+      cb[0] = ((cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((cb[0] >> 16) ^ v0) & 0xFFu];
+      cb[1] = ((cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((cb[1] >> 16) ^ v1) & 0xFFu];
+      if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];
+      if (j >= bl[1] && j < bh[1]) tb[1] = ((tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[1] >> 16) ^ v1) & 0xFFu];
+    }
+  };
+  const uint32_t nc = (nb + 3) / 4;
+  load(0, d[0]);
+  for (uint32_t c = 0; c < nc; c += 2) {
+    load(c + 1 < nc ? c + 1 : c, d[1]);
+    MI_SCHED_FENCE();
+    run(c, d[0]);
+    if (c + 1 >= nc) break;
+    load(c + 2 < nc ? c + 2 : c + 1, d[0]);
+    MI_SCHED_FENCE();
+    run(c + 1, d[1]);
   }
-  tbp[0] = tb[0];
-  tbp[1] = tb[1];
+  if (p0) tbp[0] = tb[0];
+  if (p1) tbp[1] = tb[1];
+  return (cb[0] == 0u ? 1u : 0u) | (cb[1] == 0u ? 2u : 0u);
 }
 
 // the iteration loop (tdec_body.h tdec_lane_x's source-mode sequence) with per-code-block stopping.
-// ex.crc_combine2 XORs both waves' partial CRC registers of both halves; ex.pack_wave is true on the wave
-// that packs outputs (GPU: wave F after the iteration's barrier; host: always).
+// ex.pack_wave is true on the wave that runs tdec_p2_check (GPU: wave F, after the iteration's barrier;
+// host: always); ex.share hands its verdicts to the other wave.  With early stop off (configs[0]'s fixed
+// iteration count) only the last iteration's pass runs.
 template <class Exec>
 MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
-  uint32_t active = a.live & 3u, packed = 0u;
+  uint32_t active = a.live & 3u;
   for (uint32_t it = 0; it < a.max_its && active; it++) {
-    uint32_t cF[2] = {0u, 0u}, cB[2] = {0u, 0u};
     constexpr uint32_t MK = MI_TDEC_MKQ_IT;
     if (it == 0) {
       if (MK == 0) {
-        tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex, cF, cB);
-        tdec_p2_xhalf<true, true, SRC_Q>(a, lane, ex, cF, cB);
+        tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex);
+        tdec_p2_xhalf<true, true, SRC_Q>(a, lane, ex);
       } else {
-        tdec_p2_xhalf<false, true, SRC_SB>(a, lane, ex, cF, cB);
-        tdec_p2_xhalf<true, true, SRC_SB>(a, lane, ex, cF, cB);
+        tdec_p2_xhalf<false, true, SRC_SB>(a, lane, ex);
+        tdec_p2_xhalf<true, true, SRC_SB>(a, lane, ex);
       }
     } else if (it < MK) {
-      tdec_p2_xhalf<false, false, SRC_SB>(a, lane, ex, cF, cB);
-      tdec_p2_xhalf<true, false, SRC_SB>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<false, false, SRC_SB>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_SB>(a, lane, ex);
     } else if (it == MK) {
-      tdec_p2_xhalf<false, false, SRC_MKQ>(a, lane, ex, cF, cB);
-      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<false, false, SRC_MKQ>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
     } else {
-      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex, cF, cB);
-      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex, cF, cB);
+      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
     }
-    uint32_t c[2] = {cF[0] ^ cB[0], cF[1] ^ cB[1]};
-    ex.crc_combine2(c, lane);
+    const bool last = it + 1 == a.max_its;
+    uint32_t ok = 0u;
+    if (a.early_stop || last) {   // wave-uniform
+      if (ex.pack_wave()) ok = tdec_p2_check(a, lane, active, r.tb_part);
+      ok = ex.share(ok, lane);
+    }
     uint32_t stop = 0u;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       if (!((active >> h) & 1u)) continue;
       r.its[h] = it + 1;
-      r.crc_ok[h] = c[h] == 0;
-      if ((a.early_stop && r.crc_ok[h]) || it + 1 == a.max_its) stop |= 1u << h;
+      r.crc_ok[h] = (ok >> h) & 1u;
+      if ((a.early_stop && r.crc_ok[h]) || last) stop |= 1u << h;
     }
     active &= ~stop;
-    // a half that stops while its partner goes on is packed now (its partner's iterations rewrite the
-    // decision rows); halves that stop together are packed after the loop in one pass
-    if (stop && active && ex.pack_wave()) {
-      if (stop & 1u) r.tb_part[0] = tdec_p2_pack<0>(a, lane);
-      else r.tb_part[1] = tdec_p2_pack<1>(a, lane);
-      packed |= stop;
-    }
-  }
-  if (ex.pack_wave()) {
-    const uint32_t rest = (a.live & 3u) & ~packed;
-    if (rest == 3u) {
-      tdec_p2_pack2(a, lane, r.tb_part);
-    } else {
-      if (rest & 1u) r.tb_part[0] = tdec_p2_pack<0>(a, lane);
-      if (rest & 2u) r.tb_part[1] = tdec_p2_pack<1>(a, lane);
-    }
   }
   return r;
 }
@@ -800,7 +824,7 @@ struct TdecP2ExecHost {
   static constexpr bool SHARED = false;
   template <class F, class B>
   void run(F f, B b) { f(); b(); }
-  void crc_combine2(uint32_t (&)[2], int) {}
+  uint32_t share(uint32_t v, int) { return v; }
   bool pack_wave() const { return true; }
 };
 
