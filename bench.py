@@ -105,17 +105,23 @@ def shard_range(total, rank, world):
     return start, per + (1 if rank < rem else 0)
 
 
-def reduce_over_ranks(elapsed, n_ok, n_cb, world, device="cpu"):
-    """The only cross-rank traffic: max of the elapsed time, sums of CRC-OK TBs and code blocks."""
+def reduce_over_ranks(elapsed, sums, world, device="cpu"):
+    """The only cross-rank traffic, after the timed region: every rank's elapsed time (all-gathered: the max is
+    the job's time, the list goes into the JSON) and the sums of this rank's end-of-run counters (`sums`: CRC-OK
+    bits, code blocks, CRC-OK TBs, iteration sums, payload mismatches ...).  Returns (max elapsed, [sums],
+    [elapsed per rank])."""
+    sums = [float(x) for x in sums]
     if world == 1:
-        return elapsed, float(n_ok), float(n_cb)
+        return elapsed, sums, [elapsed]
     if dist.get_backend() == "gloo":   # CPU rehearsal, or --share-gpu
         device = "cpu"
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    s = torch.tensor([float(n_ok), float(n_cb)], dtype=torch.float64, device=device)
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[dist.get_rank()] = elapsed
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)          # = all-gather of one scalar per rank
+    s = torch.tensor(sums, dtype=torch.float64, device=device)
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
-    return float(t[0]), float(s[0]), float(s[1])
+    per = [float(x) for x in t.cpu()]
+    return max(per), [float(x) for x in s.cpu()], per
 
 
 def make_pool(cfgs, snr_db, threads, first=0, h=None):
@@ -131,13 +137,30 @@ def make_pool(cfgs, snr_db, threads, first=0, h=None):
     return [r[0] for r in res], [r[1] for r in res]
 
 
+HOST_CPU_SHARE = 16   # CPUs a one-GPU job is granted on the GPU pool (nproc shows the whole machine's)
+
+
 def host_threads():
-    """CPU threads the baseline may use: this process's affinity, capped at the one-GPU box share (16)."""
+    """CPU threads the baseline may use: this process's affinity, capped at the one-GPU box share: the box runs
+    one GPU's job on a 16-CPU share of a larger machine (OMP_NUM_THREADS / MAX_JOBS are set to 16 there), so
+    `nproc` overstates what this job may use; SURVEY 8d (ii)'s "all cores" is that share."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    return max(1, min(HOST_CPU_SHARE, n))
+
+
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the baseline line (core count and model)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def run_for(seconds, nthreads, work):
@@ -187,7 +210,9 @@ def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what, i16):
     L.or_set_tdec_mode(O.TDEC_GEN)
     dec = "SSE4.1 int16 turbo (oracle/o_simd.c)" if i16 else "float srsLTE-gen turbo restatement"
     return {"value": round(bT / dtT / 1e6, 3), "unit": "Mbps", "cores": T, "kind": "port",
-            "value_1core": round(b1 / dt1 / 1e6, 3),
+            "value_1core": round(b1 / dt1 / 1e6, 3), "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "cores_note": f"all of the job's {HOST_CPU_SHARE}-CPU share of the host (the pool's per-GPU grant; "
+                          f"os.cpu_count() reports the whole machine)",
             "sample": f"{nT} subframes ({what}) through the oracle's full chain with the {dec}, {T} threads in "
                       f"{dtT:.1f} s; 1 thread: {n1} subframes in {dt1:.1f} s",
             "codeblocks_per_s": round(cT / dtT, 1)}
@@ -281,7 +306,7 @@ def bench_codeblocks(args, world, rank, dev):
     for k, t in enumerate(tbs[1:min(S, args.steps)], 1):
         assert np.array_equal(t.results()[0][:pool], dec[:pool]), f"stream {k} decoded differently"
     ber = float(np.mean(dec[:pool] != bits))
-    elapsed, _, n_all = reduce_over_ranks(elapsed, 0, n, world, dev)
+    elapsed, (n_all,), _ = reduce_over_ranks(elapsed, [n], world, dev)
     if rank:
         return None
     cbps = n_all * args.steps / elapsed
@@ -326,7 +351,8 @@ def bench_codeblocks(args, world, rank, dev):
                                "value_1core": round(m1 * K / dt1 / 1e6, 4),
                                "sample": f"{mT} code blocks K=6144 x 8 iterations through the {dec}, {T} threads "
                                          f"in {dtT:.1f} s; 1 thread: {m1} in {dt1:.1f} s",
-                               "codeblocks_per_s": round(mT / dtT, 2)}
+                               "codeblocks_per_s": round(mT / dtT, 2), "cpu_model": cpu_model(),
+                               "host_cpus_visible": os.cpu_count()}
     tb.close()
     return out
 
@@ -618,10 +644,13 @@ def dry_run(args, world, rank):
     good = sum(int(np.array_equal(pay[i * 549:(i + 1) * 549], tb_payload(first + i, 549))) for i in range(n))
     shards = [None] * world
     dist.all_gather_object(shards, [first, n, good])
-    elapsed, n_ok, n_cb = reduce_over_ranks(elapsed, int(ok.sum()), n, world)
+    elapsed, (n_ok, n_cb, its_sum, n_bad), per = reduce_over_ranks(
+        elapsed, [int(ok.sum()), n, int(its.sum()), n - good], world)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "shards": shards, "crc_ok": n_ok, "subframes": n_cb,
-                          "elapsed_max_s": elapsed}), flush=True)
+                          "crc_ok_rate": n_ok / n_cb, "mean_turbo_iterations": its_sum / n_cb,
+                          "payload_mismatches": n_bad, "elapsed_max_s": elapsed, "elapsed_per_rank_s": per}),
+              flush=True)
 
 
 def main():
@@ -724,14 +753,18 @@ def main():
     m = measure(args, cfgs, pool_iq, pool_tb, world, dev, args.steps, args.warmup)
     batch, stage, nprof, elapsed = m["batch"], m["stage"], m["nprof"], m["elapsed"]
     n_ok, its, bad, bits_ok = m["n_ok"], m["its"], m["bad"], m["bits_ok"]
-    elapsed, bits_all, ncb_all = reduce_over_ranks(elapsed, bits_ok, batch.n_codeblocks, world, dev)
+    # global counters: CRC-OK bits, code blocks, CRC-OK TBs, TB iterations, TBs, payload mismatches (every rank)
+    elapsed, (bits_all, ncb_all, ok_all, its_all, tb_all, bad_all), per_rank = reduce_over_ranks(
+        elapsed, [bits_ok, batch.n_codeblocks, n_ok, int(its.sum()), B, bad], world, dev)
     # the same shard in the turbo decoder's waterfall region (every code block iterates): reported beside value
     itr = None
     if args.config == 4 and args.iterating_snr > 0:
         ipool_iq, ipool_tb = make_pool(cfgs[:P], args.iterating_snr, threads, first, h)
         isteps = max(1, min(args.steps, 5))
         im = measure(args, cfgs, ipool_iq, ipool_tb, world, dev, isteps, 1)
-        iel, ibits, incb = reduce_over_ranks(im["elapsed"], im["bits_ok"], im["batch"].n_codeblocks, world, dev)
+        iel, (ibits, incb, iok, iits, itb, ibad), _ = reduce_over_ranks(
+            im["elapsed"], [im["bits_ok"], im["batch"].n_codeblocks, im["n_ok"], int(im["its"].sum()), B, im["bad"]],
+            world, dev)
         if rank == 0:
             ib = im["batch"]
             ims = im["stage"]["tdec"]
@@ -739,8 +772,8 @@ def main():
             itr = {"snr_db": args.iterating_snr, "steps": isteps, "ms_per_step": round(iel / isteps * 1e3, 3),
                    "Mbps": round(ibits * isteps / iel / 1e6, 2),
                    "turbo_codeblocks_per_s": round(incb * isteps / iel, 1),
-                   "crc_ok_rate": round(im["n_ok"] / B, 6), "mean_turbo_iterations": round(float(im["its"].mean()), 4),
-                   "payload_mismatches_crc_ok": im["bad"],
+                   "crc_ok_rate": round(iok / itb, 6), "mean_turbo_iterations": round(iits / itb, 4),
+                   "payload_mismatches_crc_ok": int(ibad),
                    "stage_ms_per_step": {k: round(v, 4) for k, v in im["stage"].items()},
                    "tdec_roofline": {"kernel": tdec_kernel_name(ib.turbo_sched), "bound": "hbm",
                                      "achieved": round(iach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -773,8 +806,9 @@ def main():
                        "channel_estimates": "full" if (args.ce == "full" or args.ctrl) else "compact",
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
-            "crc_ok_rate": round(n_ok / B, 6), "mean_turbo_iterations": round(float(its.mean()), 4),
-            "payload_mismatches_crc_ok": bad,
+            "crc_ok_rate": round(ok_all / tb_all, 6), "mean_turbo_iterations": round(its_all / tb_all, 4),
+            "payload_mismatches_crc_ok": int(bad_all), "subframes_all_ranks": int(tb_all),
+            "elapsed_per_rank_s": [round(x, 6) for x in per_rank],
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": tdec_kernel_name(batch.turbo_sched), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

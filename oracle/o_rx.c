@@ -261,6 +261,7 @@ int or_dlsch_decode_cbits(const float *llr, uint32_t G, uint32_t tbs, uint32_t Q
   int mode = or_get_tdec_mode();
   void *h = malloc(mode == OR_TDEC_GEN ? sizeof(or_tdec_t)
                    : mode == OR_TDEC_I16 ? sizeof(or_tdec16_t) : or_simd_tdec_size());
+  if (mode == OR_TDEC_SIMD) or_simd_tdec_init(h);   /* empty QPP-table cache: built once for the TB's K */
   float *din = (float *)malloc(sizeof(float) * 3 * (OR_TCOD_MAX_K + 4));
   uint8_t *bits = (uint8_t *)malloc(OR_TCOD_MAX_K), *b = (uint8_t *)malloc(sg.B + 8);
   uint32_t pos = 0, pb = 0, noi = 0, ncb_ok = 0;

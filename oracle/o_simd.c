@@ -21,14 +21,39 @@
 
 void or_trellis(int s, int u, int *next, int *z);
 
+/* Decoder state of one thread.  The QPP table of the last K stays valid across calls (K_tab), so a TB's code
+ * blocks (and a batch of equal-K blocks) build it once; the three input streams are de-interleaved once per
+ * code block (qs / qp1 / qp2) instead of per iteration. */
 struct or_simd_tdec {
-  uint32_t K;
-  uint32_t pi[OR_TCOD_MAX_K], pinv[OR_TCOD_MAX_K];
+  uint32_t K, K_tab;
+  uint32_t pi[OR_TCOD_MAX_K];
   int16_t  w[OR_TCOD_MAX_K], llr1[OR_TCOD_MAX_K], llr2[OR_TCOD_MAX_K];
-  int16_t  xs[OR_TCOD_MAX_K + 3], xp[OR_TCOD_MAX_K + 3];
+  int16_t  xs[OR_TCOD_MAX_K + 3], xp[OR_TCOD_MAX_K + 3], xp2[OR_TCOD_MAX_K + 3];
+  int16_t  qs[OR_TCOD_MAX_K + 8];
   int16_t  q[3 * OR_TCOD_MAX_K + 12];
+  uint8_t  bytes[OR_TCOD_MAX_K / 8 + 1];
   __m128i  beta[OR_TCOD_MAX_K + 4];
 };
+
+/* byte-wise CRC24A / CRC24B tables (register of a message byte; the bit-serial or_crc24a/b of o_common.c
+ * over the same bits gives the same remainder) */
+static uint32_t CRC_A8[256], CRC_B8[256];
+static void __attribute__((constructor)) crc_tables_init(void) {
+  for (uint32_t b = 0; b < 256; b++) {
+    uint32_t ra = b << 16, rb = b << 16;
+    for (int i = 0; i < 8; i++) {
+      ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864CFBu) : (ra << 1);
+      rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) : (rb << 1);
+    }
+    CRC_A8[b] = ra & 0xFFFFFFu;
+    CRC_B8[b] = rb & 0xFFFFFFu;
+  }
+}
+static uint32_t crc24_bytes(const uint8_t *p, uint32_t n, const uint32_t *T) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < n; i++) r = ((r << 8) & 0xFFFFFFu) ^ T[((r >> 16) ^ p[i]) & 0xFFu];
+  return r;
+}
 
 /* shuffle controls and masks derived from the trellis (see o_fec.c header) */
 static __m128i SN0, SN1, MP0, MP1, SA, SB, MA, MB, BC0;
@@ -106,32 +131,58 @@ static void quantize(const float *in, int16_t *q, uint32_t n) {
 }
 
 size_t or_simd_tdec_size(void) { return sizeof(struct or_simd_tdec) + 64; }
+/* a fresh state (the QPP-table cache starts empty) */
+void or_simd_tdec_init(void *state) {
+  struct or_simd_tdec *h = (struct or_simd_tdec *)(((uintptr_t)state + 63) & ~(uintptr_t)63);
+  h->K_tab = 0;
+}
 
 int or_simd_decode_cb(void *state, const float *in, uint32_t K, uint32_t max_its, int early_stop, int crc_type,
                       uint8_t *bits, int *crc_ok) {
   struct or_simd_tdec *h = (struct or_simd_tdec *)(((uintptr_t)state + 63) & ~(uintptr_t)63);
-  if (K > OR_TCOD_MAX_K || or_qpp(K, h->pi)) return -1;
+  if (K > OR_TCOD_MAX_K || K % 8) return -1;
+  if (h->K_tab != K) {
+    if (or_qpp(K, h->pi)) return -1;
+    h->K_tab = K;
+  }
   h->K = K;
-  for (uint32_t i = 0; i < K; i++) h->pinv[h->pi[i]] = i;
   memset(h->w, 0, sizeof(int16_t) * K);
   quantize(in, h->q, 3 * K + 12);
   const int16_t *q = h->q;
+  /* de-interleave once: systematic, parity 1 (DEC1's xp) and parity 2 (DEC2's xp), tails included */
+  for (uint32_t k = 0; k < K; k++) { h->qs[k] = q[3 * k]; h->xp[k] = q[3 * k + 1]; h->xp2[k] = q[3 * k + 2]; }
+  for (uint32_t j = 0; j < 3; j++) {
+    h->xp[K + j] = q[3 * K + 2 * j + 1];
+    h->xp2[K + j] = q[3 * K + 7 + 2 * j];
+  }
+  const uint32_t *T = crc_type ? CRC_A8 : CRC_B8;
   uint32_t its = 0;
   int ok = 0;
   do {
-    for (uint32_t k = 0; k < K; k++) { h->xs[k] = (int16_t)(q[3 * k] + h->w[k]); h->xp[k] = q[3 * k + 1]; }
-    for (uint32_t j = 0; j < 3; j++) { h->xs[K + j] = q[3 * K + 2 * j]; h->xp[K + j] = q[3 * K + 2 * j + 1]; }
+    /* DEC1 systematic + extrinsic, 8 at a time (wrapping add as the scalar int16 cast; no overflow in bounds) */
+    for (uint32_t k = 0; k < K; k += 8)
+      _mm_storeu_si128((__m128i *)(h->xs + k), _mm_add_epi16(_mm_loadu_si128((const __m128i *)(h->qs + k)),
+                                                            _mm_loadu_si128((const __m128i *)(h->w + k))));
+    for (uint32_t j = 0; j < 3; j++) h->xs[K + j] = q[3 * K + 2 * j];
     map_sse(h->xs, h->xp, h->llr1, K, h->beta);
     for (uint32_t k = 0; k < K; k++) {
-      h->xs[k] = clamp16((int32_t)h->llr1[h->pi[k]] - h->w[h->pi[k]], OR_I16_CX);
-      h->xp[k] = q[3 * k + 2];
+      const uint32_t p = h->pi[k];
+      h->xs[k] = clamp16((int32_t)h->llr1[p] - h->w[p], OR_I16_CX);
     }
-    for (uint32_t j = 0; j < 3; j++) { h->xs[K + j] = q[3 * K + 6 + 2 * j]; h->xp[K + j] = q[3 * K + 7 + 2 * j]; }
-    map_sse(h->xs, h->xp, h->llr2, K, h->beta);
-    for (uint32_t k = 0; k < K; k++) h->w[h->pi[k]] = clamp16((int32_t)h->llr2[k] - h->xs[k], OR_I16_CW);
+    for (uint32_t j = 0; j < 3; j++) h->xs[K + j] = q[3 * K + 6 + 2 * j];
+    map_sse(h->xs, h->xp2, h->llr2, K, h->beta);
+    /* extrinsic update and decisions in natural order in one pass */
+    for (uint32_t k = 0; k < K; k++) {
+      const uint32_t p = h->pi[k];
+      h->w[p] = clamp16((int32_t)h->llr2[k] - h->xs[k], OR_I16_CW);
+      bits[p] = h->llr2[k] > 0 ? 1 : 0;
+    }
     its++;
-    for (uint32_t i = 0; i < K; i++) bits[i] = h->llr2[h->pinv[i]] > 0 ? 1 : 0;
-    ok = ((crc_type ? or_crc24a(bits, K) : or_crc24b(bits, K)) == 0);
+    for (uint32_t i = 0; i < K / 8; i++) {
+      const uint8_t *b = bits + 8 * i;
+      h->bytes[i] = (uint8_t)(b[0] << 7 | b[1] << 6 | b[2] << 5 | b[3] << 4 | b[4] << 3 | b[5] << 2 | b[6] << 1 | b[7]);
+    }
+    ok = crc24_bytes(h->bytes, K / 8, T) == 0;
     if (early_stop && ok) break;
   } while (its < max_its);
   *crc_ok = ok;
@@ -148,6 +199,7 @@ typedef struct {
 static void *batch_worker(void *arg) {
   batch_job_t *j = (batch_job_t *)arg;
   void *st = malloc(or_simd_tdec_size());
+  or_simd_tdec_init(st);
   for (;;) {
     pthread_mutex_lock(&j->mu);
     uint32_t i = j->next++;

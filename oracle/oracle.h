@@ -126,6 +126,7 @@ int      or_get_tdec_mode(void);
 /* SSE4.1 int16 decoder (CPU baseline), bit-identical to or_decode_cb16.  state: or_simd_tdec_size()
  * bytes (any alignment).  Batch: n code blocks of equal K, input i at in + i*stride floats. */
 size_t   or_simd_tdec_size(void);
+void     or_simd_tdec_init(void *state);
 int      or_simd_decode_cb(void *state, const float *in, uint32_t K, uint32_t max_its, int early_stop,
                            int crc_type, uint8_t *bits, int *crc_ok);
 int      or_simd_decode_batch(const float *in, uint32_t stride, uint32_t n, uint32_t K, uint32_t max_its,

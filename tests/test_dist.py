@@ -34,8 +34,8 @@ def _worker(rank, world, port, q):
                              its.ctypes.data, None)
     good = all(np.array_equal(pe[i * 549:(i + 1) * 549], tbs[i]) for i in range(n))
     elapsed = 0.5 + rank       # stand-in timings: the max must win
-    t, n_ok, n_cb = bench.reduce_over_ranks(elapsed, int(ok.sum()), n, world)
-    q.put((rank, first, n, good, t, n_ok, n_cb))
+    t, (n_ok, n_cb, its_sum), per = bench.reduce_over_ranks(elapsed, [int(ok.sum()), n, int(its.sum())], world)
+    q.put((rank, first, n, good, t, n_ok, n_cb, its_sum, per))
     dist.destroy_process_group()
 
 
@@ -58,6 +58,8 @@ def test_two_rank_shards_without_data_path_collective(built):
     assert all(r[3] for r in res)                                     # each rank decoded its own TBs
     assert all(r[4] == 1.5 for r in res)                              # max over ranks
     assert all(r[5] == 6 and r[6] == 6 for r in res)                  # sums over ranks
+    assert all(r[7] == 6 for r in res)                                # iteration sums: 1 per TB at 30 dB
+    assert all(r[8] == [0.5, 1.5] for r in res)                       # every rank's elapsed time, in rank order
 
 
 def test_shard_range_covers_everything():
@@ -98,6 +100,9 @@ def test_bench_spawns_its_own_ranks(built, tmp_path):
     assert len(lines) == 1                                   # only rank 0 prints
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["subframes"] == total and r["crc_ok"] == total
+    # the line's statistics are global (both ranks' TBs), with each rank's elapsed time
+    assert r["crc_ok_rate"] == 1.0 and r["mean_turbo_iterations"] == 1.0 and r["payload_mismatches"] == 0
+    assert len(r["elapsed_per_rank_s"]) == 2 and r["elapsed_max_s"] == max(r["elapsed_per_rank_s"])
     assert [s[:2] for s in r["shards"]] == [[0, 3], [3, 3]]  # contiguous shards
     assert all(s[2] == s[1] for s in r["shards"])           # every TB equals the transmitted bytes
 
@@ -135,3 +140,8 @@ def test_bench_two_ranks_on_one_gpu(built):
     assert d["n_gpus"] == 2 and d["config"]["share_gpu_rehearsal"] is True
     assert d["config"]["subframes_per_gpu"] == 256
     assert d["crc_ok_rate"] == 1.0 and d["payload_mismatches_crc_ok"] == 0
+    # global statistics: both ranks' subframes, each rank's elapsed time, value from the max of them
+    assert d["subframes_all_ranks"] == 512 and d["mean_turbo_iterations"] == 1.0
+    per = d["elapsed_per_rank_s"]
+    assert len(per) == 2 and abs(d["ms_per_step"] - max(per) / 2 * 1e3) < 1e-2
+    assert abs(d["value"] - 512 * 75376 * 2 / max(per) / 1e6) < 1e-3 * d["value"]
