@@ -10,7 +10,7 @@
  * (36.212 5.1.3.2, chunk-parallel recursive encoders) -> rate matching (5.1.4.1, full circular buffer)
  * -> channel interleaver (5.2.2.8, no UCI) -> scrambling (36.211 5.3.1) -> modulation (7.1) ->
  * transform precoding (5.3.3, mixed-radix DFT of M = 12 L_prb) -> mapping (5.3.4, per-slot PRBs) +
- * DMRS (5.5.2.1, L_prb >= 3) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
+ * DMRS (5.5.2.1; L_prb 1, 2: the tabulated base sequences of 5.5.1.2) -> SC-FDMA (5.6: N-point transform, half-subcarrier shift, CP).
  * Uplink control information is multiplexed as 36.212 5.2.2.6-5.2.2.8 prescribe: CQI (O <= 11 bits: the
  * (32, O) block code; O > 11: CRC8 + tail-biting convolutional code) ahead of the data in the multiplexed
  * sequence, RI (1 or 2 bits) in the interleaver columns next to the HARQ-ACK ones (rate matching of the
@@ -65,6 +65,18 @@ int    mi_ul_batch_stage_ms(mi_ul_batch_t *b, float *ms /* MI_UL_NSTAGES */, uin
 void   mi_ul_batch_profile_reset(mi_ul_batch_t *b);
 /* algorithmic HBM bytes per run: payload read + IQ write (SURVEY.md 8d convention) */
 double mi_ul_batch_algo_bytes(const mi_ul_batch_t *b);
+
+/* PUSCH frequency hopping type 2 (subband hopping, 36.211 5.3.4; selected by the DCI format 0 / RAR hopping
+ * bits, 36.213 8.4 Table 8.4-1): the first PRB of the allocation n_vrb .. n_vrb + L - 1 in slot ns (0..19) of
+ * the frame, given the cell's pusch-HoppingOffset n_ho, hopping subbands n_sb (>= 1), the hopping mode
+ * (intra = intra- and inter-subframe, else inter-subframe) and CURRENT_TX_NB.  Every VRB is mapped by
+ *   n~_PRB = (n~_VRB + f_hop(i) N_sb^RB + ((N_sb^RB - 1) - 2 (n~_VRB mod N_sb^RB)) f_m(i)) mod (N_sb^RB N_sb),
+ * n~_VRB = n_VRB - N~_HO / 2 and n_PRB = n~_PRB + N~_HO / 2 (N_sb > 1; N~_HO = n_ho rounded up to even,
+ * N_sb^RB = floor((N_RB - N~_HO - N_RB mod 2) / N_sb)), N_sb^RB = N_RB and no offset for N_sb = 1; f_hop and
+ * f_m from the Gold sequence c(k) with c_init = N_ID^cell restarted each frame, i = ns (intra) or ns / 2.
+ * Returns the lowest PRB of the mapped set, or -1 if the set is not L contiguous PRBs inside the band. */
+int mi_ul_hop_type2(uint32_t nof_prb, uint32_t n_ho, uint32_t n_sb, int intra, uint32_t cell_id, uint32_t n_vrb,
+                    uint32_t L, uint32_t ns, uint32_t current_tx_nb);
 
 #ifdef __cplusplus
 }

@@ -19,8 +19,10 @@
  *          column by column -> SC-FDMA data symbol l takes the rows of column l;
  *   scrambling (36.211 5.3.1): c_init = n_RNTI 2^14 + sf 2^9 + N_ID; modulation as the DL (7.1);
  *   transform precoding (5.3.3): z = (1/sqrt M) DFT_M per data symbol;
- *   DMRS (5.5.2.1, M_sc >= 36 only -- the L_prb = 1, 2 base sequences are tables this restatement
- *          does not carry): ZC root q of N_ZC = largest prime < M_sc, group hopping f_gh, sequence
+ *   DMRS (5.5.2.1): for M_sc = 12 / 24 (L_prb = 1, 2) the base sequences of Tables 5.5.1.2-1 / -2
+ *          (transcribed; their low-PAPR design property is checked per row in the CPU suite, so this is
+ *          pinned by the tables' defining property, not by a reference implementation), for M_sc >= 36 the
+ *          ZC root q of N_ZC = largest prime < M_sc; group hopping f_gh, sequence
  *          hopping v (M_sc >= 72), f_ss = (N_ID + delta_ss) mod 30, alpha = 2 pi n_cs / 12 with
  *          n_cs = (n1_DMRS[cyclic_shift] + n2_DMRS[dci field] + n_PRS(n_s)) mod 12, symbol 3 of each slot;
  *   mapping (5.3.4): PRBs n_prb .. n_prb + L - 1 of symbols 0-2, 4-6 of slot 0, and of slot 1 unless
@@ -234,6 +236,70 @@ void or_dft_m(const float *in, uint32_t M, float *out, int inverse) {
   }
 }
 
+/* 36.211 Tables 5.5.1.2-1 / 5.5.1.2-2: phi(n) of the base sequences for M_sc = 12 / 24, u = 0..29 */
+static const int8_t PHI12[30][12] = {
+    {-1,  1,  3, -3,  3,  3,  1,  1,  3,  1, -3,  3},
+    { 1,  1,  3,  3,  3, -1,  1, -3, -3,  1, -3,  3},
+    { 1,  1, -3, -3, -3, -1, -3, -3,  1, -3,  1, -1},
+    {-1,  1,  1,  1,  1, -1, -3, -3,  1, -3,  3, -1},
+    {-1,  3,  1, -1,  1, -1, -3, -1,  1, -1,  1,  3},
+    { 1, -3,  3, -1, -1,  1,  1, -1, -1,  3, -3,  1},
+    {-1,  3, -3, -3, -3,  3,  1, -1,  3,  3, -3,  1},
+    {-3, -1, -1, -1,  1, -3,  3, -1,  1, -3,  3,  1},
+    { 1, -3,  3,  1, -1, -1, -1,  1,  1,  3, -1,  1},
+    { 1, -3, -1,  3,  3, -1, -3,  1,  1,  1,  1,  1},
+    {-1,  3, -1,  1,  1, -3, -3, -1, -3, -3,  3, -1},
+    { 3,  1, -1, -1,  3,  3, -3,  1,  3,  1,  3,  3},
+    { 1, -3,  1,  1, -3,  1,  1,  1, -3, -3, -3,  1},
+    { 3,  3, -3,  3, -3,  1,  1,  3, -1, -3,  3,  3},
+    {-3,  1, -1, -3, -1,  3,  1,  3,  3,  3, -1,  1},
+    { 3, -1,  1, -3, -1, -1,  1,  1,  3,  1, -1, -3},
+    { 1,  3,  1, -1,  1,  3,  3,  3, -1, -1,  3, -1},
+    {-3,  1,  1,  3, -3,  3, -3, -3,  3,  1,  3, -1},
+    {-3,  3,  1,  1, -3,  1, -3, -3, -1, -1,  1, -3},
+    {-1,  3,  1,  3,  1, -1, -1,  3, -3, -1, -3, -1},
+    {-1, -3,  1,  1,  1,  1,  3,  1, -1,  1, -3, -1},
+    {-1,  3, -1,  1, -3, -3, -3, -3, -3,  1, -1, -3},
+    { 1,  1, -3, -3, -3, -3, -1,  3, -3,  1, -3,  3},
+    { 1,  1, -1, -3, -1, -3,  1, -1,  1,  3, -1,  1},
+    { 1,  1,  3,  1,  3,  3, -1,  1, -1, -3, -3,  1},
+    { 1, -3,  3,  3,  1,  3,  3,  1, -3, -1, -1,  3},
+    { 1,  3, -3, -3,  3, -3,  1, -1, -1,  3, -1, -3},
+    {-3, -1, -3, -1, -3,  3,  1, -1,  1,  3, -3, -3},
+    {-1,  3, -3,  3, -1,  3,  3, -3,  3,  3, -1, -1},
+    { 3, -3, -3, -1, -1, -3, -1,  3, -3,  3,  1, -1}};
+static const int8_t PHI24[30][24] = {
+    {-1,  3,  1, -3,  3, -1,  1,  3, -3,  3,  1,  3, -3,  3,  1,  1, -1,  1,  3, -3,  3, -3, -1, -3},
+    {-3,  3, -3, -3, -3,  1, -3, -3,  3, -1,  1,  1,  1,  3,  1, -1,  3, -3, -3,  1,  3,  1,  1, -3},
+    { 3, -1,  3,  3,  1,  1, -3,  3,  3,  3,  3,  1, -1,  3, -1,  1,  1, -1, -3, -1, -1,  1,  3,  3},
+    {-1, -3,  1,  1,  3, -3,  1,  1, -3, -1, -1,  1,  3,  1,  3,  1, -1,  3,  1,  1, -3, -1, -3, -1},
+    {-1, -1, -1, -3, -3, -1,  1,  1,  3,  3, -1,  3, -1,  1, -1, -3,  1, -1, -3, -3,  1, -3, -1, -1},
+    {-3,  1,  1,  3, -1,  1,  3,  1, -3,  1, -3,  1,  1, -1, -1,  3, -1, -3,  3, -3, -3, -3,  1,  1},
+    { 1,  1, -1, -1,  3, -3, -3,  3, -3,  1, -1, -1,  1, -1,  1,  1, -1, -3, -1,  1, -1,  3, -1, -3},
+    {-3,  3,  3, -1, -1, -3, -1,  3,  1,  3,  1,  3,  1,  1, -1,  3,  1, -1,  1,  3, -3, -1, -1,  1},
+    {-3,  1,  3, -3,  1, -1, -3,  3, -3,  3, -1, -1, -1, -1,  1, -3, -3, -3,  1, -3, -3, -3,  1, -3},
+    { 1,  1, -3,  3,  3, -1, -3, -1,  3, -3,  3,  3,  3, -1,  1,  1, -3,  1, -1,  1,  1, -3,  1,  1},
+    {-1,  1, -3, -3,  3, -1,  3, -1, -1, -3, -3, -3, -1, -3, -3,  1, -1,  1,  3,  3, -1,  1, -1,  3},
+    { 1,  3,  3, -3, -3,  1,  3,  1, -1, -3, -3, -3,  3,  3, -3,  3,  3, -1, -3,  3, -1,  1, -3,  1},
+    { 1,  3,  3,  1,  1,  1, -1, -1,  1, -3,  3, -1,  1,  1, -3,  3,  3, -1, -3,  3, -3, -1, -3, -1},
+    { 3, -1, -1, -1, -1, -3, -1,  3,  3,  1, -1,  1,  3,  3,  3, -1,  1,  1, -3,  1,  3, -1, -3,  3},
+    {-3, -3,  3,  1,  3,  1, -3,  3,  1,  3,  1,  1,  3,  3, -1, -1, -3,  1, -3, -1,  3,  1,  1,  3},
+    {-1, -1,  1, -3,  1,  3, -3,  1, -1, -3, -1,  3,  1,  3,  1, -1, -3, -3, -1, -1, -3, -3, -3, -1},
+    {-1, -3,  3, -1, -1, -1, -1,  1,  1, -3,  3,  1,  3,  3,  1, -1,  1, -3,  1, -3,  1,  1, -3, -1},
+    { 1,  3, -1,  3,  3, -1, -3,  1, -1, -3,  3,  3,  3, -1,  1,  1,  3, -1, -3, -1,  3, -1, -1, -1},
+    { 1,  1,  1,  1,  1, -1,  3, -1, -3,  1,  1,  3, -3,  1, -3, -1,  1,  1, -3, -3,  3,  1,  1, -3},
+    { 1,  3,  3,  1, -1, -3,  3, -1,  3,  3,  3, -3,  1, -1,  1, -1, -3, -1,  1,  3, -1,  3, -3, -3},
+    {-1, -3,  3, -3, -3, -3, -1, -1, -3, -1, -3,  3,  1,  3, -3, -1,  3, -1,  1, -1,  3, -3,  1, -1},
+    {-3, -3,  1,  1, -1,  1, -1,  1, -1,  3,  1, -3, -1,  1, -1,  1, -1, -1,  3,  3, -3, -1,  1, -3},
+    {-3, -1, -3,  3,  1, -1, -3, -1, -3, -3,  3, -3,  3, -3, -1,  1,  3,  1, -3,  1,  3,  3, -1, -3},
+    {-1, -1, -1, -1,  3,  3,  3,  1,  3,  3, -3,  1,  3, -1,  3, -1,  3,  3, -3,  3,  1, -1,  3,  3},
+    { 1, -1,  3,  3, -1, -3,  3, -3, -1, -1,  3, -1,  3, -1, -1,  1,  1,  1,  1, -1, -1, -3, -1,  3},
+    { 1, -1,  1, -1,  3, -1,  3,  1,  1, -1, -1, -3,  1,  1, -3,  1,  3, -3,  1,  1, -3, -3, -1, -1},
+    {-3, -1,  1,  3,  1,  1, -3, -1, -1, -3,  3, -3,  3,  1, -3,  3, -3,  1, -1,  1, -3,  1,  1,  1},
+    {-1, -3,  3,  3,  1,  1,  3, -1, -3, -1, -1, -1,  3,  1, -3, -3, -1,  3, -3, -1, -3, -1, -3, -1},
+    {-1, -3, -1, -1,  1, -3, -1, -1,  1, -1, -3,  1,  1, -3,  1, -3, -3,  3,  1,  1, -1,  3, -1, -1},
+    { 1,  1, -1, -1, -3, -1,  3, -1,  3, -1,  1,  3,  1, -1,  3,  1,  3, -3, -3,  1, -1, -1,  1,  3}};
+
 static int is_prime(uint32_t n) {
   if (n < 2) return 0;
   for (uint32_t d = 2; d * d <= n; d++) if (n % d == 0) return 0;
@@ -257,13 +323,21 @@ int or_dmrs_params(const or_ul_cfg_t *c, uint32_t ns, uint32_t *u, uint32_t *v, 
   uint32_t prs = 0;
   for (int i = 0; i < 8; i++) prs += (uint32_t)s[8 * 7 * ns + i] << i;   /* n_PRS(n_s), N_symb^UL = 7 */
   *ncs = (N1_DMRS[c->cyclic_shift & 7] + N2_DMRS[c->n_dmrs2 & 7] + prs) % 12;
-  return M >= 36 ? 0 : -1;
+  return M == 12 || M == 24 || M >= 36 ? 0 : -1;
 }
 
 int or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r) {
   const uint32_t M = 12 * c->L_prb;
   uint32_t u, v, ncs;
   if (or_dmrs_params(c, ns, &u, &v, &ncs)) return -1;
+  if (M < 36) {   /* 5.5.1.2: r_u(n) = exp(j phi(n) pi / 4), tabulated for M_sc = 12 and 24 */
+    for (uint32_t n = 0; n < M; n++) {
+      const double ph = M_PI * (M == 12 ? PHI12[u][n] : PHI24[u][n]) / 4.0 + 2.0 * M_PI * (double)((ncs * n) % 12) / 12.0;
+      r[2 * n] = (float)cos(ph);
+      r[2 * n + 1] = (float)sin(ph);
+    }
+    return 0;
+  }
   uint32_t Nzc = M - 1;
   while (!is_prime(Nzc)) Nzc--;
   const double qb = (double)Nzc * (u + 1) / 31.0;
@@ -280,7 +354,7 @@ int or_dmrs_pusch(const or_ul_cfg_t *c, uint32_t ns, float *r) {
 
 int or_pusch_grid(const or_ul_cfg_t *c, const uint8_t *tb, float *grid) {
   const uint32_t W = 12 * c->nof_prb, M = 12 * c->L_prb, G = or_pusch_G(c);
-  if (c->n_prb + c->L_prb > c->nof_prb || M < 36) return -1;
+  if (c->n_prb + c->L_prb > c->nof_prb || M < 12) return -1;
   if (c->hop && c->n_prb1 + c->L_prb > c->nof_prb) return -1;
   uint8_t *f = (uint8_t *)malloc(G);
   float *x = (float *)malloc(sizeof(float) * 2 * 12 * M), *z = (float *)malloc(sizeof(float) * 2 * M);
@@ -338,4 +412,54 @@ int or_pusch_encode(const or_ul_cfg_t *c, const uint8_t *tb, float *iq) {
   if (!rc) rc = or_scfdma_tx(c->nof_prb, grid, iq);
   free(grid);
   return rc;
+}
+
+/* ---- PUSCH frequency hopping type 2 (36.211 5.3.4) ------------------------------------------------------
+ * Restated per VRB: n~_PRB(n_s) = (n~_VRB + f_hop(i) N_RB^sb + ((N_RB^sb - 1) - 2 (n~_VRB mod N_RB^sb)) f_m(i))
+ * mod (N_RB^sb N_sb), i = n_s (intra- and inter-subframe hopping) or floor(n_s / 2) (inter-subframe), with the
+ * pseudo-random c(k) of 7.2 initialised with N_ID^cell at the start of each frame; the hopping region is shifted
+ * by N~_RB^HO / 2 when N_sb > 1.  Writes the slot's PRB of every VRB (prb[L]); returns the lowest, or -1. */
+static uint32_t hop_fhop(const uint8_t *c, uint32_t i, uint32_t nsb) {
+  if (nsb == 1) return 0;
+  uint32_t f = 0;                            /* f_hop(-1) = 0 */
+  for (uint32_t j = 0; j <= i; j++) {
+    uint32_t x = 0;
+    for (uint32_t b = 0; b < 9; b++) x |= (uint32_t)c[10 * j + 1 + b] << b;
+    f = (nsb == 2) ? (f + x) % nsb : (f + (x % (nsb - 1)) + 1) % nsb;
+  }
+  return f;
+}
+
+int or_pusch_hop_type2(uint32_t nof_prb, uint32_t n_ho, uint32_t n_sb, int intra, uint32_t cell_id, uint32_t n_vrb,
+                       uint32_t L, uint32_t ns, uint32_t current_tx_nb, uint32_t *prb) {
+  uint8_t c[220];
+  if (n_sb < 1 || n_sb > 4 || ns > 19 || L < 1) return -1;
+  or_gold(cell_id, c, 220);
+  const uint32_t hot = (n_ho % 2) ? n_ho + 1 : n_ho;
+  uint32_t nrb_sb, off;
+  if (n_sb == 1) {
+    nrb_sb = nof_prb;
+    off = 0;
+  } else {
+    const int32_t w = (int32_t)nof_prb - (int32_t)hot - (int32_t)(nof_prb % 2);
+    if (w <= 0) return -1;
+    nrb_sb = (uint32_t)w / n_sb;
+    off = hot / 2;
+  }
+  if (!nrb_sb) return -1;
+  const uint32_t i = intra ? ns : ns / 2;
+  const uint32_t fhop = hop_fhop(c, i, n_sb);
+  const uint32_t fm = (n_sb > 1) ? c[10 * i] : (intra ? i % 2 : current_tx_nb % 2);
+  int lo = -1;
+  for (uint32_t l = 0; l < L; l++) {
+    const int32_t vt = (int32_t)(n_vrb + l) - (int32_t)off;
+    if (vt < 0 || (uint32_t)vt >= nrb_sb * n_sb) return -1;
+    const uint32_t mirror = (nrb_sb - 1) - 2 * ((uint32_t)vt % nrb_sb);   /* may wrap: modular arithmetic below */
+    const uint32_t pt = ((uint32_t)vt + fhop * nrb_sb + mirror * fm) % (nrb_sb * n_sb);
+    prb[l] = pt + off;
+    if (lo < 0 || (int)prb[l] < lo) lo = (int)prb[l];
+  }
+  for (uint32_t l = 0; l < L; l++)
+    if (prb[l] >= nof_prb) return -1;
+  return lo;
 }

@@ -224,6 +224,9 @@ int      or_dlsch_decode(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm
                          uint32_t rv, int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its,
                          uint8_t *payload, uint32_t *noi_out, uint32_t *cb_crc_ok_out);
 /* same, plus each code block's iteration count (cb_its_out[C], may be NULL) */
+/* PUSCH hopping type 2 (36.211 5.3.4): each VRB's PRB in slot ns (prb[L]); returns the lowest or -1 */
+int      or_pusch_hop_type2(uint32_t nof_prb, uint32_t n_ho, uint32_t n_sb, int intra, uint32_t cell_id,
+                            uint32_t n_vrb, uint32_t L, uint32_t ns, uint32_t current_tx_nb, uint32_t *prb);
 int      or_dlsch_decode_cbits(const float *llr, uint32_t G, uint32_t tbs, uint32_t Qm, uint32_t NL,
                                uint32_t rv, int new_tb, float *sb, uint32_t sb_stride, uint32_t max_its,
                                uint8_t *payload, uint32_t *noi_out, uint32_t *cb_crc_ok_out, uint32_t *cb_its_out);

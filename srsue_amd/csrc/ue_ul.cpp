@@ -13,6 +13,7 @@
 #include "../../include/srslte/srslte.h"
 #include "tables.h"
 #include "ul_engine.h"
+#include "../../include/mi_ul.h"
 
 struct mi_ue_ul_ctx {
   mi::UlEngine eng;
@@ -114,6 +115,24 @@ int grant_from_riv(uint32_t riv, uint32_t nof_prb, uint32_t mcs, uint32_t n_dmrs
   return SRSLTE_SUCCESS;
 }
 
+// hopping bits of a format-0 / RAR grant (36.213 8.4, Tables 8.4-1 / 8.4-2): type 1 offsets the slot-1 (or
+// odd-transmission) allocation in the PUSCH hopping band of N_RB^PUSCH PRBs; the all-ones pattern ('1' for
+// N_UL_hop = 1, '11' for 2) selects type 2 (subband hopping, resolved per slot by srslte_ue_ul_cfg_grant)
+int apply_hopping_bits(uint32_t nof_prb, uint32_t n_rb_ho, uint32_t nh, uint32_t hbits, srslte_ra_ul_grant_t* grant) {
+  if (hbits == (nh == 1 ? 1u : 3u)) {
+    grant->freq_hopping = 2;
+    return SRSLTE_SUCCESS;
+  }
+  const uint32_t N = nof_prb - ul_nho_tilde(n_rb_ho) - (nof_prb & 1u), s1 = grant->n_prb_tilde[0];
+  if (N == 0 || N > nof_prb || s1 + grant->L_prb > N) return SRSLTE_ERROR;
+  const uint32_t d = nh == 1 ? N / 2 : hbits == 0 ? N / 4 : hbits == 1 ? N - N / 4 : N / 2;
+  const uint32_t s2 = (s1 + d) % N;
+  if (s2 + grant->L_prb > N) return SRSLTE_ERROR;
+  grant->freq_hopping = 1;
+  grant->n_prb_tilde[1] = s2;
+  return SRSLTE_SUCCESS;
+}
+
 uint32_t rba_bits(uint32_t nof_prb) {
   uint32_t b = 0;
   while ((1u << b) < nof_prb * (nof_prb + 1) / 2) b++;
@@ -172,7 +191,7 @@ void srslte_ue_ul_set_cfg(srslte_ue_ul_t* q, srslte_refsignal_dmrs_pusch_cfg_t* 
 int srslte_ue_ul_cfg_grant(srslte_ue_ul_t* q, srslte_ra_ul_grant_t* grant, uint32_t tti, uint32_t rvidx,
                            uint32_t current_tx_nb) {
   if (!q || !q->ctx || !grant) return SRSLTE_ERROR_INVALID_INPUTS;
-  if (grant->freq_hopping > 1) { mi::set_error("PUSCH hopping type 2 is not supported"); return SRSLTE_ERROR; }
+  if (grant->freq_hopping > 2) return SRSLTE_ERROR_INVALID_INPUTS;
   mi::CbSegm sg;
   if (grant->mcs.tbs <= 0 || mi::cbsegm((uint32_t)grant->mcs.tbs, &sg)) return SRSLTE_ERROR;
   q->pusch_cfg.grant = *grant;
@@ -207,6 +226,21 @@ int srslte_ue_ul_cfg_grant(srslte_ue_ul_t* q, srslte_ra_ul_grant_t* grant, uint3
     c.n_prb1 = s1;
     q->pusch_cfg.grant.n_prb[0] = s0;
     q->pusch_cfg.grant.n_prb[1] = s1;
+  } else if (grant->freq_hopping == 2) {
+    // type 2 (subband hopping, 36.211 5.3.4): both slots of subframe tti % 10 through the cell's hopping
+    // pattern from the grant's first VRB (mi_ul_hop_type2)
+    const bool intra = q->hopping_cfg.hop_mode == srslte_pusch_hopping_cfg_t::SRSLTE_PUSCH_HOP_MODE_INTRA_SF;
+    int p[2];
+    for (uint32_t sl = 0; sl < 2; sl++) {
+      p[sl] = mi_ul_hop_type2(q->cell.nof_prb, q->hopping_cfg.hopping_offset, q->hopping_cfg.n_sb ? q->hopping_cfg.n_sb : 1,
+                              intra, q->cell.id, grant->n_prb_tilde[0], grant->L_prb, 2 * (tti % 10) + sl, current_tx_nb);
+      if (p[sl] < 0) { mi::set_error("type-2 hopping maps the allocation outside the band"); return SRSLTE_ERROR; }
+    }
+    c.n_prb = (uint32_t)p[0];
+    c.hop = p[1] != p[0];
+    c.n_prb1 = (uint32_t)p[1];
+    q->pusch_cfg.grant.n_prb[0] = (uint32_t)p[0];
+    q->pusch_cfg.grant.n_prb[1] = (uint32_t)p[1];
   }
   c.L_prb = grant->L_prb;
   c.tbs = (uint32_t)grant->mcs.tbs;
@@ -317,34 +351,34 @@ int srslte_dci_msg_to_ul_grant(srslte_dci_msg_t* msg, uint32_t nof_prb, uint32_t
   dci->cqi_request = take_bits(msg->data, &pos, 1) != 0;
   dci->rv_idx = mcs > 28 ? mcs - 28 : 0;
   if (grant_from_riv(riv, nof_prb, mcs, ncs, dci, grant)) return SRSLTE_ERROR;
-  if (dci->freq_hop_fl) {
-    // Table 8.4-2: type 1 offsets of the hopped allocation in the PUSCH hopping band of N_RB^PUSCH PRBs;
-    // '1' (N_UL_hop = 1) / '11' (N_UL_hop = 2) select type 2 (subband hopping), not supported
-    if (hbits == (nh == 1 ? 1u : 3u)) { mi::set_error("PUSCH hopping type 2 is not supported"); return SRSLTE_ERROR; }
-    const uint32_t N = nof_prb - ul_nho_tilde(n_rb_ho) - (nof_prb & 1u), s1 = grant->n_prb_tilde[0];
-    if (N == 0 || N > nof_prb || s1 + grant->L_prb > N) return SRSLTE_ERROR;
-    const uint32_t d = nh == 1 ? N / 2 : hbits == 0 ? N / 4 : hbits == 1 ? N - N / 4 : N / 2;
-    const uint32_t s2 = (s1 + d) % N;
-    if (s2 + grant->L_prb > N) return SRSLTE_ERROR;
-    grant->freq_hopping = 1;
-    grant->n_prb_tilde[1] = s2;
-  }
+  if (dci->freq_hop_fl) return apply_hopping_bits(nof_prb, n_rb_ho, nh, hbits, grant);
   return SRSLTE_SUCCESS;
 }
 
-int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t* rar, uint32_t nof_prb, uint32_t /*n_rb_ho*/,
+int srslte_dci_rar_to_ul_grant(srslte_dci_rar_grant_t* rar, uint32_t nof_prb, uint32_t n_rb_ho,
                                srslte_ra_ul_dci_t* dci, srslte_ra_ul_grant_t* grant) {
   if (!rar || !dci || !grant || mi::symbol_sz(nof_prb) < 0) return SRSLTE_ERROR_INVALID_INPUTS;
   memset(dci, 0, sizeof(*dci));
-  if (rar->hopping_flag) { mi::set_error("PUSCH frequency hopping is not supported"); return SRSLTE_ERROR; }
-  // 36.213 6.2: the 10-bit fixed-size resource block assignment, truncated to the b LSBs (N_RB <= 44)
-  // or zero-extended (N_RB > 44, no hopping bits), is the RIV; the truncated MCS is I_MCS 0..15
+  // 36.213 6.2: the 10-bit fixed-size resource block assignment becomes format 0's b-bit field: its b LSBs
+  // (N_RB <= 44), or (N_RB > 44) b - 10 zero bits inserted after the N_UL_hop hopping bits (none without
+  // hopping: zero-extended).  The field's N_UL_hop MSBs are the hopping bits, the rest the RIV; the truncated
+  // MCS is I_MCS 0..15
   const uint32_t b = rba_bits(nof_prb);
-  const uint32_t riv = nof_prb <= 44 ? (rar->rba & ((1u << b) - 1u)) : rar->rba;
+  const uint32_t nh = rar->hopping_flag ? (nof_prb < 50 ? 1u : 2u) : 0u;
+  uint32_t field;
+  if (nof_prb <= 44) {
+    field = rar->rba & ((1u << b) - 1u);
+  } else {
+    const uint32_t hb = (rar->rba >> (10 - nh)) & ((1u << nh) - 1u), rest = rar->rba & ((1u << (10 - nh)) - 1u);
+    field = (hb << (b - nh)) | rest;
+  }
+  const uint32_t hbits = nh ? field >> (b - nh) : 0u, riv = field & ((1u << (b - nh)) - 1u);
+  dci->freq_hop_fl = rar->hopping_flag;
   dci->tpc_pusch = rar->tpc_pusch;
   dci->cqi_request = rar->cqi_request;
   dci->ndi = true;
-  return grant_from_riv(riv, nof_prb, rar->trunc_mcs & 15u, 0, dci, grant);
+  if (grant_from_riv(riv, nof_prb, rar->trunc_mcs & 15u, 0, dci, grant)) return SRSLTE_ERROR;
+  return nh ? apply_hopping_bits(nof_prb, n_rb_ho, nh, hbits, grant) : SRSLTE_SUCCESS;
 }
 
 }  // extern "C"

@@ -19,6 +19,73 @@
 #include "ul_common.h"
 
 namespace mi {
+
+// 36.211 Tables 5.5.1.2-1 / 5.5.1.2-2: phi(n) of the base sequences r_u(n) = exp(j phi(n) pi / 4) for M_sc = 12
+// and 24 (L_prb = 1, 2), sequence-group number u = 0..29.  Transcribed from the specification; the CPU suite
+// checks every row's low-PAPR design property (tests/test_oracle_ul.py), the oracle holds its own copy.
+__constant__ int8_t UL_PHI12[30][12] = {
+    {-1,  1,  3, -3,  3,  3,  1,  1,  3,  1, -3,  3},
+    { 1,  1,  3,  3,  3, -1,  1, -3, -3,  1, -3,  3},
+    { 1,  1, -3, -3, -3, -1, -3, -3,  1, -3,  1, -1},
+    {-1,  1,  1,  1,  1, -1, -3, -3,  1, -3,  3, -1},
+    {-1,  3,  1, -1,  1, -1, -3, -1,  1, -1,  1,  3},
+    { 1, -3,  3, -1, -1,  1,  1, -1, -1,  3, -3,  1},
+    {-1,  3, -3, -3, -3,  3,  1, -1,  3,  3, -3,  1},
+    {-3, -1, -1, -1,  1, -3,  3, -1,  1, -3,  3,  1},
+    { 1, -3,  3,  1, -1, -1, -1,  1,  1,  3, -1,  1},
+    { 1, -3, -1,  3,  3, -1, -3,  1,  1,  1,  1,  1},
+    {-1,  3, -1,  1,  1, -3, -3, -1, -3, -3,  3, -1},
+    { 3,  1, -1, -1,  3,  3, -3,  1,  3,  1,  3,  3},
+    { 1, -3,  1,  1, -3,  1,  1,  1, -3, -3, -3,  1},
+    { 3,  3, -3,  3, -3,  1,  1,  3, -1, -3,  3,  3},
+    {-3,  1, -1, -3, -1,  3,  1,  3,  3,  3, -1,  1},
+    { 3, -1,  1, -3, -1, -1,  1,  1,  3,  1, -1, -3},
+    { 1,  3,  1, -1,  1,  3,  3,  3, -1, -1,  3, -1},
+    {-3,  1,  1,  3, -3,  3, -3, -3,  3,  1,  3, -1},
+    {-3,  3,  1,  1, -3,  1, -3, -3, -1, -1,  1, -3},
+    {-1,  3,  1,  3,  1, -1, -1,  3, -3, -1, -3, -1},
+    {-1, -3,  1,  1,  1,  1,  3,  1, -1,  1, -3, -1},
+    {-1,  3, -1,  1, -3, -3, -3, -3, -3,  1, -1, -3},
+    { 1,  1, -3, -3, -3, -3, -1,  3, -3,  1, -3,  3},
+    { 1,  1, -1, -3, -1, -3,  1, -1,  1,  3, -1,  1},
+    { 1,  1,  3,  1,  3,  3, -1,  1, -1, -3, -3,  1},
+    { 1, -3,  3,  3,  1,  3,  3,  1, -3, -1, -1,  3},
+    { 1,  3, -3, -3,  3, -3,  1, -1, -1,  3, -1, -3},
+    {-3, -1, -3, -1, -3,  3,  1, -1,  1,  3, -3, -3},
+    {-1,  3, -3,  3, -1,  3,  3, -3,  3,  3, -1, -1},
+    { 3, -3, -3, -1, -1, -3, -1,  3, -3,  3,  1, -1}};
+__constant__ int8_t UL_PHI24[30][24] = {
+    {-1,  3,  1, -3,  3, -1,  1,  3, -3,  3,  1,  3, -3,  3,  1,  1, -1,  1,  3, -3,  3, -3, -1, -3},
+    {-3,  3, -3, -3, -3,  1, -3, -3,  3, -1,  1,  1,  1,  3,  1, -1,  3, -3, -3,  1,  3,  1,  1, -3},
+    { 3, -1,  3,  3,  1,  1, -3,  3,  3,  3,  3,  1, -1,  3, -1,  1,  1, -1, -3, -1, -1,  1,  3,  3},
+    {-1, -3,  1,  1,  3, -3,  1,  1, -3, -1, -1,  1,  3,  1,  3,  1, -1,  3,  1,  1, -3, -1, -3, -1},
+    {-1, -1, -1, -3, -3, -1,  1,  1,  3,  3, -1,  3, -1,  1, -1, -3,  1, -1, -3, -3,  1, -3, -1, -1},
+    {-3,  1,  1,  3, -1,  1,  3,  1, -3,  1, -3,  1,  1, -1, -1,  3, -1, -3,  3, -3, -3, -3,  1,  1},
+    { 1,  1, -1, -1,  3, -3, -3,  3, -3,  1, -1, -1,  1, -1,  1,  1, -1, -3, -1,  1, -1,  3, -1, -3},
+    {-3,  3,  3, -1, -1, -3, -1,  3,  1,  3,  1,  3,  1,  1, -1,  3,  1, -1,  1,  3, -3, -1, -1,  1},
+    {-3,  1,  3, -3,  1, -1, -3,  3, -3,  3, -1, -1, -1, -1,  1, -3, -3, -3,  1, -3, -3, -3,  1, -3},
+    { 1,  1, -3,  3,  3, -1, -3, -1,  3, -3,  3,  3,  3, -1,  1,  1, -3,  1, -1,  1,  1, -3,  1,  1},
+    {-1,  1, -3, -3,  3, -1,  3, -1, -1, -3, -3, -3, -1, -3, -3,  1, -1,  1,  3,  3, -1,  1, -1,  3},
+    { 1,  3,  3, -3, -3,  1,  3,  1, -1, -3, -3, -3,  3,  3, -3,  3,  3, -1, -3,  3, -1,  1, -3,  1},
+    { 1,  3,  3,  1,  1,  1, -1, -1,  1, -3,  3, -1,  1,  1, -3,  3,  3, -1, -3,  3, -3, -1, -3, -1},
+    { 3, -1, -1, -1, -1, -3, -1,  3,  3,  1, -1,  1,  3,  3,  3, -1,  1,  1, -3,  1,  3, -1, -3,  3},
+    {-3, -3,  3,  1,  3,  1, -3,  3,  1,  3,  1,  1,  3,  3, -1, -1, -3,  1, -3, -1,  3,  1,  1,  3},
+    {-1, -1,  1, -3,  1,  3, -3,  1, -1, -3, -1,  3,  1,  3,  1, -1, -3, -3, -1, -1, -3, -3, -3, -1},
+    {-1, -3,  3, -1, -1, -1, -1,  1,  1, -3,  3,  1,  3,  3,  1, -1,  1, -3,  1, -3,  1,  1, -3, -1},
+    { 1,  3, -1,  3,  3, -1, -3,  1, -1, -3,  3,  3,  3, -1,  1,  1,  3, -1, -3, -1,  3, -1, -1, -1},
+    { 1,  1,  1,  1,  1, -1,  3, -1, -3,  1,  1,  3, -3,  1, -3, -1,  1,  1, -3, -3,  3,  1,  1, -3},
+    { 1,  3,  3,  1, -1, -3,  3, -1,  3,  3,  3, -3,  1, -1,  1, -1, -3, -1,  1,  3, -1,  3, -3, -3},
+    {-1, -3,  3, -3, -3, -3, -1, -1, -3, -1, -3,  3,  1,  3, -3, -1,  3, -1,  1, -1,  3, -3,  1, -1},
+    {-3, -3,  1,  1, -1,  1, -1,  1, -1,  3,  1, -3, -1,  1, -1,  1, -1, -1,  3,  3, -3, -1,  1, -3},
+    {-3, -1, -3,  3,  1, -1, -3, -1, -3, -3,  3, -3,  3, -3, -1,  1,  3,  1, -3,  1,  3,  3, -1, -3},
+    {-1, -1, -1, -1,  3,  3,  3,  1,  3,  3, -3,  1,  3, -1,  3, -1,  3,  3, -3,  3,  1, -1,  3,  3},
+    { 1, -1,  3,  3, -1, -3,  3, -3, -1, -1,  3, -1,  3, -1, -1,  1,  1,  1,  1, -1, -1, -3, -1,  3},
+    { 1, -1,  1, -1,  3, -1,  3,  1,  1, -1, -1, -3,  1,  1, -3,  1,  3, -3,  1,  1, -3, -3, -1, -1},
+    {-3, -1,  1,  3,  1,  1, -3, -1, -1, -3,  3, -3,  3,  1, -3,  3, -3,  1, -1,  1, -3,  1,  1,  1},
+    {-1, -3,  3,  3,  1,  1,  3, -1, -3, -1, -1, -1,  3,  1, -3, -3, -1,  3, -3, -1, -3, -1, -3, -1},
+    {-1, -3, -1, -1,  1, -3, -1, -1,  1, -1, -3,  1,  1, -3,  1, -3, -3,  3,  1,  1, -1,  3, -1, -1},
+    { 1,  1, -1, -1, -3, -1,  3, -1,  3, -1,  1,  3,  1, -1,  3,  1,  3, -3, -3,  1, -1, -1,  1,  3}};
+
 namespace {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -294,13 +361,20 @@ __global__ __launch_bounds__(UL_THREADS) void pusch_mod_kernel(const uint8_t* __
   for (uint32_t ls = l0 % 7; ls < l0 % 7 + per; ls++) {
     const uint32_t l = 7 * slot + ls, cp = cp_len((int)N, (int)ls);
     if (ls == 3) {
-      // DMRS 36.211 5.5.2.1: r(n) = exp(j alpha n) x_q(n mod N_ZC), x_q(m) = exp(-j pi q m (m+1) / N_ZC)
+      // DMRS 36.211 5.5.2.1: r(n) = exp(j alpha n) x_q(n mod N_ZC), x_q(m) = exp(-j pi q m (m+1) / N_ZC); for
+      // M_sc = 12 / 24 (nzc == 0, dq = the group u) the tabulated base sequence exp(j phi_u(n) pi / 4) (5.5.1.2)
       for (uint32_t n = t; n < M; n += UL_THREADS) {
-        const uint32_t m = n % x.nzc;
-        const uint32_t a = (uint32_t)(((uint64_t)dq * m * (m + 1)) % (2ull * x.nzc));
         const uint32_t cs = (dncs * n) % 12;
+        float ph;
+        if (x.nzc) {
+          const uint32_t m = n % x.nzc;
+          const uint32_t a = (uint32_t)(((uint64_t)dq * m * (m + 1)) % (2ull * x.nzc));
+          ph = -(float)a / (float)x.nzc + (float)cs / 6.0f;
+        } else {
+          ph = (float)(M == 12 ? UL_PHI12[dq][n] : UL_PHI24[dq][n]) * 0.25f + (float)cs / 6.0f;
+        }
         float sv, cv;
-        sincospif(-(float)a / (float)x.nzc + (float)cs / 6.0f, &sv, &cv);
+        sincospif(ph, &sv, &cv);
         buf[n] = make_float2(cv, sv);
       }
       __syncthreads();

@@ -23,7 +23,7 @@ static bool prime(uint32_t n) {
 
 int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc, uint32_t* ncs) {
   const uint32_t M = 12 * c.L_prb, fss = (c.cell_id + c.delta_ss) % 30;
-  if (M < 36 || ns >= 20) return -1;   // L_prb = 1, 2 use the tabulated base sequences (5.5.1.2)
+  if (M < 12 || ns >= 20) return -1;
   uint32_t fgh = 0;
   if (c.group_hopping) {               // 5.5.1.3: c_init = floor(N_ID / 30)
     std::vector<uint8_t> g(160);
@@ -39,6 +39,11 @@ int ul_dmrs_params(const mi_ul_cfg_t& c, uint32_t ns, uint32_t* q, uint32_t* nzc
   uint32_t prs = 0;
   for (int i = 0; i < 8; i++) prs += (uint32_t)s[8 * 7 * ns + i] << i;
   *ncs = (N1_DMRS[c.cyclic_shift & 7] + N2_DMRS[c.n_dmrs2 & 7] + prs) % 12;
+  if (M < 36) {   // L_prb = 1, 2: the tabulated base sequences of group u (5.5.1.2), marked by N_ZC = 0
+    *nzc = 0;
+    *q = u;
+    return 0;
+  }
   uint32_t N = M - 1;
   while (!prime(N)) N--;
   *nzc = N;
@@ -140,9 +145,9 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) {
     const mi_ul_cfg_t& c = cfgs[i];
     const int N = symbol_sz(c.nof_prb);
-    if (N < 0 || c.nof_prb == 0 || c.sf_idx > 9 || c.L_prb < 3 || c.n_prb + c.L_prb > c.nof_prb || (c.hop && c.n_prb1 + c.L_prb > c.nof_prb) ||
+    if (N < 0 || c.nof_prb == 0 || c.sf_idx > 9 || c.L_prb < 1 || c.n_prb + c.L_prb > c.nof_prb || (c.hop && c.n_prb1 + c.L_prb > c.nof_prb) ||
         (c.Qm != 2 && c.Qm != 4 && c.Qm != 6) || c.tbs == 0 || c.tbs % 8 || c.rv > 3) {
-      set_error("invalid UL configuration (L_prb >= 3, allocation inside the cell, Qm 2/4/6, byte-aligned TBS)");
+      set_error("invalid UL configuration (L_prb >= 1, allocation inside the cell, Qm 2/4/6, byte-aligned TBS)");
       return -1;
     }
     MiUlTx t{};
@@ -294,3 +299,38 @@ int UlPlan::build(const mi_ul_cfg_t* cfgs, uint32_t n) {
 }
 
 }  // namespace mi
+
+// 36.211 5.3.4, PUSCH hopping type 2 (include/mi_ul.h documents the mapping)
+extern "C" int mi_ul_hop_type2(uint32_t nof_prb, uint32_t n_ho, uint32_t n_sb, int intra, uint32_t cell_id,
+                               uint32_t n_vrb, uint32_t L, uint32_t ns, uint32_t current_tx_nb) {
+  if (n_sb < 1 || n_sb > 4 || L < 1 || ns >= 20 || n_vrb + L > nof_prb) return -1;
+  const uint32_t ho = n_ho + (n_ho & 1u);                 // N~_HO
+  const uint32_t nsb_rb = n_sb == 1 ? nof_prb : (nof_prb > ho + (nof_prb & 1u) ? (nof_prb - ho - (nof_prb & 1u)) / n_sb : 0);
+  const uint32_t shift = n_sb == 1 ? 0u : ho / 2;
+  if (nsb_rb == 0) return -1;
+  const uint32_t i = intra ? ns : ns / 2;
+  std::vector<uint8_t> c(10 * 20 + 10);
+  mi::gold_bits(cell_id, (uint32_t)c.size(), c.data());
+  // f_hop(i) = (f_hop(i - 1) + sum_{k = 10 i + 1}^{10 i + 9} c(k) 2^(k - (10 i + 1))) mod N_sb       (N_sb = 2)
+  //          = (f_hop(i - 1) + (sum ...) mod (N_sb - 1) + 1) mod N_sb                            (N_sb > 2)
+  uint32_t fhop = 0;
+  for (uint32_t j = 0; j <= i && n_sb > 1; j++) {
+    uint32_t sum = 0;
+    for (uint32_t k = 10 * j + 1; k <= 10 * j + 9; k++) sum += (uint32_t)c[k] << (k - (10 * j + 1));
+    fhop = n_sb == 2 ? (fhop + sum) % n_sb : (fhop + sum % (n_sb - 1) + 1) % n_sb;
+  }
+  const uint32_t fm = n_sb > 1 ? c[10 * i] : intra ? (i & 1u) : (current_tx_nb & 1u);
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (uint32_t v = n_vrb; v < n_vrb + L; v++) {
+    if (v < shift) return -1;
+    const uint32_t vt = v - shift;
+    if (vt >= nsb_rb * n_sb) return -1;
+    const uint32_t pt = (vt + fhop * nsb_rb + ((nsb_rb - 1) - 2 * (vt % nsb_rb)) * fm) % (nsb_rb * n_sb);
+    const uint32_t p = pt + shift;
+    lo = p < lo ? p : lo;
+    hi = p > hi ? p : hi;
+  }
+  if (hi - lo + 1 != L || hi >= nof_prb) return -1;
+  return (int)lo;
+}
+

@@ -4,14 +4,17 @@
  *   init_cell: srslte_ue_ul_init (:79), srslte_ue_ul_set_normalization (:83), _set_cfo_enable (:84),
  *              srslte_ue_ul_set_rnti (:128), srslte_ue_ul_set_cfg (:748)
  *   MAC:       srslte_softbuffer_tx_init (ul_harq.cc:198)
- *   per TTI:   srslte_ue_ul_set_cfo (:213), srslte_dci_msg_to_ul_grant (:429, DCI mode),
+ *   per TTI:   srslte_ue_ul_set_cfo (:213), srslte_dci_msg_to_ul_grant (:429, DCI mode), or for a random-access
+ *              response grant srslte_dci_rar_grant_unpack (phch_common.cc:122) + srslte_dci_rar_to_ul_grant (:412),
  *              srslte_ue_ul_cfg_grant(&ue_ul, grant, tti + 4, rv, tx_nb) (:551),
  *              srslte_ue_ul_pusch_encode_rnti_softbuffer(.., payload, uci_data, softbuffer, rnti, signal) (:555)
  * Input file : int32 hdr[8] = {cell_id, nof_prb, ntx, group_hopping, sequence_hopping, delta_ss, cyclic_shift,
  *              flags (1 = normalisation, 2 = CFO, bits 8-11 = I_offset_ack, bits 12-19 = pusch-HoppingOffset,
- *              bit 20 = intra-subframe hopping, bits 21-24 = I_offset_cqi, bits 25-28 = I_offset_ri)} + float cfo;
+ *              bit 20 = intra-subframe hopping, bits 21-24 = I_offset_cqi, bits 25-28 = I_offset_ri,
+ *              bits 29-30 = pusch-HoppingSubbands N_sb - 1)} + float cfo;
  *              per transmission int32
- *              p[12] = {tti, rnti, rv | CURRENT_TX_NB << 8, use_dci, n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len,
+ *              p[12] = {tti, rnti, rv | CURRENT_TX_NB << 8, use_dci (0 direct, 1 DCI format 0, 2 RAR grant: the first
+ *              20 of the 64 bit bytes), n_prb, L_prb, tbs, Qm, ncs_dmrs, pass_data, ack_len,
  *              ack} + int32 dci_nof_bits + 64 DCI bit bytes + int32 u[3] = {cqi, ri_len, ri} + 64 CQI bit bytes +
  *              tbs/8 payload bytes.  cqi > 0: a wideband CQI report of value cqi - 1 packed with
  *              srslte_cqi_value_pack as srsUE does (phch_worker.cc:517-521); cqi < 0: -cqi raw CQI bits from the
@@ -63,6 +66,7 @@ int main(int argc, char **argv) {
   dmrs_cfg.cyclic_shift = (uint32_t)hdr[6];
   pusch_hopping.hop_mode = (hdr[7] >> 20) & 1 ? SRSLTE_PUSCH_HOP_MODE_INTRA_SF : SRSLTE_PUSCH_HOP_MODE_INTER_SF;
   pusch_hopping.hopping_offset = (uint32_t)(hdr[7] >> 12) & 255u;
+  pusch_hopping.n_sb = 1u + ((uint32_t)(hdr[7] >> 29) & 3u);
   srslte_ue_ul_set_cfg(&ue_ul, &dmrs_cfg, &srs_cfg, &pucch_cfg, &pucch_sched, &uci_cfg, &pusch_hopping, &power_ctrl);
   srslte_softbuffer_tx_t softbuffer;
   if (srslte_softbuffer_tx_init(&softbuffer, 100)) { fprintf(stderr, "softbuffer_tx\n"); return 3; }
@@ -84,7 +88,12 @@ int main(int argc, char **argv) {
     srslte_ra_ul_grant_t grant;
     memset(&grant, 0, sizeof(grant));
     int ret = 0;
-    if (p[3]) {
+    if (p[3] == 2) {   /* Msg3: the MAC's RAR grant bits, unpacked by phch_common then converted by the worker */
+      srslte_dci_rar_grant_t rar;
+      srslte_ra_ul_dci_t dci_unpacked;
+      srslte_dci_rar_grant_unpack(&rar, dci_msg.data);
+      ret = srslte_dci_rar_to_ul_grant(&rar, cell.nof_prb, pusch_hopping.hopping_offset, &dci_unpacked, &grant);
+    } else if (p[3]) {
       srslte_ra_ul_dci_t dci_unpacked;
       ret = srslte_dci_msg_to_ul_grant(&dci_msg, cell.nof_prb, pusch_hopping.hopping_offset, &dci_unpacked, &grant,
                                        (uint32_t)p[0]);

@@ -32,12 +32,18 @@ def run(cell_id, nof_prb, txs, dmrs=(0, 0, 0, 0), flags=0, cfo=0.0):
             f.write(struct.pack("f", cfo))
             for t in txs:
                 dci = t.get("dci")
-                f.write(struct.pack("12i", t["tti"], t["rnti"], t["rv"] | (t.get("tx_nb", 0) << 8), int(dci is not None),
+                use = 2 if t.get("rar") else int(dci is not None)
+                f.write(struct.pack("12i", t["tti"], t["rnti"], t["rv"] | (t.get("tx_nb", 0) << 8), use,
                                     t.get("n_prb", 0),
                                     t.get("L_prb", 0), t["tbs"], t.get("Qm", 0), t.get("ncs", 0),
                                     int(t.get("pass_data", True)), t.get("ack_len", 0), t.get("ack", 0)))
-                f.write(struct.pack("i", dci.nof_bits if dci else 0))
-                f.write(bytes(dci.data) if dci else bytes(64))
+                if t.get("rar"):
+                    bits = list(t["rar"])
+                    f.write(struct.pack("i", 20))
+                    f.write(bytes(bits + [0] * (64 - len(bits))))
+                else:
+                    f.write(struct.pack("i", dci.nof_bits if dci else 0))
+                    f.write(bytes(dci.data) if dci else bytes(64))
                 raw_cqi = list(t.get("cqi_bits", []))
                 f.write(struct.pack("3i", t["cqi_wb"] + 1 if "cqi_wb" in t else -len(raw_cqi), t.get("ri_len", 0),
                                     t.get("ri", 0)))
@@ -184,3 +190,63 @@ def test_periodic_cqi_and_ri_on_pusch_srsue_call_order():
     for t, (r, iq) in zip(txs, res):
         assert r[0] == 0
         assert rel_err(iq, oracle_iq(9, 50, t, t["tti"] % 10, ioff=6, cqi_ioff=9, ri_ioff=6)) < TOL
+
+
+def rar_bits(hop, rba, tmcs, tpc=1, delay=0, cqi=0):
+    """the 20 RAR UL-grant bits (36.213 6.2) as the MAC hands them to the PHY (phy.cc:248, phch_common.cc:122)"""
+    return [int(b) for b in f"{hop:01b}{rba:010b}{tmcs:04b}{tpc:03b}{delay:01b}{cqi:01b}"]
+
+
+@pytest.mark.parametrize("nof_prb,start,L,tmcs", [(25, 7, 1, 3), (50, 12, 2, 6), (6, 0, 1, 0), (100, 40, 2, 10)])
+def test_msg3_rar_grant_small_allocation(nof_prb, start, L, tmcs):
+    """srsUE's Msg3 path (phch_worker.cc:412-415 then :551-555): the RAR grant's 20 bits -> rar_grant_unpack ->
+    rar_to_ul_grant -> cfg_grant -> pusch_encode, 1- and 2-PRB allocations (the tabulated DMRS base sequences of
+    36.211 5.5.1.2), with group hopping on; the IQ matches the oracle's transmitter within 1e-4."""
+    from test_ul_grant import riv, ul_mcs
+    from srsue_amd import abi
+    qm, itbs = ul_mcs(tmcs)
+    T = abi.lib().srslte_ra_tbs_from_idx(itbs, L)
+    t = dict(tti=21, rnti=0x3C, rv=0, rar=rar_bits(0, riv(nof_prb, start, L), tmcs), tbs=T, tb=tb(40 + L, T))
+    (r, iq), = run(11, nof_prb, [t], dmrs=(1, 0, 2, 3))
+    assert r[0] == 0 and (r[1], r[2], r[4], r[6]) == (start, L, qm, start)
+    assert rel_err(iq, oracle_iq(11, nof_prb, t, t["tti"] % 10, dmrs=(1, 0, 2, 3), n_prb=start, L=L, Qm=qm,
+                                 ncs=0)) < TOL
+
+
+@pytest.mark.parametrize("n_sb,intra,via", [(1, True, "dci"), (2, False, "dci"), (3, True, "dci"), (4, True, "rar"),
+                                            (2, True, "rar")])
+def test_type2_subband_hopping_srsue_call_order(n_sb, intra, via):
+    """PUSCH hopping type 2 (36.211 5.3.4): the all-ones hopping bits of a format-0 or RAR grant, the cell's
+    pusch-HoppingSubbands / -Offset / hopping mode from set_cfg, several TTIs and CURRENT_TX_NB values; the slot
+    PRBs cfg_grant chooses equal the oracle's restatement (or_pusch_hop_type2) and the IQ matches the oracle's
+    transmitter on those PRBs within 1e-4."""
+    import ctypes as C
+    from test_ul_grant import riv, ul_mcs
+    from srsue_amd import abi
+    nof_prb, n_ho, start, L, mcs = 50, 4, 9, 2, 6
+    qm, itbs = ul_mcs(mcs)
+    T = abi.lib().srslte_ra_tbs_from_idx(itbs, L)
+    data = tb(50 + n_sb, T)
+    if via == "dci":
+        grant = dict(dci=format0(nof_prb, start, L, mcs, ncs=2, hop=1, hbits=3))
+    else:
+        # N = 50 > 44: the RBA's 2 MSBs are the hopping bits ('11': type 2), its 8 LSBs the RIV's low bits
+        grant = dict(rar=rar_bits(1, (3 << 8) | riv(nof_prb, start, L), mcs))
+    flags = (n_ho << 12) | ((1 << 20) if intra else 0) | ((n_sb - 1) << 29)
+    txs = [dict(tti=tt, rnti=0x46, rv=0, tx_nb=k, tbs=T, tb=data, **grant) for k, tt in enumerate((3, 8, 17, 26))]
+    res = run(5, nof_prb, txs, flags=flags)
+    O.lib().or_pusch_hop_type2.restype = C.c_int
+    moved = 0
+    for t, (r, iq) in zip(txs, res):
+        sf = t["tti"] % 10
+        s = []
+        for sl in range(2):
+            prb = (C.c_uint32 * L)()
+            s.append(O.lib().or_pusch_hop_type2(nof_prb, n_ho, n_sb, int(intra), 5, start, L, 2 * sf + sl, t["tx_nb"], prb))
+        assert min(s) >= 0
+        assert r[0] == 0 and (r[1], r[6]) == tuple(s), (t, r, s)
+        moved += s[0] != start or s[1] != start
+        ncs = 0 if via == "rar" else 2
+        ref = oracle_iq(5, nof_prb, t, sf, n_prb=s[0], L=L, Qm=qm, ncs=ncs, n_prb1=s[1] if s[1] != s[0] else None)
+        assert rel_err(iq, ref) < TOL
+    assert moved > 0

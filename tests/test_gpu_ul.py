@@ -21,6 +21,9 @@ CASES = [  # nof_prb, n_prb, L_prb, tbs, Qm, rv, sf, cell, gh, sh, dss, cs, n2 [
     (100, 10, 75, 25456, 6, 2, 4, 7, 0, 1, 3, 2, 5),     # 64QAM, rv 2, sequence hopping
     (50, 5, 24, 5736, 2, 1, 7, 33, 1, 0, 0, 7, 3),       # group hopping, rv 1
     (25, 0, 3, 512, 2, 0, 0, 301, 0, 0, 0, 1, 1),        # L = 3 (smallest ZC DMRS), C = 1, 8 filler bits
+    (25, 7, 1, 104, 2, 0, 3, 17, 0, 0, 0, 2, 1),         # L = 1: tabulated 12-point DMRS (36.211 5.5.1.2-1)
+    (50, 12, 2, 256, 4, 1, 6, 88, 1, 0, 2, 5, 3),        # L = 2: tabulated 24-point DMRS, group hopping, rv 1
+    (6, 0, 1, 56, 2, 0, 9, 29, 0, 0, 0, 0, 0, 1, 1, 5),  # L = 1 with HARQ-ACK (Msg3-sized grant)
     (6, 1, 5, 600, 4, 3, 9, 2, 1, 0, 29, 4, 6),          # 1.4 MHz, rv 3
     (75, 30, 45, 12216, 4, 0, 5, 11, 0, 1, 0, 3, 0),     # N = 1536
     (15, 0, 15, 4008, 6, 0, 2, 12, 0, 0, 0, 0, 2),       # 3 MHz, N = 256

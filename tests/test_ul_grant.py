@@ -3,7 +3,8 @@ srslte_dci_msg_to_ul_grant (DCI format 0, 36.212 5.3.3.1.1; phch_worker.cc:429) 
 srslte_dci_rar_to_ul_grant (random-access response grant, 36.213 6.2; phch_worker.cc:412).  These are
 host functions of the product library (no GPU call), checked against the spec fields: RIV decoding
 (36.213 8.1.1), the UL MCS table (36.213 Table 8.6.1-1), the TBS spot columns, the DMRS cyclic-shift
-field and the rejection of unsupported inputs (frequency hopping, format 1A bits, wrong size)."""
+field, frequency hopping (type 1 offsets, type 2 subband hopping: mi_ul_hop_type2 against the oracle's
+independent restatement of 36.211 5.3.4), RAR hopping bits, and the rejection of bad inputs."""
 import ctypes as C
 
 import pytest
@@ -120,12 +121,17 @@ def test_format0_type1_hopping(built, N, n_ho, start, L, hbits):
     assert (g.n_prb_tilde[0], g.n_prb_tilde[1]) == (start, hop_expect(N, n_ho, start, hbits))
 
 
+@pytest.mark.parametrize("N,hbits", [(100, 3), (25, 1), (50, 3), (6, 1)])
+def test_format0_type2_hopping_bits(built, N, hbits):
+    """Table 8.4-1: the all-ones hopping pattern selects type 2; the grant keeps the VRB start for cfg_grant."""
+    m = format0(N, 1, 2, 10, hop=1, hbits=hbits)
+    g, d = UlGrant(), UlDci()
+    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), N, 2, C.byref(d), C.byref(g), 0) == 0
+    assert g.freq_hopping == 2 and g.n_prb_tilde[0] == 1 and g.L_prb == 2
+
+
 def test_format0_rejections(built):
     g, d = UlGrant(), UlDci()
-    m = format0(100, 0, 6, 20, hop=1, hbits=3)
-    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 0, C.byref(d), C.byref(g), 0) != 0   # type 2 hopping
-    m = format0(25, 0, 6, 20, hop=1, hbits=1)
-    assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 25, 0, C.byref(d), C.byref(g), 0) != 0    # type 2 hopping
     m = format0(100, 90, 6, 20, hop=1, hbits=0)
     assert lib().srslte_dci_msg_to_ul_grant(C.byref(m), 100, 8, C.byref(d), C.byref(g), 0) != 0   # beyond the band
     m = format0(100, 0, 100, 20)
@@ -149,6 +155,76 @@ def test_rar_grant(built, N, start, L, tmcs):
     qm, itbs = ul_mcs(tmcs)
     assert (g.n_prb[0], g.L_prb, g.Qm, g.mcs.idx) == (start, L, qm, tmcs)
     assert g.mcs.tbs == abi.lib().srslte_ra_tbs_from_idx(itbs, L)
-    assert d.cqi_request and d.tpc_pusch == 3
-    r.hopping_flag = True
-    assert lib().srslte_dci_rar_to_ul_grant(C.byref(r), N, 0, C.byref(d), C.byref(g)) != 0
+    assert d.cqi_request and d.tpc_pusch == 3 and g.freq_hopping == 0
+
+
+@pytest.mark.parametrize("N,start,L,hb,n_ho", [(25, 3, 2, 0, 2), (6, 0, 1, 0, 0), (15, 2, 1, 1, 0), (50, 4, 1, 0, 4),
+                                               (100, 10, 2, 1, 6), (100, 7, 1, 3, 0), (75, 2, 3, 2, 2)])
+def test_rar_grant_hopping(built, N, start, L, hb, n_ho):
+    """36.213 6.2 with the hopping flag: the N_UL_hop MSBs of format 0's b-bit field are hopping bits.  N <= 44:
+    the field is the RBA's b LSBs; N > 44: b - 10 zeros are inserted after the hopping bits.  Msg3-sized
+    allocations (1-3 PRBs) with type 1 and type 2 patterns."""
+    b, nh = rba_bits(N), (1 if N < 50 else 2)
+    r_ = riv(N, start, L)
+    if N <= 44:
+        rba = (hb << (b - nh)) | r_
+    else:
+        assert r_ < (1 << (10 - nh))
+        rba = (hb << (10 - nh)) | r_
+    r = RarGrant(True, rba, 5, 1, False, False)
+    g, d = UlGrant(), UlDci()
+    rc = lib().srslte_dci_rar_to_ul_grant(C.byref(r), N, n_ho, C.byref(d), C.byref(g))
+    assert rc == 0 and d.freq_hop_fl == 1 and g.L_prb == L and g.n_prb_tilde[0] == start
+    if hb == (1 if nh == 1 else 3):
+        assert g.freq_hopping == 2
+    else:
+        assert g.freq_hopping == 1 and g.n_prb_tilde[1] == hop_expect(N, n_ho, start, hb)
+
+
+def _hop2_lib():
+    L = abi.lib()
+    L.mi_ul_hop_type2.restype = C.c_int
+    L.mi_ul_hop_type2.argtypes = [C.c_uint32] * 4 + [C.c_uint32] * 5
+    L.mi_ul_hop_type2.argtypes[3] = C.c_int
+    return L
+
+
+def test_type2_hopping_matches_oracle(built):
+    """mi_ul_hop_type2 (the product's host planner, ue_ul.cpp cfg_grant) == the oracle's per-VRB restatement of
+    36.211 5.3.4 over bandwidths, subband counts 1-4, hopping offsets, both hopping modes, all 20 slots, odd and
+    even CURRENT_TX_NB, cell ids and allocations; the mapped slot allocations are contiguous and in the band,
+    and both see the pattern move (f_hop / mirroring) across slots."""
+    import numpy as np
+    L, OL = _hop2_lib(), O.lib()
+    OL.or_pusch_hop_type2.restype = C.c_int
+    rng = np.random.default_rng(11)
+    n_ok = n_moved = 0
+    for _ in range(1500):
+        N = int(rng.choice([6, 15, 25, 50, 75, 100]))
+        nsb = int(rng.integers(1, 5))
+        nho = int(rng.integers(0, min(N // 2, 12) + 1))
+        intra = int(rng.integers(0, 2))
+        cid = int(rng.integers(0, 504))
+        Lp = int(rng.integers(1, 4))
+        v = int(rng.integers(0, N - Lp + 1))
+        txnb = int(rng.integers(0, 4))
+        starts = []
+        for ns in range(20):
+            prb = (C.c_uint32 * Lp)()
+            o = OL.or_pusch_hop_type2(N, nho, nsb, intra, cid, v, Lp, ns, txnb, prb)
+            if o >= 0 and sorted(prb[:]) != list(range(o, o + Lp)):
+                o = -1                                         # a non-contiguous set is not a valid slot
+            p = L.mi_ul_hop_type2(N, nho, nsb, intra, cid, v, Lp, ns, txnb)
+            assert p == o, (N, nsb, nho, intra, cid, Lp, v, txnb, ns, p, o)
+            if p >= 0:
+                n_ok += 1
+                assert p + Lp <= N
+            starts.append(p)
+        n_moved += len(set(starts)) > 1
+        if not intra:
+            assert all(starts[2 * k] == starts[2 * k + 1] for k in range(10))   # inter-subframe: per subframe
+    assert n_ok > 10000 and n_moved > 700
+    # N_sb = 1, intra- and inter-subframe: odd slots mirror the allocation about the band centre
+    for N, v, Lp in ((25, 3, 2), (100, 40, 1), (6, 0, 3)):
+        assert L.mi_ul_hop_type2(N, 0, 1, 1, 7, v, Lp, 0, 0) == v
+        assert L.mi_ul_hop_type2(N, 0, 1, 1, 7, v, Lp, 1, 0) == N - v - Lp
