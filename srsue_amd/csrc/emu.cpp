@@ -4,6 +4,7 @@
 // each lane's code to completion in turn reproduces the GPU result operation for operation; the
 // CPU test suite uses it to check planner + rate de-matching + turbo + TB assembly bit-exactly
 // against the oracle without a GPU.
+#include <algorithm>
 #include <string.h>
 
 #include <vector>
@@ -25,6 +26,12 @@ static uint32_t crc8[256], crc8b[256];   // CRC24A / CRC24B byte tables
 // form, 2 = recompute form, 3 = two code blocks per lane (int16 only, tdec_p2_body.h)
 static int g_x = 0;
 extern "C" void emu_set_tdec_x(int on) { g_x = on; }
+// packed decoder: waterfall compaction after iteration 0 (tdec_p2_body.h P2ContSrc; tdec.hip tdec_cont_*),
+// continuation pairs filled in REVERSE lane order (the GPU's order depends on atomics: results may not)
+static int g_compact = 0;
+static uint64_t g_cont_cbs = 0;
+extern "C" void emu_set_tdec_compact(int on) { g_compact = on; g_cont_cbs = 0; }
+extern "C" uint64_t emu_cont_codeblocks() { return g_cont_cbs; }
 template <bool Q16>
 static mi::TdecLaneResult emu_lane_x(const mi::TdecArgs& a, int lane) {
   mi::TdecExecHost ex;
@@ -153,7 +160,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.K = gA.K;
         a.F[0] = l0.F; a.F[1] = paired ? l1.F : l0.F;
         a.crc24a[0] = l0.crc24a; a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
-        a.max_its = max_its; a.early_stop = 1;
+        a.max_its = g_compact && max_its > 1 ? 1 : max_its; a.early_stop = 1;
         mi::TdecP2ExecHost ex;
         const mi::TdecP2Result r = mi::tdec_p2_lane(a, lane, ex);
         for (int h = 0; h < 2; h++) {
@@ -161,6 +168,78 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
           cits[li[h]] = r.its[h];
           ccrc[li[h]] = r.crc_ok[h];
           ctbp[li[h]] = r.tb_part[h];
+        }
+      }
+    }
+    if (g_compact && max_its > 1) {
+      // each group's pair (its first group) and half
+      std::vector<uint32_t> pa(P.groups.size()), ph(P.groups.size());
+      for (size_t pp = 0; pp < P.pairs.size(); pp += 2)
+        for (int h = 0; h < 2; h++)
+          if (P.pairs[pp + h] != 0xFFFFFFFFu) { pa[P.pairs[pp + h]] = P.pairs[pp]; ph[P.pairs[pp + h]] = h; }
+      std::vector<uint32_t> ks;
+      for (const MiGroupDesc& g : P.groups)
+        if (std::find(ks.begin(), ks.end(), g.K) == ks.end()) ks.push_back(g.K);
+      for (uint32_t K : ks) {
+        std::vector<uint32_t> cont;   // continuing code blocks of this K, reverse lane order
+        for (size_t gi = P.groups.size(); gi-- > 0;)
+          if (P.groups[gi].K == K)
+            for (int l = mi::LANES - 1; l >= 0; l--) {
+              const uint32_t li = P.groups[gi].lane0 + l;
+              if (P.lanes[li].valid && !ccrc[li]) cont.push_back(li);
+            }
+        g_cont_cbs += cont.size();
+        const uint32_t gi0 = [&] { uint32_t g = 0; while (P.groups[g].K != K) g++; return g; }();
+        const MiKTab& kt = P.ktabs[P.groups[gi0].ktab];
+        const uint32_t* pos = &P.kdata[kt.pos_off];
+        for (size_t p0 = 0; p0 < cont.size(); p0 += 2 * mi::LANES) {
+          std::vector<uint32_t> cscr((size_t)(7 * K + 20) * mi::LANES, 0u);
+          std::vector<uint8_t> cdec((size_t)K * mi::LANES, 0);
+          for (int lane = 0; lane < mi::LANES; lane++) {
+            uint32_t li[2] = {0, 0}, live = 0;
+            mi::P2ContSrc src[2] = {};
+            for (int h = 0; h < 2; h++) {
+              const size_t d = p0 + (size_t)h * mi::LANES + lane;
+              if (d >= cont.size()) continue;
+              li[h] = cont[d];
+              live |= 1u << h;
+              const uint32_t g = li[h] / mi::LANES;
+              src[h] = {&sb[P.groups[g].sb_off], wms[g].data(),
+                        reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li[h] % mi::LANES, ph[g]};
+            }
+            if (!live) continue;
+            for (uint32_t r = 0; r < mi::p2_cont_rows(K); r++)
+              cscr[mi::p2_cont_dst(K, r) * mi::LANES + lane] = mi::p2_cont_row(src, live, pos, K, r);
+          }
+          for (int lane = 0; lane < mi::LANES; lane++) {
+            uint32_t li[2] = {0, 0};
+            mi::TdecArgsP2 a{};
+            for (int h = 0; h < 2; h++) {
+              const size_t d = p0 + (size_t)h * mi::LANES + lane;
+              if (d < cont.size()) { li[h] = cont[d]; a.live |= 1u << h; }
+            }
+            if (!a.live) continue;
+            if (!(a.live & 2u)) li[1] = li[0];
+            a.scr = cscr.data();
+            a.q = a.scr + (size_t)(4 * K + 8) * mi::LANES;
+            a.pos = pos; a.pi = &P.kdata[kt.pi_off];
+            a.crc8 = crc8; a.crc8b = crc8b;
+            a.dec = cdec.data();
+            for (int h = 0; h < 2; h++) {
+              a.cb_bytes[h] = &cbb[(size_t)li[h] * mi::CB_BYTES_STRIDE];
+              a.F[h] = P.lanes[li[h]].F;
+              a.crc24a[h] = P.lanes[li[h]].crc24a;
+            }
+            a.K = K; a.max_its = max_its; a.early_stop = 1;
+            mi::TdecP2ExecHost ex;
+            const mi::TdecP2Result r = mi::tdec_p2_lane<true>(a, lane, ex);
+            for (int h = 0; h < 2; h++) {
+              if (!((a.live >> h) & 1u)) continue;
+              cits[li[h]] = r.its[h];
+              ccrc[li[h]] = r.crc_ok[h];
+              ctbp[li[h]] = r.tb_part[h];
+            }
+          }
         }
       }
     }

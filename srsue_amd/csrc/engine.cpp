@@ -136,6 +136,11 @@ int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
          d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
          d_cbcrc.ensure(P.lanes.size() * 4) && d_cbtbp.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
          d_tbits.ensure(nsf * 4);
+    if (tdec_compact()) {
+      const uint32_t np = cont_max_pairs();
+      ok = ok && d_cont.ensure((P.lanes.size() + 1) * 4) && d_cscr.ensure((size_t)np * cont_pair_u32() * 4) &&
+           d_cdec.ensure((size_t)np * P.groups[0].K * LANES);
+    }
     if (alloc_sb) {
       size_t before = d_sb.bytes;
       ok = ok && d_sb.ensure(P.sb_floats * 4);
@@ -336,6 +341,20 @@ int Engine::tdec_crossed() const {
   return form;
 }
 
+bool Engine::tdec_compact() const {
+  const Plan& P = plan;
+  if (P.groups.empty() || use_win() || !q16() || tdec_crossed() != 3 || !early_stop || max_its < 2) return false;
+  if (const char* e = getenv("MI_TDEC_COMPACT")) if (!atoi(e)) return false;   // A/B
+  for (size_t g = 0; g < P.groups.size(); g++)
+    if (P.groups[g].K != P.groups[0].K || P.groups[g].lane0 != g * LANES) return false;
+  return true;
+}
+size_t Engine::cont_pair_u32() const {
+  const uint32_t K = plan.groups.empty() ? 0 : plan.groups[0].K;
+  return ((size_t)(7 * K + 20) * LANES + 63) & ~(size_t)63;   // w, llr1, checkpoints, q rows (tdec_p2_body.h)
+}
+uint32_t Engine::cont_max_pairs() const { return (uint32_t)((plan.lanes.size() + 2 * LANES - 1) / (2 * LANES)); }
+
 // turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts
 void Engine::launch_turbo(float* sb, hipStream_t st) {
   const Plan& P = plan;
@@ -354,10 +373,23 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
   launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                  (uint32_t)P.groups.size(), st);
   if (tdec_crossed() == 3 && q16()) {
+    // compaction needs its buffers (ensure_work sized them for this plan and max_its); without them the
+    // packed decoder runs every iteration itself -- the same results either way
+    const bool cont = tdec_compact() && d_cscr.bytes >= (size_t)cont_max_pairs() * cont_pair_u32() * 4 &&
+                      d_cont.bytes >= (P.lanes.size() + 1) * 4 &&
+                      d_cdec.bytes >= (size_t)cont_max_pairs() * P.groups[0].K * LANES;
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                    d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), d_pairs.as<uint32_t>(),
-                   (uint32_t)(P.pairs.size() / 2), max_its, early_stop, st);
+                   (uint32_t)(P.pairs.size() / 2), cont ? 1u : max_its, early_stop, st);
+    if (cont) {
+      // the code blocks still failing after iteration 0, compacted into dense pairs for iterations 1 ..
+      launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
+                       d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
+                       d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
+                       (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
+                       cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048, st);
+    }
     return;
   }
   launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),

@@ -39,6 +39,11 @@ struct Engine {
   // lane form: 0 one wavefront per group, 1 crossed, 2 crossed (recompute form), 3 crossed with two code
   // blocks per lane (packed int16, tdec_p2_body.h)
   int tdec_crossed() const;
+  // waterfall compaction of the packed decoder after iteration 0 (tdec.hip launch_tdec_cont): schedule 3,
+  // early stop, max_its > 1, one K (pairs are groups 2j, 2j + 1); MI_TDEC_COMPACT=0 (env, A/B) disables
+  bool tdec_compact() const;
+  size_t cont_pair_u32() const;   // continuation pair scratch, u32 words
+  uint32_t cont_max_pairs() const;
   void launch_turbo(float* sb, hipStream_t st);
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
@@ -46,7 +51,7 @@ struct Engine {
       d_fftlist, d_tw, d_pairs;
   // data buffers
   DevBuf d_grid, d_ce, d_metrics, d_e, d_sb, d_wm, d_scratch, d_dec, d_cbbytes, d_cbits, d_cbcrc, d_cbtbp, d_payload, d_tbok,
-      d_tbits;
+      d_tbits, d_cont, d_cscr, d_cdec;
   std::map<int, size_t> tw_off;   // FFT size -> float2 offset in d_tw
   // the plan's descriptor tables, packed 256-B aligned into one page-locked host buffer and copied to
   // one device arena with a single DMA per upload (the per-TTI API re-plans every call)

@@ -26,6 +26,9 @@
 #ifndef MI_RM_IDLE_OFF
 #define MI_RM_IDLE_OFF 0
 #endif
+#ifndef MI_RM_XCD
+#define MI_RM_XCD 1   // XCD-aware work-item order (A/B switch)
+#endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
 #endif
@@ -189,7 +192,12 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   // the work item: (group, chunk) from the planner's list of chunks with received LLRs, or the 2-D grid
   uint32_t gi = blockIdx.y, ci = blockIdx.x;
   if (items) {
-    const uint32_t it = items[blockIdx.x];
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one), so XCD x takes
+    // the x-th contiguous eighth of the work list in order -- the chunks active on one XCD at a time are
+    // neighbours (the same few groups / subframes), whose grid lines, channel-estimate rows and RE tables then
+    // stay in that XCD's L2 (MI355X_MICROARCH.md, workgroup dispatch; speed only, any order is correct)
+    const uint32_t n = gridDim.x, b = blockIdx.x, x = b % 8u;
+    const uint32_t it = items[MI_RM_XCD ? x * (n / 8u) + min(x, n % 8u) + b / 8u : b];
     gi = it >> 9;
     ci = it & 511u;
   }

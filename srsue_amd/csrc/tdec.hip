@@ -246,6 +246,122 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
                      ktab_data, pairs, max_its, early_stop);
 }
 
+// ---- waterfall compaction (tdec_p2_body.h P2ContSrc): one K, early stop, iteration 0 done by
+// tdec_kernel_p2x (max_its 1).  cont[0] = number of continuing code blocks, cont[1 ..] = their lane indices;
+// continuation pair p holds cont[1 + 128 p + 64 h + lane] in half h of lane `lane`.
+// 1. one wavefront per group: the lanes whose code block failed its CRC claim consecutive slots
+__global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc* __restrict__ groups,
+                                                              const MiLaneDesc* __restrict__ lanes,
+                                                              const uint32_t* __restrict__ cb_crc, uint32_t* cont) {
+  const uint32_t lane = threadIdx.x, li = groups[blockIdx.x].lane0 + lane;
+  const bool act = lanes[li].valid && !cb_crc[li];
+  const uint64_t m = __ballot(act);
+  if (!m) return;
+  const int lead = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)lane == lead) base = atomicAdd(cont, (uint32_t)__popcll(m));
+  base = __shfl(base, lead);
+  if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
+}
+
+// 2. the gather: a wavefront per (continuation pair, 64-row chunk), lane = continuation lane, both halves
+constexpr uint32_t CONT_ROWS = 64;
+__global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __restrict__ sb,
+                                                               const uint32_t* __restrict__ wm,
+                                                               const float* __restrict__ scratch,
+                                                               const MiGroupDesc* __restrict__ groups,
+                                                               const uint32_t* __restrict__ pos,
+                                                               const uint32_t* __restrict__ cont,
+                                                               uint32_t* __restrict__ cscr, size_t pair_u32, uint32_t K) {
+  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), R = p2_cont_rows(K);
+  const uint32_t nc = (R + CONT_ROWS - 1) / CONT_ROWS, lane = threadIdx.x % LANES;
+  for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * nc; u += gridDim.x * 4) {
+    const uint32_t p = u / nc, c = u % nc;
+    P2ContSrc s[2] = {};
+    uint32_t live = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t d = p * 2 * LANES + h * LANES + lane;
+      if (d >= n) continue;
+      const uint32_t li = cont[1 + d], g = li / LANES;   // plan.cpp: group g = lanes 64 g .. 64 g + 63
+      live |= 1u << h;
+      s[h].sb = sb + groups[g].sb_off;
+      s[h].wm = wm + (size_t)g * WM_STRIDE;
+      s[h].scr = reinterpret_cast<const uint32_t*>(scratch + groups[g & ~1u].scratch_off);   // pairs (2j, 2j + 1)
+      s[h].ls = li % LANES;
+      s[h].hs = g & 1u;
+    }
+    uint32_t* dst = cscr + (size_t)p * pair_u32;
+    const uint32_t r0 = c * CONT_ROWS, r1 = min(R, r0 + CONT_ROWS);
+#pragma unroll 8
+    for (uint32_t r = r0; r < r1; r++) dst[p2_cont_dst(K, r) * LANES + lane] = p2_cont_row(s, live, pos, K, r);
+  }
+}
+
+// 3. iterations 1 .. max_its - 1 of the continuing code blocks, dense pairs
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
+void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
+                     const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
+                     const uint32_t* __restrict__ cont, size_t pair_u32, uint32_t K, uint32_t max_its) {
+  __shared__ uint32_t crc8[256], crc8b[256];
+  __shared__ uint32_t xs[LANES];
+  const uint32_t n = cont[0], p = blockIdx.x;
+  if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
+    crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+    crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x % LANES;
+  const uint32_t d0 = p * 2 * LANES + lane, d1 = d0 + LANES;
+  TdecArgsP2 a{};
+  a.live = (d0 < n ? 1u : 0u) | (d1 < n ? 2u : 0u);
+  if (!a.live) return;   // the same on both wavefronts
+  const uint32_t li[2] = {cont[1 + d0], (a.live & 2u) ? cont[1 + d1] : cont[1 + d0]};
+  const MiLaneDesc l0 = lanes[li[0]], l1 = lanes[li[1]];
+  a.scr = cscr + (size_t)p * pair_u32;
+  a.q = a.scr + (size_t)(4 * K + 8) * LANES;
+  a.pos = kdata + kt.pos_off;
+  a.pi = kdata + kt.pi_off;
+  a.crc8 = crc8;
+  a.crc8b = crc8b;
+  a.dec = cdec + (size_t)p * K * LANES;
+  a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
+  a.cb_bytes[1] = out.cb_bytes + (size_t)li[1] * CB_BYTES_STRIDE;
+  a.K = K;
+  a.F[0] = l0.F;
+  a.F[1] = l1.F;
+  a.crc24a[0] = l0.crc24a;
+  a.crc24a[1] = l1.crc24a;
+  a.max_its = max_its;
+  a.early_stop = 1;
+  TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
+  const TdecP2Result r = tdec_p2_lane<true>(a, lane, ex);
+  if (ex.wave) return;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (!((a.live >> h) & 1u)) continue;
+    out.its[li[h]] = r.its[h];
+    out.crc_ok[li[h]] = r.crc_ok[h];
+    out.tb_part[li[h]] = r.tb_part[h];
+  }
+}
+
+void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch, uint8_t* cb_bytes, uint32_t* cb_its,
+                      uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
+                      const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
+                      uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
+                      hipStream_t st) {
+  if (!n_groups || !max_pairs) return;
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  (void)hipMemsetAsync(cont, 0, 4, st);
+  hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
+  hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
+                     ktab_data + kt.pos_off, cont, cscr, pair_u32, K);
+  hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes, ktab_data, kt, cont,
+                     pair_u32, K, max_its);
+}
+
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,
                  uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes, const MiKTab* ktabs,
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,

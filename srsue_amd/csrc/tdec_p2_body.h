@@ -777,13 +777,18 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
 // ex.pack_wave is true on the wave that runs tdec_p2_check (GPU: wave F, after the iteration's barrier;
 // host: always); ex.share hands its verdicts to the other wave.  With early stop off (configs[0]'s fixed
 // iteration count) only the last iteration's pass runs.
-template <class Exec>
+// CONT (waterfall compaction, tdec.hip): the code blocks continue from iteration 1 in a dense continuation
+// pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
+template <bool CONT = false, class Exec>
 MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
-  for (uint32_t it = 0; it < a.max_its && active; it++) {
+  for (uint32_t it = CONT ? 1u : 0u; it < a.max_its && active; it++) {
     constexpr uint32_t MK = MI_TDEC_MKQ_IT;
-    if (it == 0) {
+    if constexpr (CONT) {
+      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
+    } else if (it == 0) {
       if (MK == 0) {
         tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex);
         tdec_p2_xhalf<true, true, SRC_Q>(a, lane, ex);
@@ -818,6 +823,45 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     active &= ~stop;
   }
   return r;
+}
+
+// ---- waterfall compaction (tdec.hip tdec_cont_*, emu.cpp) ---------------------------------------------
+// At 21.5 dB most code blocks pass their CRC after iteration 0 and the lanes that go on iterate in
+// sparse wavefronts (a pair's cost is its slowest code block).  With early stop the decode therefore runs
+// iteration 0 over all pairs, then gathers the code blocks whose CRC failed into dense continuation
+// pairs and runs iterations 1.. there (tdec_p2_lane<true>).  The gather builds exactly the state
+// iteration 1 reads: the packed q rows that the SRC_MKQ pass would create (window masks applied:
+// unmaterialised rows are the group's zero row, i.e. q = 0) and the iteration-0 extrinsic rows w; llr1,
+// checkpoints and decisions are rewritten by every iteration.  The two halves of a lane never interact,
+// so which code blocks share a continuation lane does not change any result.
+// Continuation pair layout = the pair scratch layout (w, llr1, checkpoints, q rows at (4K + 8) rows);
+// gathered rows r = 0 .. 3K + 11 are q rows, r = 3K + 12 .. 4K + 11 are w rows 0 .. K - 1.
+struct P2ContSrc {
+  const float* sb;      // the code block's group softbuffer
+  const uint32_t* wm;   // the group's window masks
+  const uint32_t* scr;  // the scratch of the group's pair (w rows: packed, this code block = half hs)
+  uint32_t ls, hs;      // lane in the group, half in the pair
+};
+MI_HD inline uint32_t p2_cont_rows(uint32_t K) { return 4 * K + 12; }
+MI_HD inline size_t p2_cont_dst(uint32_t K, uint32_t r) {   // u32 row of gathered row r in the pair layout
+  return r < 3 * K + 12 ? (size_t)(4 * K + 8) + r : (size_t)(r - (3 * K + 12));
+}
+MI_HD inline uint32_t p2_cont_row(const P2ContSrc (&s)[2], uint32_t live, const uint32_t* pos, uint32_t K,
+                                  uint32_t r) {
+  const uint32_t nq = 3 * K + 12;
+  if (r < nq) {
+    float v[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      v[h] = ((live >> h) & 1u) && ((s[h].wm[r / 12] >> (r % 12)) & 1u) ? s[h].sb[(size_t)pos[r] * LANES + s[h].ls]
+                                                                       : 0.0f;
+    return p2_bits(q16_pair(v[0], v[1]));
+  }
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)(r - nq) * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
+  return w[0] | (w[1] << 16);
 }
 
 struct TdecP2ExecHost {

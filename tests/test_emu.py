@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from helpers import oracle_dlsch, oracle_front, tb_bytes
+from helpers import oracle_dlsch, oracle_dlsch_cbits, oracle_front, tb_bytes
 from srsue_amd import abi
 
 CASES = [  # nof_prb, ports, tbs, Qm, snr, sf, rv, cell
@@ -120,13 +120,16 @@ def test_emulated_segment_parallel_turbo_bit_exact(built, nprb, ports, tbs, qm, 
     assert np.array_equal(pe, opay)
 
 
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("snr0", [18.6, 30.0])
-def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0):
+def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     """The packed decoder (two code blocks per lane, tdec_p2_body.h) on a batch whose code blocks fill
     PAIRED groups: 11 subframes of 20 MHz MCS-28 (143 code blocks of K = 5824: one pair + one unpaired
     group) at per-subframe SNRs across the waterfall (code blocks of one lane stop at different
     iterations, some never), plus a 1.4 MHz subframe (another K, unpaired); every TB against the
-    oracle's int16 decoder: payload, CRC verdict, iterations."""
+    oracle's int16 decoder: payload, CRC verdict, iterations, and every code block's iterations.
+    compact: the waterfall compaction (iteration 0 over the pairs, then the CRC-failing code blocks
+    gathered -- in reverse lane order, so with new partners -- into continuation pairs, tdec_p2_lane<true>)."""
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(11)]
     cfgs.append(abi.sf_cfg(cell_id=301, nof_prb=6, sf_idx=2, tbs=4392, Qm=6))
     snrs = [snr0 + 0.35 * (i % 5) for i in range(len(cfgs))]
@@ -138,22 +141,33 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0):
     pe = np.zeros(offs[-1] + cfgs[-1].tbs // 8, np.uint8)
     eok = np.zeros(n, np.uint32)
     eits = np.zeros(n, np.uint32)
-    cbits = np.zeros(64 * 4, np.uint32)
+    cbits = np.zeros(64 * 4, np.uint32)   # 4 groups: 1 of K = 4416 (1.4 MHz), 3 of K = 5824
     flat = np.concatenate(llrs).astype(np.float32)
-    abi.emu().emu_set_tdec_i16(1)
-    abi.emu().emu_set_tdec_x(3)
+    E = abi.emu()
+    E.emu_set_tdec_i16(1)
+    E.emu_set_tdec_x(3)
+    E.emu_set_tdec_compact(int(compact))
+    E.emu_cont_codeblocks.restype = C.c_uint64
     try:
-        rc = abi.emu().emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
-                                      eok.ctypes.data, eits.ctypes.data, cbits.ctypes.data)
+        rc = E.emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
+                              eok.ctypes.data, eits.ctypes.data, cbits.ctypes.data)
+        n_cont = E.emu_cont_codeblocks()
     finally:
-        abi.emu().emu_set_tdec_i16(0)
-        abi.emu().emu_set_tdec_x(0)
+        E.emu_set_tdec_i16(0)
+        E.emu_set_tdec_x(0)
+        E.emu_set_tdec_compact(0)
     assert rc == 0
+    # lanes sorted by K (plan.cpp), each K's groups padded to 64 lanes: the 1.4 MHz code block is group 0
+    lane = 64
     for i, c in enumerate(cfgs):
         with O.tdec_mode(O.TDEC_I16):
-            ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
+            ok, opay, onoi, ocb = oracle_dlsch_cbits(c, llrs[i])
         assert bool(eok[i]) == ok, i
         assert eits[i] == onoi, i
         assert np.array_equal(pe[offs[i]:offs[i] + c.tbs // 8], opay), i
+        if i < 11:
+            assert np.array_equal(cbits[lane:lane + len(ocb)], ocb), i
+            lane += len(ocb)
     if snr0 < 20:
-        assert len(set(cbits[:143].tolist())) >= 3   # code blocks of one lane stopped at different iterations
+        assert len(set(cbits[64:64 + 143].tolist())) >= 3   # code blocks of one lane stopped at different its
+        assert not compact or n_cont > 20

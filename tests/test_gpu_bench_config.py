@@ -153,3 +153,29 @@ def test_bench_iterating_shape_compact_vs_oracle():
     for k, j in enumerate(sample):
         assert orc[k][0] == exp[k][0] and np.array_equal(orc[k][1], exp[k][1]), f"pool entry {j}: oracle front"
     b.close()
+
+
+def test_waterfall_compaction_matches_uncompacted(monkeypatch):
+    """Test C: the waterfall compaction (tdec.hip launch_tdec_cont: iteration 0 over the group pairs, the code
+    blocks whose CRC failed gathered into dense continuation pairs for iterations 1..) against the packed
+    decoder running every iteration in place (MI_TDEC_COMPACT=0): identical TB CRCs, TB and per-code-block
+    iterations and payload on a 16-25 dB mix -- continuation partners differ between runs (slot order is
+    atomic), so this also checks that a lane's two halves never interact."""
+    pool = 40
+    n = -(-min_subframes_for_p2() // pool) * pool
+    pcfgs = [abi.sf_cfg(nof_prb=100, sf_idx=SF_CYCLE[j % 8], tbs=TBS, Qm=6, rnti=0x46) for j in range(pool)]
+    iqs = [abi.tx_subframe(c, tb_bytes(7000 + j, TBS), snr_db=16.0 + 9.0 * j / (pool - 1), seed=0xC000 + j)
+           for j, c in enumerate(pcfgs)]
+    outs = []
+    for compact in ("1", "0", "1"):
+        monkeypatch.setenv("MI_TDEC_COMPACT", compact)
+        b, _ = run_bench_config(n, iqs)
+        assert b.turbo_sched == "p2", b.turbo_sched
+        outs.append([b.download(k, np.uint32 if k != abi.BUF_PAYLOAD else np.uint8)
+                     for k in (abi.BUF_TB_CRC, abi.BUF_TB_ITS, abi.BUF_CB_ITS, abi.BUF_PAYLOAD)])
+        b.close()
+    for k, name in enumerate(("TB CRC", "TB its", "CB its", "payload")):
+        assert np.array_equal(outs[0][k], outs[1][k]), name
+        assert np.array_equal(outs[2][k], outs[1][k]), name
+    crc, cbits = outs[0][0], outs[0][2][:C * n]
+    assert 0 < crc.sum() < n and set(np.unique(cbits).tolist()) >= {1, 2, 3, 4}

@@ -300,3 +300,31 @@ def test_ue_dl_concurrent_worker_instances():
     assert d["mismatches_vs_sequential"] == 0 and d["errors"] == 0 and d["crc_ok_payload_mismatches"] == 0
     # both outcomes occur (CFI 3 at MCS 28 and the waterfall half fail some TTIs), and decodes iterate
     assert d["crc_ok"] >= 20 and d["crc_failed"] > 0 and d["iterating_ttis"] > 0, d
+
+
+def test_ue_dl_plan_memo_eviction_srsue_call_order():
+    """The per-TTI plan memos evict least-recently-used entries (Engine::plan_memo: 32 PDSCH / front-end plans;
+    ue_dl.cpp ctrl_plan: 64 control plans keyed by (sf_idx, CFI, RNTI, PHICH query)).  120 TTIs cycle 10 subframe
+    indices x 8 RNTIs x 5 TBS values (MCS 24-28) -- 50 PDSCH configurations and 80 control plans, both far past
+    their memo sizes -- in an order that revisits recently used, long-evicted and never-seen entries; every TTI
+    must still decode exactly as a fresh decode: CFI, CRC, iterations and payload equal to the oracle's and to the
+    transmitted TB."""
+    tbs_list = [abi.lib().srslte_ra_tbs_from_idx(i, 100) for i in (22, 23, 24, 25, 26)]
+    rntis = [0x46 + 17 * k for k in range(8)]
+    subs, tbs_sent = [], []
+    for t in range(120):
+        sf = (t * 7) % 10
+        cfg = abi.sf_cfg(nof_prb=100, sf_idx=sf, tbs=tbs_list[(t // 3) % 5], Qm=6, rnti=rntis[(t * 3 + t // 10) % 8])
+        tb = tb_bytes(2000 + t, cfg.tbs)
+        iq = abi.tx_subframe(cfg, tb, snr_db=30.0, seed=3000 + t)
+        subs.append((cfg, iq, True, 0, True))
+        tbs_sent.append(tb)
+    keys_pdsch = {(c.sf_idx, c.tbs, c.rnti) for c, *_ in subs}
+    keys_ctrl = {(c.sf_idx, c.rnti) for c, *_ in subs}
+    assert len(keys_pdsch) > 32 and len(keys_ctrl) > 64
+    res = run_harness(1, 100, 1, subs)
+    for (c, iq, *_), tb, (ret, cf, noi, met, pay) in zip(subs, tbs_sent, res):
+        _, _, _, ollr = oracle_front(c, iq)
+        ok, opay, onoi, _ = oracle_dlsch(c, ollr, i16=True)
+        assert cf == 1 and ret == 0 and ok, (c.sf_idx, c.tbs, hex(c.rnti))
+        assert np.array_equal(pay, tb) and np.array_equal(pay, opay) and noi == onoi
