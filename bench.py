@@ -598,10 +598,33 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
             its = b.download(abi.BUF_TB_ITS, np.uint32)[:B]
             n_ok = int(crc.sum())
             bits_ok = float(sum(c.tbs for c, o in zip(cfgs, crc) if o))
+            cb_its = b.download(abi.BUF_CB_ITS, np.uint32)
     for b in batches[1:]:
         b.close()
     return {"batch": batch, "stage": stage, "nprof": nprof, "elapsed": elapsed, "n_ok": n_ok, "its": its,
-            "bad": bad, "bits_ok": bits_ok}
+            "bad": bad, "bits_ok": bits_ok, "cb_its": cb_its}
+
+
+def wave_iterations(batch, cb_its):
+    """Where the turbo iterations go: per code block, and per packed-decoder wavefront pair
+    (a group pair = 128 code blocks: lanes 128 j .. 128 j + 127; without compaction a pair runs until its slowest
+    code block stops).  Histograms of iteration counts, from the decoder's own per-code-block output."""
+    n = batch.n_codeblocks
+    cb = np.asarray(cb_its[:(batch.n_groups * 64)], np.int64)
+    valid = cb > 0
+    out = {"cb_its_hist": {int(v): int(c) for v, c in zip(*np.unique(cb[valid], return_counts=True))},
+           "cb_mean_its": round(float(cb[valid].mean()), 4), "codeblocks": int(n),
+           "codeblocks_past_iteration_0": int((cb > 1).sum())}
+    if batch.turbo_sched == "p2":
+        npair = len(cb) // 128
+        pm = cb[:npair * 128].reshape(npair, 128).max(axis=1)
+        out["pair_max_its_hist"] = {int(v): int(c) for v, c in zip(*np.unique(pm, return_counts=True))}
+        out["pair_iterations_without_compaction"] = int(pm.sum())
+        out["compaction"] = batch.turbo_compact
+        if batch.turbo_compact:
+            # iteration 0 over every pair, then dense pairs of the continuing code blocks
+            out["continuation_pairs"] = int(-(-int((cb > 1).sum()) // 128))
+    return out
 
 
 def spawn_ranks(n):
@@ -774,6 +797,7 @@ def main():
                    "turbo_codeblocks_per_s": round(incb * isteps / iel, 1),
                    "crc_ok_rate": round(iok / itb, 6), "mean_turbo_iterations": round(iits / itb, 4),
                    "payload_mismatches_crc_ok": int(ibad),
+                   "turbo_waves": wave_iterations(ib, im["cb_its"]),
                    "stage_ms_per_step": {k: round(v, 4) for k, v in im["stage"].items()},
                    "tdec_roofline": {"kernel": tdec_kernel_name(ib.turbo_sched), "bound": "hbm",
                                      "achieved": round(iach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -133,6 +133,10 @@ uint32_t mi_dl_batch_n_codeblocks(const mi_dl_batch_t *b);
  * the crossed schedule (two wavefronts per group), 3 = the same in its recompute form, 4 = two code blocks
  * per lane (packed int16, crossed), 0 = lane per code block, one wavefront per group */
 int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
+/* 1 when schedule 4 runs with waterfall compaction: iteration 0 over every group pair, then the code blocks
+ * whose CRC failed gathered into dense continuation pairs for the remaining iterations (early stop,
+ * max_its > 1, one code-block size; the environment variable MI_TDEC_COMPACT=0 disables it for A/B runs) */
+int    mi_dl_batch_turbo_compact(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 
 /* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =

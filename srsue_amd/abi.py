@@ -87,6 +87,7 @@ def lib():
             "mi_dl_batch_algo_bytes": (C.c_double, [vp, C.c_int]),
             "mi_dl_batch_n_codeblocks": (u32, [vp]),
             "mi_dl_batch_turbo_win": (C.c_int, [vp]),
+            "mi_dl_batch_turbo_compact": (C.c_int, [vp]),
             "mi_tdec_turbo_win": (C.c_int, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
@@ -278,6 +279,11 @@ class Batch:
     def turbo_sched(self):
         """'win' (latency form), 'lanex' (lane per code block, two wavefronts per group) or 'lane'"""
         return {1: "win", 2: "lanex", 3: "lanexr", 4: "p2"}.get(lib().mi_dl_batch_turbo_win(self.h), "lane")
+
+    @property
+    def turbo_compact(self):
+        """True when the packed decoder compacts the CRC-failing code blocks after iteration 0 (tdec.hip)."""
+        return lib().mi_dl_batch_turbo_compact(self.h) == 1
 
     @property
     def n_groups(self):

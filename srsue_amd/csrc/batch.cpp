@@ -121,6 +121,7 @@ static int turbo_sched(const mi::Engine& e) {
   return x == 3 ? 4 : x == 2 ? 3 : x ? 2 : 0;
 }
 int mi_dl_batch_turbo_win(const mi_dl_batch_t* b) { return turbo_sched(b->eng); }
+int mi_dl_batch_turbo_compact(const mi_dl_batch_t* b) { return b->eng.tdec_compact() ? 1 : 0; }
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
 
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */

@@ -68,6 +68,13 @@ MI_HD inline P2 q16_pair(float a, float b) {
 #endif
 }
 
+// DEC2's systematic input x2(k) = clamp(llr1(k) - w(k)) (tdec_body.h) is formed by DEC1 when it emits
+// step k -- w(k) is the a-priori row DEC1 has just read in natural order, and it is still the value DEC2
+// would read at row pi(k): DEC2 rewrites that row only after reading it -- and stored in the llr1 rows, so
+// DEC2 loads one interleaved row per step instead of two (MI_TDEC_P2_X2; identical integers)
+#ifndef MI_TDEC_P2_X2
+#define MI_TDEC_P2_X2 1
+#endif
 // raw loads of one window (BETA_W steps), converted only at use (software pipelining, tdec_body.h):
 //   q-row passes: s0 / s1 = packed q rows;  softbuffer passes: a0/b0, a1/b1 = groups A / B floats
 //   DEC1: s0 = systematic, s1 = parity 1, r0 = w;   DEC2: s0 = parity 2, r0 = llr1[pi], r1 = w[pi]
@@ -116,7 +123,7 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
         r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i + 2, lane);
       }
       r.r0[i] = row_ld(llr1, pk, lane);
-      r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
+      if constexpr (!MI_TDEC_P2_X2) r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
     }
   }
 }
@@ -200,18 +207,21 @@ MI_HD inline void p2_xs_xp(const TdecArgsP2& a, const TdecWinP2& r, int i, uint3
     xs = c0 + p2_from_bits(r.r0[i]);
     xp = c1;
   } else {
-    xs = p2_clamp(p2_from_bits(r.r0[i]) - p2_from_bits(r.r1[i]), (int)I16_CX);
+    if constexpr (MI_TDEC_P2_X2) xs = p2_from_bits(r.r0[i]);
+    else xs = p2_clamp(p2_from_bits(r.r0[i]) - p2_from_bits(r.r1[i]), (int)I16_CX);
     xp = p2_chan0<SQ>(r, i);
   }
 }
 
-// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1; DEC2 updates w at row pi(k) (pk, carried
-// from the window's loads) and stores the two decision bits there (the code-block CRCs are taken from
-// the decision rows after the iteration: tdec_p2_check)
+// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1 (MI_TDEC_P2_X2: x2 = clamp(llr1 - w), xs =
+// the step's a-priori w); DEC2 updates w at row pi(k) (pk, carried from the window's loads) and stores
+// the two decision bits there (the code-block CRCs are taken from the decision rows after the iteration:
+// tdec_p2_check)
 template <bool DEC2>
 MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, uint32_t pk, P2 llr, P2 xs) {
   if (!DEC2) {
-    row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(llr), i);
+    const P2 v = MI_TDEC_P2_X2 ? p2_clamp(llr - xs, (int)I16_CX) : llr;
+    row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(v), i);
   } else {
     row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
     const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
@@ -287,6 +297,12 @@ MI_HD inline void p2_beta_window_mkq(const TdecArgsP2& a, int lane, const TdecWi
   }
   norm8<true>(b);
 }
+// the emit's last operand: DEC2 its systematic input xs, DEC1 (x2 form) the step's a-priori w
+template <bool DEC2>
+MI_HD inline P2 p2_emit_x(const TdecWinP2& w, const P2 (&xs)[BETA_W], int i) {
+  if constexpr (DEC2 || !MI_TDEC_P2_X2) return xs[i];
+  else return p2_from_bits(w.r0[i]);
+}
 // wave F, phase 2: beta_{base+1..base+4} recomputed from the closing checkpoint, then alpha + LLRs
 template <bool DEC2, bool SQ>
 MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&al)[8]) {
@@ -298,7 +314,8 @@ MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2
 #pragma unroll
   for (int i = BETA_W - 2; i >= 0; i--) beta_step<false>(bw[i + 1], xs[i + 1], xp[i + 1], bw[i]);
 #pragma unroll
-  for (int i = 0; i < BETA_W; i++) p2_emit<DEC2>(a, lane, base, i, w.pk[i], alpha_step<false>(al, bw[i], xs[i], xp[i]), xs[i]);
+  for (int i = 0; i < BETA_W; i++)
+    p2_emit<DEC2>(a, lane, base, i, w.pk[i], alpha_step<false>(al, bw[i], xs[i], xp[i]), p2_emit_x<DEC2>(w, xs, i));
   norm8<true>(al);
 }
 // wave B, phase 2: alpha of the window recomputed from its opening checkpoint (window 0: the start
@@ -330,7 +347,7 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
     else if (FIRST_WIN && i == 1) llr = llr_step<0x11u>(aw[i], b, xs[i], xp[i]);
     else if (FIRST_WIN && i == 2) llr = llr_step<0x55u>(aw[i], b, xs[i], xp[i]);
     else llr = llr_step(aw[i], b, xs[i], xp[i]);
-    p2_emit<DEC2>(a, lane, base, i, w.pk[i], llr, xs[i]);
+    p2_emit<DEC2>(a, lane, base, i, w.pk[i], llr, p2_emit_x<DEC2>(w, xs, i));
     P2 nb[8];
     beta_step<false>(b, xs[i], xp[i], nb);
 #pragma unroll
@@ -366,6 +383,7 @@ struct TdecWin8P2 {
 struct TdecX8P2 {
   P2 xs[2 * BETA_W], xp[2 * BETA_W];
   uint32_t pk[2 * BETA_W];   // DEC2: pi(k) of the pair's steps
+  P2 w[2 * BETA_W];          // DEC1, x2 form: the steps' a-priori w (the emit's operand)
 };
 
 template <bool DEC2, bool SQ>
@@ -380,7 +398,18 @@ MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t bas
       x.pk[i] = r.lo.pk[i];
       x.pk[BETA_W + i] = r.hi.pk[i];
     }
+  } else if constexpr (MI_TDEC_P2_X2) {
+#pragma unroll
+    for (int i = 0; i < BETA_W; i++) {
+      x.w[i] = p2_from_bits(r.lo.r0[i]);
+      x.w[BETA_W + i] = p2_from_bits(r.hi.r0[i]);
+    }
   }
+}
+template <bool DEC2>
+MI_HD inline P2 p2_emit_x8(const TdecX8P2& x, int i) {
+  if constexpr (DEC2 || !MI_TDEC_P2_X2) return x.xs[i];
+  else return x.w[i];
 }
 MI_HD inline void p2_cp8(P2 (&d)[8], const P2 (&s)[8]) {
 #pragma unroll
@@ -417,7 +446,8 @@ template <bool DEC2>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
                                    P2 (&al)[8]) {
   P2 B4[8], Bm[8], Bt[8];
-#define emit(I, BN) p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), x.xs[I])
+#define emit(I, BN) \
+  p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
   p2_cp8_opaque(B4, B8);
   p2_beta_run<7, 4>(B4, x);
   norm8<true>(B4);
@@ -463,7 +493,7 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
   else if (FIRST_WIN && I == 1) llr = llr_step<0x11u>(av, b, x.xs[I], x.xp[I]);
   else if (FIRST_WIN && I == 2) llr = llr_step<0x55u>(av, b, x.xs[I], x.xp[I]);
   else llr = llr_step(av, b, x.xs[I], x.xp[I]);
-  p2_emit<DEC2>(a, lane, base, I, x.pk[I], llr, x.xs[I]);
+  p2_emit<DEC2>(a, lane, base, I, x.pk[I], llr, p2_emit_x8<DEC2>(x, I));
   P2 nb[8];
   beta_step<false>(b, x.xs[I], x.xp[I], nb);
   p2_cp8(b, nb);
