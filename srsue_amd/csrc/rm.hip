@@ -27,7 +27,10 @@
 #define MI_RM_IDLE_OFF 0
 #endif
 #ifndef MI_RM_XCD
-#define MI_RM_XCD 1   // XCD-aware work-item order (A/B switch)
+#define MI_RM_XCD 0   // XCD-aware work-item order (A/B switch; off: profiles/r3/ab_rm_xcd)
+#endif
+#ifndef MI_RM_XCD_BLOCK
+#define MI_RM_XCD_BLOCK 64   // work items per XCD block
 #endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
@@ -192,12 +195,16 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   // the work item: (group, chunk) from the planner's list of chunks with received LLRs, or the 2-D grid
   uint32_t gi = blockIdx.y, ci = blockIdx.x;
   if (items) {
-    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one), so XCD x takes
-    // the x-th contiguous eighth of the work list in order -- the chunks active on one XCD at a time are
-    // neighbours (the same few groups / subframes), whose grid lines, channel-estimate rows and RE tables then
-    // stay in that XCD's L2 (MI355X_MICROARCH.md, workgroup dispatch; speed only, any order is correct)
-    const uint32_t n = gridDim.x, b = blockIdx.x, x = b % 8u;
-    const uint32_t it = items[MI_RM_XCD ? x * (n / 8u) + min(x, n % 8u) + b / 8u : b];
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one), so XCD x
+    // takes blocks x, x + 8, x + 16, ... of RM_XCD_BLOCK consecutive work items -- the chunks active on one XCD
+    // at a time are neighbours (the same group / subframes), whose grid lines, channel-estimate rows and RE
+    // tables then stay in that XCD's L2, while the blocks' round-robin keeps the XCDs' shares of a mixed
+    // batch balanced (contiguous eighths per XCD: configs[4]'s rm 1.2 -> 2.2 ms, one XCD holding the big
+    // cells).  The tail past the last whole round of 8 blocks keeps launch order.  Speed only: any order
+    // is correct (MI355X_MICROARCH.md, workgroup dispatch)
+    constexpr uint32_t XB = MI_RM_XCD_BLOCK;
+    const uint32_t n = gridDim.x, b = blockIdx.x, full = n / (8u * XB) * (8u * XB), j = b / 8u;
+    const uint32_t it = items[MI_RM_XCD && b < full ? ((j / XB) * 8u + b % 8u) * XB + j % XB : b];
     gi = it >> 9;
     ci = it & 511u;
   }
