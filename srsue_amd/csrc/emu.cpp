@@ -208,8 +208,13 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
                         reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li[h] % mi::LANES, ph[g]};
             }
             if (!live) continue;
-            for (uint32_t r = 0; r < mi::p2_cont_rows(K); r++)
-              cscr[mi::p2_cont_dst(K, r) * mi::LANES + lane] = mi::p2_cont_row(src, live, pos, K, r);
+            uint32_t* cq = &cscr[(size_t)(4 * K + 8) * mi::LANES];
+            for (uint32_t w = 0; w < mi::p2_cont_qwins(K); w++) {
+              uint32_t q[3 * mi::BETA_W];
+              mi::p2_cont_qwin(src, live, pos, w, q);
+              for (int i = 0; i < 3 * mi::BETA_W; i++) cq[(size_t)(3 * mi::BETA_W * w + i) * mi::LANES + lane] = q[i];
+            }
+            for (uint32_t k = 0; k < K; k++) cscr[(size_t)k * mi::LANES + lane] = mi::p2_cont_wrow(src, live, k);
           }
           for (int lane = 0; lane < mi::LANES; lane++) {
             uint32_t li[2] = {0, 0};

@@ -264,8 +264,9 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
   if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
 }
 
-// 2. the gather: a wavefront per (continuation pair, 64-row chunk), lane = continuation lane, both halves
-constexpr uint32_t CONT_ROWS = 64;
+// 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 w rows);
+// lane = continuation lane, both halves
+constexpr uint32_t CONT_QW = 8, CONT_WR = 96;
 __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __restrict__ sb,
                                                                const uint32_t* __restrict__ wm,
                                                                const float* __restrict__ scratch,
@@ -273,10 +274,10 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
                                                                const uint32_t* __restrict__ pos,
                                                                const uint32_t* __restrict__ cont,
                                                                uint32_t* __restrict__ cscr, size_t pair_u32, uint32_t K) {
-  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), R = p2_cont_rows(K);
-  const uint32_t nc = (R + CONT_ROWS - 1) / CONT_ROWS, lane = threadIdx.x % LANES;
-  for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * nc; u += gridDim.x * 4) {
-    const uint32_t p = u / nc, c = u % nc;
+  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
+  const uint32_t nqw = p2_cont_qwins(K), nqt = (nqw + CONT_QW - 1) / CONT_QW, per = nqt + (K + CONT_WR - 1) / CONT_WR;
+  for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * per; u += gridDim.x * 4) {
+    const uint32_t p = u / per, c = u % per;
     P2ContSrc s[2] = {};
     uint32_t live = 0;
 #pragma unroll
@@ -292,9 +293,19 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
       s[h].hs = g & 1u;
     }
     uint32_t* dst = cscr + (size_t)p * pair_u32;
-    const uint32_t r0 = c * CONT_ROWS, r1 = min(R, r0 + CONT_ROWS);
+    if (c < nqt) {
+      uint32_t* dq = dst + (size_t)(4 * K + 8) * LANES;
+      for (uint32_t w = c * CONT_QW; w < min(nqw, (c + 1) * CONT_QW); w++) {
+        uint32_t q[3 * BETA_W];
+        p2_cont_qwin(s, live, pos, w, q);
+#pragma unroll
+        for (int i = 0; i < 3 * BETA_W; i++) dq[(size_t)(3 * BETA_W * w + i) * LANES + lane] = q[i];
+      }
+    } else {
+      const uint32_t k0 = (c - nqt) * CONT_WR, k1 = min(K, k0 + CONT_WR);
 #pragma unroll 8
-    for (uint32_t r = r0; r < r1; r++) dst[p2_cont_dst(K, r) * LANES + lane] = p2_cont_row(s, live, pos, K, r);
+      for (uint32_t k = k0; k < k1; k++) dst[(size_t)k * LANES + lane] = p2_cont_wrow(s, live, k);
+    }
   }
 }
 

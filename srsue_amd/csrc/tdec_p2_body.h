@@ -864,33 +864,37 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
 // unmaterialised rows are the group's zero row, i.e. q = 0) and the iteration-0 extrinsic rows w; llr1,
 // checkpoints and decisions are rewritten by every iteration.  The two halves of a lane never interact,
 // so which code blocks share a continuation lane does not change any result.
-// Continuation pair layout = the pair scratch layout (w, llr1, checkpoints, q rows at (4K + 8) rows);
-// gathered rows r = 0 .. 3K + 11 are q rows, r = 3K + 12 .. 4K + 11 are w rows 0 .. K - 1.
+// Continuation pair layout = the pair scratch layout: w rows at 0, q rows at (4K + 8) rows.  The gather
+// goes by q window (12 rows: one window-mask word per source) and by w row.
 struct P2ContSrc {
   const float* sb;      // the code block's group softbuffer
   const uint32_t* wm;   // the group's window masks
   const uint32_t* scr;  // the scratch of the group's pair (w rows: packed, this code block = half hs)
   uint32_t ls, hs;      // lane in the group, half in the pair
 };
-MI_HD inline uint32_t p2_cont_rows(uint32_t K) { return 4 * K + 12; }
-MI_HD inline size_t p2_cont_dst(uint32_t K, uint32_t r) {   // u32 row of gathered row r in the pair layout
-  return r < 3 * K + 12 ? (size_t)(4 * K + 8) + r : (size_t)(r - (3 * K + 12));
-}
-MI_HD inline uint32_t p2_cont_row(const P2ContSrc (&s)[2], uint32_t live, const uint32_t* pos, uint32_t K,
-                                  uint32_t r) {
-  const uint32_t nq = 3 * K + 12;
-  if (r < nq) {
-    float v[2];
+MI_HD inline uint32_t p2_cont_qwins(uint32_t K) { return K / BETA_W + 1; }   // 3 (K + 4) q rows, incl. the tail
+// q rows 12 w .. 12 w + 11 of one continuation lane (both halves), packed
+MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uint32_t* pos, uint32_t w,
+                               uint32_t (&q)[3 * BETA_W]) {
+  uint32_t m[2];
 #pragma unroll
-    for (int h = 0; h < 2; h++)
-      v[h] = ((live >> h) & 1u) && ((s[h].wm[r / 12] >> (r % 12)) & 1u) ? s[h].sb[(size_t)pos[r] * LANES + s[h].ls]
-                                                                       : 0.0f;
-    return p2_bits(q16_pair(v[0], v[1]));
+  for (int h = 0; h < 2; h++) m[h] = ((live >> h) & 1u) ? s[h].wm[w] : 0u;
+  float v[3 * BETA_W][2];
+#pragma unroll
+  for (int i = 0; i < 3 * BETA_W; i++) {
+    const size_t row = pos[3 * BETA_W * w + i];
+#pragma unroll
+    for (int h = 0; h < 2; h++) v[i][h] = ((m[h] >> i) & 1u) ? s[h].sb[row * LANES + s[h].ls] : 0.0f;
   }
+#pragma unroll
+  for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
+}
+// w row k of one continuation lane: each half's 16-bit extrinsic from its source pair's packed row
+MI_HD inline uint32_t p2_cont_wrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t k) {
   uint32_t w[2];
 #pragma unroll
   for (int h = 0; h < 2; h++)
-    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)(r - nq) * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
+    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)k * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
   return w[0] | (w[1] << 16);
 }
 
