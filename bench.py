@@ -679,7 +679,8 @@ def dry_run(args, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    # 200 steps (~2.4 s of decoding at the headline): long enough for an outside GPU-activity sampler to see
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sf-per-gpu", type=int, default=12500, help="subframes per GPU per step")
     ap.add_argument("--pool", type=int, default=256, help="distinct synthetic subframes per rank")
@@ -783,7 +784,7 @@ def main():
     itr = None
     if args.config == 4 and args.iterating_snr > 0:
         ipool_iq, ipool_tb = make_pool(cfgs[:P], args.iterating_snr, threads, first, h)
-        isteps = max(1, min(args.steps, 5))
+        isteps = max(1, min(args.steps, 40))
         im = measure(args, cfgs, ipool_iq, ipool_tb, world, dev, isteps, 1)
         iel, (ibits, incb, iok, iits, itb, ibad), _ = reduce_over_ranks(
             im["elapsed"], [im["bits_ok"], im["batch"].n_codeblocks, im["n_ok"], int(im["its"].sum()), B, im["bad"]],
