@@ -69,7 +69,7 @@ size_t tab_span(size_t bytes) { return (std::max<size_t>(bytes, 1) + 255) & ~(si
                       tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),   \
                       tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),      \
                       tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items),         \
-                      tab(d_pairs, P.pairs)}
+                      tab(d_rmrecs, P.rm_recs), tab(d_pairs, P.pairs)}
 
 int Engine::stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t st) {
   const Plan& P = plan;
@@ -255,11 +255,11 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                       d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind, rm_items(),
-                      P.rm_busy, (uint32_t)P.rm_items.size(), compact, st);
+                      rm_recs(), P.rm_busy, (uint32_t)P.rm_items.size(), compact, st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,
-                        rm_items(), P.rm_busy, (uint32_t)P.rm_items.size(), st);
+                        rm_items(), rm_recs(), P.rm_busy, (uint32_t)P.rm_items.size(), st);
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC)) {
       launch_turbo(sb, st);

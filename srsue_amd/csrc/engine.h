@@ -56,8 +56,9 @@ struct Engine {
   // the plan's descriptor tables, packed 256-B aligned into one page-locked host buffer and copied to
   // one device arena with a single DMA per upload (the per-TTI API re-plans every call)
   DevBuf d_tables;
-  DevBuf d_rmitems;   // Plan::rm_items (view into d_tables)
+  DevBuf d_rmitems, d_rmrecs;   // Plan::rm_items, Plan::rm_recs (views into d_tables)
   const uint32_t* rm_items() const { return plan.rm_items.empty() ? nullptr : d_rmitems.as<uint32_t>(); }
+  const uint4* rm_recs() const { return plan.rm_recs.empty() ? nullptr : d_rmrecs.as<uint4>(); }
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
   hipEvent_t stage_done = nullptr;   // the last DMA out of h_stage (waited for before h_stage is rewritten)

@@ -20,12 +20,14 @@ void launch_demap(const float2* grid, const float2* ce, float* e, const MiSfDesc
 // rate de-matching + HARQ combining into the group-interleaved softbuffer (srslte_rm_turbo_rx)
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups,
-                       uint32_t max_ncb, const uint32_t* items, uint32_t n_busy, uint32_t n_items, hipStream_t st);
+                       uint32_t max_ncb, const uint32_t* items, const uint4* recs /* Plan::rm_recs */, uint32_t n_busy,
+                       uint32_t n_items, hipStream_t st);
 // demap fused into rate de-matching: LLRs computed from grid + ce inside the rm staging (no LLR stream)
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind /* Qm + 8 TM2 common to all lanes, 0 = mixed */,
-                     const uint32_t* items /* Plan::rm_items, NULL = every chunk */, uint32_t n_busy, uint32_t n_items,
+                     const uint32_t* items /* Plan::rm_items, NULL = every chunk */,
+                     const uint4* recs /* Plan::rm_recs: the busy items' folded records */, uint32_t n_busy, uint32_t n_items,
                      bool compact_ce, hipStream_t st);
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
 // window masks of the sparse softbuffer rows (which decoder inputs have a materialised row)

@@ -43,7 +43,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   has_pdsch = with_pdsch;
   cb_K = cb_n = 0;
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
-  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
   rm_busy = 0;
   rm_rep = false;
@@ -303,6 +303,11 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       for (uint32_t c = 0; c < nch; c++) (busy[c] ? rm_items : idle).push_back(((uint32_t)gi << 9) | c);
     }
     rm_busy = (uint32_t)rm_items.size();
+    rm_recs.clear();
+    for (uint32_t it : rm_items) {
+      const MiGroupDesc& g = groups[it >> 9];
+      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | ((it & 511u) << 16), (uint32_t)g.sb_off, (uint32_t)(g.sb_off >> 32)});
+    }
     rm_items.insert(rm_items.end(), idle.begin(), idle.end());
   }
   // TB -> lane lists
@@ -353,7 +358,7 @@ void Plan::build_pairs() {
 int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   if (!cb_size_valid(K) || ncb_req == 0) { set_error("invalid code block size"); return -1; }
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
-  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear();
+  groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
   rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();

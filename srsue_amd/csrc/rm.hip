@@ -26,11 +26,8 @@
 #ifndef MI_RM_IDLE_OFF
 #define MI_RM_IDLE_OFF 0
 #endif
-#ifndef MI_RM_XCD
-#define MI_RM_XCD 0   // XCD-aware work-item order (A/B switch; off: profiles/r3/ab_rm_xcd)
-#endif
-#ifndef MI_RM_XCD_BLOCK
-#define MI_RM_XCD_BLOCK 64   // work items per XCD block
+#ifndef MI_RM_RECS
+#define MI_RM_RECS 1   // one folded work-item record per workgroup (A/B switch: 0 = item -> group descriptor)
 #endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
@@ -183,7 +180,8 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
-                                                        const uint32_t* __restrict__ items) {
+                                                        const uint32_t* __restrict__ items,
+                                                        const uint4* __restrict__ recs) {
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
@@ -192,41 +190,48 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
   __shared__ uint32_t rs_ga[FUSED ? RM_NW : 1][RM_NSEG], rs_gb[FUSED ? RM_NW : 1][RM_NSEG],
       rs_ta[FUSED ? RM_NW : 1][RM_NSEG], rs_u0[FUSED ? RM_NW : 1][RM_NSEG], rs_pre[FUSED ? RM_NW : 1][RM_NSEG + 1];
-  // the work item: (group, chunk) from the planner's list of chunks with received LLRs, or the 2-D grid
-  uint32_t gi = blockIdx.y, ci = blockIdx.x;
-  if (items) {
-    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one), so XCD x
-    // takes blocks x, x + 8, x + 16, ... of RM_XCD_BLOCK consecutive work items -- the chunks active on one XCD
-    // at a time are neighbours (the same group / subframes), whose grid lines, channel-estimate rows and RE
-    // tables then stay in that XCD's L2, while the blocks' round-robin keeps the XCDs' shares of a mixed
-    // batch balanced (contiguous eighths per XCD: configs[4]'s rm 1.2 -> 2.2 ms, one XCD holding the big
-    // cells).  The tail past the last whole round of 8 blocks keeps launch order.  Speed only: any order
-    // is correct (MI355X_MICROARCH.md, workgroup dispatch)
-    constexpr uint32_t XB = MI_RM_XCD_BLOCK;
-    const uint32_t n = gridDim.x, b = blockIdx.x, full = n / (8u * XB) * (8u * XB), j = b / 8u;
-    const uint32_t it = items[MI_RM_XCD && b < full ? ((j / XB) * 8u + b % 8u) * XB + j % XB : b];
-    gi = it >> 9;
-    ci = it & 511u;
+  // the work item: (group, chunk) from the planner's work list, or the 2-D grid.  With the list, each workgroup
+  // reads one 16-B record {lane0, Ncb | chunk << 16, softbuffer offset} (Plan::rm_recs): the group descriptor
+  // is folded in, one dependent global load less at the head of every chunk's chain
+  uint32_t lane0, Ncb, ci;
+  uint64_t sb_off;
+  if (MI_RM_RECS && recs) {
+    const uint4 r = recs[blockIdx.x];
+    lane0 = r.x;
+    Ncb = r.y & 0xFFFFu;
+    ci = r.y >> 16;
+    sb_off = (uint64_t)r.z | ((uint64_t)r.w << 32);
+  } else {
+    uint32_t gi = blockIdx.y;
+    ci = blockIdx.x;
+    if (items) {
+      const uint32_t it = items[blockIdx.x];
+      gi = it >> 9;
+      ci = it & 511u;
+    }
+    const MiGroupDesc g = groups[gi];
+    lane0 = g.lane0;
+    Ncb = g.Ncb;
+    sb_off = g.sb_off;
   }
-  const MiGroupDesc g = groups[gi];
   const uint32_t pa = ci * RM_CHUNK;
-  if (pa >= g.Ncb) return;
+  if (pa >= Ncb) return;
   const uint32_t tid = threadIdx.x;
-  float* sbg = sb + g.sb_off;
-  uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb)) + pa;   // map rounded up to 256 B
+  float* sbg = sb + sb_off;
+  uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(Ncb)) + pa;   // map rounded up to 256 B
   int busy = 0;
   if (tid < LANES) {
-    const MiLaneDesc ld = lanes[g.lane0 + tid];
+    const MiLaneDesc ld = lanes[lane0 + tid];
     uint32_t j0 = 0, nr = 0;
     if (ld.valid) {
-      const uint32_t* ch = kdata + ld.rank_off + g.Ncb;
+      const uint32_t* ch = kdata + ld.rank_off + Ncb;
       const uint32_t ra = ch[pa / RM_CHUNK];
       nr = ch[pa / RM_CHUNK + 1] - ra;
       j0 = ra >= ld.r0 ? ra - ld.r0 : ra + ld.Nv - ld.r0;   // LLR index of the chunk's first rank
     }
     s_j0[tid] = j0; s_nr[tid] = nr; s_nv[tid] = ld.Nv; s_E[tid] = ld.E;
     if constexpr (FUSED) {
-      const MiLaneSrc src = fz.src[g.lane0 + tid];
+      const MiLaneSrc src = fz.src[lane0 + tid];
       s_src[tid] = src;
       s_eoff[tid] = src.eb;   // LLR index of the code block's first LLR within its subframe
     } else {
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
     busy = nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv);
     const uint64_t comb = __ballot(ld.valid && !ld.new_tb), fresh = __ballot(ld.valid && ld.new_tb);
     if (tid == 0) { s_comb = comb != 0; s_new = fresh != 0; }
-    if (ci == 0) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;   // the group's zero row
+    if (ci == 0) sbg[(size_t)Ncb * LANES + tid] = 0.0f;   // the group's zero row
   }
   if (tid < RM_CHUNK / 4) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
@@ -367,10 +372,10 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
   constexpr int NP = RM_CHUNK / RM_NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
-  const uint32_t pw = pa + NP * (uint32_t)wave, np = g.Ncb > pw ? min(g.Ncb - pw, (uint32_t)NP) : 0u;
-  const MiLaneDesc ld = lanes[g.lane0 + lane];
+  const uint32_t pw = pa + NP * (uint32_t)wave, np = Ncb > pw ? min(Ncb - pw, (uint32_t)NP) : 0u;
+  const MiLaneDesc ld = lanes[lane0 + lane];
   const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + ld.rank_off);
-  const uint32_t* ch = kdata + ld.rank_off + g.Ncb;
+  const uint32_t* ch = kdata + ld.rank_off + Ncb;
   const uint32_t ra = ld.valid ? ch[pa / RM_CHUNK] : 0;
   const uint32_t j0 = s_j0[lane], nv = ld.Nv, E = ld.E;
   const bool rep = E > nv, comb = s_comb, fresh = s_new;
@@ -475,25 +480,27 @@ static void rm_idle(float* sb, const MiGroupDesc* groups, const MiLaneDesc* lane
 
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* /*ktabs*/, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
-                       const uint32_t* items, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
+                       const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
   hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(RM_NT), 0, st, e, sb,
-                     groups, lanes, ktab_data, RmFuse{}, items);
+                     groups, lanes, ktab_data, RmFuse{}, items, items ? recs : nullptr);
 }
 
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
-                     const uint32_t* items, uint32_t n_busy, uint32_t n_items, bool compact_ce, hipStream_t st) {
+                     const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, bool compact_ce,
+                     hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
   const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise, (uint32_t)compact_ce};
 #define MI_RM_LAUNCH(...) \
-  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items)
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items, \
+                     items ? recs : nullptr)
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
