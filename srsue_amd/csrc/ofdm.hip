@@ -56,6 +56,19 @@ template <> __device__ __forceinline__ void dft<8>(float2 (&v)[8]) {
   v[3] = c_add(e3, o3); v[7] = c_sub(e3, o3);
 }
 
+// Padded LDS layout of the first stage's output: float2 index a -> a + a / 32 (one pad slot per 32).  Thread j
+// writes 8 j + r (r < 8), which with ds_write_b64's 16-lane groups and 32 banks is an 8-way conflict; the pad
+// spreads it (LDS write cycles per 2048-point FFT 1,536 -> 768, the minimum being 512; the second stage's reads
+// stay conflict-free; bank model of MI355X_MICROARCH.md 'LDS').  Only this one buffer hand-off is padded, and
+// both sides keep immediate offsets: 8 j + r -> (8 j + j / 4) + r, and j + r NB -> (j + j / 32) + r (NB + NB / 32)
+// since every NB here is a multiple of 32 -- no address registers are added (an XOR swizzle, 640 cycles,
+// needed one per access and spilled).
+#ifndef MI_OFDM_PAD
+#define MI_OFDM_PAD 1
+#endif
+constexpr int OFDM_PAD_SH = 5;
+__device__ __forceinline__ int lpad(int a) { return MI_OFDM_PAD ? a + (a >> OFDM_PAD_SH) : a; }
+
 // One Stockham stage (decimation in time): butterfly j reads x[j + r N/R], twiddles by
 // W_{Ns R}^{(j mod Ns) r}, writes y[(j / Ns) Ns R + j mod Ns + r Ns].
 // IQ sample i of a symbol: fc32, or UHD sc16 (fc32 = sc16 / 32768, exact in fp32) -- MI_DL_FLAG_IQ_SC16
@@ -76,7 +89,7 @@ __device__ __forceinline__ float2 tw_at(const float2* tw2, int t) {
   return hi ? make_float2(-w.x, -w.y) : w;
 }
 
-template <int N, int R, bool FIRST, typename IQ>
+template <int N, int R, bool FIRST, typename IQ, bool PAD_IN = false>   // PAD_IN: the input was written padded
 __device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gsrc, const float2* tw, int Ns) {
   constexpr int NB = N / R;
   constexpr int PER = (NB + 255) / 256;
@@ -87,7 +100,16 @@ __device__ __forceinline__ void fft_stage(float2* buf, const IQ* __restrict__ gs
     const int j = tid + p * 256;
     if (j < NB) {
 #pragma unroll
-      for (int r = 0; r < R; r++) v[p][r] = FIRST ? load_iq(gsrc, j + r * NB) : buf[j + r * NB];
+      for (int r = 0; r < R; r++) {
+        if constexpr (FIRST) {
+          v[p][r] = load_iq(gsrc, j + r * NB);
+        } else if constexpr (PAD_IN) {
+          static_assert(NB % (1 << OFDM_PAD_SH) == 0, "padded hand-off: NB a multiple of 32");
+          v[p][r] = buf[lpad(j) + r * lpad(NB)];
+        } else {
+          v[p][r] = buf[j + r * NB];
+        }
+      }
     }
   }
   __syncthreads();
@@ -139,8 +161,9 @@ __device__ __forceinline__ void first_stage(float2* buf, FirstIn<N>& f) {
     const int j = tid + p * 256;
     if (j < FirstIn<N>::NB) {
       dft<8>(f.v[p]);
+      const int L = lpad(j * 8);   // lpad(8 j + r) = lpad(8 j) + r for r < 8
 #pragma unroll
-      for (int r = 0; r < 8; r++) buf[j * 8 + r] = f.v[p][r];
+      for (int r = 0; r < 8; r++) buf[L + r] = f.v[p][r];
     }
   }
   __syncthreads();
@@ -149,21 +172,21 @@ __device__ __forceinline__ void first_stage(float2* buf, FirstIn<N>& f) {
 template <int N, typename IQ>
 __device__ __forceinline__ void fft_rest(float2* buf, const float2* tw) {
   if constexpr (N == 2048) {
-    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 8, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
     fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 512);
   } else if constexpr (N == 1536) {
-    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 8, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
     fft_stage<N, 3, false, IQ>(buf, nullptr, tw, 512);
   } else if constexpr (N == 1024) {
-    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 8, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
     fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 256);
   } else if constexpr (N == 512) {
-    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 8, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 64);
   } else if constexpr (N == 256) {
-    fft_stage<N, 8, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
+    fft_stage<N, 8, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 64);
   } else {
     static_assert(N == 128, "unsupported FFT size");
-    fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 32);
+    fft_stage<N, 4, false, IQ, true>(buf, nullptr, tw, 8); fft_stage<N, 4, false, IQ>(buf, nullptr, tw, 32);
   }
 }
 
@@ -179,7 +202,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI_OFDM_WAV
                                                       const MiSfDesc* __restrict__ sfs,
                                                       const uint32_t* __restrict__ list,
                                                       const float2* __restrict__ twg, uint32_t W, int per) {
-  __shared__ float2 buf[N];
+  __shared__ float2 buf[N + (MI_OFDM_PAD ? N >> OFDM_PAD_SH : 0)];
   __shared__ float2 tw[N / 2];   // half-wave table (tw_at)
   const MiSfDesc d = sfs[list[blockIdx.x]];
   for (int t = threadIdx.x; t < N / 2; t += 256) tw[t] = twg[t];
