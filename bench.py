@@ -551,7 +551,7 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     S = max(1, args.streams)
     compact = args.ce == "compact" and not args.ctrl   # --ctrl reads the batch's full channel estimates
     batches = [abi.Batch(cfgs, max_its=args.max_its, profile=True, tdec_i16=args.tdec == "i16", sched=args.sched,
-                         compact_ce=compact) for _ in range(S)]
+                         compact_ce=compact, keep_llr=args.llr_stream) for _ in range(S)]
     batch = batches[0]
     d_iq = torch.empty(2 * batch.iq_samples, dtype=torch.float32, device=dev)
     if len(pool_iq) == B and len({len(x) for x in pool_iq}) > 1:
@@ -699,6 +699,9 @@ def main():
                          "4 for the low-occupancy configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; "
                          "profiles/r2/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--llr-stream", action="store_true",
+                    help="A/B: demap writes the LLR stream and rate de-matching reads it (MI_DL_FLAG_KEEP_LLR; full "
+                         "channel estimates) instead of the fused demap")
     ap.add_argument("--share-gpu", action="store_true",
                     help="N-rank rehearsal on one GPU: every rank on GPU 0, gloo collectives (not a scaling number)")
     ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
@@ -828,7 +831,8 @@ def main():
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
-                       "channel_estimates": "full" if (args.ce == "full" or args.ctrl) else "compact",
+                       "channel_estimates": "full" if (args.ce == "full" or args.ctrl or args.llr_stream) else "compact",
+                       **({"llr_stream": True} if args.llr_stream else {}),
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(ok_all / tb_all, 6), "mean_turbo_iterations": round(its_all / tb_all, 4),
