@@ -278,6 +278,10 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
 #define MI_POS(a, t) ((uint32_t)(t))
 #define MI_PI(a, k) ((a).pi[k])
 #define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
+#elif defined(MI_TDEC_DIAG_NOPI)   // timing diagnostic only: QPP table lookups replaced by a hash (wrong results)
+#define MI_POS(a, t) ((a).pos[t])
+#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
+#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
 #elif defined(MI_TDEC_DIAG_NOTAB)   // timing diagnostic only: table lookups replaced by hashes (wrong results)
 #define MI_POS(a, t) ((((uint32_t)(t) * 40503u) >> 2) & 16383u)
 #define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
