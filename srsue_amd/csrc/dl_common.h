@@ -120,6 +120,10 @@ struct MiLaneDesc {          // one per code block (lane of a group)
   uint32_t crc24a;           // 1 when C == 1 (code-block CRC is the TB CRC24A)
   uint32_t tb;               // owning TB
   uint32_t valid;            // 0 for padding lanes of a partial group
+  // where the code block's payload bytes go (PDSCH batches): CB bytes F/8 .. are payload bytes pay_st ..
+  // (tb_kernel's copy; the packed decoder writes them there directly), up to the CB CRC and, when the code
+  // block carries it (tbcrc = 1: C == 1 or the last code block), the TB CRC
+  uint32_t pay_st, tbcrc;
   uint32_t pad;
 };
 

@@ -105,6 +105,13 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
   return r;
 }
 
+// the packed decoder writes each code block's payload run in place (tdec.hip p2_out)
+static void emu_p2_out(mi::TdecArgsP2& a, int h, uint8_t* payload, const MiLaneDesc& ld) {
+  a.cb_bytes[h] = payload + ld.pay_st - ld.F / 8;
+  a.crc24a[h] = ld.crc24a | (ld.tbcrc << 1);
+  a.to_payload = 1;
+}
+
 extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const float* llr_concat, uint32_t max_its,
                               uint8_t* payload, uint32_t* tb_ok, uint32_t* tb_its, uint32_t* cb_its) {
   for (uint32_t b = 0; b < 256; b++) {
@@ -155,11 +162,10 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.crc8 = crc8;
         a.crc8b = crc8b;
         a.dec = &dec[gA.dec_off];
-        a.cb_bytes[0] = &cbb[(size_t)li[0] * mi::CB_BYTES_STRIDE];
-        a.cb_bytes[1] = &cbb[(size_t)li[(a.live >> 1) & 1u] * mi::CB_BYTES_STRIDE];
+        for (int h = 0; h < 2; h++) emu_p2_out(a, h, payload, P.lanes[li[(a.live >> h) & 1u ? h : 0]]);
         a.K = gA.K;
         a.F[0] = l0.F; a.F[1] = paired ? l1.F : l0.F;
-        a.crc24a[0] = l0.crc24a; a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
+
         a.max_its = g_compact && max_its > 1 ? 1 : max_its; a.early_stop = 1;
         mi::TdecP2ExecHost ex;
         const mi::TdecP2Result r = mi::tdec_p2_lane(a, lane, ex);
@@ -231,9 +237,9 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
             a.crc8 = crc8; a.crc8b = crc8b;
             a.dec = cdec.data();
             for (int h = 0; h < 2; h++) {
-              a.cb_bytes[h] = &cbb[(size_t)li[h] * mi::CB_BYTES_STRIDE];
+              emu_p2_out(a, h, payload, P.lanes[li[h]]);
               a.F[h] = P.lanes[li[h]].F;
-              a.crc24a[h] = P.lanes[li[h]].crc24a;
+
             }
             a.K = K; a.max_its = max_its; a.early_stop = 1;
             mi::TdecP2ExecHost ex;
@@ -292,7 +298,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       const uint8_t* src = &cbb[(size_t)lanes[r] * mi::CB_BYTES_STRIDE + (r == 0 ? tb.F / 8 : 0)];
       buf.insert(buf.end(), src, src + mi::tb_cb_nbytes(tb, r));
     }
-    memcpy(payload + tb.pay_off, buf.data(), tb.tbs / 8);
+    if (!(g_x == 3 && g_q16)) memcpy(payload + tb.pay_off, buf.data(), tb.tbs / 8);   // p2: written in place
     // TB CRC from the decoder's per-code-block partial registers (tb_kernel's formulation)
     uint32_t crc = 0;
     for (uint32_t r = 0; r < tb.C; r++) crc ^= mi::tb_crc_term(tb, r, ctbp[lanes[r]]);

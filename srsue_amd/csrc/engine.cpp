@@ -268,7 +268,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
                 d_cbits.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(),
-                d_cblist.as<uint32_t>(), d_kdata.as<uint32_t>(), st);
+                d_cblist.as<uint32_t>(), d_kdata.as<uint32_t>(), !tb_copied, st);
     mark(6);
   } else {
     for (int i = 3; i <= 6; i++) mark(i);
@@ -358,6 +358,7 @@ uint32_t Engine::cont_max_pairs() const { return (uint32_t)((plan.lanes.size() +
 // turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts
 void Engine::launch_turbo(float* sb, hipStream_t st) {
   const Plan& P = plan;
+  tb_copied = false;
   if (use_win()) {
     uint32_t kmax = 0;
     for (const MiGroupDesc& g : P.groups) kmax = std::max(kmax, g.K);
@@ -375,20 +376,25 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
   if (tdec_crossed() == 3 && q16()) {
     // compaction needs its buffers (ensure_work sized them for this plan and max_its); without them the
     // packed decoder runs every iteration itself -- the same results either way
+    // PDSCH batches: the decoder writes the payload bytes in place (tb_kernel then only combines the CRCs)
+    const bool direct = P.has_pdsch && !P.cb_n;
+    tb_copied = direct;
     const bool cont = tdec_compact() && d_cscr.bytes >= (size_t)cont_max_pairs() * cont_pair_u32() * 4 &&
                       d_cont.bytes >= (P.lanes.size() + 1) * 4 &&
                       d_cdec.bytes >= (size_t)cont_max_pairs() * P.groups[0].K * LANES;
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                    d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), d_pairs.as<uint32_t>(),
-                   (uint32_t)(P.pairs.size() / 2), cont ? 1u : max_its, early_stop, st);
+                   (uint32_t)(P.pairs.size() / 2), cont ? 1u : max_its, early_stop, direct ? d_payload.as<uint8_t>() : nullptr,
+                   st);
     if (cont) {
       // the code blocks still failing after iteration 0, compacted into dense pairs for iterations 1 ..
       launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
                        d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                        d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
                        (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
-                       cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048, st);
+                       cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048,
+                       direct ? d_payload.as<uint8_t>() : nullptr, st);
     }
     return;
   }

@@ -42,7 +42,9 @@ void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* d
 void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes,
                     uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                     const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
-                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, hipStream_t st);
+                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop,
+                    uint8_t* payload /* PDSCH batches: payload bytes written in place; nullptr = cb_bytes rows */,
+                    hipStream_t st);
 // waterfall compaction after iteration 0 of launch_tdec_p2 (one K, early stop; tdec_p2_body.h P2ContSrc):
 // gather the CRC-failing code blocks into dense continuation pairs (cscr: max_pairs x pair_u32 words, cdec:
 // max_pairs x K x 64 bytes, cont: 1 + lanes words) and decode iterations 1 .. max_its - 1 there
@@ -50,7 +52,7 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch,
                       uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                       const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
                       uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      hipStream_t st);
+                      uint8_t* payload, hipStream_t st);
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
 void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,
@@ -63,6 +65,7 @@ void launch_cb_scatter(const float* d, float* sb, const MiGroupDesc* groups, con
 // TB assembly + CRC24A + payload packing
 void launch_tb(const uint8_t* cb_bytes, uint8_t* payload, uint32_t* tb_crc_ok, uint32_t* tb_its,
                const uint32_t* cb_its, const uint32_t* cb_tbp, const MiTbDesc* tbs, uint32_t n_tb,
-               const uint32_t* cb_list, const uint32_t* kdata, hipStream_t st);
+               const uint32_t* cb_list, const uint32_t* kdata, bool copy /* false: payload already written */,
+               hipStream_t st);
 
 }  // namespace mi

@@ -213,6 +213,17 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
           ld.crc24a = sg.C == 1 ? 1 : 0;
           ld.tb = cr.tb;
           ld.valid = 1;
+          {
+            // payload run of CB r (tb_kernel's closed form): bytes s(r) .. s(r + 1) - 1 of the TB, clipped at
+            // TBS / 8 (the last code block also carries the TB CRC)
+            const MiTbDesc& tb = tbs[cr.tb];
+            auto s_of = [&](uint32_t r) {
+              const uint32_t nm = r < tb.Cm ? r : tb.Cm;
+              return nm * (tb.Km / 8) + (r - nm) * (tb.Kp / 8) - (r ? tb.F / 8 : 0) - (tb.C > 1 ? 3 * r : 0);
+            };
+            ld.pay_st = tb.pay_off + s_of(cr.r);
+            ld.tbcrc = (sg.C == 1 || cr.r + 1 == sg.C) ? 1 : 0;
+          }
           // rank table offset: one copy per (K, F) in kdata
           ld.rank_off = 0xFFFFFFFFu;
           lanes.push_back(ld);

@@ -18,7 +18,7 @@ __global__ __launch_bounds__(64 * TB_NW) void tb_kernel(const uint8_t* __restric
                                                 const uint32_t* __restrict__ cb_tbp,
                                                 const MiTbDesc* __restrict__ tbs,
                                                 const uint32_t* __restrict__ cb_list,
-                                                const uint32_t* __restrict__ kdata) {
+                                                const uint32_t* __restrict__ kdata, uint32_t copy) {
   __shared__ uint32_t s_start[TB_MAX_C + 1], s_src[TB_MAX_C];
   const MiTbDesc t = tbs[blockIdx.x];
   const uint32_t* lanes = cb_list + t.cb_list;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(64 * TB_NW) void tb_kernel(const uint8_t* __restric
   // of TB_BATCH independent loads per lane, issued before the stores (a byte-per-iteration loop
   // serialised one load round trip per 64 bytes: 30 us for one TB)
   const uint32_t wv = tid >> 6, ln = tid & 63;
-  for (uint32_t r = wv; r < t.C; r += TB_NW) {
+  for (uint32_t r = wv; copy && r < t.C; r += TB_NW) {   // copy = 0: the packed decoder wrote the payload
     const uint32_t st0 = s_start[r], n = s_start[r + 1] - st0, src = s_src[r];
     for (uint32_t j0 = ln; j0 < n; j0 += 64u * TB_BATCH) {
       uint8_t v[TB_BATCH];
@@ -73,16 +73,16 @@ __global__ __launch_bounds__(64 * TB_NW) void tb_kernel(const uint8_t* __restric
 
 void launch_tb(const uint8_t* cb_bytes, uint8_t* payload, uint32_t* tb_crc_ok, uint32_t* tb_its, const uint32_t* cb_its,
                const uint32_t* cb_tbp, const MiTbDesc* tbs, uint32_t n_tb, const uint32_t* cb_list,
-               const uint32_t* kdata, hipStream_t st) {
+               const uint32_t* kdata, bool copy, hipStream_t st) {
   if (!n_tb) return;
   // small batches (per-TTI latency): 16 wavefronts, all code blocks of a 20 MHz TB in one round;
   // large batches: 4 wavefronts per TB, the batch itself fills the GPU (16 measured 50 % slower there)
   if (n_tb < 1024)
     hipLaunchKernelGGL(tb_kernel<16>, dim3(n_tb), dim3(1024), 0, st, cb_bytes, payload, tb_crc_ok, tb_its, cb_its,
-                       cb_tbp, tbs, cb_list, kdata);
+                       cb_tbp, tbs, cb_list, kdata, (uint32_t)copy);
   else
     hipLaunchKernelGGL(tb_kernel<4>, dim3(n_tb), dim3(256), 0, st, cb_bytes, payload, tb_crc_ok, tb_its, cb_its,
-                       cb_tbp, tbs, cb_list, kdata);
+                       cb_tbp, tbs, cb_list, kdata, (uint32_t)copy);
 }
 
 }  // namespace mi

@@ -12,7 +12,15 @@ struct TdecOut {            // per code block (lane index li) results
   uint32_t* its;            // iterations used
   uint32_t* crc_ok;         // CB CRC verdict of the last iteration
   uint32_t* tb_part;        // partial TB-CRC24A register (tb_kernel combines them)
+  uint8_t* payload;         // packed decoder, PDSCH batches: payload bytes written in place (MiLaneDesc pay_st /
+                            // pay_n), no code-block rows; nullptr = rows
 };
+// the packed decoder's output of one half: the code block's payload run, or its row; crc24a bit 1 = the code
+// block carries the TB CRC (tdec_p2_check)
+__device__ inline void p2_out(TdecArgsP2& a, int h, const TdecOut& out, uint32_t li, const MiLaneDesc& ld) {
+  a.cb_bytes[h] = out.payload ? out.payload + ld.pay_st - ld.F / 8 : out.cb_bytes + (size_t)li * CB_BYTES_STRIDE;
+  a.crc24a[h] = ld.crc24a | (ld.tbcrc << 1);
+}
 
 // crossed schedule (tdec_body.h tdec_lane_x): wave 0 = F, wave 1 = B of the same 64 code blocks
 struct TdecExecGpu {
@@ -215,13 +223,13 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.crc8 = crc8;
   a.crc8b = crc8b;
   a.dec = dec + gA.dec_off;
-  a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
-  a.cb_bytes[1] = out.cb_bytes + (size_t)((a.live & 2u) ? li[1] : li[0]) * CB_BYTES_STRIDE;
+  p2_out(a, 0, out, li[0], l0);
+  if (a.live & 2u) p2_out(a, 1, out, li[1], l1);
+  else p2_out(a, 1, out, li[0], l0);
+  a.to_payload = out.payload != nullptr;
   a.K = K;
   a.F[0] = l0.F;
   a.F[1] = paired ? l1.F : l0.F;
-  a.crc24a[0] = l0.crc24a;
-  a.crc24a[1] = paired ? l1.crc24a : l0.crc24a;
   a.max_its = max_its;
   a.early_stop = early_stop;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
@@ -239,9 +247,9 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
 void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes,
                     uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                     const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
-                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, hipStream_t st) {
+                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, uint8_t* payload, hipStream_t st) {
   if (!n_pairs) return;
-  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
                      ktab_data, pairs, max_its, early_stop);
 }
@@ -337,13 +345,12 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.crc8 = crc8;
   a.crc8b = crc8b;
   a.dec = cdec + (size_t)p * K * LANES;
-  a.cb_bytes[0] = out.cb_bytes + (size_t)li[0] * CB_BYTES_STRIDE;
-  a.cb_bytes[1] = out.cb_bytes + (size_t)li[1] * CB_BYTES_STRIDE;
+  p2_out(a, 0, out, li[0], l0);
+  p2_out(a, 1, out, li[1], l1);
+  a.to_payload = out.payload != nullptr;
   a.K = K;
   a.F[0] = l0.F;
   a.F[1] = l1.F;
-  a.crc24a[0] = l0.crc24a;
-  a.crc24a[1] = l1.crc24a;
   a.max_its = max_its;
   a.early_stop = 1;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
@@ -362,9 +369,9 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch,
                       uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                       const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
                       uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      hipStream_t st) {
+                      uint8_t* payload, hipStream_t st) {
   if (!n_groups || !max_pairs) return;
-  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   (void)hipMemsetAsync(cont, 0, 4, st);
   hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
@@ -378,7 +385,7 @@ void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* d
                  const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its, uint32_t early_stop, bool q16,
                  int crossed, hipStream_t st) {
   if (!n_groups) return;
-  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp};
+  const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, nullptr};
   if (crossed == 2 && q16) {
     hipLaunchKernelGGL(tdec_kernel_i16xr, dim3(n_groups), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,
                        ktabs, ktab_data, max_its, early_stop);

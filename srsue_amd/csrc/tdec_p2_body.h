@@ -46,8 +46,10 @@ struct TdecArgsP2 {
   const uint32_t* crc8b;  // [256] CRC24B byte table
   uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][7]
   uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
-  uint8_t* cb_bytes[2];   // each half's packed output row
-  uint32_t K, F[2], crc24a[2], max_its, early_stop;
+  uint8_t* cb_bytes[2];   // each half's packed output: byte j of the code block at cb_bytes[h][j]: its row
+  uint32_t to_payload;    // (every byte), or -- wave-uniform flag -- the TB payload (its payload bytes only)
+  uint32_t K, F[2], max_its, early_stop;
+  uint32_t crc24a[2];     // bit 0: C == 1 (CB CRC = TB CRC24A); bit 1: the code block carries the TB CRC
   uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
@@ -753,8 +755,8 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     bl[h] = a.F[h] / 8;
-    bh[h] = a.K / 8 - (a.crc24a[h] ? 0 : 3);
-    ct[h] = a.crc24a[h] ? a.crc8 : a.crc8b;
+    bh[h] = a.K / 8 - ((a.crc24a[h] & 1u) ? 0 : 3);
+    ct[h] = (a.crc24a[h] & 1u) ? a.crc8 : a.crc8b;
   }
   const bool p0 = act & 1u, p1 = (act >> 1) & 1u;
   const uint32_t nb = a.K / 8;
@@ -779,8 +781,11 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
         v0 |= (dd[8 * jj + q] & 1u) << (7 - q);
         v1 |= ((dd[8 * jj + q] >> 1) & 1u) << (7 - q);
       }
-      if (p0) a.cb_bytes[0][j] = (uint8_t)v0;
-      if (p1) a.cb_bytes[1][j] = (uint8_t)v1;
+      // payload bytes: F/8 .. the CB CRC, less the TB CRC where the code block carries it (tb_kernel's run)
+      const bool s0 = !a.to_payload || (j >= bl[0] && j < bh[0] - 3 * ((a.crc24a[0] >> 1) & 1u));
+      const bool s1 = !a.to_payload || (j >= bl[1] && j < bh[1] - 3 * ((a.crc24a[1] >> 1) & 1u));
+      if (p0 && s0) a.cb_bytes[0][j] = (uint8_t)v0;
+      if (p1 && s1) a.cb_bytes[1][j] = (uint8_t)v1;
       cb[0] = ((cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((cb[0] >> 16) ^ v0) & 0xFFu];
       cb[1] = ((cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((cb[1] >> 16) ^ v1) & 0xFFu];
       if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];
