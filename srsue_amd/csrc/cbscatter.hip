@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict
   float* sbg = sb + g.sb_off;
   for (uint32_t i = w; i < (uint32_t)SC_T; i += 4) {
     const uint32_t t = t0 + i;
-    if (t < T) sbg[(size_t)pos[t] * LANES + q] = tile[q][i];
+    if (t < T) sbg[(size_t)(MI_SB_NAT ? t : pos[t]) * LANES + q] = tile[q][i];   // dl_common.h MI_SB_NAT
   }
   if (blockIdx.x == 0) {   // every row written: the whole map materialised, plus the zero row
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb));

@@ -178,6 +178,13 @@ namespace mi {
 // receive an LLR (or must keep a HARQ history) and rewrites the map; the turbo decoder fetches
 // unmaterialised rows from the zero row (L2-resident) instead of HBM.  Punctured positions never
 // cost HBM traffic and a reset only needs the map cleared.
+// Softbuffer rows in decoder-input order (MI_SB_NAT, default): the value of circular-buffer position p lives in
+// row ipos[p] -- the decoder input index t it feeds (MiKTab::ipos_off; dummy positions have none and are never
+// materialised) -- so the turbo decoder reads rows t = 3 k + stream in sequence, with no position table on its
+// path; rate de-matching does the mapping once when it writes.  The row map stays indexed by position p.
+#ifndef MI_SB_NAT
+#define MI_SB_NAT 1
+#endif
 __host__ __device__ inline size_t sb_map_off(uint32_t Ncb) { return (size_t)(Ncb + 1) * LANES; }   // floats
 __host__ __device__ inline size_t sb_group_floats(uint32_t Ncb) {
   return sb_map_off(Ncb) + (size_t)((Ncb + 255) / 256) * LANES;

@@ -86,7 +86,7 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
   c.lmap = lmap.data();
   for (uint32_t t = 0; t < P; t++) mi::win_load_map(c, t, P, sbg, g.Ncb);
   for (uint32_t t = 0; t < P; t++)
-    mi::win_load(c, t, P, sbg, g.Ncb, kdata + kt.ipos_off, kdata + kt.pi_off, lane, ld.F);
+    mi::win_load(c, t, P, sbg, g.Ncb, kdata + (MI_SB_NAT ? kt.pos_off : kt.ipos_off), kdata + kt.pi_off, lane, ld.F);
   const uint32_t* tab = kdata + (ld.crc24a ? kt.crca_off : kt.crcb_off);
   mi::TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < max_its; it++) {
@@ -136,7 +136,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       const MiGroupDesc& g = P.groups[gi];
       float* sbg = &sb[g.sb_off];
       uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
-      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p);
+      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p,
+                                                              &P.kdata[P.ktabs[g.ktab].ipos_off]);
       const MiKTab& kt = P.ktabs[g.ktab];
       wms[gi].resize(g.K / mi::BETA_W + 1);
       for (uint32_t w = 0; w < wms[gi].size(); w++) wms[gi][w] = mi::tdec_window_mask(map, &P.kdata[kt.pos_off], w);
@@ -259,7 +260,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
     if (g_x == 3 && g_q16) break;
     float* sbg = &sb[g.sb_off];
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
-    for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p);
+    for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p,
+                                                              &P.kdata[P.ktabs[g.ktab].ipos_off]);
     const MiKTab& kt = P.ktabs[g.ktab];
     std::vector<uint32_t> wm(g.K / mi::BETA_W + 1);
     for (uint32_t w = 0; w < wm.size(); w++) wm[w] = mi::tdec_window_mask(map, &P.kdata[kt.pos_off], w);

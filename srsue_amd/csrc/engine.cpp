@@ -254,7 +254,8 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     if (fuse)
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
-                      d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind, rm_items(),
+                      d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind,
+                      rm_items(),
                       rm_recs(), P.rm_busy, (uint32_t)P.rm_items.size(), compact, st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),

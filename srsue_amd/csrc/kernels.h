@@ -25,7 +25,8 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
 // demap fused into rate de-matching: LLRs computed from grid + ce inside the rm staging (no LLR stream)
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                     const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind /* Qm + 8 TM2 common to all lanes, 0 = mixed */,
+                     const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
+                     uint32_t unit_kind /* Qm + 8 TM2 common to all lanes, 0 = mixed */,
                      const uint32_t* items /* Plan::rm_items, NULL = every chunk */,
                      const uint4* recs /* Plan::rm_recs: the busy items' folded records */, uint32_t n_busy, uint32_t n_items,
                      bool compact_ce, hipStream_t st);

@@ -317,7 +317,9 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     rm_recs.clear();
     for (uint32_t it : rm_items) {
       const MiGroupDesc& g = groups[it >> 9];
-      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | ((it & 511u) << 16), (uint32_t)g.sb_off, (uint32_t)(g.sb_off >> 32)});
+      // the softbuffer offset in units of 64 floats (every group region is a multiple: sb_group_floats)
+      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | ((it & 511u) << 16), (uint32_t)(g.sb_off / LANES),
+                                     ktabs[g.ktab].ipos_off});
     }
     rm_items.insert(rm_items.end(), idle.begin(), idle.end());
   }

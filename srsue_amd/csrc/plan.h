@@ -30,7 +30,8 @@ struct PlanData {
   // of every group included: it writes the group's zero row), then the other chunks (rm_busy items first)
   std::vector<uint32_t> rm_items;
   uint32_t rm_busy = 0;
-  // per busy item, its folded record (rm.hip): lane0, Ncb | chunk << 16, softbuffer float offset lo, hi
+  // per busy item, its folded record (rm.hip): lane0, Ncb | chunk << 16, softbuffer float offset / 64, the
+  // K table's ipos offset (dl_common.h MI_SB_NAT)
   std::vector<uint32_t> rm_recs;
   bool rm_rep = false;                    // some code block repeats LLRs (E > N_v): no compact estimates
   std::vector<MiGroupDesc> groups;

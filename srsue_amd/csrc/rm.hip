@@ -181,7 +181,8 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
                                                         const uint32_t* __restrict__ items,
-                                                        const uint4* __restrict__ recs) {
+                                                        const uint4* __restrict__ recs,
+                                                        const MiKTab* __restrict__ ktabs) {
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
@@ -191,16 +192,17 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   __shared__ uint32_t rs_ga[FUSED ? RM_NW : 1][RM_NSEG], rs_gb[FUSED ? RM_NW : 1][RM_NSEG],
       rs_ta[FUSED ? RM_NW : 1][RM_NSEG], rs_u0[FUSED ? RM_NW : 1][RM_NSEG], rs_pre[FUSED ? RM_NW : 1][RM_NSEG + 1];
   // the work item: (group, chunk) from the planner's work list, or the 2-D grid.  With the list, each workgroup
-  // reads one 16-B record {lane0, Ncb | chunk << 16, softbuffer offset} (Plan::rm_recs): the group descriptor
-  // is folded in, one dependent global load less at the head of every chunk's chain
-  uint32_t lane0, Ncb, ci;
+  // reads one 16-B record {lane0, Ncb | chunk << 16, softbuffer offset / 64, ipos offset} (Plan::rm_recs): the
+  // group descriptor is folded in, one dependent global load less at the head of every chunk's chain
+  uint32_t lane0, Ncb, ci, ipos_off;
   uint64_t sb_off;
   if (MI_RM_RECS && recs) {
     const uint4 r = recs[blockIdx.x];
     lane0 = r.x;
     Ncb = r.y & 0xFFFFu;
     ci = r.y >> 16;
-    sb_off = (uint64_t)r.z | ((uint64_t)r.w << 32);
+    sb_off = (uint64_t)r.z * LANES;
+    ipos_off = r.w;
   } else {
     uint32_t gi = blockIdx.y;
     ci = blockIdx.x;
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
     lane0 = g.lane0;
     Ncb = g.Ncb;
     sb_off = g.sb_off;
+    ipos_off = ktabs[g.ktab].ipos_off;
   }
   const uint32_t pa = ci * RM_CHUNK;
   if (pa >= Ncb) return;
@@ -381,13 +384,19 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   const bool rep = E > nv, comb = s_comb, fresh = s_new;
   // materialised-before bits of the wave's rows (wave-uniform)
   const uint32_t was_m = (uint32_t)__ballot(lane < NP && (uint32_t)lane < np && map[NP * wave + lane] != 0);
+  // the softbuffer rows of the wave's positions (dl_common.h MI_SB_NAT): lane i < NP holds ipos[pw + i], read
+  // back wave-uniform per position (dummy positions are never written)
+  const uint32_t rowv = MI_SB_NAT && (uint32_t)lane < np ? kdata[ipos_off + pw + lane] : pw + (uint32_t)lane;
+  auto row_of = [&](int i) -> size_t {
+    return MI_SB_NAT ? (size_t)(uint32_t)__builtin_amdgcn_readlane((int)rowv, i) : (size_t)(pw + i);
+  };
   int32_t rk[NP];
   float old[NP];
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     const uint32_t p = pw + i;
     rk[i] = (ld.valid && (uint32_t)i < np) ? rank[p] : -2;
-    old[i] = (((was_m >> i) & 1u) && ld.valid && !ld.new_tb) ? sbg[(size_t)p * LANES + lane] : 0.0f;
+    old[i] = (((was_m >> i) & 1u) && ld.valid && !ld.new_tb) ? sbg[row_of(i) * LANES + lane] : 0.0f;
   }
   uint32_t mat_m = 0;
 #pragma unroll
@@ -413,9 +422,9 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
     const bool mat = MI_RM_DENSE || any || (was && comb);   // row holds data after this launch
     if (mat && (MI_RM_DENSE || any || !was || fresh) && ld.valid) {
 #if MI_RM_NT
-      __builtin_nontemporal_store(v, &sbg[(size_t)p * LANES + lane]);
+      __builtin_nontemporal_store(v, &sbg[row_of(i) * LANES + lane]);
 #else
-      sbg[(size_t)p * LANES + lane] = v;
+      sbg[row_of(i) * LANES + lane] = v;
 #endif
     }
     mat_m |= (uint32_t)mat << i;
@@ -430,7 +439,8 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
 // materialised and its fresh lanes are zeroed, otherwise the row is dropped from the map.
 __global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, const MiGroupDesc* __restrict__ groups,
                                                      const MiLaneDesc* __restrict__ lanes,
-                                                     const uint32_t* __restrict__ items, uint32_t n) {
+                                                     const uint32_t* __restrict__ items, uint32_t n,
+                                                     const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t it = items[i];
@@ -458,8 +468,9 @@ __global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, co
   for (uint32_t p = 0; p < np; p++) {
     if (!map[p]) continue;
     if (!comb) { map[p] = 0; continue; }
+    const size_t row = MI_SB_NAT ? kdata[ktabs[g.ktab].ipos_off + pa + p] : pa + p;   // dl_common.h MI_SB_NAT
     for (int l = 0; l < LANES; l++)
-      if ((fresh >> l) & 1u) sbg[(size_t)(pa + p) * LANES + l] = 0.0f;
+      if ((fresh >> l) & 1u) sbg[row * LANES + l] = 0.0f;
   }
 }
 
@@ -469,38 +480,38 @@ static dim3 rm_grid(const uint32_t* items, uint32_t n_busy, uint32_t n_groups, u
   return items ? dim3(n_busy) : dim3((max_ncb + RM_CHUNK - 1) / RM_CHUNK, n_groups);
 }
 static void rm_idle(float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes, const uint32_t* items,
-                    uint32_t n_busy, uint32_t n_items, hipStream_t st) {
+                    uint32_t n_busy, uint32_t n_items, const MiKTab* ktabs, const uint32_t* kdata, hipStream_t st) {
 #if MI_RM_IDLE_OFF   // A/B only: skip the idle chunks entirely
   return;
 #endif
   if (items && n_items > n_busy)
     hipLaunchKernelGGL(rm_idle_kernel, dim3((n_items - n_busy + 255) / 256), dim3(256), 0, st, sb, groups, lanes,
-                       items + n_busy, n_items - n_busy);
+                       items + n_busy, n_items - n_busy, ktabs, kdata);
 }
 
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                       const MiKTab* /*ktabs*/, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
+                       const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
                        const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
-  rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
+  rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
   hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(RM_NT), 0, st, e, sb,
-                     groups, lanes, ktab_data, RmFuse{}, items, items ? recs : nullptr);
+                     groups, lanes, ktab_data, RmFuse{}, items, items ? recs : nullptr, ktabs);
 }
 
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                     const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
+                     const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
                      const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, bool compact_ce,
                      hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
-  rm_idle(sb, groups, lanes, items, n_busy, n_items, st);
+  rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
   const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise, (uint32_t)compact_ce};
 #define MI_RM_LAUNCH(...) \
   hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items, \
-                     items ? recs : nullptr)
+                     items ? recs : nullptr, ktabs)
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;

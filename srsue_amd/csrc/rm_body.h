@@ -32,7 +32,8 @@ MI_HD inline float rm_value(const MiLaneDesc& ld, const int32_t* rank, const flo
 // row p of a group (all lanes) with the sparse-row rule of rm_combine_kernel: the row is materialised
 // after the launch iff some lane receives an LLR there, or it was materialised and a lane combines
 MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, const float* e, float* sbg,
-                                 uint8_t* map, uint32_t p) {
+                                 uint8_t* map, uint32_t p, const uint32_t* ipos) {
+  const size_t row = MI_SB_NAT ? ipos[p] : p;   // dl_common.h MI_SB_NAT
   bool comb = false, any = false;
   for (int l = 0; l < LANES; l++) comb |= lds[l].valid && !lds[l].new_tb;
   const bool was = map[p] != 0;
@@ -42,14 +43,14 @@ MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, c
     v[l] = 0.0f;
     if (!ld.valid) continue;
     bool got;
-    const float old = (was && !ld.new_tb) ? sbg[(size_t)p * LANES + l] : 0.0f;
+    const float old = (was && !ld.new_tb) ? sbg[row * LANES + l] : 0.0f;
     v[l] = rm_value(ld, reinterpret_cast<const int32_t*>(kdata + ld.rank_off), e, old, p, &got);
     any |= got;
   }
   const bool mat = any || (was && comb);
   if (mat)
     for (int l = 0; l < LANES; l++)
-      if (lds[l].valid) sbg[(size_t)p * LANES + l] = v[l];
+      if (lds[l].valid) sbg[row * LANES + l] = v[l];
   map[p] = mat ? 1 : 0;
 }
 

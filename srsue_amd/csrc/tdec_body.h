@@ -274,7 +274,7 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
   else row_st(scr, row, lane, v, crow);
 }
 
-#if defined(MI_TDEC_DIAG_SEQ)   // timing diagnostic only: softbuffer rows read in natural order (wrong results)
+#if MI_SB_NAT || defined(MI_TDEC_DIAG_SEQ)   // rows in decoder-input order (dl_common.h MI_SB_NAT)
 #define MI_POS(a, t) ((uint32_t)(t))
 #define MI_PI(a, k) ((a).pi[k])
 #define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
@@ -318,7 +318,7 @@ MI_HD inline uint32_t wmask(const TdecArgs& a, uint32_t w) { return a.wm[w]; }
 struct PosW { uint32_t v[12]; };
 MI_HD inline PosW pos_window(const uint32_t* pos, uint32_t t0) {
   PosW P;
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(MI_TDEC_DIAG_NOTAB) && !defined(MI_TDEC_DIAG_SEQ)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MI_TDEC_DIAG_NOTAB) && !defined(MI_TDEC_DIAG_SEQ) && !MI_SB_NAT
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(4))) u4 cu4;
   cu4* q = (cu4*)(pos + t0);
@@ -332,7 +332,7 @@ MI_HD inline PosW pos_window(const uint32_t* pos, uint32_t t0) {
 #endif
   return P;
 }
-#if defined(MI_TDEC_DIAG_NOTAB) || defined(MI_TDEC_DIAG_SEQ)
+#if defined(MI_TDEC_DIAG_NOTAB) || defined(MI_TDEC_DIAG_SEQ) || MI_SB_NAT
 #define MI_POSW(a, t0) PosW{{MI_POS(a, t0), MI_POS(a, t0 + 1), MI_POS(a, t0 + 2), MI_POS(a, t0 + 3), MI_POS(a, t0 + 4), \
                              MI_POS(a, t0 + 5), MI_POS(a, t0 + 6), MI_POS(a, t0 + 7), MI_POS(a, t0 + 8), MI_POS(a, t0 + 9), \
                              MI_POS(a, t0 + 10), MI_POS(a, t0 + 11)}}

@@ -887,7 +887,7 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
   float v[3 * BETA_W][2];
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) {
-    const size_t row = pos[3 * BETA_W * w + i];
+    const size_t row = MI_SB_NAT ? 3 * BETA_W * w + i : pos[3 * BETA_W * w + i];
 #pragma unroll
     for (int h = 0; h < 2; h++) v[i][h] = ((m[h] >> i) & 1u) ? s[h].sb[row * LANES + s[h].ls] : 0.0f;
   }

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(P) void tdec_win_kernel(const float* __restrict__ s
   for (uint32_t b = t; b < 256; b += P) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
   win_load_map(c, t, P, sb + g.sb_off, g.Ncb);
   __syncthreads();
-  win_load(c, t, P, sb + g.sb_off, g.Ncb, kdata + kt.ipos_off, kdata + kt.pi_off, li % LANES, ld.F);
+  win_load(c, t, P, sb + g.sb_off, g.Ncb, kdata + (MI_SB_NAT ? kt.pos_off : kt.ipos_off), kdata + kt.pi_off, li % LANES,
+           ld.F);
   __syncthreads();
 #if MI_WIN_DIAG_STOP == 1   // timing diagnostics only (phase cut-offs, wrong outputs)
   return;

@@ -261,12 +261,36 @@ MI_HD inline void win_load_map(const WinCb& c, uint32_t t, uint32_t P, const flo
 // position-table and softbuffer loads of a batch are independent (one round trip per batch of B per
 // thread) and consecutive threads read consecutive rows.  (Gathering in decoder order -- position,
 // then map, then value: three dependent loads, B = 8 -- was 53 us of a 174 us single-subframe decode.)
+// tab = the position table pos (rows in decoder-input order, MI_SB_NAT: row t is read whatever its state and
+// kept when its position pos[t] is materialised -- the row and table loads stay independent) or ipos
 MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb,
-                           const uint32_t* ipos, const uint32_t* pi32, uint32_t lane, uint32_t F) {
+                           const uint32_t* tab, const uint32_t* pi32, uint32_t lane, uint32_t F) {
 #ifndef MI_WIN_LOAD_B
 #define MI_WIN_LOAD_B 24
 #endif
   constexpr uint32_t B = MI_WIN_LOAD_B;
+#if MI_SB_NAT
+  const uint32_t T = 3 * (c.K + 4);
+  for (uint32_t t0 = t; t0 < T; t0 += B * P) {
+    uint32_t pp[B];
+    float xx[B];
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) {
+      const uint32_t i = t0 + b * P;
+      pp[b] = i < T ? tab[i] : 0u;
+      xx[b] = i < T ? sbg[(size_t)i * LANES + lane] : 0.0f;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < B; b++) {
+      const uint32_t i = t0 + b * P;
+      if (i >= T) continue;
+      float x = c.lmap[pp[b]] ? q16f(xx[b]) : 0.0f;
+      if (i < 3 * F && i % 3 != 2) x = -I16_CI;
+      c.q[i] = (int16_t)x;
+    }
+  }
+#else
+  const uint32_t* ipos = tab;
   for (uint32_t p0 = t; p0 < Ncb; p0 += B * P) {
     uint32_t ii[B];
     float xx[B];
@@ -285,6 +309,7 @@ MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* 
       c.q[i] = (int16_t)x;
     }
   }
+#endif
   for (uint32_t k = t; k < c.K; k += P) {
     c.pi[k] = (uint16_t)pi32[k];
     c.w[k] = 0;
