@@ -89,10 +89,24 @@ struct TdecWinP2 {
   uint32_t ck[7];
 };
 
+#ifndef MI_TDEC_P2_OOB
+// 1: unmaterialised rows read out of range (0) instead of from the zero row.  Fewer SGPR spills (249 vs 334)
+// but slower: same-box A/B profiles/r3/ab_oob, tdec_kernel_p2x 6.61/6.74 ms vs 6.54/6.56 ms with the zero row.
+#define MI_TDEC_P2_OOB 0
+#endif
 MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
 MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
   const bool on = (m >> dt) & 1u;
+#if MI_SB_NAT && MI_TDEC_P2_OOB && defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+  // rows in decoder-input order (dl_common.h MI_SB_NAT): row P.v[0] + dt; an unmaterialised row reads as 0
+  // through an out-of-range VGPR offset (the range check covers the VGPR offset, not soffset: tdec_body.h
+  // sb_in) -- no zero-row select, no per-input row register
+  const uint32_t so = (P.v[0] + dt) * (uint32_t)(LANES * sizeof(float));
+  const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb[h]), vo, so, 0));
+#else
   return row_ld(a.sb[h], on ? P.v[dt] : a.zrow[h], lane);   // tdec_body.h sb_in
+#endif
 }
 
 template <bool DEC2, bool FIRST, bool SQ>
