@@ -138,6 +138,11 @@ int    mi_dl_batch_turbo_win(const mi_dl_batch_t *b);
  * max_its > 1, one code-block size; the environment variable MI_TDEC_COMPACT=0 disables it for A/B runs) */
 int    mi_dl_batch_turbo_compact(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
+/* groups whose rate de-matching runs in the direct form (every valid lane a new TB with one rank table, one
+ * k0 rank, one modulation, E <= N_v: each LLR written straight to its softbuffer row); the others gather per
+ * circular-buffer position.  The environment variable MI_RM_DIRECT=0 (read at planning) disables the direct
+ * form for A/B runs; the softbuffer is bit-identical either way. */
+uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
 
 /* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =
  * srsLTE turbodecoder_test).  n_cb code blocks of size K; decoder input per block = 3(K+4) fp32

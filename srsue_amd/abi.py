@@ -90,6 +90,7 @@ def lib():
             "mi_dl_batch_turbo_compact": (C.c_int, [vp]),
             "mi_tdec_turbo_win": (C.c_int, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
+            "mi_dl_batch_rm_direct_groups": (u32, [vp]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
             "mi_turbo_encode": (C.c_int, [vp, u32, u32, vp]),
             "mi_tdec_create": (vp, [u32, u32, u32, C.c_int, C.c_int, u32]),
@@ -288,6 +289,11 @@ class Batch:
     @property
     def n_groups(self):
         return lib().mi_dl_batch_n_groups(self.h)
+
+    @property
+    def rm_direct_groups(self):
+        """groups rate-de-matched in the direct form (rm.hip rm_direct_kernel; MI_RM_DIRECT=0 disables)"""
+        return lib().mi_dl_batch_rm_direct_groups(self.h)
 
     def payload(self, sf, all_payload=None):
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)

@@ -123,6 +123,7 @@ static int turbo_sched(const mi::Engine& e) {
 int mi_dl_batch_turbo_win(const mi_dl_batch_t* b) { return turbo_sched(b->eng); }
 int mi_dl_batch_turbo_compact(const mi_dl_batch_t* b) { return b->eng.tdec_compact() ? 1 : 0; }
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
+uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t* b) { return (uint32_t)(b->eng.plan.rm_direct.size() / 8); }
 
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */
 struct mi_tdec_batch {

@@ -36,21 +36,11 @@ __device__ __forceinline__ void demap_unit(const MiPdschDesc& pd, uint32_t u, co
                                            float* __restrict__ e, float noise) {
   if (pd.tm != 2) {
     const uint32_t r = re[u];
-    const float2 y = g[r], h = c0[r];
-    const float den = h.x * h.x + h.y * h.y + noise;
-    const float2 x = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
-    demap_store<QM>(x, scr, u * QM, e);
+    demap_store<QM>(eq_single(g[r], c0[r], noise), scr, u * QM, e);
   } else {
     const uint32_t ra = re[2 * u], rb = re[2 * u + 1];
-    const float2 r0 = g[ra], r1 = g[rb];
-    const float2 h00 = c0[ra], h01 = c0[rb], h10 = c1[ra], h11 = c1[rb];
-    float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
-    if (hh <= 0.f) hh = 1e-9f;
-    const float s = 1.41421356237309504880f / hh;
-    const float2 x0 = make_float2(s * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
-                                  s * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
-    const float2 x1 = make_float2(s * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
-                                  s * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
+    float2 x0, x1;
+    eq_sfbc(g[ra], g[rb], c0[ra], c0[rb], c1[ra], c1[rb], &x0, &x1);
     demap_store<QM>(x0, scr, 2 * u * QM, e);
     demap_store<QM>(x1, scr, (2 * u + 1) * QM, e);
   }

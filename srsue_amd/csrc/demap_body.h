@@ -7,6 +7,35 @@
 
 namespace mi {
 
+// Equalisation, shared by every path that forms LLRs (demap_kernel, the fused staging and the direct form of
+// rate de-matching, the single-LLR repetition path), so that all give the same floats.  Floating-point
+// contraction is off here: the default (fast) lets the compiler fuse a multiply into an add or not depending
+// on the surrounding code, which made two of these paths differ in the last bits; uncontracted, the
+// arithmetic is also the oracle's (plain C, no FMA).
+#if defined(__clang__)
+#define MI_FP_EXACT _Pragma("clang fp contract(off)")
+#else
+#define MI_FP_EXACT
+#endif
+// TM1 MMSE: y h* / (|h|^2 + noise)
+__device__ __forceinline__ float2 eq_single(float2 y, float2 h, float noise) {
+  MI_FP_EXACT
+  const float den = h.x * h.x + h.y * h.y + noise;
+  return make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
+}
+// TM2 SFBC (Alamouti) pair: symbols x0 (k = 0) and x1 (k = 1) of REs ra / rb
+__device__ __forceinline__ void eq_sfbc(float2 r0, float2 r1, float2 h00, float2 h01, float2 h10, float2 h11,
+                                       float2* x0, float2* x1) {
+  MI_FP_EXACT
+  float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
+  if (hh <= 0.f) hh = 1e-9f;
+  const float sc = 1.41421356237309504880f / hh;
+  *x0 = make_float2(sc * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
+                    sc * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
+  *x1 = make_float2(sc * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
+                    sc * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
+}
+
 template <int QM>
 __device__ __forceinline__ float pam_level(int lab) {
   // lab: this dimension's bits, MSB first (36.211 7.1 Gray mapping, separable I/Q)
@@ -24,6 +53,7 @@ __device__ __forceinline__ float pam_level(int lab) {
 // writes the QM/2 LLRs of one dimension at llr[0], llr[2], llr[4] (I at even, Q at odd slots)
 template <int QM>
 __device__ __forceinline__ void demap_dim(float x, float* llr) {
+  MI_FP_EXACT
   constexpr int NB = QM / 2, NL = 1 << NB;
   float d2[NL];
 #pragma unroll
@@ -46,6 +76,7 @@ __device__ __forceinline__ void demap_dim(float x, float* llr) {
 // register-array index)
 template <int QM>
 __device__ __forceinline__ float demap_bit(float x, uint32_t j) {
+  MI_FP_EXACT
   constexpr int NB = QM / 2, NL = 1 << NB;
   float d2[NL];
 #pragma unroll
@@ -78,22 +109,12 @@ __device__ __forceinline__ float demap_llr(const MiPdschDesc& pd, uint32_t gi, c
   float2 x;
   if (pd.tm != 2) {
     const uint32_t r = re[s];
-    const float2 y = g[r], h = c0[r];
-    const float den = h.x * h.x + h.y * h.y + noise;
-    x = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
+    x = eq_single(g[r], c0[r], noise);
   } else {
     const uint32_t u = s >> 1, ra = re[2 * u], rb = re[2 * u + 1];
-    const float2 r0 = g[ra], r1 = g[rb];
-    const float2 h00 = c0[ra], h01 = c0[rb], h10 = c1[ra], h11 = c1[rb];
-    float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
-    if (hh <= 0.f) hh = 1e-9f;
-    const float sc = 1.41421356237309504880f / hh;
-    if ((s & 1) == 0)
-      x = make_float2(sc * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
-                      sc * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
-    else
-      x = make_float2(sc * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
-                      sc * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
+    float2 x0, x1;
+    eq_sfbc(g[ra], g[rb], c0[ra], c0[rb], c1[ra], c1[rb], &x0, &x1);
+    x = (s & 1) == 0 ? x0 : x1;
   }
   const float v = demap_bit<QM>((b & 1) ? x.y : x.x, b >> 1);   // I: even bits, Q: odd bits
   return ((scr[gi >> 5] >> (gi & 31)) & 1u) ? -v : v;

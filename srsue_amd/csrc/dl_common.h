@@ -145,6 +145,16 @@ struct MiGroupDesc {         // one per wavefront group of <= 64 code blocks of 
   uint64_t dec_off;          // byte offset of decision bytes [K][64]
 };
 
+// a direct group of rate de-matching (rm.hip, Plan::rm_direct): what rm_direct_map_kernel needs
+struct MiRmDirect {
+  uint32_t lane0, Ncb;
+  uint32_t sb64;             // the group's softbuffer offset / 64 floats
+  uint32_t rrow_off;         // uint32 offset of the (K, F) rank -> softbuffer row table [N_v] in kdata
+  uint32_t r0, Nv;           // the lanes' common k0 rank and non-null position count
+  uint32_t emax_kind;        // largest E of the group's lanes | (Qm + 8 TM2) << 24
+  uint32_t rank_off;         // the (K, F) rank table (kdata)
+};
+
 struct MiKTab {              // per K, device resident
   uint32_t K, Ncb;
   uint32_t pos_off;          // uint32 offset: pos[3*(K+4)] circular-buffer position of d_i(k)

@@ -69,7 +69,7 @@ size_t tab_span(size_t bytes) { return (std::max<size_t>(bytes, 1) + 255) & ~(si
                       tab(d_scr, P.scr_tab), tab(d_sfs, P.sfs), tab(d_lanes, P.lanes), tab(d_lanesrc, P.lane_src),   \
                       tab(d_groups, P.groups), tab(d_ktabs, P.ktabs), tab(d_kdata, P.kdata), tab(d_tbs, P.tbs),      \
                       tab(d_cblist, P.cb_list), tab(d_fftlist, P.fft_list_flat), tab(d_rmitems, P.rm_items),         \
-                      tab(d_rmrecs, P.rm_recs), tab(d_pairs, P.pairs)}
+                      tab(d_rmrecs, P.rm_recs), tab(d_pairs, P.pairs), tab(d_rmdir, P.rm_direct)}
 
 int Engine::stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t st) {
   const Plan& P = plan;
@@ -251,6 +251,9 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                    d_pds.as<MiPdschDesc>(), d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), nsf,
                    P.max_units, noise, st);
     mark(3);
+    // the direct groups' row maps (Plan::rm_direct) before the combine kernel stages their chunks
+    launch_rm_direct_maps(sb, d_kdata.as<uint32_t>(), reinterpret_cast<const MiRmDirect*>(d_rmdir.as<uint32_t>()),
+                          (uint32_t)(P.rm_direct.size() / 8), st);
     if (fuse)
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),

@@ -58,6 +58,7 @@ struct Engine {
   // one device arena with a single DMA per upload (the per-TTI API re-plans every call)
   DevBuf d_tables;
   DevBuf d_rmitems, d_rmrecs;   // Plan::rm_items, Plan::rm_recs (views into d_tables)
+  DevBuf d_rmdir;               // Plan::rm_direct
   const uint32_t* rm_items() const { return plan.rm_items.empty() ? nullptr : d_rmitems.as<uint32_t>(); }
   const uint4* rm_recs() const { return plan.rm_recs.empty() ? nullptr : d_rmrecs.as<uint4>(); }
   void* h_stage = nullptr;

@@ -30,6 +30,8 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
                      const uint32_t* items /* Plan::rm_items, NULL = every chunk */,
                      const uint4* recs /* Plan::rm_recs: the busy items' folded records */, uint32_t n_busy, uint32_t n_items,
                      bool compact_ce, hipStream_t st);
+// row maps and zero rows of Plan::rm_direct's groups (rm.hip rm_direct_map_kernel), before the combine launch
+void launch_rm_direct_maps(float* sb, const uint32_t* ktab_data, const MiRmDirect* dgs, uint32_t ndg, hipStream_t st);
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
 // window masks of the sparse softbuffer rows (which decoder inputs have a materialised row)
 void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,

@@ -4,6 +4,7 @@
 #include "tb_body.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -45,6 +46,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
+  rm_direct.clear();
   rm_busy = 0;
   rm_rep = false;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
@@ -291,6 +293,48 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       }
     }
   }
+  // direct groups (rm.hip): every valid lane new, one rank table, one k0 rank, one unit kind, whole units, E <= N_v;
+  // their rank -> row tables (row = ipos[p] under MI_SB_NAT) into kdata.  MI_RM_DIRECT=0 in the environment
+  // sends every group through the general combine (A/B and parity tests).
+  std::vector<uint8_t> direct(groups.size(), 0);
+  std::vector<uint32_t> direct_rrow(groups.size(), 0);
+  {
+    const char* env = getenv("MI_RM_DIRECT");
+    const bool off = env && !atoi(env);
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> rrow_off;
+    for (size_t gi = 0; gi < groups.size() && !off; gi++) {
+      const MiGroupDesc& g = groups[gi];
+      const MiLaneDesc* L = &lanes[g.lane0];
+      int f = -1;
+      bool ok = true;
+      uint32_t emax = 0, kind = 0;
+      for (uint32_t q = 0; q < (uint32_t)LANES && ok; q++) {
+        if (!L[q].valid) continue;
+        const uint32_t k = lane_src[g.lane0 + q].qm + 8 * lane_src[g.lane0 + q].tm2;
+        if (f < 0) { f = (int)q; kind = k; }
+        const uint32_t U = (k & 7u) * (k >> 3 ? 2u : 1u);   // LLRs per demap unit: whole units per code block
+        ok = L[q].new_tb && L[q].E <= L[q].Nv && L[q].rank_off == L[f].rank_off && L[q].r0 == L[f].r0 &&
+             L[q].Nv == L[f].Nv && k == kind && L[q].E % U == 0 && lane_src[g.lane0 + q].eb % U == 0;
+        emax = std::max(emax, L[q].E);
+      }
+      if (!ok || f < 0) continue;
+      const MiLaneDesc& l0 = L[f];
+      const auto key = std::make_pair(g.K, l0.F);
+      auto ro = rrow_off.find(key);
+      if (ro == rrow_off.end()) {
+        const auto& rk = rank_cache[key].first;
+        std::vector<uint32_t> rrow(l0.Nv, 0u);
+        for (uint32_t p = 0; p < (uint32_t)rk.size(); p++)
+          if (rk[p] >= 0) rrow[(uint32_t)rk[p]] = MI_SB_NAT ? kdata[ktabs[g.ktab].ipos_off + p] : p;
+        ro = rrow_off.emplace(key, (uint32_t)kdata.size()).first;
+        kdata.insert(kdata.end(), rrow.begin(), rrow.end());
+      }
+      direct[gi] = 1;
+      direct_rrow[gi] = ro->second;
+      rm_direct.insert(rm_direct.end(), {g.lane0, g.Ncb, (uint32_t)(g.sb_off / LANES), ro->second, l0.r0, l0.Nv,
+                                         emax | (kind << 24), l0.rank_off});
+    }
+  }
   // rate de-matching chunks with received LLRs (rm.hip): the kernel's per-lane test
   // (nr > 0 && (E >= Nv || j0 < E || j0 + nr > Nv)) over the distinct lane parameters of each group
   {
@@ -311,15 +355,19 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
           if (nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv)) busy[c] = 1;
         }
       }
-      for (uint32_t c = 0; c < nch; c++) (busy[c] ? rm_items : idle).push_back(((uint32_t)gi << 9) | c);
+      for (uint32_t c = 0; c < nch; c++)
+        if (busy[c]) rm_items.push_back(((uint32_t)gi << 9) | c);
+        else if (!direct[gi]) idle.push_back(((uint32_t)gi << 9) | c);   // direct groups: the map kernel
     }
     rm_busy = (uint32_t)rm_items.size();
     rm_recs.clear();
     for (uint32_t it : rm_items) {
       const MiGroupDesc& g = groups[it >> 9];
       // the softbuffer offset in units of 64 floats (every group region is a multiple: sb_group_floats)
-      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | ((it & 511u) << 16), (uint32_t)(g.sb_off / LANES),
-                                     ktabs[g.ktab].ipos_off});
+      // Ncb < 2^15 (<= 18,444): bit 15 flags a direct group, whose last field is its rank -> row table
+      const bool dr = direct[it >> 9];
+      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | (dr ? 1u << 15 : 0u) | ((it & 511u) << 16),
+                                     (uint32_t)(g.sb_off / LANES), dr ? direct_rrow[it >> 9] : ktabs[g.ktab].ipos_off});
     }
     rm_items.insert(rm_items.end(), idle.begin(), idle.end());
   }
@@ -373,6 +421,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
+  rm_direct.clear();
   rm_busy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;

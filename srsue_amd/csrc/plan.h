@@ -33,6 +33,11 @@ struct PlanData {
   // per busy item, its folded record (rm.hip): lane0, Ncb | chunk << 16, softbuffer float offset / 64, the
   // K table's ipos offset (dl_common.h MI_SB_NAT)
   std::vector<uint32_t> rm_recs;
+  // direct groups (rm.hip, Plan::build): every valid lane a new TB with the same rank table, the same k0 rank
+  // and E <= N_v -- each received position gets exactly one LLR.  Their busy chunks are in rm_items (record
+  // flag: rank-driven stores), their idle chunks are not: rm_direct_map_kernel rewrites their whole row map
+  // from these records (MiRmDirect, 8 u32 each)
+  std::vector<uint32_t> rm_direct;
   bool rm_rep = false;                    // some code block repeats LLRs (E > N_v): no compact estimates
   std::vector<MiGroupDesc> groups;
   // pairs of equal-K groups for the packed two-code-blocks-per-lane turbo decoder (tdec_p2_body.h):

@@ -29,6 +29,9 @@
 #ifndef MI_RM_RECS
 #define MI_RM_RECS 1   // one folded work-item record per workgroup (A/B switch: 0 = item -> group descriptor)
 #endif
+#ifndef MI_RM_DIRECT_FORM
+#define MI_RM_DIRECT_FORM 1   // rank-driven stores for Plan::rm_direct groups (0: their records run the general combine)
+#endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
 #endif
@@ -105,24 +108,12 @@ __device__ __forceinline__ UnitIn fused_data(const RmFuse& f, const MiLaneSrc& s
   d.s1 = x.s1;
   return d;
 }
+// the U = Qm (TM1) or 2 Qm (TM2) descrambled LLRs of unit u, in LLR order
 template <int QM, bool TM2>
-__device__ __forceinline__ void fused_compute(const RmFuse& f, const UnitIn& d, uint32_t u, uint32_t ga, uint32_t gb,
-                                              uint32_t ta, float* tile) {
+__device__ __forceinline__ void fused_llrs(const RmFuse& f, const UnitIn& d, uint32_t u, float* out) {
   float2 x[2];
-  if constexpr (!TM2) {
-    const float2 y = d.r0, h = d.h00;
-    const float den = h.x * h.x + h.y * h.y + f.noise;
-    x[0] = make_float2((y.x * h.x + y.y * h.y) / den, (y.y * h.x - y.x * h.y) / den);
-  } else {
-    const float2 r0 = d.r0, r1 = d.r1, h00 = d.h00, h01 = d.h01, h10 = d.h10, h11 = d.h11;
-    float hh = h00.x * h00.x + h00.y * h00.y + h11.x * h11.x + h11.y * h11.y;
-    if (hh <= 0.f) hh = 1e-9f;
-    const float sc = 1.41421356237309504880f / hh;
-    x[0] = make_float2(sc * ((h00.x * r0.x + h00.y * r0.y) + (h11.x * r1.x + h11.y * r1.y)),
-                       sc * ((h00.x * r0.y - h00.y * r0.x) + (h11.y * r1.x - h11.x * r1.y)));
-    x[1] = make_float2(sc * (-(h10.x * r0.x + h10.y * r0.y) + (h01.x * r1.x + h01.y * r1.y)),
-                       sc * (-(h10.y * r0.x - h10.x * r0.y) + (h01.x * r1.y - h01.y * r1.x)));
-  }
+  if constexpr (!TM2) x[0] = eq_single(d.r0, d.h00, f.noise);
+  else eq_sfbc(d.r0, d.r1, d.h00, d.h01, d.h10, d.h11, &x[0], &x[1]);
   constexpr int NS = TM2 ? 2 : 1, U = QM * NS;
   float l[U];
 #pragma unroll
@@ -135,8 +126,21 @@ __device__ __forceinline__ void fused_compute(const RmFuse& f, const UnitIn& d, 
   for (int b = 0; b < U; b++) {
     const uint32_t i = bit0 + b;
     const uint32_t word = (i >> 5) == w0 ? d.s0 : d.s1;
-    const float v = ((word >> (i & 31)) & 1u) ? -l[b] : l[b];
-    if (i >= ga && i < gb) tile[ta + (i - ga)] = v;
+    out[b] = ((word >> (i & 31)) & 1u) ? -l[b] : l[b];
+  }
+}
+// ... into the tile positions of [ga, gb)
+template <int QM, bool TM2>
+__device__ __forceinline__ void fused_compute(const RmFuse& f, const UnitIn& d, uint32_t u, uint32_t ga, uint32_t gb,
+                                              uint32_t ta, float* tile) {
+  constexpr int U = QM * (TM2 ? 2 : 1);
+  float v[U];
+  fused_llrs<QM, TM2>(f, d, u, v);
+  const uint32_t bit0 = u * U;
+#pragma unroll
+  for (int b = 0; b < U; b++) {
+    const uint32_t i = bit0 + b;
+    if (i >= ga && i < gb) tile[ta + (i - ga)] = v[b];
   }
 }
 template <int QM, bool TM2>
@@ -187,6 +191,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
   __shared__ uint32_t s_comb, s_new;
+  __shared__ uint32_t s_dra, s_dnr;   // direct groups: the chunk's first rank and rank count (every lane's)
   // fused staging: per-lane sources, and per wavefront RM_NSEG (row, segment) LLR runs -> demap units
   __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
   __shared__ uint32_t rs_ga[FUSED ? RM_NW : 1][RM_NSEG], rs_gb[FUSED ? RM_NW : 1][RM_NSEG],
@@ -196,10 +201,12 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   // group descriptor is folded in, one dependent global load less at the head of every chunk's chain
   uint32_t lane0, Ncb, ci, ipos_off;
   uint64_t sb_off;
+  bool direct = false;   // a Plan::rm_direct group: r.w is its rank -> row table
   if (MI_RM_RECS && recs) {
     const uint4 r = recs[blockIdx.x];
     lane0 = r.x;
-    Ncb = r.y & 0xFFFFu;
+    Ncb = r.y & 0x7FFFu;
+    direct = MI_RM_DIRECT_FORM && ((r.y >> 15) & 1u);
     ci = r.y >> 16;
     sb_off = (uint64_t)r.z * LANES;
     ipos_off = r.w;
@@ -225,10 +232,10 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   int busy = 0;
   if (tid < LANES) {
     const MiLaneDesc ld = lanes[lane0 + tid];
-    uint32_t j0 = 0, nr = 0;
+    uint32_t j0 = 0, nr = 0, ra = 0;
     if (ld.valid) {
       const uint32_t* ch = kdata + ld.rank_off + Ncb;
-      const uint32_t ra = ch[pa / RM_CHUNK];
+      ra = ch[pa / RM_CHUNK];
       nr = ch[pa / RM_CHUNK + 1] - ra;
       j0 = ra >= ld.r0 ? ra - ld.r0 : ra + ld.Nv - ld.r0;   // LLR index of the chunk's first rank
     }
@@ -244,9 +251,13 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
     busy = nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv);
     const uint64_t comb = __ballot(ld.valid && !ld.new_tb), fresh = __ballot(ld.valid && ld.new_tb);
     if (tid == 0) { s_comb = comb != 0; s_new = fresh != 0; }
+    if (direct && fresh && tid == (uint32_t)(__ffsll((unsigned long long)fresh) - 1)) {
+      s_dra = ra;
+      s_dnr = nr;
+    }
     if (ci == 0) sbg[(size_t)Ncb * LANES + tid] = 0.0f;   // the group's zero row
   }
-  if (tid < RM_CHUNK / 4) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
+  if (tid < RM_CHUNK / 4 && !direct) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
   if (!__syncthreads_or(busy)) return;
 #if MI_RM_DIAG_PROLOGUE   // timing diagnostic only: the descriptor chain alone (wrong results)
@@ -375,6 +386,19 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
   constexpr int NP = RM_CHUNK / RM_NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
+  if (direct) {
+    // rank-driven stores: wavefront w owns tile columns (ranks s_dra + t) t = NP w .. NP w + NP - 1
+    const uint32_t t0 = NP * (uint32_t)wave, nr = s_dnr;
+    const uint32_t nt = nr > t0 ? min(nr - t0, (uint32_t)NP) : 0u;
+    const uint32_t rowv = (uint32_t)lane < nt ? kdata[ipos_off + s_dra + t0 + lane] : 0u;
+    const bool lvalid = s_E[lane] != 0u;   // valid lanes receive E > 0 LLRs
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+      const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)rowv, i);
+      if ((uint32_t)i < nt && lvalid) sbg[(size_t)row * LANES + lane] = 0.0f + tile[lane][t0 + i];
+    }
+    return;
+  }
   const uint32_t pw = pa + NP * (uint32_t)wave, np = Ncb > pw ? min(Ncb - pw, (uint32_t)NP) : 0u;
   const MiLaneDesc ld = lanes[lane0 + lane];
   const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + ld.rank_off);
@@ -402,7 +426,6 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     if ((uint32_t)i >= np) continue;   // uniform: only the group's last wavefront has np < NP
-    const uint32_t p = pw + i;
     float v = old[i];
     bool c = false;
     if (rk[i] >= 0) {
@@ -472,6 +495,41 @@ __global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, co
     for (int l = 0; l < LANES; l++)
       if ((fresh >> l) & 1u) sbg[row * LANES + l] = 0.0f;
   }
+}
+
+// ---- direct groups (Plan::rm_direct) ---------------------------------------------------------------
+// Groups whose valid lanes all start a new TB with one rank table, one k0 rank and E <= N_v: every received
+// circular-buffer position gets exactly one LLR, LLR j of every lane at rank (r0 + j) mod N_v.  Their busy
+// chunks run rm_combine_kernel's staging unchanged, then a rank-driven store phase: tile column t is rank
+// ra + t for every lane, so a wavefront reads the rows of its 32 ranks with one coalesced load of the
+// (K, F) rank -> row table and stores each as a 256-B row (0.0f + LLR; 0.0f past a lane's E, where the tile
+// holds 0) -- no rank / map loads, no ballots.  Their row maps and zero rows come from rm_direct_map_kernel
+// (materialised iff some lane receives the position), so their idle chunks need no rm_idle_kernel and no
+// stale row of an earlier plan survives.  (A lane-per-code-block form without the LDS transpose, one demap
+// unit per lane and wavefront, measured 6.6 ms against 3.85: 64 code blocks' scattered grid / estimate loads
+// per instruction, profiles/r3/ab_rm_direct.)
+// the direct groups' row maps and zero rows: RM_DIRECT_MAPB workgroups per group stride over its positions
+constexpr uint32_t RM_DIRECT_MAPB = 8;
+__global__ __launch_bounds__(256) void rm_direct_map_kernel(float* __restrict__ sb, const uint32_t* __restrict__ kdata,
+                                                           const MiRmDirect* __restrict__ dgs) {
+  const MiRmDirect d = dgs[blockIdx.x / RM_DIRECT_MAPB];
+  const uint32_t part = blockIdx.x % RM_DIRECT_MAPB;
+  float* sbg = sb + (size_t)d.sb64 * LANES;
+  if (part == 0 && threadIdx.x < LANES) sbg[(size_t)d.Ncb * LANES + threadIdx.x] = 0.0f;   // the zero row
+  uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(d.Ncb));
+  const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + d.rank_off);
+  const uint32_t emax = d.emax_kind & 0xFFFFFFu;
+  for (uint32_t p = part * 256 + threadIdx.x; p < d.Ncb; p += RM_DIRECT_MAPB * 256) {
+    const int32_t rk = rank[p];
+    uint32_t j = (uint32_t)rk + d.Nv - d.r0;   // the LLR index the position receives
+    if (j >= d.Nv) j -= d.Nv;
+    map[p] = (rk >= 0 && j < emax) ? 1 : 0;
+  }
+}
+
+void launch_rm_direct_maps(float* sb, const uint32_t* ktab_data, const MiRmDirect* dgs, uint32_t ndg, hipStream_t st) {
+  if (ndg)
+    hipLaunchKernelGGL(rm_direct_map_kernel, dim3(ndg * RM_DIRECT_MAPB), dim3(256), 0, st, sb, ktab_data, dgs);
 }
 
 // the chunk work list (busy items with the combine kernel, idle items with rm_idle_kernel), or without

@@ -123,6 +123,42 @@ def test_compact_channel_estimates_identical_softbuffer(snr):
     assert res[0][0].any()
 
 
+@pytest.mark.parametrize("snr", [30.0, 19.0])
+def test_direct_rate_dematching_identical_softbuffer(snr, monkeypatch):
+    """Direct groups of rate de-matching (Plan::rm_direct, rm.hip): groups whose lanes are all new TBs with one
+    rank table, one k0 rank, one modulation and E <= N_v store their staged LLRs rank by rank through the rank ->
+    row table, with row maps from rm_direct_map_kernel.  The softbuffer arena (every float, row-map byte and zero row) must be bit-identical to
+    the per-position gather of rm_combine_kernel (MI_RM_DIRECT=0), after one run and after a second run over
+    the first run's rows, and so payload, TB CRC and per-code-block iterations.  The batch mixes direct TM1
+    and TM2 groups (a partial one with padding lanes) with gather groups (mixed modulation, filler bits, rv 2)."""
+    cfgs = [abi.sf_cfg(**c) for c in CASES] + [abi.sf_cfg(**CASES[0]) for _ in range(8)] + \
+        [abi.sf_cfg(**CASES[1]) for _ in range(8)]
+    iqs, _ = make_subframes(cfgs, snr_db=snr, seed0=int(snr) + 11)
+    res, ndirect = [], []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("MI_RM_DIRECT", direct)
+        b = abi.Batch(cfgs, max_its=4, tdec_i16=True, compact_ce=True)
+        ndirect.append(b.rm_direct_groups)
+        flat = np.zeros(2 * b.iq_samples, np.float32)
+        for i, iq in enumerate(iqs):
+            flat[2 * b.iq_offset(i):2 * b.iq_offset(i) + len(iq)] = iq
+        d = torch.from_numpy(flat).cuda()
+        out = []
+        for _ in range(2):
+            b.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            out += [b.download(abi.BUF_SB, np.uint32), b.download(abi.BUF_PAYLOAD, np.uint8),
+                    b.download(abi.BUF_TB_CRC, np.uint32), b.download(abi.BUF_CB_ITS, np.uint32)]
+        res.append(out)
+        b.close()
+    assert ndirect[0] >= 2 and ndirect[1] == 0, ndirect
+    for a, c in zip(res[0], res[1]):
+        assert np.array_equal(a, c)
+    assert res[0][0].any()
+    if snr >= 30.0:
+        assert res[0][2].all()
+
+
 @pytest.mark.parametrize("i16,sched", DECODERS)
 @pytest.mark.parametrize("snr", [15.0, 17.5, 18.5, 19.5, 21.0])
 def test_turbo_bit_exact_on_identical_llrs(snr, i16, sched):
