@@ -259,11 +259,11 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                       d_scr.as<uint32_t>(), noise, sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                       d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb, P.unit_kind,
                       rm_items(),
-                      rm_recs(), P.rm_busy, (uint32_t)P.rm_items.size(), compact, st);
+                      rm_recs(), P.rm_busy, P.rm_dbusy, (uint32_t)P.rm_items.size(), compact, st);
     else if (mask & (1u << MI_DL_STAGE_RM))
       launch_rm_combine(d_e.as<float>(), sb, d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(),
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,
-                        rm_items(), rm_recs(), P.rm_busy, (uint32_t)P.rm_items.size(), st);
+                        rm_items(), rm_recs(), P.rm_busy, P.rm_dbusy, (uint32_t)P.rm_items.size(), st);
     mark(4);
     if (mask & (1u << MI_DL_STAGE_TDEC)) {
       launch_turbo(sb, st);

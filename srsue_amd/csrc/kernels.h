@@ -21,6 +21,7 @@ void launch_demap(const float2* grid, const float2* ce, float* e, const MiSfDesc
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups,
                        uint32_t max_ncb, const uint32_t* items, const uint4* recs /* Plan::rm_recs */, uint32_t n_busy,
+                       uint32_t n_dbusy /* Plan::rm_dbusy */,
                        uint32_t n_items, hipStream_t st);
 // demap fused into rate de-matching: LLRs computed from grid + ce inside the rm staging (no LLR stream)
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
@@ -28,7 +29,8 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
                      const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
                      uint32_t unit_kind /* Qm + 8 TM2 common to all lanes, 0 = mixed */,
                      const uint32_t* items /* Plan::rm_items, NULL = every chunk */,
-                     const uint4* recs /* Plan::rm_recs: the busy items' folded records */, uint32_t n_busy, uint32_t n_items,
+                     const uint4* recs /* Plan::rm_recs: the busy items' folded records */, uint32_t n_busy,
+                     uint32_t n_dbusy /* Plan::rm_dbusy: the leading direct-group items */, uint32_t n_items,
                      bool compact_ce, hipStream_t st);
 // row maps and zero rows of Plan::rm_direct's groups (rm.hip rm_direct_map_kernel), before the combine launch
 void launch_rm_direct_maps(float* sb, const uint32_t* ktab_data, const MiRmDirect* dgs, uint32_t ndg, hipStream_t st);

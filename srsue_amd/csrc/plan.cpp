@@ -47,7 +47,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
   rm_direct.clear();
-  rm_busy = 0;
+  rm_busy = rm_dbusy = 0;
   rm_rep = false;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
@@ -338,7 +338,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   // rate de-matching chunks with received LLRs (rm.hip): the kernel's per-lane test
   // (nr > 0 && (E >= Nv || j0 < E || j0 + nr > Nv)) over the distinct lane parameters of each group
   {
-    std::vector<uint32_t> idle;
+    std::vector<uint32_t> idle, gbusy;
     rm_items.clear();
     for (size_t gi = 0; gi < groups.size(); gi++) {
       const uint32_t Ncb = groups[gi].Ncb, nch = (Ncb + RM_CHUNK - 1) / RM_CHUNK;
@@ -356,9 +356,11 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         }
       }
       for (uint32_t c = 0; c < nch; c++)
-        if (busy[c]) rm_items.push_back(((uint32_t)gi << 9) | c);
+        if (busy[c]) (direct[gi] ? rm_items : gbusy).push_back(((uint32_t)gi << 9) | c);
         else if (!direct[gi]) idle.push_back(((uint32_t)gi << 9) | c);   // direct groups: the map kernel
     }
+    rm_dbusy = (uint32_t)rm_items.size();   // direct groups' chunks first (their own launch, rm.hip)
+    rm_items.insert(rm_items.end(), gbusy.begin(), gbusy.end());
     rm_busy = (uint32_t)rm_items.size();
     rm_recs.clear();
     for (uint32_t it : rm_items) {

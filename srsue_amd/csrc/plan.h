@@ -30,6 +30,7 @@ struct PlanData {
   // of every group included: it writes the group's zero row), then the other chunks (rm_busy items first)
   std::vector<uint32_t> rm_items;
   uint32_t rm_busy = 0;
+  uint32_t rm_dbusy = 0;                  // the leading busy items that belong to direct groups (rm_direct)
   // per busy item, its folded record (rm.hip): lane0, Ncb | chunk << 16, softbuffer float offset / 64, the
   // K table's ipos offset (dl_common.h MI_SB_NAT)
   std::vector<uint32_t> rm_recs;

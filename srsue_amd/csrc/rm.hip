@@ -32,6 +32,12 @@
 #ifndef MI_RM_DIRECT_FORM
 #define MI_RM_DIRECT_FORM 1   // rank-driven stores for Plan::rm_direct groups (0: their records run the general combine)
 #endif
+#ifndef MI_RM_DIRECT_WPE
+#define MI_RM_DIRECT_WPE 8   // 8-wavefront direct workgroups: waves per SIMD the registers must allow (8: 4 per CU)
+#endif
+#ifndef MI_RM_DIRECT_PIPE1
+#define MI_RM_DIRECT_PIPE1 1   // direct workgroups stage unit after unit (0: the 3-stage pipeline; same-box 2.34-2.40 vs 2.44-2.49 ms)
+#endif
 #ifndef MI_RM_DENSE
 #define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
 #endif
@@ -40,7 +46,7 @@ namespace mi {
 
 // workgroup shape: RM_NW wavefronts per chunk, each owning RM_CHUNK / RM_NW = 32 consecutive positions
 // in the combine and 64 / RM_NW code-block rows (2 row-segments each) in the staging
-constexpr int RM_NW = RM_CHUNK / 32, RM_NT = 64 * RM_NW, RM_NSEG = 2 * LANES / RM_NW;
+constexpr int RM_NW = RM_CHUNK / 32, RM_NT = 64 * RM_NW;
 static_assert(RM_CHUNK == 128 || RM_CHUNK == 256, "rm.hip: 128- or 256-position chunks");
 
 // Fused demap -> rate de-matching (MI_DL_FLAG_KEEP_LLR off): instead of reading the LLR stream e, the
@@ -178,35 +184,39 @@ __device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src
   }
 }
 
-// FQ / FT: the batch's common modulation order and transmission mode (FQ = 0: mixed, per-unit switch)
-template <bool FUSED, int FQ = 0, bool FT = false>
-__global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
+// FQ / FT: the batch's common modulation order and transmission mode (FQ = 0: mixed, per-unit switch).
+// NW / DIR: wavefronts per workgroup; DIR = every item is a direct group's chunk (MI_RM_DIRECT_SPLIT: those run
+// as 8-wavefront workgroups -- the same tile, each wavefront staging 8 rows and storing 16 ranks -- in a
+// launch of their own, whose instantiation carries none of the general combine's registers)
+template <bool FUSED, int FQ = 0, bool FT = false, int NW = RM_NW, bool DIR = false>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? MI_RM_DIRECT_WPE : 1) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
                                                         const uint32_t* __restrict__ items,
                                                         const uint4* __restrict__ recs,
                                                         const MiKTab* __restrict__ ktabs) {
+  constexpr int NSEG = 2 * LANES / NW;   // (row, segment) LLR runs per wavefront in the staging
   __shared__ float tile[LANES][RM_CHUNK + 1];
   __shared__ uint32_t s_j0[LANES], s_nr[LANES], s_nv[LANES], s_E[LANES];
   __shared__ uint64_t s_eoff[LANES];
   __shared__ uint32_t s_comb, s_new;
   __shared__ uint32_t s_dra, s_dnr;   // direct groups: the chunk's first rank and rank count (every lane's)
-  // fused staging: per-lane sources, and per wavefront RM_NSEG (row, segment) LLR runs -> demap units
+  // fused staging: per-lane sources, and per wavefront NSEG (row, segment) LLR runs -> demap units
   __shared__ MiLaneSrc s_src[FUSED ? LANES : 1];
-  __shared__ uint32_t rs_ga[FUSED ? RM_NW : 1][RM_NSEG], rs_gb[FUSED ? RM_NW : 1][RM_NSEG],
-      rs_ta[FUSED ? RM_NW : 1][RM_NSEG], rs_u0[FUSED ? RM_NW : 1][RM_NSEG], rs_pre[FUSED ? RM_NW : 1][RM_NSEG + 1];
+  __shared__ uint32_t rs_ga[FUSED ? NW : 1][NSEG], rs_gb[FUSED ? NW : 1][NSEG],
+      rs_ta[FUSED ? NW : 1][NSEG], rs_u0[FUSED ? NW : 1][NSEG], rs_pre[FUSED ? NW : 1][NSEG + 1];
   // the work item: (group, chunk) from the planner's work list, or the 2-D grid.  With the list, each workgroup
   // reads one 16-B record {lane0, Ncb | chunk << 16, softbuffer offset / 64, ipos offset} (Plan::rm_recs): the
   // group descriptor is folded in, one dependent global load less at the head of every chunk's chain
   uint32_t lane0, Ncb, ci, ipos_off;
   uint64_t sb_off;
-  bool direct = false;   // a Plan::rm_direct group: r.w is its rank -> row table
+  bool direct = DIR;   // a Plan::rm_direct group: r.w is its rank -> row table
   if (MI_RM_RECS && recs) {
     const uint4 r = recs[blockIdx.x];
     lane0 = r.x;
     Ncb = r.y & 0x7FFFu;
-    direct = MI_RM_DIRECT_FORM && ((r.y >> 15) & 1u);
+    direct = DIR || (MI_RM_DIRECT_FORM && ((r.y >> 15) & 1u));
     ci = r.y >> 16;
     sb_off = (uint64_t)r.z * LANES;
     ipos_off = r.w;
@@ -266,20 +276,20 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
 #endif
   // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
   // all of a wavefront's loads issued before its LDS writes
-  constexpr int ROWS = LANES / RM_NW, PER = RM_CHUNK / 64;
+  constexpr int ROWS = LANES / NW, PER = RM_CHUNK / 64;
   if constexpr (FUSED) {
     // Every LLR computed from grid + ce, one demap unit (an RE, or an SFBC RE pair: all its Qm or 2 Qm
     // LLRs, as demap_kernel computes them) per thread and step.  Wavefront w owns code-block rows
-    // l = w + RM_NW r; each row's LLR run (j0 + t) mod Nv, t < nr, clipped to [0, E), is at most two
-    // contiguous runs (row-segments); the units of the wavefront's RM_NSEG row-segments are dealt to its 64
+    // l = w + NW r; each row's LLR run (j0 + t) mod Nv, t < nr, clipped to [0, E), is at most two
+    // contiguous runs (row-segments); the units of the wavefront's NSEG row-segments are dealt to its 64
     // threads flat, so all threads work and their loads are independent.
     const uint32_t w = tid >> 6, q = tid & 63;
 #pragma unroll
     for (int r = 0; r < ROWS; r++)
-      for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + RM_NW * r][t] = 0.0f;
+      for (uint32_t t = q; t < RM_CHUNK; t += 64) tile[w + NW * r][t] = 0.0f;
     uint32_t nu = 0;
-    if (q < RM_NSEG) {
-      const uint32_t l = w + RM_NW * (q >> 1), seg = q & 1;
+    if (q < NSEG) {
+      const uint32_t l = w + NW * (q >> 1), seg = q & 1;
       const uint32_t j0 = s_j0[l], nr = s_nr[l], nv = s_nv[l], E = s_E[l];
       const uint32_t ta = seg ? nv - j0 : 0, tb = seg ? nr : (nr < nv - j0 ? nr : nv - j0);
       uint32_t ga = 0, gb = 0, u0 = 0;
@@ -295,53 +305,60 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
       }
       rs_ga[w][q] = ga; rs_gb[w][q] = gb; rs_ta[w][q] = ta; rs_u0[w][q] = u0;
     }
-    // units before each row-segment: inclusive wavefront scan of nu (lanes >= RM_NSEG contribute 0)
+    // units before each row-segment: inclusive wavefront scan of nu (lanes >= NSEG contribute 0)
     uint32_t incl = nu;
 #pragma unroll
-    for (int d = 1; d < RM_NSEG; d <<= 1) {
+    for (int d = 1; d < NSEG; d <<= 1) {
       const uint32_t t = __shfl_up(incl, d, 64);
       if (q >= (uint32_t)d) incl += t;
     }
-    if (q < RM_NSEG) rs_pre[w][q + 1] = incl;
+    if (q < NSEG) rs_pre[w][q + 1] = incl;
     if (q == 0) rs_pre[w][0] = 0;
-    const uint32_t total = __shfl(incl, RM_NSEG - 1, 64);
+    const uint32_t total = __shfl(incl, NSEG - 1, 64);
     __syncthreads();
     auto locate = [&](uint32_t fi) {   // row-segment rs with rs_pre[rs] <= fi < rs_pre[rs + 1]
-      uint32_t lo = 0, hi = RM_NSEG;
+      uint32_t lo = 0, hi = NSEG;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (rs_pre[w][mid] <= fi) lo = mid; else hi = mid;
       }
       return lo;
     };
-    if constexpr (FQ != 0) {
+    if constexpr (FQ != 0 && DIR && MI_RM_DIRECT_PIPE1) {
+      // direct 8-wavefront form (A/B): ~3 units per thread, one unit after the other; occupancy hides latency
+      for (uint32_t fi = q; fi < total; fi += 64) {
+        const uint32_t lo = locate(fi), l = w + NW * (lo >> 1);
+        fused_unit<FQ, FT>(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo],
+                           tile[l]);
+      }
+    } else if constexpr (FQ != 0) {
       // uniform modulation: three-stage software pipeline over the thread's units (fi, fi + 64, ...):
       // the RE-table / scrambling loads run two units ahead, the grid / channel-estimate loads one
       // unit ahead, so each unit's two dependent HBM round trips overlap earlier units' arithmetic
       uint32_t fi = q;
       if (fi < total) {
         uint32_t loA = locate(fi), uA = rs_u0[w][loA] + (fi - rs_pre[w][loA]);
-        UnitIn dA = fused_data<FT>(fz, s_src[w + RM_NW * (loA >> 1)], fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loA >> 1)], uA));
+        UnitIn dA = fused_data<FT>(fz, s_src[w + NW * (loA >> 1)], fused_idx<FQ, FT>(fz, s_src[w + NW * (loA >> 1)], uA));
         uint32_t loB = 0, uB = 0;
         UnitIdx iB{};
         if (fi + 64 < total) {
           loB = locate(fi + 64);
           uB = rs_u0[w][loB] + (fi + 64 - rs_pre[w][loB]);
-          iB = fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loB >> 1)], uB);
+          iB = fused_idx<FQ, FT>(fz, s_src[w + NW * (loB >> 1)], uB);
         }
         for (;; fi += 64) {
           const bool hasB = fi + 64 < total, hasC = fi + 128 < total;
           UnitIn dB{};
-          if (hasB) dB = fused_data<FT>(fz, s_src[w + RM_NW * (loB >> 1)], iB);
+          if (hasB) dB = fused_data<FT>(fz, s_src[w + NW * (loB >> 1)], iB);
           uint32_t loC = 0, uC = 0;
           UnitIdx iC{};
           if (hasC) {
             loC = locate(fi + 128);
             uC = rs_u0[w][loC] + (fi + 128 - rs_pre[w][loC]);
-            iC = fused_idx<FQ, FT>(fz, s_src[w + RM_NW * (loC >> 1)], uC);
+            iC = fused_idx<FQ, FT>(fz, s_src[w + NW * (loC >> 1)], uC);
           }
 #if !MI_RM_SKIP_UNITS   // diagnostic A/B only: staging without the demap arithmetic (wrong LLRs)
-          fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + RM_NW * (loA >> 1)]);
+          fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + NW * (loA >> 1)]);
 #endif
           if (!hasB) break;
           loA = loB; uA = uB; dA = dB;
@@ -350,7 +367,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
       }
     } else {
       for (uint32_t fi = q; fi < total; fi += 64) {
-        const uint32_t lo = locate(fi), l = w + RM_NW * (lo >> 1);
+        const uint32_t lo = locate(fi), l = w + NW * (lo >> 1);
         fused_unit_any(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo],
                        tile[l]);
       }
@@ -361,7 +378,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
     const uint32_t w = tid >> 6, q = tid & 63;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
-      const uint32_t l = w + RM_NW * r;
+      const uint32_t l = w + NW * r;
       const uint32_t nr = s_nr[l], nv = s_nv[l], E = s_E[l];
       const float* el = e + s_eoff[l];
 #pragma unroll
@@ -375,7 +392,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
 #pragma unroll
     for (int r = 0; r < ROWS; r++)
 #pragma unroll
-      for (int c = 0; c < PER; c++) tile[w + RM_NW * r][q + 64 * c] = v[r][c];
+      for (int c = 0; c < PER; c++) tile[w + NW * r][q + 64 * c] = v[r][c];
   }
   }
   __syncthreads();
@@ -384,7 +401,7 @@ __global__ __launch_bounds__(RM_NT) void rm_combine_kernel(const float* __restri
   return;
 #endif
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
-  constexpr int NP = RM_CHUNK / RM_NW;
+  constexpr int NP = RM_CHUNK / NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
   if (direct) {
     // rank-driven stores: wavefront w owns tile columns (ranks s_dra + t) t = NP w .. NP w + NP - 1
@@ -547,29 +564,62 @@ static void rm_idle(float* sb, const MiGroupDesc* groups, const MiLaneDesc* lane
                        items + n_busy, n_items - n_busy, ktabs, kdata);
 }
 
+// the direct groups' chunks lead the busy items (Plan::rm_dbusy): with MI_RM_DIRECT_SPLIT they run in their own
+// 8-wavefront launch, the general chunks after them
+#ifndef MI_RM_DIRECT_SPLIT
+#define MI_RM_DIRECT_SPLIT 1
+#endif
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
-                       const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, hipStream_t st) {
+                       const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_dbusy, uint32_t n_items,
+                       hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
-  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy, n_groups, max_ncb), dim3(RM_NT), 0, st, e, sb,
-                     groups, lanes, ktab_data, RmFuse{}, items, items ? recs : nullptr, ktabs);
+  uint32_t skip = 0;
+  if (MI_RM_DIRECT_SPLIT && items && n_dbusy) {
+    hipLaunchKernelGGL((rm_combine_kernel<false, 0, false, 8, true>), dim3(n_dbusy), dim3(512), 0, st, e, sb, groups,
+                       lanes, ktab_data, RmFuse{}, items, recs, ktabs);
+    skip = n_dbusy;
+    if (skip == n_busy) return;
+  }
+  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy - skip, n_groups, max_ncb), dim3(RM_NT), 0, st, e,
+                     sb, groups, lanes, ktab_data, RmFuse{}, items ? items + skip : nullptr,
+                     items ? recs + skip : nullptr, ktabs);
 }
 
 void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane_src, const uint32_t* re_tab,
                      const uint32_t* scr_tab, float noise, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                      const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb, uint32_t unit_kind,
-                     const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_items, bool compact_ce,
-                     hipStream_t st) {
+                     const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_dbusy, uint32_t n_items,
+                     bool compact_ce, hipStream_t st) {
   if (!n_groups) return;
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
-  const dim3 g = rm_grid(items, n_busy, n_groups, max_ncb);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise, (uint32_t)compact_ce};
+  uint32_t skip = 0;
+  if (MI_RM_DIRECT_SPLIT && items && n_dbusy) {
 #define MI_RM_LAUNCH(...) \
-  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items, \
-                     items ? recs : nullptr, ktabs)
+  hipLaunchKernelGGL((__VA_ARGS__), dim3(n_dbusy), dim3(512), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items, \
+                     recs, ktabs)
+    switch (unit_kind) {   // Qm + 8 * (TM2)
+      case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false, 8, true>); break;
+      case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false, 8, true>); break;
+      case 6: MI_RM_LAUNCH(rm_combine_kernel<true, 6, false, 8, true>); break;
+      case 10: MI_RM_LAUNCH(rm_combine_kernel<true, 2, true, 8, true>); break;
+      case 12: MI_RM_LAUNCH(rm_combine_kernel<true, 4, true, 8, true>); break;
+      case 14: MI_RM_LAUNCH(rm_combine_kernel<true, 6, true, 8, true>); break;
+      default: MI_RM_LAUNCH(rm_combine_kernel<true, 0, false, 8, true>); break;
+    }
+#undef MI_RM_LAUNCH
+    skip = n_dbusy;
+    if (skip == n_busy) return;
+  }
+  const dim3 g = rm_grid(items, n_busy - skip, n_groups, max_ncb);
+  const uint32_t* it = items ? items + skip : nullptr;
+  const uint4* rc = items ? recs + skip : nullptr;
+#define MI_RM_LAUNCH(...) \
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, it, rc, ktabs)
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
