@@ -35,6 +35,14 @@
 #ifndef MI_RM_DIRECT_WPE
 #define MI_RM_DIRECT_WPE 8   // 8-wavefront direct workgroups: waves per SIMD the registers must allow (8: 4 per CU)
 #endif
+#ifndef MI_RM_GENERAL_NW
+#define MI_RM_GENERAL_NW 8   // wavefronts per workgroup of the general (non-direct) chunks
+#endif
+#ifndef MI_RM_GENERAL_WPE
+#define MI_RM_GENERAL_WPE 6   // with 8 wavefronts: waves per SIMD its registers must allow (80 VGPRs, 3 groups per CU)
+#endif
+// same box, configs[4] mix on one stream (profiles/r3/ab_rm_split/ab_g8*): general chunks 977 us with 4-wavefront
+// groups (122 VGPRs, 4 waves per SIMD), 918 us with 8 at 6 waves per SIMD, 1,121 us at 8 (45 VGPRs spilled)
 #ifndef MI_RM_DIRECT_PIPE1
 #define MI_RM_DIRECT_PIPE1 1   // direct workgroups stage unit after unit (0: the 3-stage pipeline; same-box 2.34-2.40 vs 2.44-2.49 ms)
 #endif
@@ -46,7 +54,7 @@ namespace mi {
 
 // workgroup shape: RM_NW wavefronts per chunk, each owning RM_CHUNK / RM_NW = 32 consecutive positions
 // in the combine and 64 / RM_NW code-block rows (2 row-segments each) in the staging
-constexpr int RM_NW = RM_CHUNK / 32, RM_NT = 64 * RM_NW;
+constexpr int RM_NW = RM_CHUNK / 32;
 static_assert(RM_CHUNK == 128 || RM_CHUNK == 256, "rm.hip: 128- or 256-position chunks");
 
 // Fused demap -> rate de-matching (MI_DL_FLAG_KEEP_LLR off): instead of reading the LLR stream e, the
@@ -189,7 +197,7 @@ __device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src
 // as 8-wavefront workgroups -- the same tile, each wavefront staging 8 rows and storing 16 ranks -- in a
 // launch of their own, whose instantiation carries none of the general combine's registers)
 template <bool FUSED, int FQ = 0, bool FT = false, int NW = RM_NW, bool DIR = false>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? MI_RM_DIRECT_WPE : 1) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
+__global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_GENERAL_WPE : 1)) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
@@ -583,7 +591,8 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
     skip = n_dbusy;
     if (skip == n_busy) return;
   }
-  hipLaunchKernelGGL(rm_combine_kernel<false>, rm_grid(items, n_busy - skip, n_groups, max_ncb), dim3(RM_NT), 0, st, e,
+  hipLaunchKernelGGL((rm_combine_kernel<false, 0, false, MI_RM_GENERAL_NW>), rm_grid(items, n_busy - skip, n_groups, max_ncb),
+                     dim3(64 * MI_RM_GENERAL_NW), 0, st, e,
                      sb, groups, lanes, ktab_data, RmFuse{}, items ? items + skip : nullptr,
                      items ? recs + skip : nullptr, ktabs);
 }
@@ -619,15 +628,17 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
   const uint32_t* it = items ? items + skip : nullptr;
   const uint4* rc = items ? recs + skip : nullptr;
 #define MI_RM_LAUNCH(...) \
-  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(RM_NT), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, it, rc, ktabs)
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(64 * MI_RM_GENERAL_NW), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, \
+                     it, rc, ktabs)
+  constexpr int GNW = MI_RM_GENERAL_NW;
   switch (unit_kind) {   // Qm + 8 * (TM2)
-    case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false>); break;
-    case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false>); break;
-    case 6: MI_RM_LAUNCH(rm_combine_kernel<true, 6, false>); break;
-    case 10: MI_RM_LAUNCH(rm_combine_kernel<true, 2, true>); break;
-    case 12: MI_RM_LAUNCH(rm_combine_kernel<true, 4, true>); break;
-    case 14: MI_RM_LAUNCH(rm_combine_kernel<true, 6, true>); break;
-    default: MI_RM_LAUNCH(rm_combine_kernel<true>); break;
+    case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false, GNW>); break;
+    case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false, GNW>); break;
+    case 6: MI_RM_LAUNCH(rm_combine_kernel<true, 6, false, GNW>); break;
+    case 10: MI_RM_LAUNCH(rm_combine_kernel<true, 2, true, GNW>); break;
+    case 12: MI_RM_LAUNCH(rm_combine_kernel<true, 4, true, GNW>); break;
+    case 14: MI_RM_LAUNCH(rm_combine_kernel<true, 6, true, GNW>); break;
+    default: MI_RM_LAUNCH(rm_combine_kernel<true, 0, false, GNW>); break;
   }
 #undef MI_RM_LAUNCH
 }
