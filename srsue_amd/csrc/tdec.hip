@@ -250,8 +250,14 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
                     uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, uint8_t* payload, hipStream_t st) {
   if (!n_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
-  hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes, ktabs,
-                     ktab_data, pairs, max_its, early_stop);
+  // MI_TDEC_P2_LDS (A/B knob, bytes): unused dynamic LDS per workgroup, capping the workgroups one CU holds
+  // (e.g. 29,000 B: 5 of 160 KB) so the dispatcher spreads the pairs evenly over the CUs
+  static const size_t dyn_lds = [] {
+    const char* e = getenv("MI_TDEC_P2_LDS");
+    return e ? (size_t)atol(e) : (size_t)0;
+  }();
+  hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), dyn_lds, st, sb, wm, scratch, dec, out, groups, lanes,
+                     ktabs, ktab_data, pairs, max_its, early_stop);
 }
 
 // ---- waterfall compaction (tdec_p2_body.h P2ContSrc): one K, early stop, iteration 0 done by
