@@ -725,9 +725,13 @@ def main():
                          "inside the fused demap (MI_DL_FLAG_CE_COMPACT, identical LLRs); full = all 14 symbols")
     ap.add_argument("--streams", type=int, default=0,
                     help="workspaces / HIP streams the steps rotate over (consecutive batches overlap); 1 = serial; "
-                         "0 = auto: 1 for the headline shard (its turbo kernel already fills the GPU: +5-8 %% with 2-4), "
-                         "4 for the low-occupancy configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; "
-                         "profiles/r2/streams)")
+                         "0 = auto: 4 for the headline shard (+13-15 %%: one batch's front end and rate de-matching run "
+                         "beside the previous batch's turbo decoder; profiles/r3/ab_streams*) and for the low-occupancy "
+                         "configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; profiles/r2/streams)")
+    ap.add_argument("--iterating-streams", type=int, default=0,
+                    help="--streams of the waterfall block; 0 = auto (= --streams: its continuation holds 0.74 "
+                         "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
+                         "profiles/r3/ab_streams*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--llr-stream", action="store_true",
                     help="A/B: demap writes the LLR stream and rate de-matching reads it (MI_DL_FLAG_KEEP_LLR; full "
@@ -760,7 +764,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))                     # before anything touches the GPU
     if args.streams <= 0:
-        args.streams = 4 if args.config in (3, 5) else 3 if args.config == 1 else 1
+        args.streams = 4 if args.config in (3, 4, 5) else 3 if args.config == 1 else 1
     if args.config == 2:
         args.sf_per_gpu = 1
     elif args.config == 3 and args.sf_per_gpu == 12500:
@@ -818,15 +822,16 @@ def main():
     if args.config == 4 and args.iterating_snr > 0:
         ipool_iq, ipool_tb = make_pool(cfgs[:P], args.iterating_snr, threads, first, h)
         isteps = max(1, min(args.steps, 40))
-        im = measure(args, cfgs, ipool_iq, ipool_tb, world, dev, isteps, 1)
+        iargs = argparse.Namespace(**{**vars(args), "streams": args.iterating_streams or args.streams})
+        im = measure(iargs, cfgs, ipool_iq, ipool_tb, world, dev, isteps, 1)
         iel, (ibits, incb, iok, iits, itb, ibad), _ = reduce_over_ranks(
             im["elapsed"], [im["bits_ok"], im["batch"].n_codeblocks, im["n_ok"], int(im["its"].sum()), B, im["bad"]],
             world, dev)
         if rank == 0:
             ib = im["batch"]
-            ims = im["stage"]["tdec"]
+            ims = im["iso"][0]["tdec"] if im["iso"] else im["stage"]["tdec"]
             iach = ib.algo_bytes(4) / (ims * 1e-3) / 1e9
-            itr = {"snr_db": args.iterating_snr, "steps": isteps, "ms_per_step": round(iel / isteps * 1e3, 3),
+            itr = {"snr_db": args.iterating_snr, "steps": isteps, "streams": iargs.streams, "ms_per_step": round(iel / isteps * 1e3, 3),
                    "Mbps": round(ibits * isteps / iel / 1e6, 2),
                    "turbo_codeblocks_per_s": round(incb * isteps / iel, 1),
                    "crc_ok_rate": round(iok / itb, 6), "mean_turbo_iterations": round(iits / itb, 4),
@@ -835,7 +840,8 @@ def main():
                    "stage_ms_per_step": {k: round(v, 4) for k, v in im["stage"].items()},
                    "tdec_roofline": {"kernel": tdec_kernel_name(ib.turbo_sched), "bound": "hbm",
                                      "achieved": round(iach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": round(iach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(ims, 4)},
+                                     "frac": round(iach / HBM_PEAK_GBS, 5),
+                                     **roofline_timing(im["stage"], im["nprof"], im["iso"])},
                    "what": f"the same {B}-subframe shard at {args.iterating_snr:g} dB AWGN (turbo waterfall region, "
                            f"max_its {args.max_its}): Mbps counts CRC-OK TBs only"}
         im["batch"].close()

@@ -15,6 +15,7 @@ run c1 --config 1 --cpu-seconds 9
 run c5 --config 5 --cpu-seconds 6
 run c5_s1 --config 5 --streams 1 --no-cpu-baseline
 run c4 --cpu-seconds 9
+run c4_s1 --streams 1 --no-cpu-baseline
 run c4_gen --tdec gen --cpu-seconds 6 --iterating-snr 0
 run ul --ul --cpu-seconds 6 --steps 5 --iterating-snr 0
 echo done
