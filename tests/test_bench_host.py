@@ -37,3 +37,34 @@ def test_wave_iterations_other_schedules_have_no_pair_fields():
     w = bench.wave_iterations(FakeBatch(2, 128, sched="lanexr", compact=False), cb)
     assert "pair_max_its_hist" not in w and "continuation_pairs" not in w
     assert w["cb_its_hist"] == {1: 128}
+
+
+class FakeRunner:
+    """Counts runs; stage_ms() reports a fixed isolated duration (abi.Batch / TdecBatch profiling interface)."""
+    def __init__(self):
+        self.runs, self.resets = 0, 0
+
+    def profile_reset(self):
+        self.resets += 1
+        self.runs = 0
+
+    def stage_ms(self):
+        return {"tdec": 6.4, "rm": 2.4}, self.runs
+
+
+def test_isolated_stages_only_for_overlapped_steps(monkeypatch):
+    """--streams S > 1: the roofline divides by isolated re-runs after the timed region (one workspace alone,
+    each run synchronised), the overlapped average stays beside it; S == 1 keeps the timed region's events."""
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda dev=None: None)
+    r = FakeRunner()
+    assert bench.isolated_stages(r, None, "cpu", 1, 200) is None and r.resets == 0
+
+    def run():
+        r.runs += 1
+    st, n = bench.isolated_stages(r, run, "cpu", 4, 200)
+    assert r.resets == 1 and n == 10 and st["tdec"] == 6.4
+    assert bench.isolated_stages(r, run, "cpu", 4, 3)[1] == 3
+    t = bench.roofline_timing({"tdec": 19.3}, 200, (st, n))
+    assert t["avg_launch_ms"] == 6.4 and t["launches_averaged"] == 10
+    assert t["avg_launch_ms_overlapped"] == 19.3 and t["launches_averaged_overlapped"] == 200
+    assert bench.roofline_timing({"tdec": 6.5}, 200, None) == {"avg_launch_ms": 6.5, "launches_averaged": 200}
