@@ -168,6 +168,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.F[0] = l0.F; a.F[1] = paired ? l1.F : l0.F;
 
         a.max_its = g_compact && max_its > 1 ? 1 : max_its; a.early_stop = 1;
+        a.no_w = a.max_its == 1;   // tdec.hip tdec_kernel_p2x
         mi::TdecP2ExecHost ex;
         const mi::TdecP2Result r = mi::tdec_p2_lane(a, lane, ex);
         for (int h = 0; h < 2; h++) {
@@ -221,7 +222,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               mi::p2_cont_qwin(src, live, pos, w, q);
               for (int i = 0; i < 3 * mi::BETA_W; i++) cq[(size_t)(3 * mi::BETA_W * w + i) * mi::LANES + lane] = q[i];
             }
-            for (uint32_t k = 0; k < K; k++) cscr[(size_t)k * mi::LANES + lane] = mi::p2_cont_wrow(src, live, k);
+            for (uint32_t k = 0; k < K; k++)
+              cscr[(size_t)(K + k) * mi::LANES + lane] = mi::p2_cont_xrow(src, live, K, k);
           }
           for (int lane = 0; lane < mi::LANES; lane++) {
             uint32_t li[2] = {0, 0};

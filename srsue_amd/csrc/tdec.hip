@@ -232,6 +232,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.F[1] = paired ? l1.F : l0.F;
   a.max_its = max_its;
   a.early_stop = early_stop;
+  a.no_w = max_its == 1;   // nothing reads this launch's w rows (the continuation re-forms them)
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   const TdecP2Result r = tdec_p2_lane(a, lane, ex);
   if (ex.wave) return;
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
   if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
 }
 
-// 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 w rows);
+// 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 x2 rows);
 // lane = continuation lane, both halves
 constexpr uint32_t CONT_QW = 8, CONT_WR = 96;
 __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __restrict__ sb,
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
     } else {
       const uint32_t k0 = (c - nqt) * CONT_WR, k1 = min(K, k0 + CONT_WR);
 #pragma unroll 8
-      for (uint32_t k = k0; k < k1; k++) dst[(size_t)k * LANES + lane] = p2_cont_wrow(s, live, k);
+      for (uint32_t k = k0; k < k1; k++) dst[(size_t)(K + k) * LANES + lane] = p2_cont_xrow(s, live, K, k);
     }
   }
 }

@@ -51,6 +51,8 @@ struct TdecArgsP2 {
   uint32_t K, F[2], max_its, early_stop;
   uint32_t crc24a[2];     // bit 0: C == 1 (CB CRC = TB CRC24A); bit 1: the code block carries the TB CRC
   uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
+  uint32_t no_w;          // wave-uniform: DEC2 stores no extrinsic rows w (a one-iteration launch: nothing reads
+                          // them -- the compaction continuation re-runs DEC2 of iteration 0 instead, tdec_p2_lane)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 
@@ -239,7 +241,7 @@ MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, u
     const P2 v = MI_TDEC_P2_X2 ? p2_clamp(llr - xs, (int)I16_CX) : llr;
     row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(v), i);
   } else {
-    row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
+    if (!a.no_w) row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
     const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
     const uint32_t b0 = (ng >> 15) & 1u, b1 = ng >> 31;
     row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 1)));
@@ -832,6 +834,9 @@ template <bool CONT = false, class Exec>
 MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
+  // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
+  // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
+  if constexpr (CONT) tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
   for (uint32_t it = CONT ? 1u : 0u; it < a.max_its && active; it++) {
     constexpr uint32_t MK = MI_TDEC_MKQ_IT;
     if constexpr (CONT) {
@@ -880,8 +885,10 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
 // iteration 0 over all pairs, then gathers the code blocks whose CRC failed into dense continuation
 // pairs and runs iterations 1.. there (tdec_p2_lane<true>).  The gather builds exactly the state
 // iteration 1 reads: the packed q rows that the SRC_MKQ pass would create (window masks applied:
-// unmaterialised rows are the group's zero row, i.e. q = 0) and the iteration-0 extrinsic rows w; llr1,
-// checkpoints and decisions are rewritten by every iteration.  The two halves of a lane never interact,
+// unmaterialised rows are the group's zero row, i.e. q = 0) and the iteration-0 extrinsic rows w -- formed by
+// re-running iteration 0's DEC2 pass on the gathered iteration-0 DEC1 outputs (x2 rows), because the
+// one-iteration first launch stores no w rows (no_w: 12 KB per code block less at the headline, where no code
+// block continues); llr1, checkpoints and decisions are rewritten by every iteration.  The two halves of a lane never interact,
 // so which code blocks share a continuation lane does not change any result.
 // Continuation pair layout = the pair scratch layout: w rows at 0, q rows at (4K + 8) rows.  The gather
 // goes by q window (12 rows: one window-mask word per source) and by w row.
@@ -908,12 +915,13 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
 }
-// w row k of one continuation lane: each half's 16-bit extrinsic from its source pair's packed row
-MI_HD inline uint32_t p2_cont_wrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t k) {
+// x2 row k (the llr1 rows, at K) of one continuation lane: each half's 16-bit iteration-0 DEC1 output from its
+// source pair's packed row
+MI_HD inline uint32_t p2_cont_xrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t K, uint32_t k) {
   uint32_t w[2];
 #pragma unroll
   for (int h = 0; h < 2; h++)
-    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)k * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
+    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)(K + k) * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
   return w[0] | (w[1] << 16);
 }
 

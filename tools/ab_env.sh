@@ -9,7 +9,7 @@ shift
 mkdir -p $OUT
 for rep in 1 2; do
   for e in "$@"; do
-    tag=$(echo "$e r$rep" | tr ' =-' '___')
+    tag=$(echo "$e r$rep" | tr ' =/.-' '_____')
     if [ "$e" = "-" ]; then envs=(); else envs=($e); fi
     env "${envs[@]}" timeout -k 10 200 python3 $R/bench.py --no-cpu-baseline --iterating-snr 0 ${BENCH_ARGS:-} \
       > $OUT/$tag.json 2> $OUT/$tag.err || exit 1
