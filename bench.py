@@ -124,6 +124,24 @@ def reduce_over_ranks(elapsed, sums, world, device="cpu"):
     return max(per), [float(x) for x in s.cpu()], per
 
 
+def rank_devices(world, dev):
+    """Every rank's device identity (name, gfx arch, PCI domain:bus:device, UUID), gathered over the run's process
+    group after the timed region: a multi-GPU line shows that its N ranks ran on N distinct cards (the driver's
+    SCALE runs), a --share-gpu rehearsal that they shared one.  dev None = the CPU rehearsal (no GPU)."""
+    if dev is None:
+        me = {"device": "cpu (test-only host emulation)"}
+    else:
+        p = torch.cuda.get_device_properties(dev)
+        me = {"device": p.name, "arch": getattr(p, "gcnArchName", ""), "cuda_index": dev.index,
+              "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid)}
+    me = {"rank": dist.get_rank() if world > 1 else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **me}
+    if world == 1:
+        return [me]
+    allr = [None] * world
+    dist.all_gather_object(allr, me)
+    return allr
+
+
 def make_pool(cfgs, snr_db, threads, first=0, h=None):
     """Distinct synthetic subframes from the product's transmitter (mi_tx_subframe), CPU threads.
     Subframe g (global index) carries TB splitmix64(0x5EED0000 + g) and noise seed 0xA5A5 + g."""
@@ -308,6 +326,7 @@ def bench_codeblocks(args, world, rank, dev):
         assert np.array_equal(t.results()[0][:pool], dec[:pool]), f"stream {k} decoded differently"
     ber = float(np.mean(dec[:pool] != bits))
     elapsed, (n_all,), _ = reduce_over_ranks(elapsed, [n], world, dev)
+    devices = rank_devices(world, dev)
     if rank:
         return None
     cbps = n_all * args.steps / elapsed
@@ -324,8 +343,10 @@ def bench_codeblocks(args, world, rank, dev):
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
            "roofline": {"kernel": tdec_kernel_name(tb.turbo_sched), "bound": "hbm", "achieved": round(ach, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-                        "algorithmic_bytes_per_launch": ab, **roofline_timing(stage, nprof, iso)}}
-    if world == 1 and not args.no_cpu_baseline:
+                        "algorithmic_bytes_per_launch": ab, **roofline_timing(stage, nprof, iso)},
+           "rank_devices": devices}
+    # the CPU baseline: rank 0, after the reduction (outside the timed region), at every N
+    if not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         L, T, i16 = O.lib(), host_threads(), args.tdec == "i16"
@@ -607,6 +628,178 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
             "bad": bad, "bits_ok": bits_ok, "cb_its": cb_its, "iso": iso}
 
 
+def varied_cfgs(P, first):
+    """A pool of P distinct 20 MHz TM1 grants as a multi-UE receiver sees them (srsUE re-derives
+    the grant every TTI, phch_worker.cc:297 -> :337): per subframe an RNTI from a seeded set of 64, MCS 20-28 (64QAM,
+    36.213 Table 7.1.7.1-1) and rv 0 or (one in four) 2, all new transmissions."""
+    rng = np.random.default_rng(0x5EED5 + first)
+    rntis = [int(x) for x in rng.integers(0x003D, 0xFFF4, 64)]
+    out = []
+    for i in range(P):
+        mcs = int(rng.integers(20, 29))
+        out.append(abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=SF_CYCLE[(first + i) % 8], cfi=1, tm=1,
+                              rnti=rntis[int(rng.integers(0, 64))], rv=2 if rng.integers(0, 4) == 3 else 0,
+                              tbs=TBS_100[mcs - 2], Qm=6))
+    return out
+
+
+def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
+    """The streaming receiver with the grant re-derived every step: step i decodes list i % J (a 12,500-subframe
+    configuration, IQ buffer iqs[i % J] laid out for it).  With replan, every step's plan is BUILT from scratch on a
+    pool of `threads` host planner threads (mi_dl_plan_build, no GPU call) while earlier steps decode, then swapped
+    into the step's workspace (mi_dl_batch_replan: table upload on the step's stream) before its run; without, each
+    workspace keeps one list's plan (the static replay the headline measures).  S workspaces on S streams as in
+    measure().  Returns (elapsed, CRC-OK bits per list, replan ms on the main thread, payload mismatches)."""
+    import collections
+    S = max(1, args.streams)
+    J = len(lists)
+    # one workspace per stream; static mode needs S a multiple of J so that each stream always runs one list
+    batches = [abi.Batch(lists[k % J], max_its=args.max_its, profile=False, tdec_i16=args.tdec == "i16",
+                         sched=args.sched, compact_ce=True) for k in range(S)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    sptr = [st.cuda_stream for st in streams]
+    D = max(1, threads)
+    plans = [abi.Plan() for _ in range(D + 1)]   # D building + one ready ahead of the step that takes it
+    ex = cf.ThreadPoolExecutor(max_workers=D)
+    queue = collections.deque()                  # FIFO of (build future, plan object, list index): step i gets list i % J
+    nxt = [0]
+
+    def submit(p):
+        j = nxt[0] % J
+        nxt[0] += 1
+        queue.append((ex.submit(p.build, lists[j]), p, j))
+
+    rep_t = [0.0, 0]
+    last_list = [None] * S
+
+    def step(i):
+        b = batches[i % S]
+        if replan:
+            fut, p, j = queue.popleft()
+            fut.result()
+            t = time.perf_counter()
+            b.replan(p, sptr[i % S])
+            rep_t[0] += time.perf_counter() - t
+            rep_t[1] += 1
+            submit(p)            # the plan object now holds the previous data: rebuild it for a later step
+        else:
+            j = i % S % J
+        b.run(iqs[j].data_ptr(), sptr[i % S])
+        last_list[i % S] = j
+    try:
+        if replan:
+            for p in plans:
+                submit(p)
+        for i in range(warmup * S):
+            step(i)
+        torch.cuda.synchronize(dev)
+        rep_t[:] = [0.0, 0]
+        t0 = time.perf_counter()
+        for i in range(warmup * S, warmup * S + steps):
+            step(i)
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+    finally:
+        for fut, _, _ in queue:
+            fut.cancel()
+        ex.shutdown(wait=True)
+    bits = [0.0] * J
+    bad = 0
+    seen = set()
+    for k, b in enumerate(batches):
+        j = last_list[k]
+        if j is None or j in seen:
+            continue
+        seen.add(j)
+        crc = b.download(abi.BUF_TB_CRC, np.uint32)[:len(b.cfgs)]
+        bits[j] = float(sum(b.cfgs[i].tbs for i in range(len(crc)) if crc[i]))
+        pay = b.download(abi.BUF_PAYLOAD, np.uint8)
+        bad += sum(int(not np.array_equal(b.payload(i, pay), args._pool_tb[j][i % len(args._pool_tb[j])]))
+                   for i in range(len(crc)) if crc[i])
+    for b in batches:
+        b.close()
+    for p in plans:
+        p.close()
+    nsteps_per_list = [sum(1 for i in range(warmup * S, warmup * S + steps) if (i % J if replan else i % S % J) == j)
+                       for j in range(J)]
+    total_bits = sum(bits[j] * nsteps_per_list[j] for j in range(J))
+    return elapsed, total_bits, (rep_t[0] / max(1, rep_t[1])) * 1e3, bad, bits
+
+
+def bench_planning(args, cfgs, pool_iq, pool_tb, dev, threads, value_mbps):
+    """what planning per-TTI grants costs the batched throughput.
+    plan_ms: host build time of mi_dl_plan_build (one thread, warm caches = the lookup tables srslte_ue_dl_set_rnti
+    pregenerates; cold = the first build of a new planner) for (a) a fresh shard of varied grants (varied_cfgs) and
+    (b) configs[4]'s mixed cells, plus the default shard; then the pipelined mode (every step re-planned on host
+    threads while earlier steps decode) on the default shard -- comparable to `value` -- and on the varied grants,
+    beside the same varied workload replayed with static plans.  Reported beside value, never as value."""
+    B = len(cfgs)
+    P = len(pool_iq)
+    out = {}
+
+    def tbuild(cl, reps=3):
+        p = abi.Plan()
+        arr = abi.cfg_array(cl)
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            p.build(arr)
+            t.append((time.perf_counter() - t0) * 1e3)
+        p.close()
+        return round(t[0], 2), round(min(t[1:]), 2)
+    vpool = varied_cfgs(P, 0)
+    varied = [vpool[i % P] for i in range(B)]
+    c_head = tbuild(cfgs)
+    c_var = tbuild(varied)
+    c_mix = tbuild(config_cfgs(5, B, 0))
+    out["plan_ms"] = {"default_shard": {"cold": c_head[0], "warm": c_head[1]},
+                      "varied_grants": {"cold": c_var[0], "warm": c_var[1]},
+                      "configs4_mixed": {"cold": c_mix[0], "warm": c_mix[1]},
+                      "what": f"mi_dl_plan_build of {B} subframes on one host thread (cold: a new planner; warm: its "
+                              "caches of scrambling words / RE lists / per-K tables filled)"}
+    steps = max(4, min(args.steps, args.plan_steps))
+    D = max(1, min(args.plan_threads, threads))
+    sfl = len(pool_iq[0])
+    d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
+    iq_head = torch.empty(B * sfl, dtype=torch.float32, device=dev)
+    iq_head.view(B, sfl).copy_(d_pool[torch.arange(B, device=dev) % P])
+    del d_pool
+    args._pool_tb = [pool_tb]
+    el, bits, rep_ms, bad, _ = replan_steps(args, [abi.cfg_array(cfgs)], [iq_head], dev, steps, 1, D)
+    out["pipelined_default"] = {"Mbps": round(bits / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 3),
+                                "vs_value": round(bits / el / 1e6 / value_mbps, 4) if value_mbps else None,
+                                "replan_ms_main_thread": round(rep_ms, 3), "payload_mismatches_crc_ok": bad,
+                                "steps": steps, "planner_threads": D,
+                                "what": "the default shard with its plan rebuilt from scratch for every step on host "
+                                        "planner threads (mi_dl_plan_build) while earlier steps decode, swapped in by "
+                                        "mi_dl_batch_replan before the step's run"}
+    del iq_head
+    # varied grants: two assignments of the varied pool to the shard's positions, each with its own IQ buffer
+    vq, vt = make_pool(vpool, args.snr, threads, 0)
+    lists, iqs = [], []
+    d_pool = torch.from_numpy(np.stack(vq)).to(dev)
+    for j in range(2):
+        idx = (np.arange(B) + 37 * j) % P
+        lists.append(abi.cfg_array([vpool[i] for i in idx]))
+        buf = torch.empty(B * sfl, dtype=torch.float32, device=dev)
+        buf.view(B, sfl).copy_(d_pool[torch.from_numpy(idx).to(dev)])
+        iqs.append(buf)
+    del d_pool
+    args._pool_tb = [[vt[i] for i in (np.arange(B) + 37 * j) % P] for j in range(2)]
+    el_s, bits_s, _, bad_s, per_s = replan_steps(args, lists, iqs, dev, steps, 1, D, replan=False)
+    el_p, bits_p, rep_p, bad_p, per_p = replan_steps(args, lists, iqs, dev, steps, 1, D, replan=True)
+    out["varied_static"] = {"Mbps": round(bits_s / el_s / 1e6, 2), "ms_per_step": round(el_s / steps * 1e3, 3),
+                            "crc_ok_bits_per_list": per_s, "payload_mismatches_crc_ok": bad_s}
+    out["pipelined_varied"] = {"Mbps": round(bits_p / el_p / 1e6, 2), "ms_per_step": round(el_p / steps * 1e3, 3),
+                               "vs_static": round((bits_p / el_p) / (bits_s / el_s), 4) if bits_s else None,
+                               "replan_ms_main_thread": round(rep_p, 3), "payload_mismatches_crc_ok": bad_p,
+                               "crc_ok_bits_per_list": per_p, "steps": steps, "planner_threads": D,
+                               "what": f"{B} subframes of varied grants (varied_cfgs: 64 RNTIs, MCS 20-28, rv 0/2), two "
+                                       "alternating assignments, every step re-planned on host threads"}
+    del iqs
+    return out
+
+
 def isolated_stages(runner, run_once, dev, S, steps):
     """With --streams S > 1 the timed steps overlap, so the per-stage HIP-event durations of the timed region
     include other streams' kernels sharing the GPU and are not per-kernel figures.  After the
@@ -699,11 +892,18 @@ def dry_run(args, world, rank):
     dist.all_gather_object(shards, [first, n, good])
     elapsed, (n_ok, n_cb, its_sum, n_bad), per = reduce_over_ranks(
         elapsed, [int(ok.sum()), n, int(its.sum()), n - good], world)
+    devices = rank_devices(world, None)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "shards": shards, "crc_ok": n_ok, "subframes": n_cb,
-                          "crc_ok_rate": n_ok / n_cb, "mean_turbo_iterations": its_sum / n_cb,
-                          "payload_mismatches": n_bad, "elapsed_max_s": elapsed, "elapsed_per_rank_s": per}),
-              flush=True)
+        out = {"dry_run": True, "n_gpus": world, "shards": shards, "crc_ok": n_ok, "subframes": n_cb,
+               "crc_ok_rate": n_ok / n_cb, "mean_turbo_iterations": its_sum / n_cb, "payload_mismatches": n_bad,
+               "elapsed_max_s": elapsed, "elapsed_per_rank_s": per, "rank_devices": devices}
+        if not args.no_cpu_baseline:   # the same rank-0 baseline leg as the GPU line, on this rank's subframes
+            iq = [abi.tx_subframe(c, tb_payload(first + i, c.tbs // 8), snr_db=30.0, seed=0xA5A5 + first + i)
+                  for i, c in enumerate(cfgs)]
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs, iq,
+                                               [tb_payload(first + i, c.tbs // 8) for i, c in enumerate(cfgs)],
+                                               "6-PRB rehearsal subframes", True)
+        print(json.dumps(out), flush=True)
 
 
 def main():
@@ -733,6 +933,10 @@ def main():
                          "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
                          "profiles/r3/ab_streams*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plan-steps", type=int, default=40,
+                    help="default config: steps of the planning block (per-step re-planning on host threads, VERDICT r3 "
+                         "item 3); 0 = skip the block")
+    ap.add_argument("--plan-threads", type=int, default=4, help="host planner threads of the pipelined mode")
     ap.add_argument("--llr-stream", action="store_true",
                     help="A/B: demap writes the LLR stream and rate de-matching reads it (MI_DL_FLAG_KEEP_LLR; full "
                          "channel estimates) instead of the fused demap")
@@ -817,6 +1021,7 @@ def main():
     # global counters: CRC-OK bits, code blocks, CRC-OK TBs, TB iterations, TBs, payload mismatches (every rank)
     elapsed, (bits_all, ncb_all, ok_all, its_all, tb_all, bad_all), per_rank = reduce_over_ranks(
         elapsed, [bits_ok, batch.n_codeblocks, n_ok, int(its.sum()), B, bad], world, dev)
+    devices = rank_devices(world, dev)
     # the same shard in the turbo decoder's waterfall region (every code block iterates): reported beside value
     itr = None
     if args.config == 4 and args.iterating_snr > 0:
@@ -873,7 +1078,7 @@ def main():
             "turbo_codeblocks_per_s": round(cbps, 1),
             "crc_ok_rate": round(ok_all / tb_all, 6), "mean_turbo_iterations": round(its_all / tb_all, 4),
             "payload_mismatches_crc_ok": int(bad_all), "subframes_all_ranks": int(tb_all),
-            "elapsed_per_rank_s": [round(x, 6) for x in per_rank],
+            "elapsed_per_rank_s": [round(x, 6) for x in per_rank], "rank_devices": devices,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": tdec_kernel_name(batch.turbo_sched), "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -884,13 +1089,15 @@ def main():
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
         if itr:
             out["iterating"] = itr
+        if args.config == 4 and args.plan_steps > 0 and world == 1:
+            out["planning"] = bench_planning(args, cfgs, pool_iq, pool_tb, dev, threads, mbps)
         if args.ctrl:
             out["ctrl"] = bench_ctrl(args, batch, dev)
         if args.ul:
             out["ul"] = bench_ul(args, B, dev)
         if args.sync:
             out["sync"] = bench_sync(args, batch, dev)
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:   # rank 0 at every N, after the reduction (outside the timed region)
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
                                                args.tdec == "i16")
         print(json.dumps(out), flush=True)

@@ -144,6 +144,21 @@ uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
  * form for A/B runs; the softbuffer is bit-identical either way. */
 uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
 
+/* ---- streaming re-planning (srsUE re-derives the grant every TTI: phch_worker.cc:297 -> :337).
+ * The planner is split from the device: mi_dl_plan_build runs the whole host planning of a batch (RE lists,
+ * scrambling words, segmentation, 64-lane grouping, rate-matching work lists) with NO HIP call, so host
+ * threads can plan step i+1 while the GPU decodes step i; mi_dl_batch_replan then swaps the built plan into a
+ * batch and enqueues its table upload on `stream` -- ordered after the batch's earlier work on that stream,
+ * so the caller passes the stream the batch runs on.  The plan object keeps its lookup caches (scrambling
+ * words per (RNTI, sf, G), CRS per cell, per-K tables: srslte_ue_dl_set_rnti's pregeneration) across builds,
+ * and after a replan it holds the batch's previous plan, ready to be rebuilt.  One plan object per planning
+ * thread; a batch's work buffers only grow (a larger plan reallocates them, synchronously). */
+typedef struct mi_dl_plan mi_dl_plan_t;
+mi_dl_plan_t *mi_dl_plan_create(void);
+void   mi_dl_plan_destroy(mi_dl_plan_t *p);
+int    mi_dl_plan_build(mi_dl_plan_t *p, const mi_dl_sf_cfg_t *cfgs, uint32_t n_sf);   /* host only; 0 = ok */
+int    mi_dl_batch_replan(mi_dl_batch_t *b, mi_dl_plan_t *p, void *stream);          /* 0 = ok */
+
 /* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =
  * srsLTE turbodecoder_test).  n_cb code blocks of size K; decoder input per block = 3(K+4) fp32
  * LLRs in triplet order d0_k d1_k d2_k with the 36.212 tail layout, LLR > 0 => bit 1 (device

@@ -459,7 +459,13 @@ int or_pusch_hop_type2(uint32_t nof_prb, uint32_t n_ho, uint32_t n_sb, int intra
     prb[l] = pt + off;
     if (lo < 0 || (int)prb[l] < lo) lo = (int)prb[l];
   }
-  for (uint32_t l = 0; l < L; l++)
+  /* a slot's allocation must stay one contiguous PRB run (SC-FDMA, 36.211 5.3.4): an allocation crossing a
+     subband edge under mirroring maps to a split set, which is rejected (as the product's mi_ul_hop_type2) */
+  uint32_t hi = 0;
+  for (uint32_t l = 0; l < L; l++) {
     if (prb[l] >= nof_prb) return -1;
+    if (prb[l] > hi) hi = prb[l];
+  }
+  if (hi - (uint32_t)lo + 1 != L) return -1;
   return lo;
 }

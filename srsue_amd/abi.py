@@ -91,6 +91,10 @@ def lib():
             "mi_tdec_turbo_win": (C.c_int, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
             "mi_dl_batch_rm_direct_groups": (u32, [vp]),
+            "mi_dl_plan_create": (vp, []),
+            "mi_dl_plan_destroy": (None, [vp]),
+            "mi_dl_plan_build": (C.c_int, [vp, vp, u32]),
+            "mi_dl_batch_replan": (C.c_int, [vp, vp, vp]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
             "mi_turbo_encode": (C.c_int, [vp, u32, u32, vp]),
             "mi_tdec_create": (vp, [u32, u32, u32, C.c_int, C.c_int, u32]),
@@ -233,6 +237,14 @@ class Batch:
         if rc:
             raise RuntimeError("mi_dl_batch_run: " + last_error())
 
+    def replan(self, plan, stream_ptr=None):
+        """Swap plan's built configuration in (mi_dl_batch_replan): table upload enqueued on stream_ptr, the
+        stream this batch runs on; plan then holds the previous configuration's data, ready for a rebuild."""
+        cfgs = plan.cfgs
+        if lib().mi_dl_batch_replan(self.h, plan.h, C.c_void_p(stream_ptr or 0)):
+            raise RuntimeError("mi_dl_batch_replan: " + last_error())
+        plan.cfgs, self.cfgs = self.cfgs, cfgs
+
     def run_stages(self, mask, d_iq_ptr=None, stream_ptr=None):
         rc = lib().mi_dl_batch_run_stages(self.h, C.c_void_p(d_iq_ptr or 0), C.c_void_p(stream_ptr or 0), mask)
         if rc:
@@ -299,6 +311,34 @@ class Batch:
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)
         off = lib().mi_dl_batch_payload_offset(self.h, sf)
         return p[off:off + self.cfgs[sf].tbs // 8]
+
+
+class Plan:
+    """Owns one mi_dl_plan_t: host-only planning of a batch (no GPU call; ctypes releases the GIL, so worker
+    threads plan while the main thread keeps the GPU busy), swapped into a Batch by Batch.replan()."""
+
+    def __init__(self):
+        self.h = lib().mi_dl_plan_create()
+        self.cfgs = None
+
+    def build(self, cfgs):
+        """cfgs: a list of SfCfg, or a prebuilt cfg_array (no per-call Python conversion)."""
+        arr = cfgs if isinstance(cfgs, C.Array) else cfg_array(list(cfgs))
+        self.cfgs = arr
+        if lib().mi_dl_plan_build(self.h, C.cast(arr, C.c_void_p), len(arr)):
+            raise RuntimeError("mi_dl_plan_build: " + last_error())
+        return self
+
+    def close(self):
+        if self.h:
+            lib().mi_dl_plan_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Ctrl:

@@ -125,6 +125,36 @@ int mi_dl_batch_turbo_compact(const mi_dl_batch_t* b) { return b->eng.tdec_compa
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t* b) { return (uint32_t)b->eng.plan.groups.size(); }
 uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t* b) { return (uint32_t)(b->eng.plan.rm_direct.size() / 8); }
 
+/* ---- streaming re-planning (include/mi_dl.h) ------------------------------------------------ */
+struct mi_dl_plan {
+  mi::Plan plan;
+  std::vector<mi_dl_sf_cfg_t> cfgs;
+  bool built = false;
+};
+
+mi_dl_plan_t* mi_dl_plan_create(void) { return new mi_dl_plan(); }
+void mi_dl_plan_destroy(mi_dl_plan_t* p) { delete p; }
+
+int mi_dl_plan_build(mi_dl_plan_t* p, const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf) {
+  if (!p || !cfgs || !n_sf) { mi::set_error("empty batch"); return -1; }
+  p->built = false;
+  if (p->plan.build(cfgs, n_sf, true)) return -1;
+  p->cfgs.assign(cfgs, cfgs + n_sf);
+  p->built = true;
+  return 0;
+}
+
+int mi_dl_batch_replan(mi_dl_batch_t* b, mi_dl_plan_t* p, void* stream) {
+  if (!b || !p || !p->built) { mi::set_error("mi_dl_batch_replan: no built plan"); return -1; }
+  const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the active plan data and the built one trade places (the planner's caches stay with each object)
+  std::swap(static_cast<mi::PlanData&>(b->eng.plan), static_cast<mi::PlanData&>(p->plan));
+  std::swap(b->cfgs, p->cfgs);
+  p->built = false;
+  b->eng.last_stream = st;
+  return b->eng.upload(st, true);
+}
+
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */
 struct mi_tdec_batch {
   mi::Engine eng;

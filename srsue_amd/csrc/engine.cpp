@@ -251,8 +251,10 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                    d_pds.as<MiPdschDesc>(), d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), nsf,
                    P.max_units, noise, st);
     mark(3);
-    // the direct groups' row maps (Plan::rm_direct) before the combine kernel stages their chunks
-    launch_rm_direct_maps(sb, d_kdata.as<uint32_t>(), reinterpret_cast<const MiRmDirect*>(d_rmdir.as<uint32_t>()),
+    // the direct groups' row maps (Plan::rm_direct) before the combine kernel stages their chunks -- only in a
+    // run that rate de-matches (a run without RM must leave the softbuffer, maps included, untouched)
+    if (mask & (1u << MI_DL_STAGE_RM))
+      launch_rm_direct_maps(sb, d_kdata.as<uint32_t>(), reinterpret_cast<const MiRmDirect*>(d_rmdir.as<uint32_t>()),
                           (uint32_t)(P.rm_direct.size() / 8), st);
     if (fuse)
       launch_rm_fused(d_grid.as<float2>(), d_ce.as<float2>(), d_lanesrc.as<MiLaneSrc>(), d_re.as<uint32_t>(),

@@ -1,6 +1,10 @@
 // plan.cpp -- batch planner (see engine.cpp header): RE lists, scrambling words, CRS tables,
 // code-block segmentation, rate-matching splits and 64-lane grouping of equal-K code blocks.
 #include "plan.h"
+#ifdef MI_PLAN_PROF
+#include <chrono>
+#include <cstdio>
+#endif
 #include "tb_body.h"
 
 #include <math.h>
@@ -8,8 +12,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <set>
 #include <tuple>
+#include <unordered_map>
 
 namespace mi {
 
@@ -40,7 +46,16 @@ void Plan::add_ktab(uint32_t K) {
   ktabs.push_back(t);
 }
 
+#ifdef MI_PLAN_PROF
+#define PLAN_T(name) do { auto _n = std::chrono::steady_clock::now(); fprintf(stderr, " %s %.2f", name, std::chrono::duration<double, std::milli>(_n - _pt).count()); _pt = _n; } while (0)
+#else
+#define PLAN_T(name) ((void)0)
+#endif
 int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
+#ifdef MI_PLAN_PROF
+  auto _pt = std::chrono::steady_clock::now();
+  fprintf(stderr, "\n");
+#endif
   has_pdsch = with_pdsch;
   cb_K = cb_n = 0;
   cells.clear(); crs.clear(); pds.clear(); re_tab.clear(); scr_tab.clear(); sfs.clear(); lanes.clear();
@@ -54,15 +69,26 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   max_units = max_ncb = n_cb = 0;
   bytes_compulsory = 0;
   for (double& b : stage_bytes) b = 0;
+  sfs.reserve(n);
+  tbs.reserve(n);
 
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cell_idx;
-  std::map<std::vector<uint32_t>, uint32_t> pd_idx;
+  std::unordered_map<ReKey, uint32_t, ReKeyHash> re_idx;        // -> offset in re_tab (this build)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> scr_idx;   // (cell, rnti, sf, G) -> scr_tab
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> pd_idx;
   std::map<int, std::vector<uint32_t>> fft_map;
   std::vector<uint32_t> re;
 
-  struct CbRef { uint32_t K, tb, r; };
-  std::vector<CbRef> cbs;
+  // code blocks: per TB the index of its first one (cb_first), per code block its K, E and LLR offset
   std::vector<CbSegm> segs(n);
+  std::vector<uint32_t> cb_first(n + 1, 0), cb_E;
+  std::vector<uint64_t> cb_eoff;
+  cb_E.reserve((size_t)n * 4);
+  cb_eoff.reserve((size_t)n * 4);
+  uint32_t last_tbs = 0;
+  CbSegm last_sg{};
+  ReKey rk{}, last_rk{};
+  uint32_t last_re = 0xFFFFFFFFu;
 
   for (uint32_t s = 0; s < n; s++) {
     const mi_dl_sf_cfg_t& c = cfgs[s];
@@ -109,26 +135,50 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       if (c.tm == 2 && c.nof_ports != 2) { set_error("TM2 needs 2 ports"); return -1; }
       if (c.Qm != 2 && c.Qm != 4 && c.Qm != 6) { set_error("Qm must be 2, 4 or 6"); return -1; }
       if (c.tbs == 0 || c.tbs % 8) { set_error("TBS must be a positive multiple of 8"); return -1; }
-      std::vector<uint32_t> pk = {ci, c.cfi, c.sf_idx, c.Qm, c.tm, c.rnti};
-      for (uint32_t p = 0; p < c.nof_prb; p++) pk.push_back(c.prb_mask[p] ? 1u : 0u);
-      uint32_t pi_;
-      auto pit = pd_idx.find(pk);
-      if (pit == pd_idx.end()) {
-        pi_ = (uint32_t)pds.size();
-        pd_idx[pk] = pi_;
-        const uint32_t nre = pdsch_re_list(c.cell_id, c.nof_prb, c.nof_ports, c.cfi, c.sf_idx, c.prb_mask, re);
-        if (c.tm == 2 && (nre & 1)) { set_error("odd RE count for SFBC"); return -1; }
-        MiPdschDesc pd{ci, c.sf_idx, nre, c.Qm, c.tm, nre * c.Qm, (uint32_t)re_tab.size(), (uint32_t)scr_tab.size()};
-        re_tab.insert(re_tab.end(), re.begin(), re.end());
-        const uint32_t G = pd.G, nw = (G + 31) / 32 + 1;
-        auto sk = std::make_tuple(c.cell_id, c.rnti, c.sf_idx, G);
+      // the RE list of (cell, cfi, sf, mask): consecutive subframes usually repeat the previous key
+      rk.cell_id = c.cell_id; rk.nof_prb = c.nof_prb; rk.nof_ports = c.nof_ports; rk.cfi = c.cfi; rk.sf = c.sf_idx;
+      memset(rk.mask, 0, sizeof(rk.mask));
+      for (uint32_t p = 0; p < c.nof_prb; p++) rk.mask[p] = c.prb_mask[p];
+      uint32_t re_off;
+      if (last_re != 0xFFFFFFFFu && rk == last_rk) {
+        re_off = last_re;
+      } else {
+        auto ri = re_idx.find(rk);
+        if (ri == re_idx.end()) {
+          auto& cached = re_cache[rk];
+          if (cached.empty()) {
+            pdsch_re_list(c.cell_id, c.nof_prb, c.nof_ports, c.cfi, c.sf_idx, c.prb_mask, re);
+            cached.reserve(re.size() + 1);
+            cached.push_back((uint32_t)re.size());   // [0] = count (an empty list stays distinguishable)
+            cached.insert(cached.end(), re.begin(), re.end());
+          }
+          ri = re_idx.emplace(rk, (uint32_t)re_tab.size()).first;
+          re_tab.insert(re_tab.end(), cached.begin(), cached.end());   // count, then the list
+        }
+        re_off = last_re = ri->second;
+        last_rk = rk;
+      }
+      const uint32_t nre = re_tab[re_off];
+      if (c.tm == 2 && (nre & 1)) { set_error("odd RE count for SFBC"); return -1; }
+      const uint32_t G = nre * c.Qm;
+      const auto sk = std::make_tuple(c.cell_id, c.rnti, c.sf_idx, G);
+      auto si = scr_idx.find(sk);
+      if (si == scr_idx.end()) {
         auto& words = scr_cache[sk];
         if (words.empty()) {
-          words.resize(nw);
+          words.resize((G + 31) / 32 + 1);
           gold_words((c.rnti << 14) | (c.sf_idx << 9) | c.cell_id, G, words.data());
         }
+        si = scr_idx.emplace(sk, (uint32_t)scr_tab.size()).first;
         scr_tab.insert(scr_tab.end(), words.begin(), words.end());
-        pds.push_back(pd);
+      }
+      const auto pk = std::make_tuple(ci, c.sf_idx, re_off, si->second, c.Qm, c.tm);
+      auto pit = pd_idx.find(pk);
+      uint32_t pi_;
+      if (pit == pd_idx.end()) {
+        pi_ = (uint32_t)pds.size();
+        pd_idx.emplace(pk, pi_);
+        pds.push_back(MiPdschDesc{ci, c.sf_idx, nre, c.Qm, c.tm, G, re_off + 1, si->second});
       } else {
         pi_ = pit->second;
       }
@@ -138,21 +188,34 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       e_floats += align4(pd.G);
       const uint32_t units = pd.tm == 2 ? pd.nre / 2 : pd.nre;
       max_units = std::max(max_units, units);
-      // ---- transport block
-      CbSegm sg;
-      if (cbsegm(c.tbs, &sg)) { set_error("segmentation failed"); return -1; }
+      // ---- transport block (segmentation depends on the TBS only)
+      if (c.tbs != last_tbs) {
+        if (cbsegm(c.tbs, &last_sg)) { set_error("segmentation failed"); return -1; }
+        last_tbs = c.tbs;
+      }
+      const CbSegm& sg = last_sg;
       segs[s] = sg;
       MiTbDesc tb{};
       tb.tbs = c.tbs; tb.C = sg.C; tb.Kp = sg.Kp; tb.Km = sg.Km; tb.Cm = sg.Cm; tb.F = sg.F;
       tb.pay_off = (uint32_t)payload_bytes;
       payload_bytes += c.tbs / 8;
       tbs.push_back(tb);
-      for (uint32_t r = 0; r < sg.C; r++) cbs.push_back({r < sg.Cm ? sg.Km : sg.Kp, s, r});
+      const uint32_t NL = c.tm == 2 ? (c.nl_td ? c.nl_td : 2) : 1;
+      uint64_t eo = sd.e_off;
+      cb_first[s] = (uint32_t)cb_E.size();
+      for (uint32_t r = 0; r < sg.C; r++) {
+        const uint32_t E = rm_E(pd.G, sg.C, c.Qm, NL, r);
+        cb_E.push_back(E);
+        cb_eoff.push_back(eo);
+        eo += E;
+      }
       stage_bytes[MI_DL_STAGE_DEMAP] += (double)pd.nre * 8 * (1 + c.nof_ports) + (double)pd.G * 4;
       bytes_compulsory += (double)c.tbs / 8;
     }
     sfs.push_back(sd);
   }
+  cb_first[n] = (uint32_t)cb_E.size();
+  PLAN_T("sf");
   for (auto& kv : fft_map) {
     fft_lists.push_back(kv);
     fft_list_off.push_back(fft_list_flat.size());
@@ -161,8 +224,48 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   }
   if (!with_pdsch) return 0;
 
-  // ---- group code blocks of equal K into 64-lane wavefront groups
-  std::stable_sort(cbs.begin(), cbs.end(), [](const CbRef& a, const CbRef& b) { return a.K < b.K; });
+  PLAN_T("fft");
+  // ---- group code blocks of equal K into 64-lane wavefront groups: a stable counting sort by K (TB order,
+  // then r, within each K)
+  struct CbRef { uint32_t K, tb, r; };
+  const uint32_t ncbs = cb_first[n];
+  std::vector<CbRef> cbs(ncbs);
+  {
+    std::map<uint32_t, uint32_t> kcount;
+    for (uint32_t s = 0; s < n; s++) {
+      const CbSegm& sg = segs[s];
+      if (sg.Cm) kcount[sg.Km] += sg.Cm;
+      kcount[sg.Kp] += sg.C - sg.Cm;
+    }
+    std::map<uint32_t, uint32_t> kpos;
+    uint32_t acc = 0;
+    for (auto& kv : kcount) { kpos[kv.first] = acc; acc += kv.second; }
+    uint32_t lastK = 0, *slot = nullptr;
+    for (uint32_t s = 0; s < n; s++) {
+      const CbSegm& sg = segs[s];
+      for (uint32_t r = 0; r < sg.C; r++) {
+        const uint32_t K = r < sg.Cm ? sg.Km : sg.Kp;
+        if (K != lastK || !slot) { slot = &kpos[K]; lastK = K; }
+        cbs[(*slot)++] = CbRef{K, s, r};
+      }
+    }
+  }
+  PLAN_T("sort");
+  // per (K, F, rv): the rank table, N_v and the rank of k0 (r0), computed once
+  struct LaneRm { const std::vector<int32_t>* rk; uint32_t Nv, r0; };
+  std::unordered_map<uint64_t, LaneRm> lrm;
+  auto lane_rm = [&](uint32_t K, uint32_t F, uint32_t rv) -> const LaneRm& {
+    const uint64_t key = (uint64_t)K | ((uint64_t)F << 16) | ((uint64_t)rv << 32);
+    auto it = lrm.find(key);
+    if (it != lrm.end()) return it->second;
+    auto& rkc = rank_cache[{K, F}];
+    if (rkc.first.empty()) cb_rank_table(K, F, rkc.first, &rkc.second);
+    const uint32_t k0 = k0_of(K, rv), Ncb = ncb_of(K);
+    uint32_t r0 = 0;
+    for (uint32_t p = 0; p < k0 && p < Ncb; p++) r0 += rkc.first[p] >= 0 ? 1 : 0;
+    return lrm.emplace(key, LaneRm{&rkc.first, rkc.second, r0 % rkc.second}).first->second;
+  };
+  lanes.reserve((ncbs / LANES + 256) * LANES);
   std::map<uint32_t, uint32_t> ktab_idx;
   for (size_t i = 0; i < cbs.size();) {
     const uint32_t K = cbs[i].K;
@@ -179,6 +282,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     }
     const uint32_t Ncb = ncb_of(K);
     max_ncb = std::max(max_ncb, Ncb);
+    const size_t gsz = sb_group_floats(Ncb), ssz = (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
     for (size_t g0 = i; g0 < j; g0 += LANES) {
       MiGroupDesc g{};
       g.K = K; g.Ncb = Ncb; g.ktab = kt;
@@ -186,8 +290,8 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       g.sb_off = sb_floats;
       g.scratch_off = scratch_floats;
       g.dec_off = dec_bytes;
-      sb_floats += sb_group_floats(Ncb);
-      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
+      sb_floats += gsz;
+      scratch_floats += ssz;
       dec_bytes += (size_t)K * LANES;
       groups.push_back(g);
       for (size_t q = 0; q < (size_t)LANES; q++) {
@@ -196,20 +300,13 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
           const CbRef& cr = cbs[g0 + q];
           const mi_dl_sf_cfg_t& c = cfgs[cr.tb];
           const CbSegm& sg = segs[cr.tb];
-          const MiPdschDesc& pd = pds[sfs[cr.tb].pdsch];
           const uint32_t F = cr.r == 0 ? sg.F : 0;
-          const uint32_t NL = c.tm == 2 ? (c.nl_td ? c.nl_td : 2) : 1;
-          uint64_t eo = sfs[cr.tb].e_off;
-          for (uint32_t rr = 0; rr < cr.r; rr++) eo += rm_E(pd.G, sg.C, c.Qm, NL, rr);
-          ld.e_off = eo;
-          ld.E = rm_E(pd.G, sg.C, c.Qm, NL, cr.r);
-          auto& rk = rank_cache[{K, F}];
-          if (rk.first.empty()) cb_rank_table(K, F, rk.first, &rk.second);
-          ld.Nv = rk.second;
-          const uint32_t k0 = k0_of(K, c.rv);
-          uint32_t r0 = 0;
-          for (uint32_t p = 0; p < k0 && p < Ncb; p++) r0 += rk.first[p] >= 0 ? 1 : 0;
-          ld.r0 = r0 % ld.Nv;
+          const uint32_t cbi = cb_first[cr.tb] + cr.r;
+          ld.e_off = cb_eoff[cbi];
+          ld.E = cb_E[cbi];
+          const LaneRm& lr = lane_rm(K, F, c.rv);
+          ld.Nv = lr.Nv;
+          ld.r0 = lr.r0;
           ld.F = F;
           ld.new_tb = c.new_tb ? 1 : 0;
           ld.crc24a = sg.C == 1 ? 1 : 0;
@@ -219,11 +316,9 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
             // payload run of CB r (tb_kernel's closed form): bytes s(r) .. s(r + 1) - 1 of the TB, clipped at
             // TBS / 8 (the last code block also carries the TB CRC)
             const MiTbDesc& tb = tbs[cr.tb];
-            auto s_of = [&](uint32_t r) {
-              const uint32_t nm = r < tb.Cm ? r : tb.Cm;
-              return nm * (tb.Km / 8) + (r - nm) * (tb.Kp / 8) - (r ? tb.F / 8 : 0) - (tb.C > 1 ? 3 * r : 0);
-            };
-            ld.pay_st = tb.pay_off + s_of(cr.r);
+            const uint32_t r = cr.r, nm = r < tb.Cm ? r : tb.Cm;
+            ld.pay_st = tb.pay_off + nm * (tb.Km / 8) + (r - nm) * (tb.Kp / 8) - (r ? tb.F / 8 : 0) -
+                        (tb.C > 1 ? 3 * r : 0);
             ld.tbcrc = (sg.C == 1 || cr.r + 1 == sg.C) ? 1 : 0;
           }
           // rank table offset: one copy per (K, F) in kdata
@@ -231,7 +326,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
           lanes.push_back(ld);
           stage_bytes[MI_DL_STAGE_RM] += (double)ld.E * 4 + (double)Ncb * 4 * (ld.new_tb ? 1 : 2);
           stage_bytes[MI_DL_STAGE_TDEC] += (double)(3 * K + 12) * 4 + (double)K / 8;
-          bytes_compulsory += (double)ncb_of(K) * 4 * (ld.new_tb ? 1 : 2);
+          bytes_compulsory += (double)Ncb * 4 * (ld.new_tb ? 1 : 2);
           n_cb++;
         } else {
           lanes.push_back(ld);
@@ -239,9 +334,10 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       }
     }
     if (((j - i + LANES - 1) / LANES) & 1)   // odd group count: padding for the unpaired group's pair scratch
-      scratch_floats += (size_t)LANES * (2 * K + 8 * (K / TDEC_CK_MIN + 1));
+      scratch_floats += ssz;
     i = j;
   }
+  PLAN_T("lanes");
   build_pairs();
   // fused demap sources of every lane
   lane_src.assign(lanes.size(), MiLaneSrc{0, 0, 0, 0, 0, 2, 0, 0, 0});
@@ -266,33 +362,39 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
     else if (k != unit_kind) mixed = true;
   }
   if (mixed) unit_kind = 0;
+  PLAN_T("lanesrc");
   // rank tables into kdata, patch lane offsets
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rank_off;
-  for (size_t gi = 0; gi < groups.size(); gi++) {
-    for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
-      MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
-      if (!ld.valid) continue;
-      auto key = std::make_pair(groups[gi].K, ld.F);
-      auto ro = rank_off.find(key);
-      if (ro == rank_off.end()) {
-        const auto& rk = rank_cache[key].first;
-        uint32_t off = (uint32_t)kdata.size();
-        for (int32_t v : rk) kdata.push_back((uint32_t)v);
-        // chunk table: non-null positions before c * RM_CHUNK, c = 0 .. ceil(Ncb / RM_CHUNK)
-        const uint32_t nch = (uint32_t)((rk.size() + RM_CHUNK - 1) / RM_CHUNK);
-        uint32_t cnt = 0;
-        for (uint32_t c = 0, p = 0; c <= nch; c++) {
-          const uint32_t end = std::min<uint32_t>(c * RM_CHUNK, (uint32_t)rk.size());
-          for (; p < end; p++) cnt += rk[p] >= 0 ? 1 : 0;
-          kdata.push_back(cnt);
+  {
+    std::pair<uint32_t, uint32_t> lastk{0xFFFFFFFFu, 0};
+    uint32_t lasto = 0;
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+      for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+        MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
+        if (!ld.valid) continue;
+        const auto key = std::make_pair(groups[gi].K, ld.F);
+        if (key == lastk) { ld.rank_off = lasto; continue; }
+        auto ro = rank_off.find(key);
+        if (ro == rank_off.end()) {
+          const auto& rk = rank_cache[key].first;
+          uint32_t off = (uint32_t)kdata.size();
+          for (int32_t v : rk) kdata.push_back((uint32_t)v);
+          // chunk table: non-null positions before c * RM_CHUNK, c = 0 .. ceil(Ncb / RM_CHUNK)
+          const uint32_t nch = (uint32_t)((rk.size() + RM_CHUNK - 1) / RM_CHUNK);
+          uint32_t cnt = 0;
+          for (uint32_t c = 0, p = 0; c <= nch; c++) {
+            const uint32_t end = std::min<uint32_t>(c * RM_CHUNK, (uint32_t)rk.size());
+            for (; p < end; p++) cnt += rk[p] >= 0 ? 1 : 0;
+            kdata.push_back(cnt);
+          }
+          ro = rank_off.emplace(key, off).first;
         }
-        rank_off[key] = off;
-        ld.rank_off = off;
-      } else {
-        ld.rank_off = ro->second;
+        ld.rank_off = lasto = ro->second;
+        lastk = key;
       }
     }
   }
+  PLAN_T("rank");
   // direct groups (rm.hip): every valid lane new, one rank table, one k0 rank, one unit kind, whole units, E <= N_v;
   // their rank -> row tables (row = ipos[p] under MI_SB_NAT) into kdata.  MI_RM_DIRECT=0 in the environment
   // sends every group through the general combine (A/B and parity tests).
@@ -335,65 +437,94 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
                                          emax | (kind << 24), l0.rank_off});
     }
   }
+  PLAN_T("direct");
   // rate de-matching chunks with received LLRs (rm.hip): the kernel's per-lane test
-  // (nr > 0 && (E >= Nv || j0 < E || j0 + nr > Nv)) over the distinct lane parameters of each group
+  // (nr > 0 && (E >= Nv || j0 < E || j0 + nr > Nv)), i.e. chunk c's rank run [ch[c], ch[c + 1]) meets the lane's
+  // circular window of ranks [r0, r0 + E) mod N_v -- found per distinct lane parameters by binary search over the
+  // monotone chunk table, marked in a difference array
   {
     std::vector<uint32_t> idle, gbusy;
+    std::vector<int32_t> diff;
+    std::vector<std::array<uint32_t, 4>> seen;
     rm_items.clear();
+    rm_items.reserve((size_t)groups.size() * 80);
     for (size_t gi = 0; gi < groups.size(); gi++) {
       const uint32_t Ncb = groups[gi].Ncb, nch = (Ncb + RM_CHUNK - 1) / RM_CHUNK;
-      std::vector<uint8_t> busy(nch, 0);
-      busy[0] = 1;
-      std::set<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>> seen;
+      diff.assign(nch + 1, 0);
+      diff[0] += 1;   // chunk 0 always (it writes the group's zero row)
+      diff[1] -= 1;
+      seen.clear();
       for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
         const MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
-        if (!ld.valid || !seen.insert(std::make_tuple(ld.rank_off, ld.r0, ld.Nv, ld.E)).second) continue;
-        const uint32_t* ch = &kdata[(size_t)ld.rank_off + Ncb];
-        for (uint32_t c = 0; c < nch; c++) {
-          const uint32_t ra = ch[c], nr = ch[c + 1] - ra;
-          const uint32_t j0 = ra >= ld.r0 ? ra - ld.r0 : ra + ld.Nv - ld.r0;
-          if (nr > 0 && (ld.E >= ld.Nv || j0 < ld.E || j0 + nr > ld.Nv)) busy[c] = 1;
+        if (!ld.valid) continue;
+        const std::array<uint32_t, 4> sk{ld.rank_off, ld.r0, ld.Nv, ld.E};
+        if (std::find(seen.begin(), seen.end(), sk) != seen.end()) continue;
+        seen.push_back(sk);
+        const uint32_t* ch = &kdata[(size_t)ld.rank_off + Ncb];   // ch[0..nch], monotone
+        // chunks whose rank run meets [a, b): ch[c + 1] > a and ch[c] < b (and nr > 0)
+        auto mark = [&](uint32_t a, uint32_t b) {
+          if (a >= b) return;
+          const uint32_t c0 = (uint32_t)(std::upper_bound(ch + 1, ch + nch + 1, a) - (ch + 1));
+          const uint32_t c1 = (uint32_t)(std::lower_bound(ch, ch + nch, b) - ch);   // first chunk with ch[c] >= b
+          if (c0 < c1) { diff[c0] += 1; diff[c1] -= 1; }
+        };
+        if (ld.E >= ld.Nv) {
+          mark(0, ld.Nv);
+        } else if (ld.r0 + ld.E <= ld.Nv) {
+          mark(ld.r0, ld.r0 + ld.E);
+        } else {
+          mark(ld.r0, ld.Nv);
+          mark(0, ld.r0 + ld.E - ld.Nv);
         }
       }
-      for (uint32_t c = 0; c < nch; c++)
-        if (busy[c]) (direct[gi] ? rm_items : gbusy).push_back(((uint32_t)gi << 9) | c);
+      int32_t acc = 0;
+      for (uint32_t c = 0; c < nch; c++) {
+        acc += diff[c];
+        if (acc > 0) (direct[gi] ? rm_items : gbusy).push_back(((uint32_t)gi << 9) | c);
         else if (!direct[gi]) idle.push_back(((uint32_t)gi << 9) | c);   // direct groups: the map kernel
+      }
     }
     rm_dbusy = (uint32_t)rm_items.size();   // direct groups' chunks first (their own launch, rm.hip)
     rm_items.insert(rm_items.end(), gbusy.begin(), gbusy.end());
     rm_busy = (uint32_t)rm_items.size();
-    rm_recs.clear();
-    for (uint32_t it : rm_items) {
+    rm_recs.resize((size_t)rm_busy * 4);
+    for (uint32_t k = 0; k < rm_busy; k++) {
+      const uint32_t it = rm_items[k];
       const MiGroupDesc& g = groups[it >> 9];
       // the softbuffer offset in units of 64 floats (every group region is a multiple: sb_group_floats)
       // Ncb < 2^15 (<= 18,444): bit 15 flags a direct group, whose last field is its rank -> row table
       const bool dr = direct[it >> 9];
-      rm_recs.insert(rm_recs.end(), {g.lane0, g.Ncb | (dr ? 1u << 15 : 0u) | ((it & 511u) << 16),
-                                     (uint32_t)(g.sb_off / LANES), dr ? direct_rrow[it >> 9] : ktabs[g.ktab].ipos_off});
+      uint32_t* rec = &rm_recs[(size_t)k * 4];
+      rec[0] = g.lane0;
+      rec[1] = g.Ncb | (dr ? 1u << 15 : 0u) | ((it & 511u) << 16);
+      rec[2] = (uint32_t)(g.sb_off / LANES);
+      rec[3] = dr ? direct_rrow[it >> 9] : ktabs[g.ktab].ipos_off;
     }
     rm_items.insert(rm_items.end(), idle.begin(), idle.end());
   }
-  // TB -> lane lists
-  std::vector<std::vector<uint32_t>> tb_lanes(n);
-  for (size_t gi = 0; gi < groups.size(); gi++)
-    for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
-      const MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
-      if (ld.valid) tb_lanes[ld.tb].push_back(groups[gi].lane0 + q);
-    }
-  // lanes of a TB were appended in CB order within each K run; K- blocks (r < Cm) come first
-  for (uint32_t s = 0; s < n; s++) {
-    auto& v = tb_lanes[s];
-    // order by CB index r: CBs with K- precede K+ ones (36.212 5.1.2), K runs are sorted ascending
-    tbs[s].cb_list = (uint32_t)cb_list.size();
-    cb_list.insert(cb_list.end(), v.begin(), v.end());
+  PLAN_T("busy");
+  // TB -> lane lists (counting sort by TB; lanes of a TB in group order = CB order within each K run, K- blocks
+  // (r < Cm) first: 36.212 5.1.2)
+  {
+    std::vector<uint32_t> cnt(n + 1, 0);
+    for (const MiLaneDesc& ld : lanes)
+      if (ld.valid) cnt[ld.tb + 1]++;
+    for (uint32_t s = 0; s < n; s++) cnt[s + 1] += cnt[s];
+    cb_list.assign(cnt[n], 0);
+    for (uint32_t s = 0; s < n; s++) tbs[s].cb_list = cnt[s];
+    for (size_t gi = 0; gi < groups.size(); gi++)
+      for (uint32_t q = 0; q < (uint32_t)LANES; q++) {
+        const MiLaneDesc& ld = lanes[groups[gi].lane0 + q];
+        if (ld.valid) cb_list[cnt[ld.tb]++] = groups[gi].lane0 + q;
+      }
   }
+  PLAN_T("tblist");
   // TB-CRC multipliers per segmentation: CB r's partial CRC register is shifted over the payload bytes
-  // that follow it (tb_body.h tb_crc_term), precomputed once per distinct TB shape
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> mul_off;
+  // that follow it (tb_body.h tb_crc_term), precomputed once per distinct TB shape (= per TBS)
+  std::unordered_map<uint32_t, uint32_t> mul_off;
   for (uint32_t s = 0; s < n; s++) {
     MiTbDesc& t = tbs[s];
-    const auto key = std::make_tuple(t.tbs, t.C, t.Kp, t.Km, t.Cm, t.F);
-    auto it = mul_off.find(key);
+    auto it = mul_off.find(t.tbs);
     if (it == mul_off.end()) {
       const uint32_t off = (uint32_t)kdata.size();
       for (uint32_t r = 0; r < t.C; r++) {
@@ -401,10 +532,11 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         for (uint32_t j = r + 1; j < t.C; j++) after += tb_cb_nbytes(t, j);
         kdata.push_back(gf24_xpow8(after, CRC24A_POLY));
       }
-      it = mul_off.emplace(key, off).first;
+      it = mul_off.emplace(t.tbs, off).first;
     }
     t.crc_mul = it->second;
   }
+  PLAN_T("mul");
   return 0;
 }
 
@@ -424,7 +556,7 @@ int Plan::build_codeblocks(uint32_t K, uint32_t ncb_req, bool crc24a) {
   groups.clear(); ktabs.clear(); kdata.clear(); tbs.clear(); cb_list.clear(); fft_lists.clear(); rm_items.clear(); rm_recs.clear();
   pairs.clear();
   rm_direct.clear();
-  rm_busy = 0;
+  rm_busy = rm_dbusy = 0;
   fft_list_flat.clear(); fft_list_off.clear(); fft_W.clear();
   iq_samples = grid_elems = ce_elems = e_floats = sb_floats = scratch_floats = dec_bytes = payload_bytes = 0;
   max_units = max_ncb = n_cb = 0;

@@ -3,7 +3,9 @@
 #pragma once
 #include <map>
 #include <string>
+#include <cstring>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "dl_common.h"
@@ -63,6 +65,26 @@ struct PlanData {
   uint32_t cb_K = 0, cb_n = 0;
 };
 
+// A PDSCH RE list depends on the cell, CFI, subframe and PRB mask only (not on RNTI, Qm or the transmission
+// mode): one list per distinct key per build (and across builds: re_cache), shared by every descriptor that uses it
+struct ReKey {
+  uint32_t cell_id, nof_prb, nof_ports, cfi, sf;
+  uint8_t mask[(NRB_MAX + 3) & ~3];   // whole words: no padding bytes
+  bool operator==(const ReKey& o) const { return !memcmp(this, &o, sizeof(ReKey)); }
+  bool operator<(const ReKey& o) const { return memcmp(this, &o, sizeof(ReKey)) < 0; }
+};
+struct ReKeyHash {
+  size_t operator()(const ReKey& k) const {
+    uint64_t h = 1469598103934665603ull;
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&k);
+    for (size_t i = 0; i < sizeof(ReKey) / 8; i++) h = (h ^ w[i]) * 1099511628211ull;
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(&k);
+    for (size_t i = sizeof(ReKey) / 8 * 8; i < sizeof(ReKey); i++) h = (h ^ b[i]) * 1099511628211ull;
+    return (size_t)(h ^ (h >> 29));
+  }
+};
+static_assert(sizeof(ReKey) == 20 + ((NRB_MAX + 3) & ~3), "ReKey must be padding-free (memcmp / hash over its bytes)");
+
 struct Plan : PlanData {
   void build_pairs();
   // cached per-key tables (kept across rebuilds)
@@ -71,6 +93,8 @@ struct Plan : PlanData {
   std::map<uint32_t, std::vector<std::vector<uint32_t>>> kpos_cache;   // K -> {pos, pi, crcA, crcB}
   void add_ktab(uint32_t K);   // appends K's tables to kdata and a MiKTab to ktabs
   std::map<std::pair<uint32_t, uint32_t>, std::pair<std::vector<int32_t>, uint32_t>> rank_cache;
+  // PDSCH RE lists per (cell, CFI, sf, PRB mask) (plan.cpp ReKey): [0] = count, then the grid indices
+  std::unordered_map<ReKey, std::vector<uint32_t>, ReKeyHash> re_cache;
 
   // has_pdsch = false plans only OFDM + channel estimation (per-TTI front half)
   int build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool has_pdsch);

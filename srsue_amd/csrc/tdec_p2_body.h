@@ -46,8 +46,9 @@ struct TdecArgsP2 {
   const uint32_t* crc8b;  // [256] CRC24B byte table
   uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][7]
   uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
-  uint8_t* cb_bytes[2];   // each half's packed output: byte j of the code block at cb_bytes[h][j]: its row
-  uint32_t to_payload;    // (every byte), or -- wave-uniform flag -- the TB payload (its payload bytes only)
+  uint8_t* cb_bytes[2];   // each half's packed output: byte j of the code block at cb_bytes[h][j - cb_skip[h]]: its
+  uint32_t cb_skip[2];    // row (every byte, skip 0), or -- wave-uniform flag to_payload -- the TB payload at the code
+  uint32_t to_payload;    // block's first payload byte (its payload bytes j >= F/8 only, skip F/8)
   uint32_t K, F[2], max_its, early_stop;
   uint32_t crc24a[2];     // bit 0: C == 1 (CB CRC = TB CRC24A); bit 1: the code block carries the TB CRC
   uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
@@ -800,8 +801,8 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
       // payload bytes: F/8 .. the CB CRC, less the TB CRC where the code block carries it (tb_kernel's run)
       const bool s0 = !a.to_payload || (j >= bl[0] && j < bh[0] - 3 * ((a.crc24a[0] >> 1) & 1u));
       const bool s1 = !a.to_payload || (j >= bl[1] && j < bh[1] - 3 * ((a.crc24a[1] >> 1) & 1u));
-      if (p0 && s0) a.cb_bytes[0][j] = (uint8_t)v0;
-      if (p1 && s1) a.cb_bytes[1][j] = (uint8_t)v1;
+      if (p0 && s0) a.cb_bytes[0][j - a.cb_skip[0]] = (uint8_t)v0;
+      if (p1 && s1) a.cb_bytes[1][j - a.cb_skip[1]] = (uint8_t)v1;
       cb[0] = ((cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((cb[0] >> 16) ^ v0) & 0xFFu];
       cb[1] = ((cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((cb[1] >> 16) ^ v1) & 0xFFu];
       if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];

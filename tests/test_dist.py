@@ -93,8 +93,8 @@ def test_bench_spawns_its_own_ranks(built, tmp_path):
     np.savez(path, **llrs)
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run-llr", str(path)],
-                         env=env, capture_output=True, text=True, timeout=240)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run-llr", str(path),
+                          "--cpu-seconds", "1.5"], env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1                                   # only rank 0 prints
@@ -105,6 +105,9 @@ def test_bench_spawns_its_own_ranks(built, tmp_path):
     assert len(r["elapsed_per_rank_s"]) == 2 and r["elapsed_max_s"] == max(r["elapsed_per_rank_s"])
     assert [s[:2] for s in r["shards"]] == [[0, 3], [3, 3]]  # contiguous shards
     assert all(s[2] == s[1] for s in r["shards"])           # every TB equals the transmitted bytes
+    # the N-rank line is complete: rank 0's CPU baseline and every rank's device identity
+    assert r["cpu_baseline"]["value"] > 0 and r["cpu_baseline"]["cores"] >= 1 and r["cpu_baseline"]["kind"] == "port"
+    assert [d["rank"] for d in r["rank_devices"]] == [0, 1]
 
 
 def test_bench_rejects_world_mismatch(built):
@@ -131,7 +134,7 @@ def test_bench_two_ranks_on_one_gpu(built):
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--sf-per-gpu",
-                        "256", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--iterating-snr", "0"],
+                        "256", "--steps", "2", "--warmup", "1", "--cpu-seconds", "1.5", "--iterating-snr", "0"],
                        cwd=root, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -145,3 +148,8 @@ def test_bench_two_ranks_on_one_gpu(built):
     per = d["elapsed_per_rank_s"]
     assert len(per) == 2 and abs(d["ms_per_step"] - max(per) / 2 * 1e3) < 1e-2
     assert abs(d["value"] - 512 * 75376 * 2 / max(per) / 1e6) < 1e-3 * d["value"]
+    # the N-rank line carries rank 0's CPU baseline and each rank's device identity (here: both on the one card)
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["kind"] == "port"
+    devs = d["rank_devices"]
+    assert [x["rank"] for x in devs] == [0, 1] and all(x["pci_bus_id"] and x["device"] for x in devs)
+    assert len({x["pci_bus_id"] for x in devs}) == 1       # --share-gpu: one card

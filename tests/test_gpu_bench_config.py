@@ -179,3 +179,38 @@ def test_waterfall_compaction_matches_uncompacted(monkeypatch):
         assert np.array_equal(outs[2][k], outs[1][k]), name
     crc, cbits = outs[0][0], outs[0][2][:C * n]
     assert 0 < crc.sum() < n and set(np.unique(cbits).tolist()) >= {1, 2, 3, 4}
+
+
+def test_configs2_tm2_at_size_vs_oracle():
+    """Test D: BASELINE configs[2] at its stated size in the bench's configuration -- 1,000 x
+    20 MHz TM2 (2-port SFBC, Alamouti) 64QAM MCS-28 subframes through the bench's channel (h = 0.8+0.3j,
+    -0.4+0.5j), compact estimates, fused demap, automatic turbo schedule (crossed lanes at this size) -- on a
+    24-29 dB pool of 40 distinct subframes (TM2's waterfall through this channel) so that code blocks iterate.  Every CRC-OK TB equals its transmitted
+    bytes; 16 pool entries (all 25 copies of each) equal the oracle int16 decode of the GPU front end's LLRs: TB
+    CRC, TB and per-code-block iterations, payload; those LLRs are within 1e-4 of the oracle front end's."""
+    n, pool = 1000, 40
+    H = [0.8 + 0.3j, -0.4 + 0.5j]
+    snrs = [24.0 + 5.0 * j / (pool - 1) for j in range(pool)]   # TM2's waterfall through this channel: 24-28 dB
+    pcfgs = [abi.sf_cfg(nof_prb=100, nof_ports=2, tm=2, sf_idx=SF_CYCLE[j % 8], tbs=TBS, Qm=6, rnti=0x46)
+             for j in range(pool)]
+    tbs_pool = [tb_bytes(8000 + j, TBS) for j in range(pool)]
+    iqs = [abi.tx_subframe(c, tbs_pool[j], h=H, snr_db=snrs[j], seed=0xD000 + j) for j, c in enumerate(pcfgs)]
+    sample = list(range(0, pool, pool // 16))[:16]
+    exp, orc = expected_from_gpu_llrs([pcfgs[j] for j in sample], [iqs[j] for j in sample], 4)
+    exp_full = [None] * pool
+    for k, j in enumerate(sample):
+        exp_full[j] = exp[k]
+    cfgs = [pcfgs[i % pool] for i in range(n)]
+    b = abi.Batch(cfgs, max_its=4, tdec_i16=True, compact_ce=True)
+    assert b.turbo_sched in ("lanex", "lanexr"), b.turbo_sched
+    L = 2 * abi.lib().mi_sf_len(100)
+    d_pool = torch.from_numpy(np.stack(iqs)).cuda()
+    d = torch.empty((n, L), dtype=torch.float32, device="cuda")
+    d.copy_(d_pool[torch.arange(n, device="cuda") % pool])
+    b.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    crc, CB = check_against(b, n, pool, exp_full, tbs_pool, sample)
+    assert n // 2 < crc.sum() < n and CB.max() >= 2 and (CB > 1).mean() > 0.01
+    for k, j in enumerate(sample):
+        assert orc[k][0] == exp[k][0] and np.array_equal(orc[k][1], exp[k][1]), f"pool entry {j}: oracle front"
+    b.close()

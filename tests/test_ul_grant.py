@@ -212,8 +212,8 @@ def test_type2_hopping_matches_oracle(built):
         for ns in range(20):
             prb = (C.c_uint32 * Lp)()
             o = OL.or_pusch_hop_type2(N, nho, nsb, intra, cid, v, Lp, ns, txnb, prb)
-            if o >= 0 and sorted(prb[:]) != list(range(o, o + Lp)):
-                o = -1                                         # a non-contiguous set is not a valid slot
+            if o >= 0:
+                assert sorted(prb[:]) == list(range(o, o + Lp))   # the oracle returns contiguous runs only
             p = L.mi_ul_hop_type2(N, nho, nsb, intra, cid, v, Lp, ns, txnb)
             assert p == o, (N, nsb, nho, intra, cid, Lp, v, txnb, ns, p, o)
             if p >= 0:
@@ -228,3 +228,21 @@ def test_type2_hopping_matches_oracle(built):
     for N, v, Lp in ((25, 3, 2), (100, 40, 1), (6, 0, 3)):
         assert L.mi_ul_hop_type2(N, 0, 1, 1, 7, v, Lp, 0, 0) == v
         assert L.mi_ul_hop_type2(N, 0, 1, 1, 7, v, Lp, 1, 0) == N - v - Lp
+
+
+def test_type2_hopping_subband_crossing_rejected_by_both(built):
+    """An allocation that crosses a subband edge: in slots with mirroring (f_m = 1) its VRBs map to a split PRB set,
+    which the product and the oracle both reject (-1); in slots without mirroring both give the same contiguous
+    run (the contiguity rule lives in the oracle too)."""
+    L, OL = _hop2_lib(), O.lib()
+    OL.or_pusch_hop_type2.restype = C.c_int
+    seen_split = seen_ok = 0
+    for cid in range(40):
+        for ns in range(20):
+            prb = (C.c_uint32 * 3)()
+            o = OL.or_pusch_hop_type2(50, 0, 2, 1, cid, 23, 3, ns, 0, prb)   # VRBs 23..25 across the 25-RB subbands
+            p = L.mi_ul_hop_type2(50, 0, 2, 1, cid, 23, 3, ns, 0)
+            assert p == o, (cid, ns, p, o)
+            seen_split += o < 0
+            seen_ok += o >= 0
+    assert seen_split > 0 and seen_ok > 0
