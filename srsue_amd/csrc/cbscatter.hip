@@ -27,12 +27,19 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict
   float* sbg = sb + g.sb_off;
   for (uint32_t i = w; i < (uint32_t)SC_T; i += 4) {
     const uint32_t t = t0 + i;
-    if (t < T) sbg[(size_t)(MI_SB_NAT ? t : pos[t]) * LANES + q] = tile[q][i];   // dl_common.h MI_SB_NAT
+    if (t < T) {
+      const size_t row = MI_SB_NAT ? t : pos[t];   // dl_common.h MI_SB_NAT
+      sbg[row * LANES + q] = tile[q][i];
+      sb_q16_put(sbg, g.Ncb, row * LANES + q, q16s(tile[q][i]));   // and the int16 mirror
+    }
   }
   if (blockIdx.x == 0) {   // every row written: the whole map materialised, plus the zero row
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb));
     for (uint32_t p = tid; p < g.Ncb; p += 256) map[p] = 1;
-    if (tid < LANES) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;
+    if (tid < LANES) {
+      sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;
+      sb_q16_put(sbg, g.Ncb, (size_t)g.Ncb * LANES + tid, 0);
+    }
   }
 }
 

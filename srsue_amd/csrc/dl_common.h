@@ -195,9 +195,38 @@ namespace mi {
 #ifndef MI_SB_NAT
 #define MI_SB_NAT 1
 #endif
+// The int16 mirror (round 4): after the map, [Ncb + 1][64] int16 rows holding q(x) = clamp(rint(32 x), +-511) -- the
+// int16 turbo decoder's input quantiser -- of the fp32 row with the same index.  Every writer of a softbuffer row
+// (rate de-matching, its idle settling, the zero rows, the raw code-block scatter) writes the row's mirror with it,
+// so a mirror row is valid exactly where its fp32 row is materialised (the same row map and zero row apply).  The
+// packed int16 decoder reads its channel inputs from the mirror: 128-B rows instead of 256-B rows and no
+// quantisation on its chain; the fp32 rows stay the HARQ softbuffer (srsLTE's float buffer_f, combined in float).
+// Measured and NOT the default (MI_SB_Q16=1 builds it; profiles/r4/ab_mirror): one stream, tdec 6.40-6.54 ->
+// 5.89-5.93 ms but rate de-matching 2.45-2.53 -> 2.94-2.95 ms (its writes grow by half) -- net -0.1 ms; on the
+// default 4 streams the headline loses 3 % (the chain is bound by its total traffic, and the mirror trades 26 KB of
+// turbo reads for 14 KB of rate-matching writes per code block at an HBM-write cost).  Off: no mirror space, no
+// mirror writes, the decoder quantises the fp32 rows.
+#ifndef MI_SB_Q16
+#define MI_SB_Q16 0
+#endif
 __host__ __device__ inline size_t sb_map_off(uint32_t Ncb) { return (size_t)(Ncb + 1) * LANES; }   // floats
-__host__ __device__ inline size_t sb_group_floats(uint32_t Ncb) {
+__host__ __device__ inline size_t sb_q16_off(uint32_t Ncb) {                                       // floats
   return sb_map_off(Ncb) + (size_t)((Ncb + 255) / 256) * LANES;
+}
+__host__ __device__ inline size_t sb_group_floats(uint32_t Ncb) {   // a multiple of 64 floats (256 B)
+  return sb_q16_off(Ncb) + (MI_SB_Q16 ? ((size_t)(Ncb + 1) * LANES / 2 + LANES - 1) / LANES * LANES : 0);
+}
+__host__ __device__ inline int16_t* sb_q16(float* sbg, uint32_t Ncb) {
+  return reinterpret_cast<int16_t*>(sbg + sb_q16_off(Ncb));
+}
+__host__ __device__ inline const int16_t* sb_q16(const float* sbg, uint32_t Ncb) {
+  return reinterpret_cast<const int16_t*>(sbg + sb_q16_off(Ncb));
+}
+// the mirror value of a softbuffer value (q16f, as an int16)
+__host__ __device__ inline int16_t q16s(float x) { return (int16_t)q16f(x); }
+// write element idx ([row][lane] index) of a group's mirror
+__host__ __device__ inline void sb_q16_put(float* sbg, uint32_t Ncb, size_t idx, int16_t v) {
+  if (MI_SB_Q16) sb_q16(sbg, Ncb)[idx] = v;
 }
 }  // namespace mi
 

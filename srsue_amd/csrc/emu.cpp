@@ -137,7 +137,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       const MiGroupDesc& g = P.groups[gi];
       float* sbg = &sb[g.sb_off];
       uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
-      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p,
+      for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, g.Ncb, p,
                                                               &P.kdata[P.ktabs[g.ktab].ipos_off]);
       const MiKTab& kt = P.ktabs[g.ktab];
       wms[gi].resize(g.K / mi::BETA_W + 1);
@@ -156,6 +156,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.live = (l0.valid ? 1u : 0u) | (paired && l1.valid ? 2u : 0u);
         if (!a.live) continue;
         a.sb[0] = &sb[gA.sb_off]; a.sb[1] = &sb[gB.sb_off];
+        a.sbq[0] = mi::sb_q16(a.sb[0], gA.Ncb); a.sbq[1] = mi::sb_q16(a.sb[1], gB.Ncb);
         a.wm[0] = wms[ga].data(); a.wm[1] = wms[gb].data();
         a.zrow[0] = gA.Ncb; a.zrow[1] = gB.Ncb;
         a.scr = reinterpret_cast<uint32_t*>(&scr[gA.scratch_off]);
@@ -213,7 +214,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               li[h] = cont[d];
               live |= 1u << h;
               const uint32_t g = li[h] / mi::LANES;
-              src[h] = {&sb[P.groups[g].sb_off], wms[g].data(),
+              src[h] = {&sb[P.groups[g].sb_off], mi::sb_q16(&sb[P.groups[g].sb_off], P.groups[g].Ncb), wms[g].data(),
                         reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li[h] % mi::LANES, ph[g]};
             }
             if (!live) continue;
@@ -263,7 +264,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
     if (g_x == 3 && g_q16) break;
     float* sbg = &sb[g.sb_off];
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + mi::sb_map_off(g.Ncb));
-    for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, map, p,
+    for (uint32_t p = 0; p < g.Ncb; p++) mi::rm_combine_row(&P.lanes[g.lane0], P.kdata.data(), e.data(), sbg, g.Ncb, p,
                                                               &P.kdata[P.ktabs[g.ktab].ipos_off]);
     const MiKTab& kt = P.ktabs[g.ktab];
     std::vector<uint32_t> wm(g.K / mi::BETA_W + 1);

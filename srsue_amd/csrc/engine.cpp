@@ -160,7 +160,15 @@ int Engine::upload(hipStream_t st, bool alloc_sb) {
   std::vector<size_t> offs;
   if (stage_tables(d_tables, offs, st)) return -1;
   bind_tables(d_tables, offs);
-  return ensure_work(st, alloc_sb);
+  if (ensure_work(st, alloc_sb)) return -1;
+  // per-lane outputs: padding lanes (a group's unused lanes) are never written by a decoder, so they read 0 in
+  // every batch plan, a re-planned workspace included (the kernels overwrite every valid lane's entry each run)
+  if (plan.lanes.size() && (plan.has_pdsch || plan.cb_n))
+    return hip_ok(hipMemsetAsync(d_cbits.p, 0, plan.lanes.size() * 4, st), "memset cb its") &&
+                   hip_ok(hipMemsetAsync(d_cbcrc.p, 0, plan.lanes.size() * 4, st), "memset cb crc")
+               ? 0
+               : -1;
+  return 0;
 }
 
 int Engine::plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, hipStream_t st) {

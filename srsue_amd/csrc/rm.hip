@@ -273,7 +273,10 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
       s_dra = ra;
       s_dnr = nr;
     }
-    if (ci == 0) sbg[(size_t)Ncb * LANES + tid] = 0.0f;   // the group's zero row
+    if (ci == 0) {   // the group's zero row, and its mirror's
+      sbg[(size_t)Ncb * LANES + tid] = 0.0f;
+      sb_q16_put(sbg, Ncb, (size_t)Ncb * LANES + tid, 0);
+    }
   }
   if (tid < RM_CHUNK / 4 && !direct) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
@@ -420,7 +423,11 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
 #pragma unroll
     for (int i = 0; i < NP; i++) {
       const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)rowv, i);
-      if ((uint32_t)i < nt && lvalid) sbg[(size_t)row * LANES + lane] = 0.0f + tile[lane][t0 + i];
+      if ((uint32_t)i < nt && lvalid) {
+        const float v = 0.0f + tile[lane][t0 + i];
+        sbg[(size_t)row * LANES + lane] = v;
+        sb_q16_put(sbg, Ncb, (size_t)row * LANES + lane, q16s(v));
+      }
     }
     return;
   }
@@ -474,6 +481,7 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
 #else
       sbg[row_of(i) * LANES + lane] = v;
 #endif
+      sb_q16_put(sbg, Ncb, row_of(i) * LANES + lane, q16s(v));   // the int16 mirror (dl_common.h)
     }
     mat_m |= (uint32_t)mat << i;
   }
@@ -518,7 +526,10 @@ __global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, co
     if (!comb) { map[p] = 0; continue; }
     const size_t row = MI_SB_NAT ? kdata[ktabs[g.ktab].ipos_off + pa + p] : pa + p;   // dl_common.h MI_SB_NAT
     for (int l = 0; l < LANES; l++)
-      if ((fresh >> l) & 1u) sbg[row * LANES + l] = 0.0f;
+      if ((fresh >> l) & 1u) {
+        sbg[row * LANES + l] = 0.0f;
+        sb_q16_put(sbg, g.Ncb, row * LANES + l, 0);
+      }
   }
 }
 
@@ -540,7 +551,10 @@ __global__ __launch_bounds__(256) void rm_direct_map_kernel(float* __restrict__ 
   const MiRmDirect d = dgs[blockIdx.x / RM_DIRECT_MAPB];
   const uint32_t part = blockIdx.x % RM_DIRECT_MAPB;
   float* sbg = sb + (size_t)d.sb64 * LANES;
-  if (part == 0 && threadIdx.x < LANES) sbg[(size_t)d.Ncb * LANES + threadIdx.x] = 0.0f;   // the zero row
+  if (part == 0 && threadIdx.x < LANES) {   // the zero row, and its mirror's
+    sbg[(size_t)d.Ncb * LANES + threadIdx.x] = 0.0f;
+    sb_q16_put(sbg, d.Ncb, (size_t)d.Ncb * LANES + threadIdx.x, 0);
+  }
   uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(d.Ncb));
   const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + d.rank_off);
   const uint32_t emax = d.emax_kind & 0xFFFFFFu;

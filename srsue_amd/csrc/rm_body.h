@@ -30,9 +30,11 @@ MI_HD inline float rm_value(const MiLaneDesc& ld, const int32_t* rank, const flo
 }
 
 // row p of a group (all lanes) with the sparse-row rule of rm_combine_kernel: the row is materialised
-// after the launch iff some lane receives an LLR there, or it was materialised and a lane combines
-MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, const float* e, float* sbg,
-                                 uint8_t* map, uint32_t p, const uint32_t* ipos) {
+// after the launch iff some lane receives an LLR there, or it was materialised and a lane combines; every
+// written value also goes to the row's int16 mirror
+MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, const float* e, float* sbg, uint32_t Ncb,
+                                 uint32_t p, const uint32_t* ipos) {
+  uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(Ncb));
   const size_t row = MI_SB_NAT ? ipos[p] : p;   // dl_common.h MI_SB_NAT
   bool comb = false, any = false;
   for (int l = 0; l < LANES; l++) comb |= lds[l].valid && !lds[l].new_tb;
@@ -50,7 +52,10 @@ MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, c
   const bool mat = any || (was && comb);
   if (mat)
     for (int l = 0; l < LANES; l++)
-      if (lds[l].valid) sbg[row * LANES + l] = v[l];
+      if (lds[l].valid) {
+        sbg[row * LANES + l] = v[l];
+        sb_q16_put(sbg, Ncb, row * LANES + l, q16s(v[l]));   // the int16 mirror (dl_common.h)
+      }
   map[p] = mat ? 1 : 0;
 }
 

@@ -212,6 +212,8 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   if (!a.live) return;   // the same on both wavefronts: no barrier is left waiting
   a.sb[0] = sb + gA.sb_off;
   a.sb[1] = sb + gB.sb_off;
+  a.sbq[0] = sb_q16(a.sb[0], gA.Ncb);
+  a.sbq[1] = sb_q16(a.sb[1], gB.Ncb);
   a.wm[0] = wm + (size_t)ga * WM_STRIDE;
   a.wm[1] = wm + (size_t)gb * WM_STRIDE;
   a.zrow[0] = gA.Ncb;
@@ -303,6 +305,7 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
       const uint32_t li = cont[1 + d], g = li / LANES;   // plan.cpp: group g = lanes 64 g .. 64 g + 63
       live |= 1u << h;
       s[h].sb = sb + groups[g].sb_off;
+      s[h].sbq = sb_q16(s[h].sb, groups[g].Ncb);
       s[h].wm = wm + (size_t)g * WM_STRIDE;
       s[h].scr = reinterpret_cast<const uint32_t*>(scratch + groups[g & ~1u].scratch_off);   // pairs (2j, 2j + 1)
       s[h].ls = li % LANES;

@@ -37,6 +37,7 @@ namespace mi {
 
 struct TdecArgsP2 {
   const float* sb[2];     // the two groups' softbuffers (dl_common.h sb_group_floats layout)
+  const int16_t* sbq[2];  // their int16 mirrors (dl_common.h sb_q16): what MI_TDEC_P2_QSB reads
   const uint32_t* wm[2];  // their window masks (rowmask_kernel)
   uint32_t zrow[2];       // their all-zero rows
   uint32_t* q;            // packed q rows [3 (K + 4)][64] (lo = group A, hi = group B)
@@ -57,6 +58,21 @@ struct TdecArgsP2 {
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 
+// MI_TDEC_P2_QSB (= MI_SB_Q16, off by default, dl_common.h): the channel inputs come from the softbuffer's int16 mirror (dl_common.h sb_q16_off:
+// q(x) written by rate de-matching beside every fp32 row): 2-byte loads from 128-B rows, and the pair is packed with
+// one v_lshl_or instead of quantised (2 fma + 2 med3 + perm).  Every pass reads the mirror -- later iterations too,
+// so the int16 q rows are never created (MI_TDEC_MKQ_IT does not apply); the compaction continuation still gathers
+// dense q rows (from the mirror).  The raw slot of a loaded input holds the zero-extended 16 bits.
+#ifndef MI_TDEC_P2_QSB
+#define MI_TDEC_P2_QSB MI_SB_Q16
+#endif
+// the raw slot of one loaded softbuffer input: the mirror's 16 bits zero-extended (QSB), or the fp32 value
+#if MI_TDEC_P2_QSB
+typedef uint32_t SbRaw;
+#else
+typedef float SbRaw;
+#endif
+
 // decoder-input quantiser q(x) = clamp(rint(32 x), +-511) of two floats, packed.  Device: fma(x, 32,
 // 1.5 * 2^23) rounds 32 x to the nearest (even) integer in the low mantissa bits (|32 x| < 2^22; beyond,
 // the clamp gives +-511 either way), med3 clamps in that domain, and the low 16 bits of the two results
@@ -73,6 +89,16 @@ MI_HD inline P2 q16_pair(float a, float b) {
 #endif
 }
 
+// the packed decoder input of two loaded softbuffer values (p2_sb_in): the mirror's two int16 words, or the two fp32
+// values quantised
+MI_HD inline P2 p2_qpair(SbRaw a, SbRaw b) {
+#if MI_TDEC_P2_QSB
+  return p2_from_bits(a | (b << 16));
+#else
+  return q16_pair(a, b);
+#endif
+}
+
 // DEC2's systematic input x2(k) = clamp(llr1(k) - w(k)) (tdec_body.h) is formed by DEC1 when it emits
 // step k -- w(k) is the a-priori row DEC1 has just read in natural order, and it is still the value DEC2
 // would read at row pi(k): DEC2 rewrites that row only after reading it -- and stored in the llr1 rows, so
@@ -86,7 +112,7 @@ MI_HD inline P2 q16_pair(float a, float b) {
 //   MKQ (DEC1, the q-creating pass): a0..a2 / b0..b2 = the three streams of both groups
 struct TdecWinP2 {
   uint32_t s0[BETA_W], s1[BETA_W];
-  float a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
+  SbRaw a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
   uint32_t r0[BETA_W], r1[BETA_W];
   uint32_t pk[BETA_W];   // DEC2: pi(k) of the window's steps (wave-uniform: scalar registers)
   uint32_t ck[7];
@@ -98,9 +124,11 @@ struct TdecWinP2 {
 #define MI_TDEC_P2_OOB 0
 #endif
 MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
-MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
+MI_HD inline SbRaw p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
   const bool on = (m >> dt) & 1u;
-#if MI_SB_NAT && MI_TDEC_P2_OOB && defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+#if MI_TDEC_P2_QSB
+  return (uint16_t)row_ld(a.sbq[h], on ? P.v[dt] : a.zrow[h], lane);
+#elif MI_SB_NAT && MI_TDEC_P2_OOB && defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
   // rows in decoder-input order (dl_common.h MI_SB_NAT): row P.v[0] + dt; an unmaterialised row reads as 0
   // through an out-of-range VGPR offset (the range check covers the VGPR offset, not soffset: tdec_body.h
   // sb_in) -- no zero-row select, no per-input row register
@@ -208,9 +236,9 @@ MI_HD inline void p2_ck_vec(const TdecWinP2& r, P2 (&v)[8]) { p2_ck_vec(r.ck, v)
 // decoder inputs (xs, xp) of step base + i; filler bits (k < F, known zeros; F < 64) of each half get
 // q(FILLER_LLR) = -511 in the systematic and parity-1 inputs
 template <bool SQ>
-MI_HD inline P2 p2_chan0(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s0[i]) : q16_pair(r.a0[i], r.b0[i]); }
+MI_HD inline P2 p2_chan0(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s0[i]) : p2_qpair(r.a0[i], r.b0[i]); }
 template <bool SQ>
-MI_HD inline P2 p2_chan1(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s1[i]) : q16_pair(r.a1[i], r.b1[i]); }
+MI_HD inline P2 p2_chan1(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s1[i]) : p2_qpair(r.a1[i], r.b1[i]); }
 MI_HD inline P2 p2_fill(P2 x, uint32_t k, const TdecArgsP2& a) {
   const int FILL = -(int)I16_CI;
   return p2_make(k < a.F[0] ? FILL : p2_lo(x), k < a.F[1] ? FILL : p2_hi(x));
@@ -264,9 +292,9 @@ MI_HD inline void p2_alpha_only_window(const TdecArgsP2& a, const TdecWinP2& w, 
 // the q-creating first pass (DEC1): quantise the window's three streams of both groups, store the packed
 // q rows, then the steps
 MI_HD inline void p2_store_q(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, int i, P2& q0, P2& q1) {
-  q0 = q16_pair(w.a0[i], w.b0[i]);
-  q1 = q16_pair(w.a1[i], w.b1[i]);
-  const P2 q2 = q16_pair(w.a2[i], w.b2[i]);
+  q0 = p2_qpair(w.a0[i], w.b0[i]);
+  q1 = p2_qpair(w.a1[i], w.b1[i]);
+  const P2 q2 = p2_qpair(w.a2[i], w.b2[i]);
   row_st(a.q, 3 * base, lane, p2_bits(q0), 3 * i);
   row_st(a.q, 3 * base, lane, p2_bits(q1), 3 * i + 1);
   row_st(a.q, 3 * base, lane, p2_bits(q2), 3 * i + 2);
@@ -651,7 +679,7 @@ struct TdecP2X {
         const PosW PT = MI_POSW(a, 3 * K);
 #pragma unroll
         for (int j = 0; j < 12; j++) {
-          const P2 q = q16_pair(p2_sb_in(a, 0, ma, PT, j, lane), p2_sb_in(a, 1, mb, PT, j, lane));
+          const P2 q = p2_qpair(p2_sb_in(a, 0, ma, PT, j, lane), p2_sb_in(a, 1, mb, PT, j, lane));
           row_st(a.q, 3 * K, lane, p2_bits(q), j);
           if (j < 6) { if (j & 1) tp[j / 2] = q; else tx[j / 2] = q; }
         }
@@ -661,8 +689,8 @@ struct TdecP2X {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
           const uint32_t d = t0 - 3 * K + 2 * j;
-          tx[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d, lane), p2_sb_in(a, 1, mb, PT, d, lane));
-          tp[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d + 1, lane), p2_sb_in(a, 1, mb, PT, d + 1, lane));
+          tx[j] = p2_qpair(p2_sb_in(a, 0, ma, PT, d, lane), p2_sb_in(a, 1, mb, PT, d, lane));
+          tp[j] = p2_qpair(p2_sb_in(a, 0, ma, PT, d + 1, lane), p2_sb_in(a, 1, mb, PT, d + 1, lane));
         }
       } else {
 #pragma unroll
@@ -839,7 +867,7 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
   if constexpr (CONT) tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
   for (uint32_t it = CONT ? 1u : 0u; it < a.max_its && active; it++) {
-    constexpr uint32_t MK = MI_TDEC_MKQ_IT;
+    constexpr uint32_t MK = MI_TDEC_P2_QSB ? 0xFFFFFFFFu : MI_TDEC_MKQ_IT;   // QSB: every pass reads the mirror
     if constexpr (CONT) {
       tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex);
       tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
@@ -895,6 +923,7 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
 // goes by q window (12 rows: one window-mask word per source) and by w row.
 struct P2ContSrc {
   const float* sb;      // the code block's group softbuffer
+  const int16_t* sbq;   // its int16 mirror (MI_TDEC_P2_QSB)
   const uint32_t* wm;   // the group's window masks
   const uint32_t* scr;  // the scratch of the group's pair (w rows: packed, this code block = half hs)
   uint32_t ls, hs;      // lane in the group, half in the pair
@@ -906,6 +935,17 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
   uint32_t m[2];
 #pragma unroll
   for (int h = 0; h < 2; h++) m[h] = ((live >> h) & 1u) ? s[h].wm[w] : 0u;
+#if MI_TDEC_P2_QSB
+  uint32_t v[3 * BETA_W][2];
+#pragma unroll
+  for (int i = 0; i < 3 * BETA_W; i++) {
+    const size_t row = MI_SB_NAT ? 3 * BETA_W * w + i : pos[3 * BETA_W * w + i];
+#pragma unroll
+    for (int h = 0; h < 2; h++) v[i][h] = ((m[h] >> i) & 1u) ? (uint16_t)s[h].sbq[row * LANES + s[h].ls] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 3 * BETA_W; i++) q[i] = v[i][0] | (v[i][1] << 16);
+#else
   float v[3 * BETA_W][2];
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) {
@@ -915,6 +955,7 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
   }
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
+#endif
 }
 // x2 row k (the llr1 rows, at K) of one continuation lane: each half's 16-bit iteration-0 DEC1 output from its
 // source pair's packed row
