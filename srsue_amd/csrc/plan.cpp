@@ -484,6 +484,39 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         else if (!direct[gi]) idle.push_back(((uint32_t)gi << 9) | c);   // direct groups: the map kernel
       }
     }
+    // XCD queues (round 4): workgroup b of a launch runs on XCD b mod 8 (dispatch deals blocks round-robin over
+    // the 8 XCDs; speed only, never correctness).  The chunks of one group read the same subframes' grid and
+    // channel-estimate lines -- each chunk a few REs per code block, so every line is shared by neighbouring
+    // chunks and the compact estimates' pilot rows by all of them -- but dealt in launch order they land on all
+    // eight XCDs and every XCD's L2 fetches the group's lines again (TCC_EA0_RDREQ: 6.8 GB per 12,500 subframes
+    // against ~2 GB of distinct bytes).  So whole groups go to one queue (the least-loaded one, in group order),
+    // each queue keeps its groups' chunks in order, and launch position 8 i + q takes queue q's item i; the
+    // shorter queues are padded with empty items (chunk 511: the kernel returns at its first test).
+    auto xcd_order = [](std::vector<uint32_t>& its) {
+      if (its.empty()) return;
+      std::vector<std::vector<uint32_t>> q(8);
+      std::vector<size_t> load(8, 0);
+      for (size_t a = 0; a < its.size();) {
+        size_t b = a;
+        while (b < its.size() && (its[b] >> 9) == (its[a] >> 9)) b++;   // one group's chunks
+        const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+        q[k].insert(q[k].end(), its.begin() + a, its.begin() + b);
+        load[k] += b - a;
+        a = b;
+      }
+      const size_t len = *std::max_element(load.begin(), load.end());
+      its.assign(8 * len, 0u);
+      for (size_t i = 0; i < len; i++)
+        for (size_t k = 0; k < 8; k++) its[8 * i + k] = i < q[k].size() ? q[k][i] : ((q[k].empty() ? 0u : q[k][0] >> 9) << 9) | 511u;
+    };
+    static const bool xcdq = [] {
+      const char* env = getenv("MI_RM_XCDQ");   // A/B: 0 = launch order
+      return !env || atoi(env) != 0;
+    }();
+    if (xcdq) {
+      xcd_order(rm_items);
+      xcd_order(gbusy);
+    }
     rm_dbusy = (uint32_t)rm_items.size();   // direct groups' chunks first (their own launch, rm.hip)
     rm_items.insert(rm_items.end(), gbusy.begin(), gbusy.end());
     rm_busy = (uint32_t)rm_items.size();
