@@ -31,6 +31,8 @@ extern "C" void emu_set_tdec_x(int on) { g_x = on; }
 static int g_compact = 0;
 static uint64_t g_cont_cbs = 0;
 extern "C" void emu_set_tdec_compact(int on) { g_compact = on; g_cont_cbs = 0; }
+static int g_store_w = 0;   // compaction: the first launch stores its w rows, the continuation gathers them
+extern "C" void emu_set_tdec_store_w(int on) { g_store_w = on; }
 extern "C" uint64_t emu_cont_codeblocks() { return g_cont_cbs; }
 template <bool Q16>
 static mi::TdecLaneResult emu_lane_x(const mi::TdecArgs& a, int lane) {
@@ -170,7 +172,8 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.F[0] = l0.F; a.F[1] = paired ? l1.F : l0.F;
 
         a.max_its = g_compact && max_its > 1 ? 1 : max_its; a.early_stop = 1;
-        a.no_w = a.max_its == 1;   // tdec.hip tdec_kernel_p2x
+        a.cont_w = 0;
+        a.no_w = a.max_its == 1 && !g_store_w;   // tdec.hip launch_tdec_p2
         mi::TdecP2ExecHost ex;
         const mi::TdecP2Result r = mi::tdec_p2_lane(a, lane, ex);
         for (int h = 0; h < 2; h++) {
@@ -224,8 +227,10 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               mi::p2_cont_qwin(src, live, pos, w, q);
               for (int i = 0; i < 3 * mi::BETA_W; i++) cq[(size_t)(3 * mi::BETA_W * w + i) * mi::LANES + lane] = q[i];
             }
-            for (uint32_t k = 0; k < K; k++)
-              cscr[(size_t)(K + k) * mi::LANES + lane] = mi::p2_cont_xrow(src, live, K, k);
+            for (uint32_t k = 0; k < K; k++) {
+              if (g_store_w) cscr[(size_t)k * mi::LANES + lane] = mi::p2_cont_wrow(src, live, k);
+              else cscr[(size_t)(K + k) * mi::LANES + lane] = mi::p2_cont_xrow(src, live, K, k);
+            }
           }
           for (int lane = 0; lane < mi::LANES; lane++) {
             uint32_t li[2] = {0, 0};
@@ -246,7 +251,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               a.F[h] = P.lanes[li[h]].F;
 
             }
-            a.K = K; a.max_its = max_its; a.early_stop = 1;
+            a.K = K; a.max_its = max_its; a.early_stop = 1; a.cont_w = g_store_w;
             mi::TdecP2ExecHost ex;
             const mi::TdecP2Result r = mi::tdec_p2_lane<true>(a, lane, ex);
             for (int h = 0; h < 2; h++) {

@@ -46,6 +46,7 @@ Engine::~Engine() {
     (void)hipEventDestroy(stage_done);
   }
   if (h_stage) (void)hipHostFree(h_stage);
+  if (h_cont) (void)hipHostFree(h_cont);
   for (auto& set : ev_sets)
     for (auto& e : set) (void)hipEventDestroy(e);
 }
@@ -396,11 +397,25 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
     const bool cont = tdec_compact() && d_cscr.bytes >= (size_t)cont_max_pairs() * cont_pair_u32() * 4 &&
                       d_cont.bytes >= (P.lanes.size() + 1) * 4 &&
                       d_cdec.bytes >= (size_t)cont_max_pairs() * P.groups[0].K * LANES;
+    // The one-iteration first launch stores no extrinsic rows w when few code blocks continue (the continuation
+    // re-forms them by re-running iteration 0's DEC2 from gathered x2 rows: 12 KB per code block less for all, about
+    // half an iteration more for the continuing ones); when the previous run of this workspace continued more than
+    // 2 % of its code blocks (the waterfall), it stores them and the continuation gathers them instead.  Both are
+    // exact: only the schedule depends on the history.  MI_TDEC_STORE_W=0 / 1 forces (A/B).
+    bool store_w = false;
+    if (cont) {
+      if (!h_cont && hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h_cont), 4, hipHostMallocDefault), "pinned"))
+        *h_cont = 0;
+      const char* fe = getenv("MI_TDEC_STORE_W");   // read per run: tests switch it
+      const int force = fe ? atoi(fe) : -1;
+      const uint32_t last = h_cont ? *reinterpret_cast<volatile uint32_t*>(h_cont) : 0u;
+      store_w = force >= 0 ? force != 0 : (uint64_t)last * 50 > P.lanes.size();
+    }
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                    d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), d_pairs.as<uint32_t>(),
                    (uint32_t)(P.pairs.size() / 2), cont ? 1u : max_its, early_stop, direct ? d_payload.as<uint8_t>() : nullptr,
-                   st);
+                   cont && !store_w, st);
     if (cont) {
       // the code blocks still failing after iteration 0, compacted into dense pairs for iterations 1 ..
       launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
@@ -408,7 +423,8 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
                        d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
                        (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048,
-                       direct ? d_payload.as<uint8_t>() : nullptr, st);
+                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, st);
+      if (h_cont) (void)hipMemcpyAsync(h_cont, d_cont.p, 4, hipMemcpyDeviceToHost, st);
     }
     return;
   }

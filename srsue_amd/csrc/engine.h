@@ -45,7 +45,10 @@ struct Engine {
   size_t cont_pair_u32() const;   // continuation pair scratch, u32 words
   uint32_t cont_max_pairs() const;
   void launch_turbo(float* sb, hipStream_t st);
-  bool tb_copied = false;   // the last turbo stage wrote the payload bytes itself (packed decoder, PDSCH batch)
+  bool tb_copied = false;
+  // waterfall compaction: the previous run's number of continuing code blocks (page-locked, copied back after every
+  // compacted run; read without waiting -- it only steers whether the first launch stores its extrinsic rows)
+  uint32_t* h_cont = nullptr;   // the last turbo stage wrote the payload bytes itself (packed decoder, PDSCH batch)
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,

@@ -49,6 +49,7 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
                     const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
                     uint32_t n_pairs, uint32_t max_its, uint32_t early_stop,
                     uint8_t* payload /* PDSCH batches: payload bytes written in place; nullptr = cb_bytes rows */,
+                    bool no_w /* DEC2 stores no extrinsic rows (a one-iteration first launch, tdec_p2_body.h) */,
                     hipStream_t st);
 // waterfall compaction after iteration 0 of launch_tdec_p2 (one K, early stop; tdec_p2_body.h P2ContSrc):
 // gather the CRC-failing code blocks into dense continuation pairs (cscr: max_pairs x pair_u32 words, cdec:
@@ -57,7 +58,8 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch,
                       uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                       const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
                       uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      uint8_t* payload, hipStream_t st);
+                      uint8_t* payload, bool w_stored /* the first launch stored w rows: gather them (no DEC2 re-run) */,
+                      hipStream_t st);
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
 void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,

@@ -191,7 +191,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                      const uint32_t* __restrict__ kdata, const uint32_t* __restrict__ pairs, uint32_t max_its,
-                     uint32_t early_stop) {
+                     uint32_t early_stop, uint32_t no_w) {
   __shared__ uint32_t crc8[256], crc8b[256];
   __shared__ uint32_t xs[LANES];
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
@@ -235,7 +235,8 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.F[1] = paired ? l1.F : l0.F;
   a.max_its = max_its;
   a.early_stop = early_stop;
-  a.no_w = max_its == 1;   // nothing reads this launch's w rows (the continuation re-forms them)
+  a.cont_w = 0;
+  a.no_w = no_w;   // a one-iteration first launch whose continuation re-forms the w rows (launch_tdec_p2)
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   const TdecP2Result r = tdec_p2_lane(a, lane, ex);
   if (ex.wave) return;
@@ -251,7 +252,8 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
 void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes,
                     uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                     const MiLaneDesc* lanes, const MiKTab* ktabs, const uint32_t* ktab_data, const uint32_t* pairs,
-                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, uint8_t* payload, hipStream_t st) {
+                    uint32_t n_pairs, uint32_t max_its, uint32_t early_stop, uint8_t* payload, bool no_w,
+                    hipStream_t st) {
   if (!n_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   // MI_TDEC_P2_LDS (A/B knob, bytes): unused dynamic LDS per workgroup, capping the workgroups one CU holds
@@ -261,7 +263,7 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
     return e ? (size_t)atol(e) : (size_t)0;
   }();
   hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), dyn_lds, st, sb, wm, scratch, dec, out, groups, lanes,
-                     ktabs, ktab_data, pairs, max_its, early_stop);
+                     ktabs, ktab_data, pairs, max_its, early_stop, (uint32_t)(no_w && max_its == 1));
 }
 
 // ---- waterfall compaction (tdec_p2_body.h P2ContSrc): one K, early stop, iteration 0 done by
@@ -282,8 +284,9 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
   if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
 }
 
-// 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 x2 rows);
-// lane = continuation lane, both halves
+// 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 rows of iteration 0's
+// state: the x2 rows (DEC1 outputs, at K) when the first launch stored no w rows -- the continuation re-runs DEC2 --,
+// else its w rows (at 0)); lane = continuation lane, both halves
 constexpr uint32_t CONT_QW = 8, CONT_WR = 96;
 __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __restrict__ sb,
                                                                const uint32_t* __restrict__ wm,
@@ -291,7 +294,8 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
                                                                const MiGroupDesc* __restrict__ groups,
                                                                const uint32_t* __restrict__ pos,
                                                                const uint32_t* __restrict__ cont,
-                                                               uint32_t* __restrict__ cscr, size_t pair_u32, uint32_t K) {
+                                                               uint32_t* __restrict__ cscr, size_t pair_u32, uint32_t K,
+                                                               uint32_t w_stored) {
   const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
   const uint32_t nqw = p2_cont_qwins(K), nqt = (nqw + CONT_QW - 1) / CONT_QW, per = nqt + (K + CONT_WR - 1) / CONT_WR;
   for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * per; u += gridDim.x * 4) {
@@ -322,8 +326,13 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
       }
     } else {
       const uint32_t k0 = (c - nqt) * CONT_WR, k1 = min(K, k0 + CONT_WR);
+      if (w_stored) {
 #pragma unroll 8
-      for (uint32_t k = k0; k < k1; k++) dst[(size_t)(K + k) * LANES + lane] = p2_cont_xrow(s, live, K, k);
+        for (uint32_t k = k0; k < k1; k++) dst[(size_t)k * LANES + lane] = p2_cont_wrow(s, live, k);
+      } else {
+#pragma unroll 8
+        for (uint32_t k = k0; k < k1; k++) dst[(size_t)(K + k) * LANES + lane] = p2_cont_xrow(s, live, K, k);
+      }
     }
   }
 }
@@ -332,7 +341,8 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
-                     const uint32_t* __restrict__ cont, size_t pair_u32, uint32_t K, uint32_t max_its) {
+                     const uint32_t* __restrict__ cont, size_t pair_u32, uint32_t K, uint32_t max_its,
+                     uint32_t w_stored) {
   __shared__ uint32_t crc8[256], crc8b[256];
   __shared__ uint32_t xs[LANES];
   const uint32_t n = cont[0], p = blockIdx.x;
@@ -364,6 +374,7 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.F[1] = l1.F;
   a.max_its = max_its;
   a.early_stop = 1;
+  a.cont_w = w_stored;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   const TdecP2Result r = tdec_p2_lane<true>(a, lane, ex);
   if (ex.wave) return;
@@ -380,15 +391,15 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch,
                       uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                       const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
                       uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      uint8_t* payload, hipStream_t st) {
+                      uint8_t* payload, bool w_stored, hipStream_t st) {
   if (!n_groups || !max_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   (void)hipMemsetAsync(cont, 0, 4, st);
   hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
-                     ktab_data + kt.pos_off, cont, cscr, pair_u32, K);
+                     ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored);
   hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes, ktab_data, kt, cont,
-                     pair_u32, K, max_its);
+                     pair_u32, K, max_its, (uint32_t)w_stored);
 }
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,

@@ -116,12 +116,19 @@ MI_HD inline void beta_step(const T (&bn)[8], T xs, T xp, T (&bk)[8]) {
   }
 }
 
+// The packed int16 decoder (P2) takes each 8-term maximum of the LLR as two interleaved chains joined at the end
+// (half the dependent depth); an integer maximum is exact in any order.  The float decoders keep their single chains
+// (fmaxf's choice between -0 and +0 could depend on the order).
+#ifndef MI_TDEC_P2_TREE
+#define MI_TDEC_P2_TREE 1   // A/B switch: 0 = single chains in the packed decoder too
+#endif
+
 // one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1} (NORM: alpha normalised)
 // (max(-inf, t) = t exactly, so the maxima start from the first term)
 template <bool NORM = true, class T>
 MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
   const T luz = xs + xp;
-  T c[8][2], m0 = T{}, m1 = T{};
+  T c[8][2], m0 = T{}, m1 = T{}, t8[2][8];
 #pragma unroll
   for (int s = 0; s < 8; s++) {
 #pragma unroll
@@ -129,8 +136,15 @@ MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
       const int z = tr_par(s, u);
       c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
       T t = c[s][u] + bn[tr_next(s, u)];
-      if (u) m1 = s ? fmaxf(m1, t) : t; else m0 = s ? fmaxf(m0, t) : t;
+      t8[u][s] = t;
+      if constexpr (!(MI_TDEC_P2_TREE && std::is_same<T, P2>::value)) {
+        if (u) m1 = s ? fmaxf(m1, t) : t; else m0 = s ? fmaxf(m0, t) : t;
+      }
     }
+  }
+  if constexpr (MI_TDEC_P2_TREE && std::is_same<T, P2>::value) {   // two interleaved chains per maximum (llr_step)
+    m0 = fmaxf(fmaxf(fmaxf(t8[0][0], t8[0][2]), fmaxf(t8[0][4], t8[0][6])), fmaxf(fmaxf(t8[0][1], t8[0][3]), fmaxf(t8[0][5], t8[0][7])));
+    m1 = fmaxf(fmaxf(fmaxf(t8[1][0], t8[1][2]), fmaxf(t8[1][4], t8[1][6])), fmaxf(fmaxf(t8[1][1], t8[1][3]), fmaxf(t8[1][5], t8[1][7])));
   }
   T llr = m1 - m0;
   T na[8];
@@ -274,7 +288,15 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
   else row_st(scr, row, lane, v, crow);
 }
 
-#if MI_SB_NAT || defined(MI_TDEC_DIAG_SEQ)   // rows in decoder-input order (dl_common.h MI_SB_NAT)
+#if MI_SB_NAT && defined(MI_TDEC_DIAG_NOPI)   // timing diagnostic only: the QPP table replaced by a hash (wrong results)
+#define MI_POS(a, t) ((uint32_t)(t))
+#if MI_TDEC_DIAG_NOPI == 2   // ... by the identity: DEC2's interleaved rows read in sequence
+#define MI_PI(a, k) ((uint32_t)(k))
+#else
+#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
+#endif
+#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
+#elif MI_SB_NAT || defined(MI_TDEC_DIAG_SEQ)   // rows in decoder-input order (dl_common.h MI_SB_NAT)
 #define MI_POS(a, t) ((uint32_t)(t))
 #define MI_PI(a, k) ((a).pi[k])
 #define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
@@ -764,6 +786,26 @@ MI_HD inline void alpha_fwd(T (&al)[8], T xs, T xp) {
 // packed int16 decoder's first trellis steps, where "-inf" is a finite stand-in, tdec_p2_body.h)
 template <uint32_t REACH = 0xFFu, class T>
 MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
+  if constexpr (MI_TDEC_P2_TREE && std::is_same<T, P2>::value) {
+    // packed int16: the same terms, each maximum as two interleaved chains (states of even / odd rank among the
+    // reachable ones) joined at the end: half the dependent depth, two more live accumulators
+    const T luz = xs + xp;
+    T m[2][2] = {};
+    int n = 0;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      if (!((REACH >> s) & 1u)) continue;
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int z = tr_par(s, u);
+        const T t = ((u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s]) + bn[tr_next(s, u)];
+        m[u][n & 1] = n < 2 ? t : fmaxf(m[u][n & 1], t);
+      }
+      n++;
+    }
+    const T m1 = n > 1 ? fmaxf(m[1][0], m[1][1]) : m[1][0], m0 = n > 1 ? fmaxf(m[0][0], m[0][1]) : m[0][0];
+    return m1 - m0;
+  }
   const T luz = xs + xp;
   T m0 = T{}, m1 = T{};
   bool f0 = true, f1 = true;

@@ -55,6 +55,7 @@ struct TdecArgsP2 {
   uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
   uint32_t no_w;          // wave-uniform: DEC2 stores no extrinsic rows w (a one-iteration launch: nothing reads
                           // them -- the compaction continuation re-runs DEC2 of iteration 0 instead, tdec_p2_lane)
+  uint32_t cont_w;        // continuation only: iteration 0's w rows were gathered (no DEC2 re-run)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 
@@ -591,16 +592,30 @@ MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const Tdec
 #ifndef MI_TDEC_P2_PF_Q
 #define MI_TDEC_P2_PF_Q 1
 #endif
+// the waterfall continuation (tdec_kernel_p2c) runs few wavefronts (0.74 per SIMD at the 21.5 dB bench point), each a
+// lone chain.  Its checkpoint spacing is a parameter of its own: 4-step checkpoints (6 recursion steps per 8 instead of
+// 12) shorten a lone chain (one stream, same box: waterfall tdec 21.95 -> 21.25 ms) but move twice the checkpoint bytes,
+// and beside the other streams' batches that costs more than it saves (4 streams: waterfall 56.7-57.2 Gbps with 8-step
+// checkpoints, 53.0-53.8 with 4-step ones; profiles/r4/ab_cont_ck): 8-step by default.  Its q-row loads stay one
+// window ahead (two: 17 VGPRs spilled at the 3-waves-per-SIMD budget)
+#ifndef MI_TDEC_P2C_CK8
+#define MI_TDEC_P2C_CK8 1
+#endif
+#ifndef MI_TDEC_P2C_PF_Q
+#define MI_TDEC_P2C_PF_Q 1
+#endif
 #ifndef MI_TDEC_P2_PF_SB
 #define MI_TDEC_P2_PF_SB MI_TDEC_PF_SB
 #endif
 // the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
-template <bool DEC2, bool FIRST, int SRC>
+// CK8: 8-step checkpoints (MI_TDEC_P2_CK8) or 4-step ones; PFQ: windows of q-row loads in flight (MI_TDEC_P2_PF_Q).
+// The first launch takes the defaults; the waterfall continuation its own (tdec_p2_lane)
+template <bool DEC2, bool FIRST, int SRC, bool CK8 = MI_TDEC_P2_CK8, int PFQ = MI_TDEC_P2_PF_Q>
 struct TdecP2X {
   static constexpr bool MKQ = !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = SRC == SRC_Q;    // backward-side passes read q rows
   static constexpr bool SQF = SRC != SRC_SB;   // forward-side passes read q rows
-  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_P2_PF_SB : MI_TDEC_P2_PF_Q;
+  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_P2_PF_SB : PFQ;
   using Win = TdecWinP2;
 
   MI_HD static void load1(const TdecArgsP2& a, int lane, uint32_t w, Win& r) {
@@ -616,7 +631,7 @@ struct TdecP2X {
     pipe_windows<PF, Win>(
         (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
-          if (w && (!MI_TDEC_P2_CK8 || !((h - w) & 1u))) p2_ck_store(a.scr, ck, w, lane, al);
+          if (w && (!CK8 || !((h - w) & 1u))) p2_ck_store(a.scr, ck, w, lane, al);
           if constexpr (MKQ) p2_alpha_only_window_mkq(a, lane, r, w * BETA_W, al);
           else p2_alpha_only_window<DEC2, SQB>(a, r, w * BETA_W, al);
         });
@@ -625,44 +640,44 @@ struct TdecP2X {
   MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
     const uint32_t nw = a.K / BETA_W, h = nw / 2;
     const size_t ck = (size_t)2 * a.K;
-#if MI_TDEC_P2_CK8
-    // pairs (h + 2j, h + 2j + 1), beta checkpoint h + 2j + 2; an odd count leaves window nw - 1 alone
-    const uint32_t n = nw - h, np = n / 2;
-    auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
-      p2_ck_load_to(a.scr, ck, w0 + 2, lane, r.ck);
-    };
-    if (np) {
-      TdecWin8P2 r;
-      load8(h, r);
-      for (uint32_t j = 0; j < np; j++) {
-        const uint32_t w0 = h + 2 * j;
-        TdecX8P2 x;
-        P2 B8[8];
-        p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
-        p2_ck_vec(r.ck, B8);
-        MI_SCHED_FENCE();
-        load8(j + 1 < np ? w0 + 2 : w0, r);   // the last pair reloads itself (unused)
-        MI_SCHED_FENCE();
-        p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
+    if constexpr (CK8) {
+      // pairs (h + 2j, h + 2j + 1), beta checkpoint h + 2j + 2; an odd count leaves window nw - 1 alone
+      const uint32_t n = nw - h, np = n / 2;
+      auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
+        p2_ck_load_to(a.scr, ck, w0 + 2, lane, r.ck);
+      };
+      if (np) {
+        TdecWin8P2 r;
+        load8(h, r);
+        for (uint32_t j = 0; j < np; j++) {
+          const uint32_t w0 = h + 2 * j;
+          TdecX8P2 x;
+          P2 B8[8];
+          p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+          p2_ck_vec(r.ck, B8);
+          MI_SCHED_FENCE();
+          load8(j + 1 < np ? w0 + 2 : w0, r);   // the last pair reloads itself (unused)
+          MI_SCHED_FENCE();
+          p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
+        }
       }
+      if (n & 1u) {
+        Win r;
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, (nw - 1) * BETA_W, r);
+        p2_ck_load(a.scr, ck, nw, lane, r);
+        p2_alpha_window<DEC2, SQF>(a, lane, r, (nw - 1) * BETA_W, al);
+      }
+    } else {
+      pipe_windows<PF, Win>(
+          (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
+          [&](uint32_t w, Win& r) {
+            p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
+            p2_ck_load(a.scr, ck, w + 1, lane, r);
+          },
+          [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al); });
     }
-    if (n & 1u) {
-      Win r;
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, (nw - 1) * BETA_W, r);
-      p2_ck_load(a.scr, ck, nw, lane, r);
-      p2_alpha_window<DEC2, SQF>(a, lane, r, (nw - 1) * BETA_W, al);
-    }
-#else
-    pipe_windows<PF, Win>(
-        (int)(nw - h), [h](int i) { return h + (uint32_t)i; },
-        [&](uint32_t w, Win& r) {
-          p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
-          p2_ck_load(a.scr, ck, w + 1, lane, r);
-        },
-        [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al); });
-#endif
   }
   // wave B, phase 1: tail, then beta_K .. beta_{K/2}, beta checkpoints h + 1 .. nw
   MI_HD static void b1(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
@@ -714,69 +729,69 @@ struct TdecP2X {
         [&](const Win& r, uint32_t w) {
           if constexpr (MKQ) p2_beta_window_mkq(a, lane, r, w * BETA_W, b);
           else p2_beta_window<DEC2, SQB>(a, r, w * BETA_W, b);
-          if (w > h && (!MI_TDEC_P2_CK8 || !((w - h) & 1u))) p2_ck_store(a.scr, ck, w, lane, b);
+          if (w > h && (!CK8 || !((w - h) & 1u))) p2_ck_store(a.scr, ck, w, lane, b);
         });
   }
   // wave B, phase 2: windows h - 1 .. 0 backward, LLRs of steps 0 .. K/2 - 1
   MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
-#if MI_TDEC_P2_CK8
-    // pairs (h - 2j - 2, h - 2j - 1), alpha checkpoint h - 2j - 2 (pair 0: the start state); an odd h
-    // leaves window 0 alone
-    const uint32_t np = h / 2;
-    auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
-      p2_ck_load_to(a.scr, ck, w0, lane, r.ck);   // w0 = 0: slot 0 is loaded but not used
-    };
-    if (np) {
-      TdecWin8P2 r;
-      load8(h - 2, r);
-      for (uint32_t j = 0; j < np; j++) {
-        const uint32_t w0 = h - 2 * j - 2;
-        TdecX8P2 x;
-        P2 A0[8];
-        p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
-        if (w0) {
-          p2_ck_vec(r.ck, A0);
-        } else {
-#pragma unroll
-          for (int s = 0; s < 8; s++) A0[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    if constexpr (CK8) {
+      // pairs (h - 2j - 2, h - 2j - 1), alpha checkpoint h - 2j - 2 (pair 0: the start state); an odd h
+      // leaves window 0 alone
+      const uint32_t np = h / 2;
+      auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
+        p2_ck_load_to(a.scr, ck, w0, lane, r.ck);   // w0 = 0: slot 0 is loaded but not used
+      };
+      if (np) {
+        TdecWin8P2 r;
+        load8(h - 2, r);
+        for (uint32_t j = 0; j < np; j++) {
+          const uint32_t w0 = h - 2 * j - 2;
+          TdecX8P2 x;
+          P2 A0[8];
+          p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+          if (w0) {
+            p2_ck_vec(r.ck, A0);
+          } else {
+  #pragma unroll
+            for (int s = 0; s < 8; s++) A0[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+          }
+          MI_SCHED_FENCE();
+          load8(j + 1 < np ? w0 - 2 : w0, r);   // the last pair reloads itself (unused)
+          MI_SCHED_FENCE();
+          if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b);
+          else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b);
         }
-        MI_SCHED_FENCE();
-        load8(j + 1 < np ? w0 - 2 : w0, r);   // the last pair reloads itself (unused)
-        MI_SCHED_FENCE();
-        if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b);
-        else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b);
       }
+      if (h & 1u) {
+        Win r;
+        p2_load_window<DEC2, FIRST, SQF>(a, lane, 0, r);
+        p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
+      }
+    } else {
+      pipe_windows<PF, Win>(
+          (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
+          [&](uint32_t w, Win& r) {
+            p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
+            p2_ck_load(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
+          },
+          [&](const Win& r, uint32_t w) {
+            if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b);
+            else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
+          });
     }
-    if (h & 1u) {
-      Win r;
-      p2_load_window<DEC2, FIRST, SQF>(a, lane, 0, r);
-      p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
-    }
-#else
-    pipe_windows<PF, Win>(
-        (int)h, [h](int i) { return h - 1 - (uint32_t)i; },
-        [&](uint32_t w, Win& r) {
-          p2_load_window<DEC2, FIRST, SQF>(a, lane, w * BETA_W, r);
-          p2_ck_load(a.scr, ck, w, lane, r);   // window 0: slot 0 is loaded but not used
-        },
-        [&](const Win& r, uint32_t w) {
-          if (w) p2_beta_emit_window<DEC2, SQF, false>(a, lane, r, w * BETA_W, b);
-          else p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
-        });
-#endif
   }
 };
 
 #ifndef MI_TDEC_P2_DIAG
 #define MI_TDEC_P2_DIAG 0
 #endif
-template <bool DEC2, bool FIRST, int SRC, class Exec>
+template <bool DEC2, bool FIRST, int SRC, bool CK8 = MI_TDEC_P2_CK8, int PFQ = MI_TDEC_P2_PF_Q, class Exec>
 MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
-  using X = TdecP2X<DEC2, FIRST, SRC>;
+  using X = TdecP2X<DEC2, FIRST, SRC, CK8, PFQ>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
 #if MI_TDEC_P2_DIAG != 2   // timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone
@@ -865,12 +880,15 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
   uint32_t active = a.live & 3u;
   // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
-  if constexpr (CONT) tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
+  constexpr bool CK = CONT ? MI_TDEC_P2C_CK8 : MI_TDEC_P2_CK8;
+  constexpr int PQ = CONT ? MI_TDEC_P2C_PF_Q : MI_TDEC_P2_PF_Q;
+  if constexpr (CONT)
+    if (!a.cont_w) tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
   for (uint32_t it = CONT ? 1u : 0u; it < a.max_its && active; it++) {
     constexpr uint32_t MK = MI_TDEC_P2_QSB ? 0xFFFFFFFFu : MI_TDEC_MKQ_IT;   // QSB: every pass reads the mirror
     if constexpr (CONT) {
-      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_Q, CK, PQ>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
     } else if (it == 0) {
       if (MK == 0) {
         tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex);
@@ -956,6 +974,15 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
 #endif
+}
+// w row k (at 0) of one continuation lane: each half's 16-bit iteration-0 extrinsic from its source pair's packed row
+// (a first launch that stored its w rows)
+MI_HD inline uint32_t p2_cont_wrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t k) {
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)k * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
+  return w[0] | (w[1] << 16);
 }
 // x2 row k (the llr1 rows, at K) of one continuation lane: each half's 16-bit iteration-0 DEC1 output from its
 // source pair's packed row

@@ -167,8 +167,11 @@ def test_waterfall_compaction_matches_uncompacted(monkeypatch):
     iqs = [abi.tx_subframe(c, tb_bytes(7000 + j, TBS), snr_db=16.0 + 9.0 * j / (pool - 1), seed=0xC000 + j)
            for j, c in enumerate(pcfgs)]
     outs = []
-    for compact in ("1", "0", "1"):
+    # compacted with the first launch's extrinsic rows dropped (re-formed by the continuation), uncompacted, and
+    # compacted with them stored and gathered (engine.cpp: the waterfall's choice)
+    for compact, store_w in (("1", "0"), ("0", "0"), ("1", "1")):
         monkeypatch.setenv("MI_TDEC_COMPACT", compact)
+        monkeypatch.setenv("MI_TDEC_STORE_W", store_w)
         b, _ = run_bench_config(n, iqs)
         assert b.turbo_sched == "p2", b.turbo_sched
         outs.append([b.download(k, np.uint32 if k != abi.BUF_PAYLOAD else np.uint8)

@@ -55,6 +55,32 @@ __global__ __launch_bounds__(256) void rd_rows(const T* __restrict__ p, uint32_t
   }
   sink[blockIdx.x * 256 + threadIdx.x] = acc;
 }
+// the same with U independent rows in flight per wave (unrolled), and random-row writes: the achievable bandwidth of
+// the turbo decoder's access pattern with more memory-level parallelism
+template <class T, int U>
+__global__ __launch_bounds__(256) void rd_rows_mlp(const T* __restrict__ p, uint32_t rows, uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63, nw = gridDim.x * 4;
+  for (uint32_t r = (blockIdx.x * 4 + threadIdx.x / 64) * U; r < rows; r += nw * U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t row = (uint32_t)(((uint64_t)(r + u) * 2654435761ull) % rows);
+      v[u] = p[(size_t)row * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) acc = acc * 33u + (uint32_t)v[u];
+  }
+  sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+template <class T>
+__global__ __launch_bounds__(256) void wr_rows(T* __restrict__ p, uint32_t rows) {
+  const uint32_t lane = threadIdx.x & 63, nw = gridDim.x * 4;
+  for (uint32_t r = blockIdx.x * 4 + threadIdx.x / 64; r < rows; r += nw) {
+    const uint32_t row = (uint32_t)(((uint64_t)r * 2654435761ull) % rows);
+    p[(size_t)row * 64 + lane] = (T)(r + lane);
+  }
+}
 // partial-line stores: 16 B of every 128-B line (lanes 0-3 of a wave's 64 x 4 B, i.e. 4 lanes per 256 B)
 __global__ __launch_bounds__(256) void wr_partial(uint32_t* __restrict__ p, size_t lines) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < lines * 4; i += (size_t)gridDim.x * 256)
@@ -89,6 +115,13 @@ int main() {
     rd_rows<uint16_t><<<G, 256>>>((const uint16_t*)buf, (uint32_t)(BYTES / 128), sink);   // reads BYTES
     rd_rows<uint8_t><<<G, 256>>>((const uint8_t*)buf, (uint32_t)(BYTES / 64), sink);     // reads BYTES
     wr_partial<<<G, 256>>>((uint32_t*)buf, BYTES / 128);   // writes BYTES / 8
+    rd_rows_mlp<uint32_t, 8><<<G, 256>>>((const uint32_t*)buf, (uint32_t)(BYTES / 256), sink);   // reads BYTES
+    rd_rows_mlp<uint32_t, 16><<<G, 256>>>((const uint32_t*)buf, (uint32_t)(BYTES / 256), sink);
+    rd_rows_mlp<uint32_t, 8><<<G / 4, 256>>>((const uint32_t*)buf, (uint32_t)(BYTES / 256), sink);   // 2 waves/SIMD
+    rd_rows_mlp<uint16_t, 8><<<G, 256>>>((const uint16_t*)buf, (uint32_t)(BYTES / 128), sink);
+    rd_rows_mlp<uint64_t, 8><<<G, 256>>>((const uint64_t*)buf, (uint32_t)(BYTES / 512), sink);
+    wr_rows<uint32_t><<<G, 256>>>((uint32_t*)buf, (uint32_t)(BYTES / 256));   // writes BYTES
+    wr_rows<uint8_t><<<G, 256>>>((uint8_t*)buf, (uint32_t)(BYTES / 64));      // writes BYTES
   }
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   printf("done (wr16_rows writes %zu bytes, wr_partial %zu)\n", BYTES / 2, BYTES / 8);
