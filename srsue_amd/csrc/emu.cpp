@@ -33,6 +33,10 @@ static uint64_t g_cont_cbs = 0;
 extern "C" void emu_set_tdec_compact(int on) { g_compact = on; g_cont_cbs = 0; }
 static int g_store_w = 0;   // compaction: the first launch stores its w rows, the continuation gathers them
 extern "C" void emu_set_tdec_store_w(int on) { g_store_w = on; }
+static int g_rounds = 0;    // compaction: one iteration per round, the failing code blocks re-compacted between rounds
+static uint64_t g_round_cbs = 0;
+extern "C" void emu_set_tdec_rounds(int on) { g_rounds = on; g_round_cbs = 0; }
+extern "C" uint64_t emu_round_codeblocks() { return g_round_cbs; }
 extern "C" uint64_t emu_cont_codeblocks() { return g_cont_cbs; }
 template <bool Q16>
 static mi::TdecLaneResult emu_lane_x(const mi::TdecArgs& a, int lane) {
@@ -205,22 +209,25 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         const uint32_t gi0 = [&] { uint32_t g = 0; while (P.groups[g].K != K) g++; return g; }();
         const MiKTab& kt = P.ktabs[P.groups[gi0].ktab];
         const uint32_t* pos = &P.kdata[kt.pos_off];
-        for (size_t p0 = 0; p0 < cont.size(); p0 += 2 * mi::LANES) {
-          std::vector<uint32_t> cscr((size_t)(7 * K + 20) * mi::LANES, 0u);
-          std::vector<uint8_t> cdec((size_t)K * mi::LANES, 0);
+        const size_t PU = (size_t)(7 * K + 20) * mi::LANES;   // tdec.hip: a dense continuation pair
+        const size_t np1 = (cont.size() + 2 * mi::LANES - 1) / (2 * mi::LANES);
+        std::vector<std::vector<uint32_t>> bufs(np1, std::vector<uint32_t>(PU, 0u));
+        // round 1's gather (tdec_cont_gather_kernel): q rows from the softbuffer, w or x2 rows from the source pairs
+        for (size_t p = 0; p < np1; p++)
           for (int lane = 0; lane < mi::LANES; lane++) {
-            uint32_t li[2] = {0, 0}, live = 0;
+            uint32_t live = 0;
             mi::P2ContSrc src[2] = {};
             for (int h = 0; h < 2; h++) {
-              const size_t d = p0 + (size_t)h * mi::LANES + lane;
+              const size_t d = p * 2 * mi::LANES + (size_t)h * mi::LANES + lane;
               if (d >= cont.size()) continue;
-              li[h] = cont[d];
+              const uint32_t li = cont[d];
               live |= 1u << h;
-              const uint32_t g = li[h] / mi::LANES;
+              const uint32_t g = li / mi::LANES;
               src[h] = {&sb[P.groups[g].sb_off], mi::sb_q16(&sb[P.groups[g].sb_off], P.groups[g].Ncb), wms[g].data(),
-                        reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li[h] % mi::LANES, ph[g]};
+                        reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li % mi::LANES, ph[g]};
             }
             if (!live) continue;
+            uint32_t* cscr = bufs[p].data();
             uint32_t* cq = &cscr[(size_t)(4 * K + 8) * mi::LANES];
             for (uint32_t w = 0; w < mi::p2_cont_qwins(K); w++) {
               uint32_t q[3 * mi::BETA_W];
@@ -232,35 +239,80 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               else cscr[(size_t)(K + k) * mi::LANES + lane] = mi::p2_cont_xrow(src, live, K, k);
             }
           }
-          for (int lane = 0; lane < mi::LANES; lane++) {
-            uint32_t li[2] = {0, 0};
-            mi::TdecArgsP2 a{};
-            for (int h = 0; h < 2; h++) {
-              const size_t d = p0 + (size_t)h * mi::LANES + lane;
-              if (d < cont.size()) { li[h] = cont[d]; a.live |= 1u << h; }
-            }
-            if (!a.live) continue;
-            if (!(a.live & 2u)) li[1] = li[0];
-            a.scr = cscr.data();
-            a.q = a.scr + (size_t)(4 * K + 8) * mi::LANES;
-            a.pos = pos; a.pi = &P.kdata[kt.pi_off];
-            a.crc8 = crc8; a.crc8b = crc8b;
-            a.dec = cdec.data();
-            for (int h = 0; h < 2; h++) {
-              emu_p2_out(a, h, payload, P.lanes[li[h]]);
-              a.F[h] = P.lanes[li[h]].F;
-
-            }
-            a.K = K; a.max_its = max_its; a.early_stop = 1; a.cont_w = g_store_w;
-            mi::TdecP2ExecHost ex;
-            const mi::TdecP2Result r = mi::tdec_p2_lane<true>(a, lane, ex);
-            for (int h = 0; h < 2; h++) {
-              if (!((a.live >> h) & 1u)) continue;
-              cits[li[h]] = r.its[h];
-              ccrc[li[h]] = r.crc_ok[h];
-              ctbp[li[h]] = r.tb_part[h];
+        // iterations it0 .. it_end - 1 of every dense pair (tdec_kernel_p2c)
+        auto run_pairs = [&](std::vector<std::vector<uint32_t>>& pb, const std::vector<uint32_t>& list, uint32_t it0,
+                             uint32_t it_end) {
+          for (size_t p = 0; p < pb.size(); p++) {
+            std::vector<uint8_t> cdec((size_t)K * mi::LANES, 0);
+            for (int lane = 0; lane < mi::LANES; lane++) {
+              uint32_t li[2] = {0, 0};
+              mi::TdecArgsP2 a{};
+              for (int h = 0; h < 2; h++) {
+                const size_t d = p * 2 * mi::LANES + (size_t)h * mi::LANES + lane;
+                if (d < list.size()) { li[h] = list[d]; a.live |= 1u << h; }
+              }
+              if (!a.live) continue;
+              if (!(a.live & 2u)) li[1] = li[0];
+              a.scr = pb[p].data();
+              a.q = a.scr + (size_t)(4 * K + 8) * mi::LANES;
+              a.pos = pos; a.pi = &P.kdata[kt.pi_off];
+              a.crc8 = crc8; a.crc8b = crc8b;
+              a.dec = cdec.data();
+              for (int h = 0; h < 2; h++) {
+                emu_p2_out(a, h, payload, P.lanes[li[h]]);
+                a.F[h] = P.lanes[li[h]].F;
+              }
+              a.K = K; a.max_its = max_its; a.early_stop = 1;
+              a.cont_w = it0 > 1 || g_store_w;
+              a.it0 = it0; a.it_end = it_end;
+              mi::TdecP2ExecHost ex;
+              const mi::TdecP2Result r = mi::tdec_p2_lane<true>(a, lane, ex);
+              for (int h = 0; h < 2; h++) {
+                if (!((a.live >> h) & 1u)) continue;
+                cits[li[h]] = r.its[h];
+                ccrc[li[h]] = r.crc_ok[h];
+                ctbp[li[h]] = r.tb_part[h];
+              }
             }
           }
+        };
+        if (!g_rounds) {
+          run_pairs(bufs, cont, 1, max_its);
+          continue;
+        }
+        // re-compaction rounds (tdec.hip launch_tdec_cont): one iteration each, the code blocks still failing
+        // gathered -- here in reverse slot order, so again with new partners -- into fewer dense pairs
+        run_pairs(bufs, cont, 1, 2);
+        for (uint32_t it = 2; it < max_its; it++) {
+          std::vector<uint32_t> next, srcs;
+          for (size_t d = cont.size(); d-- > 0;)
+            if (!ccrc[cont[d]]) { next.push_back(cont[d]); srcs.push_back((uint32_t)d); }
+          g_round_cbs += next.size();
+          const size_t np = (next.size() + 2 * mi::LANES - 1) / (2 * mi::LANES);
+          std::vector<std::vector<uint32_t>> nb(np, std::vector<uint32_t>(PU, 0u));
+          for (size_t p = 0; p < np; p++)   // tdec_cont_gather2_kernel
+            for (int lane = 0; lane < mi::LANES; lane++) {
+              uint32_t live = 0;
+              mi::P2ContSrc src[2] = {};
+              for (int h = 0; h < 2; h++) {
+                const size_t d = p * 2 * mi::LANES + (size_t)h * mi::LANES + lane;
+                if (d >= next.size()) continue;
+                const uint32_t e = srcs[d];
+                live |= 1u << h;
+                src[h].scr = bufs[e / (2 * mi::LANES)].data();
+                src[h].ls = e % mi::LANES;
+                src[h].hs = (e / mi::LANES) & 1u;
+              }
+              if (!live) continue;
+              for (uint32_t r = 0; r < K; r++) nb[p][(size_t)r * mi::LANES + lane] = mi::p2_cont_drow(src, live, r);
+              for (uint32_t r = 0; r < 3 * (K + 4); r++) {
+                const size_t row = (size_t)(4 * K + 8) + r;
+                nb[p][row * mi::LANES + lane] = mi::p2_cont_drow(src, live, row);
+              }
+            }
+          run_pairs(nb, next, it, it + 1);
+          cont.swap(next);
+          bufs.swap(nb);
         }
       }
     }

@@ -139,7 +139,7 @@ int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
          d_tbits.ensure(nsf * 4);
     if (tdec_compact()) {
       const uint32_t np = cont_max_pairs();
-      ok = ok && d_cont.ensure((P.lanes.size() + 1) * 4) && d_cscr.ensure((size_t)np * cont_pair_u32() * 4) &&
+      ok = ok && d_cont.ensure((3 * P.lanes.size() + 2) * 4) && d_cscr.ensure((size_t)np * cont_pair_u32() * 4) &&
            d_cdec.ensure((size_t)np * P.groups[0].K * LANES);
     }
     if (alloc_sb) {
@@ -395,7 +395,7 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
     const bool direct = P.has_pdsch && !P.cb_n;
     tb_copied = direct;
     const bool cont = tdec_compact() && d_cscr.bytes >= (size_t)cont_max_pairs() * cont_pair_u32() * 4 &&
-                      d_cont.bytes >= (P.lanes.size() + 1) * 4 &&
+                      d_cont.bytes >= (3 * P.lanes.size() + 2) * 4 &&
                       d_cdec.bytes >= (size_t)cont_max_pairs() * P.groups[0].K * LANES;
     // The one-iteration first launch stores no extrinsic rows w when few code blocks continue (the continuation
     // re-forms them by re-running iteration 0's DEC2 from gathered x2 rows: 12 KB per code block less for all, about
@@ -418,13 +418,19 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
                    cont && !store_w, st);
     if (cont) {
       // the code blocks still failing after iteration 0, compacted into dense pairs for iterations 1 ..
-      launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
+      // many continuing code blocks (the same history): one iteration per launch, re-compacting the code blocks that
+      // still fail between them, so a pair no longer runs until its slowest of 128 code blocks stops (21.5 dB:
+      // 379 + 84 + 19 pair-iterations instead of 3 x 379).  MI_TDEC_ROUNDS=0 / 1 forces (A/B).
+      const char* fr = getenv("MI_TDEC_ROUNDS");
+      const bool rounds = fr ? atoi(fr) != 0 : store_w;
+      const size_t ssz = (size_t)LANES * (2 * P.groups[0].K + 8 * (P.groups[0].K / TDEC_CK_MIN + 1));   // plan.cpp
+      launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), 2 * ssz, d_dec.as<uint8_t>(),
+                       d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
                        d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                        d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
                        (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048,
-                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, st);
-      if (h_cont) (void)hipMemcpyAsync(h_cont, d_cont.p, 4, hipMemcpyDeviceToHost, st);
+                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, h_cont, st);
     }
     return;
   }

@@ -54,11 +54,15 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
 // waterfall compaction after iteration 0 of launch_tdec_p2 (one K, early stop; tdec_p2_body.h P2ContSrc):
 // gather the CRC-failing code blocks into dense continuation pairs (cscr: max_pairs x pair_u32 words, cdec:
 // max_pairs x K x 64 bytes, cont: 1 + lanes words) and decode iterations 1 .. max_its - 1 there
-void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch, uint8_t* cb_bytes, uint32_t* cb_its,
-                      uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                      const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
-                      uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      uint8_t* payload, bool w_stored /* the first launch stored w rows: gather them (no DEC2 re-run) */,
+void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
+                      uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
+                      const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
+                      uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,
+                      uint32_t gather_wgs, uint8_t* payload,
+                      bool w_stored /* the first launch stored w rows: gather them (no DEC2 re-run) */,
+                      bool rounds /* one iteration per launch, the failing code blocks re-compacted between them;
+                                     cont holds 3 n_groups * 64 + 2 words, scratch / dec are reused as pair buffers */,
+                      uint32_t* h_count /* page-locked: the number of code blocks continuing after iteration 0 */,
                       hipStream_t st);
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS

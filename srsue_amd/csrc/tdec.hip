@@ -178,7 +178,18 @@ struct TdecP2ExecGpu {
   __device__ uint32_t share(uint32_t v, int lane) {
     if (wave == 0) xs[lane] = v;
     __syncthreads();
-    return xs[lane];
+    const uint32_t r = xs[lane];
+    __syncthreads();   // xs is reused by the next exchange
+    return r;
+  }
+  // wave B's N values of this lane, on both waves (xs holds N x 64 words)
+  template <int N>
+  __device__ void share_from_b(uint32_t (&v)[N], int lane) {
+    if (wave == 1)
+      for (int i = 0; i < N; i++) xs[i * LANES + lane] = v[i];
+    __syncthreads();
+    for (int i = 0; i < N; i++) v[i] = xs[i * LANES + lane];
+    __syncthreads();
   }
   __device__ bool pack_wave() const { return wave == 0; }
 };
@@ -193,7 +204,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
                      const uint32_t* __restrict__ kdata, const uint32_t* __restrict__ pairs, uint32_t max_its,
                      uint32_t early_stop, uint32_t no_w) {
   __shared__ uint32_t crc8[256], crc8b[256];
-  __shared__ uint32_t xs[LANES];
+  __shared__ uint32_t xs[4 * LANES];
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
     crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
     crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
@@ -284,6 +295,29 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
   if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
 }
 
+// 1'. a re-compaction round (waterfall, tdec_p2_body.h): one wavefront per 64 slots of the previous round's list; its
+// code blocks whose CRC still fails claim consecutive slots of the next list, which records each one's lane index and
+// its previous slot (src: where the gather finds its state)
+__global__ __launch_bounds__(64) void tdec_cont_assign2_kernel(const uint32_t* __restrict__ prev,
+                                                               const uint32_t* __restrict__ cb_crc, uint32_t* next,
+                                                               uint32_t* __restrict__ src) {
+  const uint32_t lane = threadIdx.x, d = blockIdx.x * LANES + lane, n = prev[0];
+  if (blockIdx.x * LANES >= n) return;   // the whole wavefront
+  const uint32_t li = d < n ? prev[1 + d] : 0u;
+  const bool act = d < n && !cb_crc[li];
+  const uint64_t m = __ballot(act);
+  if (!m) return;
+  const int lead = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)lane == lead) base = atomicAdd(next, (uint32_t)__popcll(m));
+  base = __shfl(base, lead);
+  if (act) {
+    const uint32_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
+    next[1 + slot] = li;
+    src[slot] = d;
+  }
+}
+
 // 2. the gather, grid-stride over tasks (continuation pair, 8 q windows) and (continuation pair, 96 rows of iteration 0's
 // state: the x2 rows (DEC1 outputs, at K) when the first launch stored no w rows -- the continuation re-runs DEC2 --,
 // else its w rows (at 0)); lane = continuation lane, both halves
@@ -337,14 +371,46 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
   }
 }
 
-// 3. iterations 1 .. max_its - 1 of the continuing code blocks, dense pairs
+// 2'. a re-compaction round's gather: every packed row of the state iteration it0 reads (the q rows and the w rows
+// the previous round's DEC2 stored), dense pairs -> dense pairs; grid-stride over (pair, 96-row chunk)
+__global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* __restrict__ prev, size_t prev_u32,
+                                                                const uint32_t* __restrict__ cont,
+                                                                const uint32_t* __restrict__ src,
+                                                                uint32_t* __restrict__ dst, size_t dst_u32, uint32_t K) {
+  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
+  const uint32_t nq = 3 * (K + 4), per = (K + CONT_WR - 1) / CONT_WR + (nq + CONT_WR - 1) / CONT_WR;
+  for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * per; u += gridDim.x * 4) {
+    const uint32_t p = u / per, c = u % per, nwc = (K + CONT_WR - 1) / CONT_WR;
+    P2ContSrc s[2] = {};
+    uint32_t live = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t d = p * 2 * LANES + h * LANES + lane;
+      if (d >= n) continue;
+      const uint32_t e = src[d];   // the previous round's slot: pair e / 128, half (e / 64) % 2, lane e % 64
+      live |= 1u << h;
+      s[h].scr = prev + (size_t)(e / (2 * LANES)) * prev_u32;
+      s[h].ls = e % LANES;
+      s[h].hs = (e / LANES) & 1u;
+    }
+    uint32_t* dp = dst + (size_t)p * dst_u32;
+    // rows [r0, r1): the w rows (at 0) or the q rows (at 4K + 8)
+    const size_t base = c < nwc ? 0 : (size_t)(4 * K + 8);
+    const uint32_t r0 = (c < nwc ? c : c - nwc) * CONT_WR, r1 = min(c < nwc ? K : nq, r0 + CONT_WR);
+#pragma unroll 8
+    for (uint32_t r = r0; r < r1; r++) dp[(base + r) * LANES + lane] = p2_cont_drow(s, live, base + r);
+  }
+}
+
+// 3. iterations it0 .. it_end - 1 of the continuing code blocks, dense pairs (pair stride pair_u32, decision rows
+// dec_stride bytes apart)
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
-                     const uint32_t* __restrict__ cont, size_t pair_u32, uint32_t K, uint32_t max_its,
-                     uint32_t w_stored) {
+                     const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
+                     uint32_t w_stored, uint32_t it0, uint32_t it_end) {
   __shared__ uint32_t crc8[256], crc8b[256];
-  __shared__ uint32_t xs[LANES];
+  __shared__ uint32_t xs[4 * LANES];
   const uint32_t n = cont[0], p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
@@ -365,7 +431,7 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.pi = kdata + kt.pi_off;
   a.crc8 = crc8;
   a.crc8b = crc8b;
-  a.dec = cdec + (size_t)p * K * LANES;
+  a.dec = cdec + (size_t)p * dec_stride;
   p2_out(a, 0, out, li[0], l0);
   p2_out(a, 1, out, li[1], l1);
   a.to_payload = out.payload != nullptr;
@@ -375,6 +441,8 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.max_its = max_its;
   a.early_stop = 1;
   a.cont_w = w_stored;
+  a.it0 = it0;
+  a.it_end = it_end;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   const TdecP2Result r = tdec_p2_lane<true>(a, lane, ex);
   if (ex.wave) return;
@@ -387,19 +455,47 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   }
 }
 
-void launch_tdec_cont(const float* sb, const uint32_t* wm, const float* scratch, uint8_t* cb_bytes, uint32_t* cb_its,
-                      uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
-                      const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont, uint32_t* cscr,
-                      uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its, uint32_t gather_wgs,
-                      uint8_t* payload, bool w_stored, hipStream_t st) {
+void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
+                      uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
+                      const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
+                      uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,
+                      uint32_t gather_wgs, uint8_t* payload, bool w_stored, bool rounds, uint32_t* h_count,
+                      hipStream_t st) {
   if (!n_groups || !max_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
+  const size_t nl = (size_t)n_groups * LANES + 1;   // one list: count + lane indices
+  uint32_t* lists[2] = {cont, cont + nl};
+  uint32_t* src = cont + 2 * nl;
   (void)hipMemsetAsync(cont, 0, 4, st);
   hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
+  if (h_count) (void)hipMemcpyAsync(h_count, cont, 4, hipMemcpyDeviceToHost, st);
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
                      ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored);
-  hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes, ktab_data, kt, cont,
-                     pair_u32, K, max_its, (uint32_t)w_stored);
+  const size_t cdec_stride = (size_t)K * LANES;
+  if (!rounds) {   // one launch for iterations 1 .. max_its - 1 (each pair until its slowest code block stops)
+    hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes, ktab_data, kt, cont,
+                       pair_u32, cdec_stride, K, max_its, (uint32_t)w_stored, 1u, max_its);
+    return;
+  }
+  // re-compaction: one iteration per round, the code blocks still failing gathered into fewer dense pairs for the
+  // next.  The pair buffers alternate between the continuation scratch and the groups' own scratch (free after the
+  // first gather; group pair j's region holds dense pair j: 2 (2K + 8 (K/4 + 1)) >= 7K + 20 rows of 64 lanes)
+  uint32_t* bufs[2] = {cscr, reinterpret_cast<uint32_t*>(scratch)};
+  const size_t strides[2] = {pair_u32, scr_pair_u32};
+  uint8_t* decs[2] = {cdec, dec};
+  const size_t dstrides[2] = {cdec_stride, 2 * cdec_stride};
+  for (uint32_t it = 1; it < max_its; it++) {
+    const int b = (int)((it - 1) & 1u), l = b;
+    if (it > 1) {
+      (void)hipMemsetAsync(lists[l], 0, 4, st);
+      hipLaunchKernelGGL(tdec_cont_assign2_kernel, dim3(2 * max_pairs), dim3(64), 0, st, lists[l ^ 1], cb_crc, lists[l],
+                         src);
+      hipLaunchKernelGGL(tdec_cont_gather2_kernel, dim3(gather_wgs), dim3(256), 0, st, bufs[b ^ 1], strides[b ^ 1],
+                         lists[l], src, bufs[b], strides[b], K);
+    }
+    hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes, ktab_data, kt,
+                       lists[l], strides[b], dstrides[b], K, max_its, (uint32_t)(w_stored || it > 1), it, it + 1);
+  }
 }
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,

@@ -56,9 +56,16 @@ struct TdecArgsP2 {
   uint32_t no_w;          // wave-uniform: DEC2 stores no extrinsic rows w (a one-iteration launch: nothing reads
                           // them -- the compaction continuation re-runs DEC2 of iteration 0 instead, tdec_p2_lane)
   uint32_t cont_w;        // continuation only: iteration 0's w rows were gathered (no DEC2 re-run)
+  uint32_t it0, it_end;   // continuation only: this launch runs iterations it0 .. it_end - 1 (a round of the
+                          // re-compacted waterfall: one iteration; the one-shot continuation: 1 .. max_its - 1)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 
+// timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone, 3 = no check pass (no CRC verdicts,
+// no payload), 4 = no check pass and no decision stores (tdec_p2_xhalf, tdec_p2_lane, p2_emit)
+#ifndef MI_TDEC_P2_DIAG
+#define MI_TDEC_P2_DIAG 0
+#endif
 // MI_TDEC_P2_QSB (= MI_SB_Q16, off by default, dl_common.h): the channel inputs come from the softbuffer's int16 mirror (dl_common.h sb_q16_off:
 // q(x) written by rate de-matching beside every fp32 row): 2-byte loads from 128-B rows, and the pair is packed with
 // one v_lshl_or instead of quantised (2 fma + 2 med3 + perm).  Every pass reads the mirror -- later iterations too,
@@ -273,8 +280,9 @@ MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, u
   } else {
     if (!a.no_w) row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
     const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
+    // decision byte: half 0's bit at bit 0, half 1's at bit 4 (the check pass packs 4 rows with 3 shift-ors)
     const uint32_t b0 = (ng >> 15) & 1u, b1 = ng >> 31;
-    row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 1)));
+    if (MI_TDEC_P2_DIAG != 4) row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 4)));
   }
 }
 
@@ -786,15 +794,12 @@ struct TdecP2X {
   }
 };
 
-#ifndef MI_TDEC_P2_DIAG
-#define MI_TDEC_P2_DIAG 0
-#endif
 template <bool DEC2, bool FIRST, int SRC, bool CK8 = MI_TDEC_P2_CK8, int PFQ = MI_TDEC_P2_PF_Q, class Exec>
 MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
   using X = TdecP2X<DEC2, FIRST, SRC, CK8, PFQ>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
-#if MI_TDEC_P2_DIAG != 2   // timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone
+#if MI_TDEC_P2_DIAG != 2   // timing diagnostics (MI_TDEC_P2_DIAG, above)
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
 #endif
 #if MI_TDEC_P2_DIAG != 1
@@ -809,8 +814,15 @@ MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
 // partial TB CRC24A of its payload bytes F/8 .. K/8 - (CB CRC ? 3 : 0) that tb_kernel combines.  Returns
 // bit h = half h's code-block CRC passed.  (The byte-wise register of a K-bit block equals the XOR of the
 // per-bit contributions crc_a / crc_b[k] the one-code-block kernels accumulate: CRC is linear.)
-MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2]) {
-  uint32_t bl[2], bh[2], tb[2] = {0u, 0u}, cb[2] = {0u, 0u};
+#ifndef MI_TDEC_P2_PF_CHK
+#define MI_TDEC_P2_PF_CHK 2   // decision-row chunks in flight in the check pass (1 = the round-3 form; 3: 38 VGPRs spilled)
+#endif
+// the code-block and TB CRC registers of both halves over the decision-row chunks [c0, c1) (4 bytes each), from 0;
+// the chunks' payload bytes of the halves in `act` are written
+struct P2CrcRegs { uint32_t cb[2], tb[2]; };
+MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32_t act, uint32_t c0, uint32_t c1) {
+  uint32_t bl[2], bh[2];
+  P2CrcRegs g{{0u, 0u}, {0u, 0u}};
   const uint32_t* ct[2];
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -820,52 +832,83 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
   }
   const bool p0 = act & 1u, p1 = (act >> 1) & 1u;
   const uint32_t nb = a.K / 8;
-  // the decision rows of 4 bytes (32 rows) per chunk, the next chunk's loads issued before this chunk's
-  // bits are used (rows past K are clamped to row K - 1 and their bytes never used)
-  uint32_t d[2][32];
-  auto load = [&](uint32_t c, uint32_t (&dd)[32]) {
+  // the decision rows of 4 bytes (32 rows) per chunk, MI_TDEC_P2_PF_CHK chunks' loads in flight ahead of the chunk
+  // whose bits are used (the trellis registers are dead here); rows past K are clamped to row K - 1 and their bytes
+  // never used
+  struct Chunk { uint32_t d[32]; };
+  auto load = [&](uint32_t c, Chunk& dd) {
 #pragma unroll
     for (int q = 0; q < 32; q++) {
       const uint32_t row = 32 * c + (uint32_t)q;
-      dd[q] = row_ld(a.dec, row < a.K ? row : a.K - 1, lane);
+      dd.d[q] = row_ld(a.dec, row < a.K ? row : a.K - 1, lane);
     }
   };
-  auto run = [&](uint32_t c, const uint32_t (&dd)[32]) {
+  auto run = [&](const Chunk& dd, uint32_t c) {
 #pragma unroll
     for (int jj = 0; jj < 4; jj++) {
       const uint32_t j = 4 * c + (uint32_t)jj;
       if (j >= nb) break;   // wave-uniform
-      uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        v0 |= (dd[8 * jj + q] & 1u) << (7 - q);
-        v1 |= ((dd[8 * jj + q] >> 1) & 1u) << (7 - q);
-      }
+      // rows 8 jj .. 8 jj + 7, MSB first: four rows at a time give half 0's 4 bits in bits 3..0 and half 1's in 7..4
+      // (decision byte = b0 | b1 << 4, p2_emit)
+      const uint32_t* r8 = &dd.d[8 * jj];
+      const uint32_t xa = (r8[0] << 3) | (r8[1] << 2) | (r8[2] << 1) | r8[3];
+      const uint32_t xb = (r8[4] << 3) | (r8[5] << 2) | (r8[6] << 1) | r8[7];
+      const uint32_t v0 = ((xa & 0xFu) << 4) | (xb & 0xFu), v1 = (xa & 0xF0u) | (xb >> 4);
       // payload bytes: F/8 .. the CB CRC, less the TB CRC where the code block carries it (tb_kernel's run)
       const bool s0 = !a.to_payload || (j >= bl[0] && j < bh[0] - 3 * ((a.crc24a[0] >> 1) & 1u));
       const bool s1 = !a.to_payload || (j >= bl[1] && j < bh[1] - 3 * ((a.crc24a[1] >> 1) & 1u));
       if (p0 && s0) a.cb_bytes[0][j - a.cb_skip[0]] = (uint8_t)v0;
       if (p1 && s1) a.cb_bytes[1][j - a.cb_skip[1]] = (uint8_t)v1;
-      cb[0] = ((cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((cb[0] >> 16) ^ v0) & 0xFFu];
-      cb[1] = ((cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((cb[1] >> 16) ^ v1) & 0xFFu];
-      if (j >= bl[0] && j < bh[0]) tb[0] = ((tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[0] >> 16) ^ v0) & 0xFFu];
-      if (j >= bl[1] && j < bh[1]) tb[1] = ((tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((tb[1] >> 16) ^ v1) & 0xFFu];
+      g.cb[0] = ((g.cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((g.cb[0] >> 16) ^ v0) & 0xFFu];
+      g.cb[1] = ((g.cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((g.cb[1] >> 16) ^ v1) & 0xFFu];
+      if (j >= bl[0] && j < bh[0]) g.tb[0] = ((g.tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((g.tb[0] >> 16) ^ v0) & 0xFFu];
+      if (j >= bl[1] && j < bh[1]) g.tb[1] = ((g.tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((g.tb[1] >> 16) ^ v1) & 0xFFu];
     }
   };
-  const uint32_t nc = (nb + 3) / 4;
-  load(0, d[0]);
-  for (uint32_t c = 0; c < nc; c += 2) {
-    load(c + 1 < nc ? c + 1 : c, d[1]);
-    MI_SCHED_FENCE();
-    run(c, d[0]);
-    if (c + 1 >= nc) break;
-    load(c + 2 < nc ? c + 2 : c + 1, d[0]);
-    MI_SCHED_FENCE();
-    run(c + 1, d[1]);
+  if (c1 > c0)
+    pipe_windows<MI_TDEC_P2_PF_CHK, Chunk>(
+        (int)(c1 - c0), [c0](int i) { return c0 + (uint32_t)i; }, load, run);
+  return g;
+}
+// a register shifted past L zero bytes: r x^(8 L) mod g (the byte-wise CRC is linear: R(A || B) = R(A) x^(8 |B|) ^ R(B))
+MI_HD inline uint32_t crc24_shift(uint32_t r, uint32_t L, const uint32_t* tab) {
+  for (uint32_t i = 0; i < L; i++) r = ((r << 8) & 0xFFFFFFu) ^ tab[(r >> 16) & 0xFFu];
+  return r;
+}
+// The check pass over both waves (MI_TDEC_P2_SPLIT_CHK=1, measured and not kept): wave F takes the first half of the
+// chunks, wave B the second (it waits at the barrier otherwise), each from a zero register; wave F then shifts its
+// registers past the bytes of B's half and XORs B's in -- identical registers, verdicts and payload bytes, but the
+// kernel spills more scalar registers and the step got slower (one stream 6.47-6.51 -> 6.50-6.65 ms, four streams
+// 112.3-113.0 -> 110.5-110.9 Gbps; profiles/r4/ab_split_chk), although the pass alone costs 0.45 ms of the launch
+// (a diagnostic build without it: 6.62 -> 6.14 ms at one iteration, profiles/r4/diag_chk)
+#ifndef MI_TDEC_P2_SPLIT_CHK
+#define MI_TDEC_P2_SPLIT_CHK 0
+#endif
+template <class Exec>
+MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2], Exec& ex) {
+  const uint32_t nb = a.K / 8, nc = (nb + 3) / 4;
+  P2CrcRegs g;
+  if constexpr (MI_TDEC_P2_SPLIT_CHK) {
+    const uint32_t ncf = (nc + 1) / 2, jb = 4 * ncf;   // wave B: bytes jb .. nb - 1
+    P2CrcRegs gf{{0u, 0u}, {0u, 0u}}, gb{{0u, 0u}, {0u, 0u}};
+    ex.run([&] { gf = tdec_p2_check_range(a, lane, act, 0, ncf); }, [&] { gb = tdec_p2_check_range(a, lane, act, ncf, nc); });
+    uint32_t v[4] = {gb.cb[0], gb.cb[1], gb.tb[0], gb.tb[1]};
+    ex.share_from_b(v, lane);
+    const uint32_t lcb = nb > jb ? nb - jb : 0u;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t bl = a.F[h] / 8, bh = a.K / 8 - ((a.crc24a[h] & 1u) ? 0 : 3), s = jb > bl ? jb : bl;
+      const uint32_t ltb = bh > s ? bh - s : 0u;   // TB-CRC bytes in B's half
+      const uint32_t* ct = (a.crc24a[h] & 1u) ? a.crc8 : a.crc8b;
+      g.cb[h] = crc24_shift(gf.cb[h], lcb, ct) ^ v[h];
+      g.tb[h] = crc24_shift(gf.tb[h], ltb, a.crc8) ^ v[2 + h];
+    }
+  } else {
+    g = tdec_p2_check_range(a, lane, act, 0, nc);
   }
-  if (p0) tbp[0] = tb[0];
-  if (p1) tbp[1] = tb[1];
-  return (cb[0] == 0u ? 1u : 0u) | (cb[1] == 0u ? 2u : 0u);
+  if (act & 1u) tbp[0] = g.tb[0];
+  if (act & 2u) tbp[1] = g.tb[1];
+  return (g.cb[0] == 0u ? 1u : 0u) | (g.cb[1] == 0u ? 2u : 0u);
 }
 
 // the iteration loop (tdec_body.h tdec_lane_x's source-mode sequence) with per-code-block stopping.
@@ -883,8 +926,8 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
   constexpr bool CK = CONT ? MI_TDEC_P2C_CK8 : MI_TDEC_P2_CK8;
   constexpr int PQ = CONT ? MI_TDEC_P2C_PF_Q : MI_TDEC_P2_PF_Q;
   if constexpr (CONT)
-    if (!a.cont_w) tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
-  for (uint32_t it = CONT ? 1u : 0u; it < a.max_its && active; it++) {
+    if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
+  for (uint32_t it = CONT ? a.it0 : 0u; it < (CONT ? a.it_end : a.max_its) && active; it++) {
     constexpr uint32_t MK = MI_TDEC_P2_QSB ? 0xFFFFFFFFu : MI_TDEC_MKQ_IT;   // QSB: every pass reads the mirror
     if constexpr (CONT) {
       tdec_p2_xhalf<false, false, SRC_Q, CK, PQ>(a, lane, ex);
@@ -910,7 +953,11 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     const bool last = it + 1 == a.max_its;
     uint32_t ok = 0u;
     if (a.early_stop || last) {   // wave-uniform
-      if (ex.pack_wave()) ok = tdec_p2_check(a, lane, active, r.tb_part);
+      if constexpr (MI_TDEC_P2_SPLIT_CHK) {   // both waves run the pass; wave F's verdicts go to both
+        if (MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check(a, lane, active, r.tb_part, ex);
+      } else {
+        if (ex.pack_wave() && MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check(a, lane, active, r.tb_part, ex);
+      }
       ok = ex.share(ok, lane);
     }
     uint32_t stop = 0u;
@@ -975,15 +1022,16 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
   for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
 #endif
 }
-// w row k (at 0) of one continuation lane: each half's 16-bit iteration-0 extrinsic from its source pair's packed row
-// (a first launch that stored its w rows)
-MI_HD inline uint32_t p2_cont_wrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t k) {
+// packed row `row` of one continuation lane from its sources' packed rows (each half's 16 bits from its source pair's
+// row, half hs): the w rows (at 0) after a first launch that stored them, and every row of a re-compaction round
+MI_HD inline uint32_t p2_cont_drow(const P2ContSrc (&s)[2], uint32_t live, size_t row) {
   uint32_t w[2];
 #pragma unroll
   for (int h = 0; h < 2; h++)
-    w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)k * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
+    w[h] = ((live >> h) & 1u) ? (s[h].scr[row * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
   return w[0] | (w[1] << 16);
 }
+MI_HD inline uint32_t p2_cont_wrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t k) { return p2_cont_drow(s, live, k); }
 // x2 row k (the llr1 rows, at K) of one continuation lane: each half's 16-bit iteration-0 DEC1 output from its
 // source pair's packed row
 MI_HD inline uint32_t p2_cont_xrow(const P2ContSrc (&s)[2], uint32_t live, uint32_t K, uint32_t k) {
@@ -999,6 +1047,8 @@ struct TdecP2ExecHost {
   template <class F, class B>
   void run(F f, B b) { f(); b(); }
   uint32_t share(uint32_t v, int) { return v; }
+  template <int N>
+  void share_from_b(uint32_t (&)[N], int) {}   // both waves' values are this thread's
   bool pack_wave() const { return true; }
 };
 

@@ -120,7 +120,7 @@ def test_emulated_segment_parallel_turbo_bit_exact(built, nprb, ports, tbs, qm, 
     assert np.array_equal(pe, opay)
 
 
-@pytest.mark.parametrize("compact", [False, True, "store_w"])
+@pytest.mark.parametrize("compact", [False, True, "store_w", "rounds"])
 @pytest.mark.parametrize("snr0", [18.6, 30.0])
 def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     """The packed decoder (two code blocks per lane, tdec_p2_body.h) on a batch whose code blocks fill
@@ -131,7 +131,9 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     compact: the waterfall compaction (iteration 0 over the pairs, then the CRC-failing code blocks
     gathered -- in reverse lane order, so with new partners -- into continuation pairs, tdec_p2_lane<true>);
     "store_w": the same with the first launch storing its extrinsic rows and the continuation gathering them
-    instead of re-running iteration 0's DEC2 (engine.cpp: the waterfall's choice)."""
+    instead of re-running iteration 0's DEC2 (engine.cpp: the waterfall's choice); "rounds": that, with one iteration
+    per continuation round and the code blocks still failing re-compacted (in reverse slot order, new partners again)
+    between rounds (tdec.hip launch_tdec_cont)."""
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(11)]
     cfgs.append(abi.sf_cfg(cell_id=301, nof_prb=6, sf_idx=2, tbs=4392, Qm=6))
     snrs = [snr0 + 0.35 * (i % 5) for i in range(len(cfgs))]
@@ -149,17 +151,21 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     E.emu_set_tdec_i16(1)
     E.emu_set_tdec_x(3)
     E.emu_set_tdec_compact(int(bool(compact)))
-    E.emu_set_tdec_store_w(int(compact == "store_w"))
+    E.emu_set_tdec_store_w(int(compact in ("store_w", "rounds")))
+    E.emu_set_tdec_rounds(int(compact == "rounds"))
+    E.emu_round_codeblocks.restype = C.c_uint64
     E.emu_cont_codeblocks.restype = C.c_uint64
     try:
         rc = E.emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
                               eok.ctypes.data, eits.ctypes.data, cbits.ctypes.data)
         n_cont = E.emu_cont_codeblocks()
+        n_round = E.emu_round_codeblocks()
     finally:
         E.emu_set_tdec_i16(0)
         E.emu_set_tdec_x(0)
         E.emu_set_tdec_compact(0)
         E.emu_set_tdec_store_w(0)
+        E.emu_set_tdec_rounds(0)
     assert rc == 0
     # lanes sorted by K (plan.cpp), each K's groups padded to 64 lanes: the 1.4 MHz code block is group 0
     lane = 64
@@ -175,3 +181,4 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     if snr0 < 20:
         assert len(set(cbits[64:64 + 143].tolist())) >= 3   # code blocks of one lane stopped at different its
         assert not compact or n_cont > 20
+        assert compact != "rounds" or n_round > 0   # some code blocks went through a re-compaction

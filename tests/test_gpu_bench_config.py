@@ -167,19 +167,21 @@ def test_waterfall_compaction_matches_uncompacted(monkeypatch):
     iqs = [abi.tx_subframe(c, tb_bytes(7000 + j, TBS), snr_db=16.0 + 9.0 * j / (pool - 1), seed=0xC000 + j)
            for j, c in enumerate(pcfgs)]
     outs = []
-    # compacted with the first launch's extrinsic rows dropped (re-formed by the continuation), uncompacted, and
-    # compacted with them stored and gathered (engine.cpp: the waterfall's choice)
-    for compact, store_w in (("1", "0"), ("0", "0"), ("1", "1")):
+    # compacted with the first launch's extrinsic rows dropped (re-formed by the continuation), uncompacted,
+    # compacted with them stored and gathered, and that with one iteration per round and the failing code blocks
+    # re-compacted between rounds (engine.cpp: the waterfall's choice)
+    for compact, store_w, rounds in (("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
         monkeypatch.setenv("MI_TDEC_COMPACT", compact)
         monkeypatch.setenv("MI_TDEC_STORE_W", store_w)
+        monkeypatch.setenv("MI_TDEC_ROUNDS", rounds)
         b, _ = run_bench_config(n, iqs)
         assert b.turbo_sched == "p2", b.turbo_sched
         outs.append([b.download(k, np.uint32 if k != abi.BUF_PAYLOAD else np.uint8)
                      for k in (abi.BUF_TB_CRC, abi.BUF_TB_ITS, abi.BUF_CB_ITS, abi.BUF_PAYLOAD)])
         b.close()
     for k, name in enumerate(("TB CRC", "TB its", "CB its", "payload")):
-        assert np.array_equal(outs[0][k], outs[1][k]), name
-        assert np.array_equal(outs[2][k], outs[1][k]), name
+        for o in (0, 2, 3):
+            assert np.array_equal(outs[o][k], outs[1][k]), (o, name)
     crc, cbits = outs[0][0], outs[0][2][:C * n]
     assert 0 < crc.sum() < n and set(np.unique(cbits).tolist()) >= {1, 2, 3, 4}
 
