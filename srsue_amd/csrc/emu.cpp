@@ -113,8 +113,8 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
 
 // the packed decoder writes each code block's payload run in place (tdec.hip p2_out)
 static void emu_p2_out(mi::TdecArgsP2& a, int h, uint8_t* payload, const MiLaneDesc& ld) {
-  a.cb_bytes[h] = payload + ld.pay_st;
-  a.cb_skip[h] = ld.F / 8;
+  a.out_bytes = payload;
+  a.cb_off[h] = ld.pay_st;
   a.crc24a[h] = ld.crc24a | (ld.tbcrc << 1);
   a.to_payload = 1;
 }

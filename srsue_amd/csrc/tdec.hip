@@ -18,8 +18,8 @@ struct TdecOut {            // per code block (lane index li) results
 // the packed decoder's output of one half: the code block's payload run, or its row; crc24a bit 1 = the code
 // block carries the TB CRC (tdec_p2_check)
 __device__ inline void p2_out(TdecArgsP2& a, int h, const TdecOut& out, uint32_t li, const MiLaneDesc& ld) {
-  a.cb_bytes[h] = out.payload ? out.payload + ld.pay_st : out.cb_bytes + (size_t)li * CB_BYTES_STRIDE;
-  a.cb_skip[h] = out.payload ? ld.F / 8 : 0u;
+  a.out_bytes = out.payload ? out.payload : out.cb_bytes;
+  a.cb_off[h] = out.payload ? ld.pay_st : li * CB_BYTES_STRIDE;
   a.crc24a[h] = ld.crc24a | (ld.tbcrc << 1);
 }
 

@@ -47,9 +47,11 @@ struct TdecArgsP2 {
   const uint32_t* crc8b;  // [256] CRC24B byte table
   uint32_t* scr;          // pair scratch, u32 rows: w [K][64], llr1 [K][64], checkpoints [(K/4 + 1)][64][7]
   uint8_t* dec;           // [K][64] decision bytes, bit h = code block of half h
-  uint8_t* cb_bytes[2];   // each half's packed output: byte j of the code block at cb_bytes[h][j - cb_skip[h]]: its
-  uint32_t cb_skip[2];    // row (every byte, skip 0), or -- wave-uniform flag to_payload -- the TB payload at the code
-  uint32_t to_payload;    // block's first payload byte (its payload bytes j >= F/8 only, skip F/8)
+  uint8_t* out_bytes;     // wave-uniform: the code-block rows, or -- flag to_payload -- the TB payload buffer
+  uint32_t cb_off[2];     // each half's packed output: byte j of the code block at out_bytes + cb_off[h] + j - skip,
+  uint32_t to_payload;    // skip = 0 (its row: every byte) or F/8 (payload: its bytes j >= F/8 from its first
+                          // payload byte); p2_run0.  (32-bit offsets: the per-lane state across the trellis is 2
+                          // registers, not 6)
   uint32_t K, F[2], max_its, early_stop;
   uint32_t crc24a[2];     // bit 0: C == 1 (CB CRC = TB CRC24A); bit 1: the code block carries the TB CRC
   uint32_t live;          // bit h: half h holds a code block (padding lanes / an unpaired group: 0)
@@ -60,9 +62,14 @@ struct TdecArgsP2 {
                           // re-compacted waterfall: one iteration; the one-shot continuation: 1 .. max_its - 1)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
+// the address of half h's byte j = 0 (p2_run0(a, h) + j: the bytes j in its run)
+MI_HD inline uint8_t* p2_run0(const TdecArgsP2& a, int h) {
+  return a.out_bytes + a.cb_off[h] - (a.to_payload ? a.F[h] / 8 : 0u);
+}
 
 // timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone, 3 = no check pass (no CRC verdicts,
-// no payload), 4 = no check pass and no decision stores (tdec_p2_xhalf, tdec_p2_lane, p2_emit)
+// no payload), 4 = no check pass and no decision stores (tdec_p2_xhalf, tdec_p2_lane, p2_emit), 5 = the check pass
+// without its payload byte stores
 #ifndef MI_TDEC_P2_DIAG
 #define MI_TDEC_P2_DIAG 0
 #endif
@@ -148,6 +155,20 @@ MI_HD inline SbRaw p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& 
 #endif
 }
 
+#if defined(MI_TDEC_P2_DIAG_W2) && defined(__HIP_DEVICE_COMPILE__)
+// timing diagnostic only (wrong results): both halves' inputs of a row from ONE 8-B-per-lane load of group A's rows
+// r, r + 1 (512 B per instruction) -- the access pattern of a pair-interleaved softbuffer ([row][lane][half])
+MI_HD inline void p2_sb_in2(const TdecArgsP2& a, uint32_t m, const PosW& P, uint32_t dt, int lane, SbRaw& x, SbRaw& y) {
+  const uint32_t row = ((m >> dt) & 1u) ? P.v[dt] : a.zrow[0];
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const u2 v = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(a.sb[0]), (uint32_t)lane * 8u, row * 256u, 0);
+  x = __builtin_bit_cast(float, v.x);
+  y = __builtin_bit_cast(float, v.y);
+}
+#define MI_P2_SB_PAIR(A, B, M, DT) p2_sb_in2(a, M, P, DT, lane, A, B)
+#else
+#define MI_P2_SB_PAIR(A, B, M, DT) (A = p2_sb_in(a, 0, ma, P, DT, lane), B = p2_sb_in(a, 1, mb, P, DT, lane))
+#endif
 template <bool DEC2, bool FIRST, bool SQ>
 MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
   const uint32_t* llr1 = a.scr + (size_t)a.K * LANES;
@@ -162,10 +183,8 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
         r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i);
         r.s1[i] = row_ld(a.q, 3 * base, lane, 3 * i + 1);
       } else {
-        r.a0[i] = p2_sb_in(a, 0, ma, P, 3 * i, lane);
-        r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i, lane);
-        r.a1[i] = p2_sb_in(a, 0, ma, P, 3 * i + 1, lane);
-        r.b1[i] = p2_sb_in(a, 1, mb, P, 3 * i + 1, lane);
+        MI_P2_SB_PAIR(r.a0[i], r.b0[i], ma, 3 * i);
+        MI_P2_SB_PAIR(r.a1[i], r.b1[i], ma, 3 * i + 1);
       }
       r.r0[i] = FIRST ? 0u : row_ld(a.scr, base, lane, i);
     } else {
@@ -174,8 +193,7 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
       if constexpr (SQ) {
         r.s0[i] = row_ld(a.q, 3 * base, lane, 3 * i + 2);
       } else {
-        r.a0[i] = p2_sb_in(a, 0, ma, P, 3 * i + 2, lane);
-        r.b0[i] = p2_sb_in(a, 1, mb, P, 3 * i + 2, lane);
+        MI_P2_SB_PAIR(r.a0[i], r.b0[i], ma, 3 * i + 2);
       }
       r.r0[i] = row_ld(llr1, pk, lane);
       if constexpr (!MI_TDEC_P2_X2) r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
@@ -814,12 +832,19 @@ MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
 // partial TB CRC24A of its payload bytes F/8 .. K/8 - (CB CRC ? 3 : 0) that tb_kernel combines.  Returns
 // bit h = half h's code-block CRC passed.  (The byte-wise register of a K-bit block equals the XOR of the
 // per-bit contributions crc_a / crc_b[k] the one-code-block kernels accumulate: CRC is linear.)
+// payload bytes of the check pass as aligned dword stores: 0 = one byte store per byte and half (each store
+// instruction touches 64 code blocks' lines for one byte: 0.5 ms of a 6.6 ms launch, diagnostic 5); 1 = dword stores
+// in every launch; 2 = in the first launch only (the continuation keeps byte stores)
+#ifndef MI_TDEC_P2_PAY32
+#define MI_TDEC_P2_PAY32 1
+#endif
 #ifndef MI_TDEC_P2_PF_CHK
 #define MI_TDEC_P2_PF_CHK 2   // decision-row chunks in flight in the check pass (1 = the round-3 form; 3: 38 VGPRs spilled)
 #endif
 // the code-block and TB CRC registers of both halves over the decision-row chunks [c0, c1) (4 bytes each), from 0;
 // the chunks' payload bytes of the halves in `act` are written
 struct P2CrcRegs { uint32_t cb[2], tb[2]; };
+template <bool PAY32>
 MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32_t act, uint32_t c0, uint32_t c1) {
   uint32_t bl[2], bh[2];
   P2CrcRegs g{{0u, 0u}, {0u, 0u}};
@@ -830,7 +855,6 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
     bh[h] = a.K / 8 - ((a.crc24a[h] & 1u) ? 0 : 3);
     ct[h] = (a.crc24a[h] & 1u) ? a.crc8 : a.crc8b;
   }
-  const bool p0 = act & 1u, p1 = (act >> 1) & 1u;
   const uint32_t nb = a.K / 8;
   // the decision rows of 4 bytes (32 rows) per chunk, MI_TDEC_P2_PF_CHK chunks' loads in flight ahead of the chunk
   // whose bits are used (the trellis registers are dead here); rows past K are clamped to row K - 1 and their bytes
@@ -843,7 +867,19 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
       dd.d[q] = row_ld(a.dec, row < a.K ? row : a.K - 1, lane);
     }
   };
+  // payload bytes of half h: j in [jlo, jhi) -- F/8 .. the CB CRC, less the TB CRC where the code block carries it
+  // (tb_kernel's run) -- at p2_run0(a, h) + j; every byte of a code-block row otherwise
+  // run[h] = m | (jlo + m) << 4 | (jhi + m) << 16 (one register per half; m = the misalignment of byte 0 of the run,
+  // the same for every chunk; byte j lies in the run iff jlo + m <= j + m < jhi + m)
+  uint32_t rng[2], wprev[2] = {0u, 0u};
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t jlo = a.to_payload ? bl[h] : 0u, jhi = a.to_payload ? bh[h] - 3 * ((a.crc24a[h] >> 1) & 1u) : nb;
+    const uint32_t m = (uint32_t)(uintptr_t)p2_run0(a, h) & 3u;
+    rng[h] = m | ((jlo + m) << 4) | ((jhi + m) << 16);
+  }
   auto run = [&](const Chunk& dd, uint32_t c) {
+    uint32_t w[2] = {0u, 0u};   // the chunk's 4 bytes per half, little-endian (byte 4c in bits 0..7)
 #pragma unroll
     for (int jj = 0; jj < 4; jj++) {
       const uint32_t j = 4 * c + (uint32_t)jj;
@@ -854,15 +890,54 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
       const uint32_t xa = (r8[0] << 3) | (r8[1] << 2) | (r8[2] << 1) | r8[3];
       const uint32_t xb = (r8[4] << 3) | (r8[5] << 2) | (r8[6] << 1) | r8[7];
       const uint32_t v0 = ((xa & 0xFu) << 4) | (xb & 0xFu), v1 = (xa & 0xF0u) | (xb >> 4);
-      // payload bytes: F/8 .. the CB CRC, less the TB CRC where the code block carries it (tb_kernel's run)
-      const bool s0 = !a.to_payload || (j >= bl[0] && j < bh[0] - 3 * ((a.crc24a[0] >> 1) & 1u));
-      const bool s1 = !a.to_payload || (j >= bl[1] && j < bh[1] - 3 * ((a.crc24a[1] >> 1) & 1u));
-      if (p0 && s0) a.cb_bytes[0][j - a.cb_skip[0]] = (uint8_t)v0;
-      if (p1 && s1) a.cb_bytes[1][j - a.cb_skip[1]] = (uint8_t)v1;
+      w[0] |= v0 << (8 * jj);
+      w[1] |= v1 << (8 * jj);
       g.cb[0] = ((g.cb[0] << 8) & 0xFFFFFFu) ^ ct[0][((g.cb[0] >> 16) ^ v0) & 0xFFu];
       g.cb[1] = ((g.cb[1] << 8) & 0xFFFFFFu) ^ ct[1][((g.cb[1] >> 16) ^ v1) & 0xFFu];
       if (j >= bl[0] && j < bh[0]) g.tb[0] = ((g.tb[0] << 8) & 0xFFFFFFu) ^ a.crc8[((g.tb[0] >> 16) ^ v0) & 0xFFu];
       if (j >= bl[1] && j < bh[1]) g.tb[1] = ((g.tb[1] << 8) & 0xFFFFFFu) ^ a.crc8[((g.tb[1] >> 16) ^ v1) & 0xFFu];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (MI_TDEC_P2_DIAG == 5 || !((act >> h) & 1u)) continue;
+      uint8_t* const run0 = p2_run0(a, h);   // address of byte j = run0 + j
+      if constexpr (PAY32) {
+        // aligned dword stores: the chunk's bytes sit at 4c + m .. 4c + m + 3 (mod 4); it completes the dword at 4c - m
+        // (the previous chunk's last m bytes and its first 4 - m), written whole when it lies inside the run and the
+        // previous chunk is in this range; the bytes of a dword that is not (the run's and the range's edges) go one
+        // by one.  Every byte is written exactly once, only inside the run (the neighbouring code blocks' bytes are
+        // untouched).
+        const uint32_t m = rng[h] & 3u, lo = (rng[h] >> 4) & 0xFFFu, hi = rng[h] >> 16;
+        // the dword at byte 4c - m, i.e. at 4c .. 4c + 3 in the shifted index
+        const bool full0 = c > c0 && 4 * c >= lo && 4 * c + 4 <= hi;
+        const bool full1 = c + 1 < c1 && 4 * c + 4 >= lo && 4 * c + 8 <= hi;   // the next chunk writes it
+        if (full0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+          const uint32_t v = m ? __builtin_amdgcn_alignbyte(w[h], wprev[h], 4 - m) : w[h];
+#else
+          const uint32_t v = m ? (uint32_t)((((uint64_t)w[h] << 32) | wprev[h]) >> (8 * (4 - m))) : w[h];
+#endif
+          *reinterpret_cast<uint32_t*>(run0 + (4 * c - m)) = v;
+        }
+        // uncovered bytes lie in the range's first 3 chunks (jlo + m < 11) and its last 5 (hi >= nb - 6), a
+        // wave-uniform test
+        if (c < c0 + 3 || c + 5 >= c1) {
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const uint32_t j = 4 * c + (uint32_t)b;
+            const bool covered = (uint32_t)b < 4 - m ? full0 : full1;
+            if (j + m >= lo && j + m < hi && !covered) run0[j] = (uint8_t)(w[h] >> (8 * b));
+          }
+        }
+        wprev[h] = w[h];
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t j = 4 * c + (uint32_t)b;
+          const uint32_t m = rng[h] & 3u;
+          if (j + m >= ((rng[h] >> 4) & 0xFFFu) && j + m < (rng[h] >> 16)) run0[j] = (uint8_t)(w[h] >> (8 * b));
+        }
+      }
     }
   };
   if (c1 > c0)
@@ -884,14 +959,14 @@ MI_HD inline uint32_t crc24_shift(uint32_t r, uint32_t L, const uint32_t* tab) {
 #ifndef MI_TDEC_P2_SPLIT_CHK
 #define MI_TDEC_P2_SPLIT_CHK 0
 #endif
-template <class Exec>
+template <bool PAY32, class Exec>
 MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2], Exec& ex) {
   const uint32_t nb = a.K / 8, nc = (nb + 3) / 4;
   P2CrcRegs g;
   if constexpr (MI_TDEC_P2_SPLIT_CHK) {
     const uint32_t ncf = (nc + 1) / 2, jb = 4 * ncf;   // wave B: bytes jb .. nb - 1
     P2CrcRegs gf{{0u, 0u}, {0u, 0u}}, gb{{0u, 0u}, {0u, 0u}};
-    ex.run([&] { gf = tdec_p2_check_range(a, lane, act, 0, ncf); }, [&] { gb = tdec_p2_check_range(a, lane, act, ncf, nc); });
+    ex.run([&] { gf = tdec_p2_check_range<PAY32>(a, lane, act, 0, ncf); }, [&] { gb = tdec_p2_check_range<PAY32>(a, lane, act, ncf, nc); });
     uint32_t v[4] = {gb.cb[0], gb.cb[1], gb.tb[0], gb.tb[1]};
     ex.share_from_b(v, lane);
     const uint32_t lcb = nb > jb ? nb - jb : 0u;
@@ -904,7 +979,7 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
       g.tb[h] = crc24_shift(gf.tb[h], ltb, a.crc8) ^ v[2 + h];
     }
   } else {
-    g = tdec_p2_check_range(a, lane, act, 0, nc);
+    g = tdec_p2_check_range<PAY32>(a, lane, act, 0, nc);
   }
   if (act & 1u) tbp[0] = g.tb[0];
   if (act & 2u) tbp[1] = g.tb[1];
@@ -925,6 +1000,7 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
   constexpr bool CK = CONT ? MI_TDEC_P2C_CK8 : MI_TDEC_P2_CK8;
   constexpr int PQ = CONT ? MI_TDEC_P2C_PF_Q : MI_TDEC_P2_PF_Q;
+  constexpr bool PAY = MI_TDEC_P2_PAY32 == 1 || (MI_TDEC_P2_PAY32 == 2 && !CONT);
   if constexpr (CONT)
     if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
   for (uint32_t it = CONT ? a.it0 : 0u; it < (CONT ? a.it_end : a.max_its) && active; it++) {
@@ -954,9 +1030,9 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     uint32_t ok = 0u;
     if (a.early_stop || last) {   // wave-uniform
       if constexpr (MI_TDEC_P2_SPLIT_CHK) {   // both waves run the pass; wave F's verdicts go to both
-        if (MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check(a, lane, active, r.tb_part, ex);
+        if (MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check<PAY>(a, lane, active, r.tb_part, ex);
       } else {
-        if (ex.pack_wave() && MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check(a, lane, active, r.tb_part, ex);
+        if (ex.pack_wave() && MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check<PAY>(a, lane, active, r.tb_part, ex);
       }
       ok = ex.share(ok, lane);
     }
