@@ -403,8 +403,12 @@ __global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* 
 }
 
 // 3. iterations it0 .. it_end - 1 of the continuing code blocks, dense pairs (pair stride pair_u32, decision rows
-// dec_stride bytes apart)
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
+// dec_stride bytes apart).  Its register budget is a parameter of its own (MI_TDEC_P2C_WAVES): the continuation
+// holds well under one wavefront per SIMD, so a larger budget costs it no occupancy
+#ifndef MI_TDEC_P2C_WAVES
+#define MI_TDEC_P2C_WAVES MI_TDEC_P2_WAVES
+#endif
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2C_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
