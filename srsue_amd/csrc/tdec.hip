@@ -408,6 +408,12 @@ __global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* 
 #ifndef MI_TDEC_P2C_WAVES
 #define MI_TDEC_P2C_WAVES MI_TDEC_P2_WAVES
 #endif
+// MI_TDEC_P2C_CK_LATE: the re-compaction rounds after the first (few pairs, far below the HBM rate) take 4-step
+// checkpoints -- a shorter lone chain for twice the checkpoint bytes (MI_TDEC_P2C_CK8 above)
+#ifndef MI_TDEC_P2C_CK_LATE
+#define MI_TDEC_P2C_CK_LATE 0
+#endif
+template <bool CK8>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2C_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
@@ -448,7 +454,7 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.it0 = it0;
   a.it_end = it_end;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
-  const TdecP2Result r = tdec_p2_lane<true>(a, lane, ex);
+  const TdecP2Result r = tdec_p2_lane<true, CK8>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -477,7 +483,8 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
                      ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored);
   const size_t cdec_stride = (size_t)K * LANES;
   if (!rounds) {   // one launch for iterations 1 .. max_its - 1 (each pair until its slowest code block stops)
-    hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes, ktab_data, kt, cont,
+    hipLaunchKernelGGL(tdec_kernel_p2c<MI_TDEC_P2C_CK8>, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes,
+                       ktab_data, kt, cont,
                        pair_u32, cdec_stride, K, max_its, (uint32_t)w_stored, 1u, max_its);
     return;
   }
@@ -497,8 +504,14 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
       hipLaunchKernelGGL(tdec_cont_gather2_kernel, dim3(gather_wgs), dim3(256), 0, st, bufs[b ^ 1], strides[b ^ 1],
                          lists[l], src, bufs[b], strides[b], K);
     }
-    hipLaunchKernelGGL(tdec_kernel_p2c, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes, ktab_data, kt,
-                       lists[l], strides[b], dstrides[b], K, max_its, (uint32_t)(w_stored || it > 1), it, it + 1);
+    if (MI_TDEC_P2C_CK_LATE && it > 1)
+      hipLaunchKernelGGL(tdec_kernel_p2c<false>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes,
+                         ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, (uint32_t)(w_stored || it > 1),
+                         it, it + 1);
+    else
+      hipLaunchKernelGGL(tdec_kernel_p2c<MI_TDEC_P2C_CK8>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out,
+                         lanes, ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its,
+                         (uint32_t)(w_stored || it > 1), it, it + 1);
   }
 }
 

@@ -992,13 +992,13 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
 // iteration count) only the last iteration's pass runs.
 // CONT (waterfall compaction, tdec.hip): the code blocks continue from iteration 1 in a dense continuation
 // pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
-template <bool CONT = false, class Exec>
+template <bool CONT = false, bool CKC = MI_TDEC_P2C_CK8, class Exec>
 MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
   // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
-  constexpr bool CK = CONT ? MI_TDEC_P2C_CK8 : MI_TDEC_P2_CK8;
+  constexpr bool CK = CONT ? CKC : MI_TDEC_P2_CK8;   // CKC: the continuation's spacing (tdec.hip tdec_kernel_p2c)
   constexpr int PQ = CONT ? MI_TDEC_P2C_PF_Q : MI_TDEC_P2_PF_Q;
   constexpr bool PAY = MI_TDEC_P2_PAY32 == 1 || (MI_TDEC_P2_PAY32 == 2 && !CONT);
   if constexpr (CONT)
