@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* 
 // MI_TDEC_P2C_CK_LATE: the re-compaction rounds after the first (few pairs, far below the HBM rate) take 4-step
 // checkpoints -- a shorter lone chain for twice the checkpoint bytes (MI_TDEC_P2C_CK8 above)
 #ifndef MI_TDEC_P2C_CK_LATE
-#define MI_TDEC_P2C_CK_LATE 0
+#define MI_TDEC_P2C_CK_LATE 1
 #endif
 template <bool CK8>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2C_WAVES)))
