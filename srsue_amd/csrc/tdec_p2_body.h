@@ -50,7 +50,7 @@ struct TdecArgsP2 {
   uint8_t* out_bytes;     // wave-uniform: the code-block rows, or -- flag to_payload -- the TB payload buffer
   uint32_t cb_off[2];     // each half's packed output: byte j of the code block at out_bytes + cb_off[h] + j - skip,
   uint32_t to_payload;    // skip = 0 (its row: every byte) or F/8 (payload: its bytes j >= F/8 from its first
-                          // payload byte); p2_run0.  (32-bit offsets: the per-lane state across the trellis is 2
+                          // payload byte); p2_run_off.  (32-bit offsets: the per-lane state across the trellis is 2
                           // registers, not 6)
   uint32_t K, F[2], max_its, early_stop;
   uint32_t crc24a[2];     // bit 0: C == 1 (CB CRC = TB CRC24A); bit 1: the code block carries the TB CRC
@@ -62,9 +62,11 @@ struct TdecArgsP2 {
                           // re-compacted waterfall: one iteration; the one-shot continuation: 1 .. max_its - 1)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
-// the address of half h's byte j = 0 (p2_run0(a, h) + j: the bytes j in its run)
-MI_HD inline uint8_t* p2_run0(const TdecArgsP2& a, int h) {
-  return a.out_bytes + a.cb_off[h] - (a.to_payload ? a.F[h] / 8 : 0u);
+// the offset of half h's byte j = 0 from out_bytes: byte j of its run is out_bytes[p2_run_off(a, h) + j].  Signed and
+// added only with j (>= F/8 in the run): the first code block of a TB at payload offset 0 has a negative one, and no
+// pointer before the buffer is ever formed
+MI_HD inline int64_t p2_run_off(const TdecArgsP2& a, int h) {
+  return (int64_t)a.cb_off[h] - (int64_t)(a.to_payload ? a.F[h] / 8 : 0u);
 }
 
 // timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone, 3 = no check pass (no CRC verdicts,
@@ -868,14 +870,14 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
     }
   };
   // payload bytes of half h: j in [jlo, jhi) -- F/8 .. the CB CRC, less the TB CRC where the code block carries it
-  // (tb_kernel's run) -- at p2_run0(a, h) + j; every byte of a code-block row otherwise
+  // (tb_kernel's run) -- at out_bytes[p2_run_off(a, h) + j]; every byte of a code-block row otherwise
   // run[h] = m | (jlo + m) << 4 | (jhi + m) << 16 (one register per half; m = the misalignment of byte 0 of the run,
   // the same for every chunk; byte j lies in the run iff jlo + m <= j + m < jhi + m)
   uint32_t rng[2], wprev[2] = {0u, 0u};
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t jlo = a.to_payload ? bl[h] : 0u, jhi = a.to_payload ? bh[h] - 3 * ((a.crc24a[h] >> 1) & 1u) : nb;
-    const uint32_t m = (uint32_t)(uintptr_t)p2_run0(a, h) & 3u;
+    const uint32_t m = ((uint32_t)(uintptr_t)a.out_bytes + (uint32_t)p2_run_off(a, h)) & 3u;   // (mod 4: wraps)
     rng[h] = m | ((jlo + m) << 4) | ((jhi + m) << 16);
   }
   auto run = [&](const Chunk& dd, uint32_t c) {
@@ -900,7 +902,7 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       if (MI_TDEC_P2_DIAG == 5 || !((act >> h) & 1u)) continue;
-      uint8_t* const run0 = p2_run0(a, h);   // address of byte j = run0 + j
+      const int64_t off = p2_run_off(a, h);   // byte j at out_bytes[off + j], j in the run
       if constexpr (PAY32) {
         // aligned dword stores: the chunk's bytes sit at 4c + m .. 4c + m + 3 (mod 4); it completes the dword at 4c - m
         // (the previous chunk's last m bytes and its first 4 - m), written whole when it lies inside the run and the
@@ -917,7 +919,7 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
 #else
           const uint32_t v = m ? (uint32_t)((((uint64_t)w[h] << 32) | wprev[h]) >> (8 * (4 - m))) : w[h];
 #endif
-          *reinterpret_cast<uint32_t*>(run0 + (4 * c - m)) = v;
+          *reinterpret_cast<uint32_t*>(a.out_bytes + (off + (int64_t)(4 * c) - (int64_t)m)) = v;
         }
         // uncovered bytes lie in the range's first 3 chunks (jlo + m < 11) and its last 5 (hi >= nb - 6), a
         // wave-uniform test
@@ -926,7 +928,7 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
           for (int b = 0; b < 4; b++) {
             const uint32_t j = 4 * c + (uint32_t)b;
             const bool covered = (uint32_t)b < 4 - m ? full0 : full1;
-            if (j + m >= lo && j + m < hi && !covered) run0[j] = (uint8_t)(w[h] >> (8 * b));
+            if (j + m >= lo && j + m < hi && !covered) a.out_bytes[off + (int64_t)j] = (uint8_t)(w[h] >> (8 * b));
           }
         }
         wprev[h] = w[h];
@@ -935,7 +937,8 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
         for (int b = 0; b < 4; b++) {
           const uint32_t j = 4 * c + (uint32_t)b;
           const uint32_t m = rng[h] & 3u;
-          if (j + m >= ((rng[h] >> 4) & 0xFFFu) && j + m < (rng[h] >> 16)) run0[j] = (uint8_t)(w[h] >> (8 * b));
+          if (j + m >= ((rng[h] >> 4) & 0xFFFu) && j + m < (rng[h] >> 16))
+            a.out_bytes[off + (int64_t)j] = (uint8_t)(w[h] >> (8 * b));
         }
       }
     }
