@@ -182,3 +182,41 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
         assert len(set(cbits[64:64 + 143].tolist())) >= 3   # code blocks of one lane stopped at different its
         assert not compact or n_cont > 20
         assert compact != "rounds" or n_round > 0   # some code blocks went through a re-compaction
+
+
+@pytest.mark.parametrize("base", [1, 2, 3])
+def test_emulated_packed_payload_at_misaligned_base(built, base):
+    """The packed decoder's check pass writes each code block's payload run as aligned dwords (tdec_p2_body.h
+    tdec_p2_check_range, MI_TDEC_P2_PAY32): the dword a chunk completes is the previous chunk's last m bytes and its
+    first 4 - m, m = the run's misalignment, and only the run's edges go byte by byte.  With the payload buffer at
+    base offsets 1-3 every code block's m changes; the bytes must equal the oracle's, and the bytes in front of the
+    buffer and behind it must stay untouched (no write outside any run)."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(10)]
+    cfgs.append(abi.sf_cfg(cell_id=301, nof_prb=6, sf_idx=2, tbs=4392, Qm=6))
+    iqs = [abi.tx_subframe(c, tb_bytes(300 + i, c.tbs), snr_db=30.0, seed=700 + i) for i, c in enumerate(cfgs)]
+    llrs = [oracle_front(c, iq)[3] for c, iq in zip(cfgs, iqs)]
+    arr = abi.cfg_array(cfgs)
+    n = len(cfgs)
+    E = abi.emu()
+    offs = [E.emu_payload_offset(C.cast(arr, C.c_void_p), n, i) for i in range(n)]
+    total = offs[-1] + cfgs[-1].tbs // 8
+    raw = np.full(total + 16, 0xA5, np.uint8)   # guard bytes before and after the payload
+    pe = raw[base:base + total]
+    eok = np.zeros(n, np.uint32)
+    eits = np.zeros(n, np.uint32)
+    flat = np.concatenate(llrs).astype(np.float32)
+    E.emu_set_tdec_i16(1)
+    E.emu_set_tdec_x(3)
+    try:
+        rc = E.emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
+                              eok.ctypes.data, eits.ctypes.data, None)
+    finally:
+        E.emu_set_tdec_i16(0)
+        E.emu_set_tdec_x(0)
+    assert rc == 0
+    assert np.all(raw[:base] == 0xA5) and np.all(raw[base + total:] == 0xA5)
+    for i, c in enumerate(cfgs):
+        with O.tdec_mode(O.TDEC_I16):
+            ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
+        assert ok and bool(eok[i]), i
+        assert np.array_equal(pe[offs[i]:offs[i] + c.tbs // 8], opay), i
