@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ab_r3/ is made with: mkdir ab_r3 && git archive 54cb33e bench.py srsue_amd oracle include profiles/traffic.json | tar -x -C ab_r3, then make in ab_r3/srsue_amd/csrc)
 # same-box A/B of the round-3 final build (ab_r3/: bench.py + package of commit 54cb33e with its library, not
 # committed) and the current build: configs[0] (3 streams and one stream), then the default bench
 set -o pipefail
