@@ -22,8 +22,18 @@ import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
+
+# HIP hardware queues per process (--hw-queues, default 8; 0 keeps the environment's value): the bench keeps 4
+# batches in flight on as many HIP streams, and with HIP's default of 4 queues per process the streams' kernels
+# share them with the runtime's own copies; 8 queues measured +0.7 % at the headline, 16 no better
+# (profiles/r4/ab_queues).  Set here, before torch and the HIP runtime start (the runtime reads it once); the ranks
+# bench.py spawns inherit it.
+HW_QUEUES = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--hw-queues"), "8")
+if HW_QUEUES != "0":
+    os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -339,6 +349,7 @@ def bench_codeblocks(args, world, rank, dev):
            "config": {"workload": f"configs[0] turbodecoder_test: K=6144, 8 iterations, no early stop, BPSK/AWGN "
                                   f"Eb/N0 {args.ebno:g} dB, {n} code blocks per GPU per step", "K": K, "iterations": 8,
                       "codeblocks_per_gpu": n, "turbo_arithmetic": args.tdec, "streams": S,
+                      "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                       "turbo_schedule": SCHED_DESC[tb.turbo_sched]},
            "turbo_codeblocks_per_s": round(cbps, 1), "ber": ber, "stage_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
            "roofline": {"kernel": tdec_kernel_name(tb.turbo_sched), "bound": "hbm", "achieved": round(ach, 2),
@@ -932,6 +943,9 @@ def main():
                     help="--streams of the waterfall block; 0 = auto (= --streams: its continuation holds 0.74 "
                          "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
                          "profiles/r3/ab_streams*)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process and its ranks (set before the HIP runtime starts, see "
+                         "HW_QUEUES above); 0 = keep the environment's value")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--plan-steps", type=int, default=40,
                     help="default config: steps of the planning block (per-step re-planning on host threads, VERDICT r3 "
@@ -1072,6 +1086,7 @@ def main():
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "channel_estimates": "full" if (args.ce == "full" or args.ctrl or args.llr_stream) else "compact",
                        **({"llr_stream": True} if args.llr_stream else {}),
                        "parallelism": f"replicas x{world} (no collective on the data path)"},
