@@ -140,8 +140,8 @@ int    mi_dl_batch_turbo_compact(const mi_dl_batch_t *b);
 uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
 /* groups whose rate de-matching runs in the direct form (every valid lane a new TB with one rank table, one
  * k0 rank, one modulation, E <= N_v: each LLR written straight to its softbuffer row); the others gather per
- * circular-buffer position.  The environment variable MI_RM_DIRECT=0 (read at planning) disables the direct
- * form for A/B runs; the softbuffer is bit-identical either way. */
+ * circular-buffer position.  The environment variable MI_RM_DIRECT=0 (read when the batch is created) disables
+ * the direct form for A/B runs; the softbuffer is bit-identical either way. */
 uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
 
 /* ---- streaming re-planning (srsUE re-derives the grant every TTI: phch_worker.cc:297 -> :337).
@@ -152,7 +152,13 @@ uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
  * so the caller passes the stream the batch runs on.  The plan object keeps its lookup caches (scrambling
  * words per (RNTI, sf, G), CRS per cell, per-K tables: srslte_ue_dl_set_rnti's pregeneration) across builds,
  * and after a replan it holds the batch's previous plan, ready to be rebuilt.  One plan object per planning
- * thread; a batch's work buffers only grow (a larger plan reallocates them, synchronously). */
+ * thread; a batch's work buffers only grow (a larger plan reallocates them, synchronously).
+ * HARQ continuity across a replan: the softbuffer rows of a code block are where the plan puts them, so soft
+ * combining (new_tb = 0 lanes) carries over only when the new plan lays the softbuffer out exactly as the old one
+ * (same groups, softbuffer offsets and code-block-to-lane assignment -- e.g. the same grants with a new rv).  When
+ * the layout differs and the new plan has retransmission lanes, the replan clears the softbuffer (every value
+ * RX_NULL, as srslte_softbuffer_rx_reset), so such a lane combines with nothing rather than with another code
+ * block's rows.  (New transmissions overwrite their rows; rows another layout left are settled by the kernels.) */
 typedef struct mi_dl_plan mi_dl_plan_t;
 mi_dl_plan_t *mi_dl_plan_create(void);
 void   mi_dl_plan_destroy(mi_dl_plan_t *p);

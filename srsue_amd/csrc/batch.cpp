@@ -16,8 +16,7 @@ mi_dl_batch_t* mi_dl_batch_create(const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf, uin
   b->cfgs.assign(cfgs, cfgs + n_sf);
   b->eng.max_its = max_its ? max_its : 4;
   b->eng.flags = flags;
-  (void)hipGetDevice(&b->eng.device);
-  if (b->eng.plan.build(cfgs, n_sf, true) || b->eng.upload(nullptr, true) ||
+  if (!mi::hip_ok(hipGetDevice(&b->eng.device), "device") || b->eng.plan.build(cfgs, n_sf, true) || b->eng.upload(nullptr, true) ||
       !mi::hip_ok(hipStreamSynchronize(nullptr), "upload sync")) {
     delete b;
     return nullptr;
@@ -152,7 +151,24 @@ int mi_dl_batch_replan(mi_dl_batch_t* b, mi_dl_plan_t* p, void* stream) {
   std::swap(b->cfgs, p->cfgs);
   p->built = false;
   b->eng.last_stream = st;
-  return b->eng.upload(st, true);
+  // HARQ continuity only across an identical softbuffer layout (include/mi_dl.h): p->plan now holds the old plan
+  const mi::PlanData &nw = b->eng.plan, &old = p->plan;
+  bool same = nw.groups.size() == old.groups.size() && nw.lanes.size() == old.lanes.size() && nw.cb_list == old.cb_list &&
+              nw.sb_floats == old.sb_floats;
+  for (size_t g = 0; same && g < nw.groups.size(); g++)
+    same = nw.groups[g].K == old.groups[g].K && nw.groups[g].Ncb == old.groups[g].Ncb &&
+           nw.groups[g].lane0 == old.groups[g].lane0 && nw.groups[g].sb_off == old.groups[g].sb_off;
+  for (size_t l = 0; same && l < nw.lanes.size(); l++)
+    same = nw.lanes[l].valid == old.lanes[l].valid && nw.lanes[l].tb == old.lanes[l].tb &&
+           nw.lanes[l].F == old.lanes[l].F;
+  bool combines = false;   // new transmissions overwrite their rows (stale rows of another layout are settled)
+  for (const MiLaneDesc& ld : nw.lanes) combines |= ld.valid && !ld.new_tb;
+  const size_t had = b->eng.d_sb.bytes;
+  if (b->eng.upload(st, true)) return -1;
+  // (a reallocated softbuffer was zeroed by upload)
+  if (!same && combines && had && b->eng.d_sb.bytes == had)
+    return mi::hip_ok(hipMemsetAsync(b->eng.d_sb.p, 0, b->eng.d_sb.bytes, st), "replan softbuffer reset") ? 0 : -1;
+  return 0;
 }
 
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */

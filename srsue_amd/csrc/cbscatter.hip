@@ -23,23 +23,15 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const float* __restrict
     tile[l][q] = (cb < n_cb && t0 + q < T) ? d[(size_t)cb * T + t0 + q] : 0.0f;
   }
   __syncthreads();
-  const uint32_t* pos = kdata + ktabs[g.ktab].pos_off;
   float* sbg = sb + g.sb_off;
   for (uint32_t i = w; i < (uint32_t)SC_T; i += 4) {
     const uint32_t t = t0 + i;
-    if (t < T) {
-      const size_t row = MI_SB_NAT ? t : pos[t];   // dl_common.h MI_SB_NAT
-      sbg[row * LANES + q] = tile[q][i];
-      sb_q16_put(sbg, g.Ncb, row * LANES + q, q16s(tile[q][i]));   // and the int16 mirror
-    }
+    if (t < T) sbg[(size_t)t * LANES + q] = tile[q][i];   // rows in decoder-input order (dl_common.h)
   }
   if (blockIdx.x == 0) {   // every row written: the whole map materialised, plus the zero row
     uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(g.Ncb));
     for (uint32_t p = tid; p < g.Ncb; p += 256) map[p] = 1;
-    if (tid < LANES) {
-      sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;
-      sb_q16_put(sbg, g.Ncb, (size_t)g.Ncb * LANES + tid, 0);
-    }
+    if (tid < LANES) sbg[(size_t)g.Ncb * LANES + tid] = 0.0f;
   }
 }
 

@@ -42,20 +42,9 @@ __host__ __device__ inline float ce_tt(int l) {
 __host__ __device__ inline float2 ce_time_interp(float2 a, float2 b, float tt) {
   return make_float2(__builtin_fmaf(tt, b.x - a.x, a.x), __builtin_fmaf(tt, b.y - a.y, a.y));
 }
-#ifndef MI_TDEC_CK
-#define MI_TDEC_CK 4
-#endif
-constexpr int TDEC_CK = MI_TDEC_CK;  // beta checkpoint spacing: BETA_W (one window) or 2 BETA_W
-#ifndef MI_TDEC_CK_Q16
-#define MI_TDEC_CK_Q16 4
-#endif
-constexpr int TDEC_CK_Q16 = MI_TDEC_CK_Q16;   // same for the int16 decoder (fewer VGPRs per value)
-constexpr int TDEC_CK_MIN = TDEC_CK < TDEC_CK_Q16 ? TDEC_CK : TDEC_CK_Q16;   // scratch sizing
+constexpr int TDEC_CK_MIN = 4;   // scratch sizing: one checkpoint slot per BETA_W-step window (the decoders use a subset)
 constexpr float FILLER_LLR = -10000.0f;
-#ifndef MI_RM_CHUNK
-#define MI_RM_CHUNK 128
-#endif
-constexpr int RM_CHUNK = MI_RM_CHUNK;  // circular-buffer positions per rate-dematch workgroup (64 or 128)
+constexpr int RM_CHUNK = 128;  // circular-buffer positions per rate-dematch workgroup
 constexpr int WM_STRIDE = KMAX / BETA_W + 4;   // turbo window masks per group (rowmask_kernel)
 
 __host__ __device__ inline int symbol_sz(uint32_t nof_prb) {
@@ -188,45 +177,15 @@ namespace mi {
 // receive an LLR (or must keep a HARQ history) and rewrites the map; the turbo decoder fetches
 // unmaterialised rows from the zero row (L2-resident) instead of HBM.  Punctured positions never
 // cost HBM traffic and a reset only needs the map cleared.
-// Softbuffer rows in decoder-input order (MI_SB_NAT, default): the value of circular-buffer position p lives in
-// row ipos[p] -- the decoder input index t it feeds (MiKTab::ipos_off; dummy positions have none and are never
-// materialised) -- so the turbo decoder reads rows t = 3 k + stream in sequence, with no position table on its
-// path; rate de-matching does the mapping once when it writes.  The row map stays indexed by position p.
-#ifndef MI_SB_NAT
-#define MI_SB_NAT 1
-#endif
-// The int16 mirror (round 4): after the map, [Ncb + 1][64] int16 rows holding q(x) = clamp(rint(32 x), +-511) -- the
-// int16 turbo decoder's input quantiser -- of the fp32 row with the same index.  Every writer of a softbuffer row
-// (rate de-matching, its idle settling, the zero rows, the raw code-block scatter) writes the row's mirror with it,
-// so a mirror row is valid exactly where its fp32 row is materialised (the same row map and zero row apply).  The
-// packed int16 decoder reads its channel inputs from the mirror: 128-B rows instead of 256-B rows and no
-// quantisation on its chain; the fp32 rows stay the HARQ softbuffer (srsLTE's float buffer_f, combined in float).
-// Measured and NOT the default (MI_SB_Q16=1 builds it; profiles/r4/ab_mirror): one stream, tdec 6.40-6.54 ->
-// 5.89-5.93 ms but rate de-matching 2.45-2.53 -> 2.94-2.95 ms (its writes grow by half) -- net -0.1 ms; on the
-// default 4 streams the headline loses 3 % (the chain is bound by its total traffic, and the mirror trades 26 KB of
-// turbo reads for 14 KB of rate-matching writes per code block at an HBM-write cost).  Off: no mirror space, no
-// mirror writes, the decoder quantises the fp32 rows.
-#ifndef MI_SB_Q16
-#define MI_SB_Q16 0
-#endif
+// Softbuffer rows in decoder-input order: the value of circular-buffer position p lives in row ipos[p] -- the decoder
+// input index t it feeds (MiKTab::ipos_off; dummy positions have none and are never materialised) -- so the turbo
+// decoder reads rows t = 3 k + stream in sequence, with no position table on its path; rate de-matching does the
+// mapping once when it writes.  The row map stays indexed by position p.
+// (An int16 mirror of the rows, written beside them by rate de-matching for the decoder, was measured in round 4 and
+// dropped: tdec -8 % but rate de-matching +20 %, the 4-stream headline -3 %; profiles/r4/ab_mirror.)
 __host__ __device__ inline size_t sb_map_off(uint32_t Ncb) { return (size_t)(Ncb + 1) * LANES; }   // floats
-__host__ __device__ inline size_t sb_q16_off(uint32_t Ncb) {                                       // floats
-  return sb_map_off(Ncb) + (size_t)((Ncb + 255) / 256) * LANES;
-}
 __host__ __device__ inline size_t sb_group_floats(uint32_t Ncb) {   // a multiple of 64 floats (256 B)
-  return sb_q16_off(Ncb) + (MI_SB_Q16 ? ((size_t)(Ncb + 1) * LANES / 2 + LANES - 1) / LANES * LANES : 0);
-}
-__host__ __device__ inline int16_t* sb_q16(float* sbg, uint32_t Ncb) {
-  return reinterpret_cast<int16_t*>(sbg + sb_q16_off(Ncb));
-}
-__host__ __device__ inline const int16_t* sb_q16(const float* sbg, uint32_t Ncb) {
-  return reinterpret_cast<const int16_t*>(sbg + sb_q16_off(Ncb));
-}
-// the mirror value of a softbuffer value (q16f, as an int16)
-__host__ __device__ inline int16_t q16s(float x) { return (int16_t)q16f(x); }
-// write element idx ([row][lane] index) of a group's mirror
-__host__ __device__ inline void sb_q16_put(float* sbg, uint32_t Ncb, size_t idx, int16_t v) {
-  if (MI_SB_Q16) sb_q16(sbg, Ncb)[idx] = v;
+  return sb_map_off(Ncb) + (size_t)((Ncb + 255) / 256) * LANES;
 }
 }  // namespace mi
 

@@ -92,7 +92,7 @@ static mi::TdecLaneResult emu_win_cb(const MiGroupDesc& g, const MiKTab& kt, con
   c.lmap = lmap.data();
   for (uint32_t t = 0; t < P; t++) mi::win_load_map(c, t, P, sbg, g.Ncb);
   for (uint32_t t = 0; t < P; t++)
-    mi::win_load(c, t, P, sbg, g.Ncb, kdata + (MI_SB_NAT ? kt.pos_off : kt.ipos_off), kdata + kt.pi_off, lane, ld.F);
+    mi::win_load(c, t, P, sbg, kdata + kt.pos_off, kdata + kt.pi_off, lane, ld.F);
   const uint32_t* tab = kdata + (ld.crc24a ? kt.crca_off : kt.crcb_off);
   mi::TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < max_its; it++) {
@@ -149,6 +149,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
       wms[gi].resize(g.K / mi::BETA_W + 1);
       for (uint32_t w = 0; w < wms[gi].size(); w++) wms[gi][w] = mi::tdec_window_mask(map, &P.kdata[kt.pos_off], w);
     }
+    std::vector<uint32_t> stash((size_t)mi::P2_STASH_ROWS * mi::LANES);
     for (size_t pp = 0; pp < P.pairs.size(); pp += 2) {
       const uint32_t ga = P.pairs[pp], gbi = P.pairs[pp + 1];
       const bool paired = gbi != 0xFFFFFFFFu;
@@ -162,7 +163,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.live = (l0.valid ? 1u : 0u) | (paired && l1.valid ? 2u : 0u);
         if (!a.live) continue;
         a.sb[0] = &sb[gA.sb_off]; a.sb[1] = &sb[gB.sb_off];
-        a.sbq[0] = mi::sb_q16(a.sb[0], gA.Ncb); a.sbq[1] = mi::sb_q16(a.sb[1], gB.Ncb);
+        a.stash = stash.data();   // the LDS stash of the 16-step spans (one lane at a time here)
         a.wm[0] = wms[ga].data(); a.wm[1] = wms[gb].data();
         a.zrow[0] = gA.Ncb; a.zrow[1] = gB.Ncb;
         a.scr = reinterpret_cast<uint32_t*>(&scr[gA.scratch_off]);
@@ -223,7 +224,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               const uint32_t li = cont[d];
               live |= 1u << h;
               const uint32_t g = li / mi::LANES;
-              src[h] = {&sb[P.groups[g].sb_off], mi::sb_q16(&sb[P.groups[g].sb_off], P.groups[g].Ncb), wms[g].data(),
+              src[h] = {&sb[P.groups[g].sb_off], wms[g].data(),
                         reinterpret_cast<const uint32_t*>(&scr[P.groups[pa[g]].scratch_off]), li % mi::LANES, ph[g]};
             }
             if (!live) continue;

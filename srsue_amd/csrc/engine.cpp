@@ -40,7 +40,28 @@ void DevBuf::release() {
   view = false;
 }
 
+namespace {
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+}  // namespace
+
+Engine::Engine() {
+  opts.tdec_x = env_int("MI_TDEC_X", -1);
+  opts.compact = env_int("MI_TDEC_COMPACT", -1);
+  opts.store_w = env_int("MI_TDEC_STORE_W", -1);
+  opts.rounds = env_int("MI_TDEC_ROUNDS", -1);
+  opts.win_threads = (uint32_t)std::max(0, env_int("MI_TDEC_WIN_THREADS", 0));
+  plan.rm_direct_on = env_int("MI_RM_DIRECT", 1) != 0;
+  plan.xcd_queues = env_int("MI_RM_XCDQ", 1) != 0;
+}
+
 Engine::~Engine() {
+  if (cont_ev) {
+    (void)hipEventSynchronize(cont_ev);
+    (void)hipEventDestroy(cont_ev);
+  }
   if (stage_done) {
     (void)hipEventSynchronize(stage_done);
     (void)hipEventDestroy(stage_done);
@@ -219,8 +240,9 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     }
     ev = ev_sets[ev_used++].data();
   }
+  bool ok = true;
   auto mark = [&](int i) {
-    if (prof) (void)hipEventRecord(ev[i], st);
+    if (prof) ok = hip_ok(hipEventRecord(ev[i], st), "event") && ok;
   };
   const uint32_t nsf = (uint32_t)P.sfs.size();
   // compact channel estimates (MI_DL_FLAG_CE_COMPACT): only when this run both writes and consumes them
@@ -276,9 +298,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,
                         rm_items(), rm_recs(), P.rm_busy, P.rm_dbusy, (uint32_t)P.rm_items.size(), st);
     mark(4);
-    if (mask & (1u << MI_DL_STAGE_TDEC)) {
-      launch_turbo(sb, st);
-    }
+    if (mask & (1u << MI_DL_STAGE_TDEC)) ok = launch_turbo(sb, st) && ok;
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
@@ -288,7 +308,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   } else {
     for (int i = 3; i <= 6; i++) mark(i);
   }
-  return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
+  return hip_ok(hipGetLastError(), "launch") && ok ? 0 : -1;
 }
 
 int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
@@ -305,17 +325,18 @@ int Engine::run_codeblocks(const float* d_in, hipStream_t st) {
     }
     ev = ev_sets[ev_used++].data();
   }
+  bool ok = true;
   auto mark = [&](int i) {
-    if (prof) (void)hipEventRecord(ev[i], st);
+    if (prof) ok = hip_ok(hipEventRecord(ev[i], st), "event") && ok;
   };
   for (int i = 0; i <= MI_DL_STAGE_RM; i++) mark(i);
   launch_cb_scatter(d_in, d_sb.as<float>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                     (uint32_t)P.groups.size(), P.cb_K, P.cb_n, st);
   mark(MI_DL_STAGE_TDEC);
-  launch_turbo(d_sb.as<float>(), st);
+  ok = launch_turbo(d_sb.as<float>(), st) && ok;
   mark(MI_DL_STAGE_TB);
   mark(MI_DL_NSTAGES);
-  return hip_ok(hipGetLastError(), "launch") ? 0 : -1;
+  return hip_ok(hipGetLastError(), "launch") && ok ? 0 : -1;
 }
 
 bool Engine::use_win() const {
@@ -331,7 +352,7 @@ bool Engine::use_win() const {
 // the batch's 2 G wavefronts do not fit at 4 but fit at 5 per SIMD (the headline: 2,540 groups), the
 // recompute form (92 VGPRs) keeps them all resident in one round (-6 % at the headline; at lower
 // occupancy its extra VALU makes it slower than the register form).  MI_DL_FLAG_TDEC_LANE alone = one
-// wavefront per group; MI_DL_FLAG_TDEC_X = crossed; MI_TDEC_X (env, A/B) = 0 / 1 / 2.
+// wavefront per group; MI_DL_FLAG_TDEC_X = crossed; Opts::tdec_x (MI_TDEC_X at creation, A/B) forces a form.
 int Engine::tdec_crossed() const {
   static uint32_t simds = 0;
   if (!simds) {
@@ -342,7 +363,7 @@ int Engine::tdec_crossed() const {
   }
   const uint64_t waves = 2ull * plan.groups.size();
   const int form = (q16() && waves > 4ull * simds && waves <= 5ull * simds) ? 2 : 1;
-  if (const char* e = getenv("MI_TDEC_X")) return atoi(e);   // A/B
+  if (opts.tdec_x >= 0) return opts.tdec_x;   // A/B
   if (flags & MI_DL_FLAG_TDEC_P2) return q16() ? 3 : 1;
   if (flags & MI_DL_FLAG_TDEC_XR) return q16() ? 2 : 1;
   if (flags & MI_DL_FLAG_TDEC_X) return form;
@@ -359,7 +380,7 @@ int Engine::tdec_crossed() const {
 bool Engine::tdec_compact() const {
   const Plan& P = plan;
   if (P.groups.empty() || use_win() || !q16() || tdec_crossed() != 3 || !early_stop || max_its < 2) return false;
-  if (const char* e = getenv("MI_TDEC_COMPACT")) if (!atoi(e)) return false;   // A/B
+  if (opts.compact == 0) return false;   // A/B
   for (size_t g = 0; g < P.groups.size(); g++)
     if (P.groups[g].K != P.groups[0].K || P.groups[g].lane0 != g * LANES) return false;
   return true;
@@ -371,20 +392,19 @@ size_t Engine::cont_pair_u32() const {
 uint32_t Engine::cont_max_pairs() const { return (uint32_t)((plan.lanes.size() + 2 * LANES - 1) / (2 * LANES)); }
 
 // turbo stage: the latency form (one workgroup per code block) or the lane-per-code-block wavefronts
-void Engine::launch_turbo(float* sb, hipStream_t st) {
+bool Engine::launch_turbo(float* sb, hipStream_t st) {
   const Plan& P = plan;
   tb_copied = false;
   if (use_win()) {
     uint32_t kmax = 0;
     for (const MiGroupDesc& g : P.groups) kmax = std::max(kmax, g.K);
     // threads per code block: segments of >= ~16 trellis steps (fewer fix-up rounds), at most 256
-    uint32_t th = win_threads;
-    if (!th && getenv("MI_TDEC_WIN_THREADS")) th = (uint32_t)atoi(getenv("MI_TDEC_WIN_THREADS"));   // A/B tuning
+    uint32_t th = win_threads ? win_threads : opts.win_threads;
     if (!th) th = kmax >= 4096 ? 256 : kmax >= 1024 ? 128 : 64;
     launch_tdec_win(sb, d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(),
                     d_groups.as<MiGroupDesc>(), d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                     (uint32_t)P.lanes.size(), kmax, max_its, early_stop, th, st);
-    return;
+    return true;
   }
   launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
                  (uint32_t)P.groups.size(), st);
@@ -401,15 +421,21 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
     // re-forms them by re-running iteration 0's DEC2 from gathered x2 rows: 12 KB per code block less for all, about
     // half an iteration more for the continuing ones); when the previous run of this workspace continued more than
     // 2 % of its code blocks (the waterfall), it stores them and the continuation gathers them instead.  Both are
-    // exact: only the schedule depends on the history.  MI_TDEC_STORE_W=0 / 1 forces (A/B).
+    // exact: only the schedule depends on the history.  Opts::store_w forces (A/B).
     bool store_w = false;
     if (cont) {
-      if (!h_cont && hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h_cont), 4, hipHostMallocDefault), "pinned"))
+      if (!h_cont) {
+        if (!hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h_cont), 4, hipHostMallocDefault), "pinned") ||
+            !hip_ok(hipEventCreateWithFlags(&cont_ev, hipEventDisableTiming), "event"))
+          return false;
         *h_cont = 0;
-      const char* fe = getenv("MI_TDEC_STORE_W");   // read per run: tests switch it
-      const int force = fe ? atoi(fe) : -1;
-      const uint32_t last = h_cont ? *reinterpret_cast<volatile uint32_t*>(h_cont) : 0u;
-      store_w = force >= 0 ? force != 0 : (uint64_t)last * 50 > P.lanes.size();
+      }
+      // the previous run's count, once its copy has landed (an event query, no wait); until then the last one read
+      if (cont_pending && hipEventQuery(cont_ev) == hipSuccess) {
+        cont_last = *h_cont;
+        cont_pending = false;
+      }
+      store_w = opts.store_w >= 0 ? opts.store_w != 0 : (uint64_t)cont_last * 50 > P.lanes.size();
     }
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
@@ -420,24 +446,30 @@ void Engine::launch_turbo(float* sb, hipStream_t st) {
       // the code blocks still failing after iteration 0, compacted into dense pairs for iterations 1 ..
       // many continuing code blocks (the same history): one iteration per launch, re-compacting the code blocks that
       // still fail between them, so a pair no longer runs until its slowest of 128 code blocks stops (21.5 dB:
-      // 379 + 84 + 19 pair-iterations instead of 3 x 379).  MI_TDEC_ROUNDS=0 / 1 forces (A/B).
-      const char* fr = getenv("MI_TDEC_ROUNDS");
-      const bool rounds = fr ? atoi(fr) != 0 : store_w;
+      // 379 + 84 + 19 pair-iterations instead of 3 x 379).  Opts::rounds forces (A/B).
+      const bool rounds = opts.rounds >= 0 ? opts.rounds != 0 : store_w;
       const size_t ssz = (size_t)LANES * (2 * P.groups[0].K + 8 * (P.groups[0].K / TDEC_CK_MIN + 1));   // plan.cpp
-      launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), 2 * ssz, d_dec.as<uint8_t>(),
+      if (!launch_tdec_cont(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), 2 * ssz, d_dec.as<uint8_t>(),
                        d_cbbytes.as<uint8_t>(), d_cbits.as<uint32_t>(),
                        d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
                        d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
                        (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048,
-                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, h_cont, st);
+                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, cont_pending ? nullptr : h_cont, st))
+        return false;
+      // the copy of the count (skipped while an earlier one is still unread) is complete when cont_ev is
+      if (!cont_pending) {
+        if (!hip_ok(hipEventRecord(cont_ev, st), "event")) return false;
+        cont_pending = true;
+      }
     }
-    return;
+    return true;
   }
   launch_tdec(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
               d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
               d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(),
               max_its, early_stop, q16(), tdec_crossed(), st);
+  return true;
 }
 
 int Engine::stage_ms(float* ms, uint32_t* nruns) {

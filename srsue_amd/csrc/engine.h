@@ -33,6 +33,17 @@ struct DevBuf {
 struct Engine {
   Plan plan;
   uint32_t max_its = 4, early_stop = 1, flags = 0;
+  // Schedule overrides for A/B runs and equivalence tests, read from the environment ONCE, when the engine (a batch
+  // or a per-TTI instance) is created -- never on the run path.  Every choice they force is exact: results are
+  // identical either way.  -1 / 0 = automatic.
+  //   MI_TDEC_X        turbo form (0 lane, 1 crossed, 2 crossed recompute, 3 packed pairs)
+  //   MI_TDEC_COMPACT  0 = no waterfall compaction;  MI_TDEC_STORE_W / MI_TDEC_ROUNDS  0 / 1 = force
+  //   MI_TDEC_WIN_THREADS  latency form: threads per code block;  MI_RM_DIRECT=0 / MI_RM_XCDQ=0 (Plan)
+  struct Opts {
+    int tdec_x = -1, compact = -1, store_w = -1, rounds = -1;
+    uint32_t win_threads = 0;
+  } opts;
+  Engine();
   bool q16() const { return (flags & MI_DL_FLAG_TDEC_GEN) == 0; }   // int16 turbo arithmetic (default)
   uint32_t win_threads = 0;   // latency-form turbo: threads per code block (0 = by K)
   bool use_win() const;       // latency-form (segment-parallel) turbo decoder for this plan
@@ -44,11 +55,17 @@ struct Engine {
   bool tdec_compact() const;
   size_t cont_pair_u32() const;   // continuation pair scratch, u32 words
   uint32_t cont_max_pairs() const;
-  void launch_turbo(float* sb, hipStream_t st);
+  bool launch_turbo(float* sb, hipStream_t st);   // false: a HIP call failed (mi_last_error)
   bool tb_copied = false;
-  // waterfall compaction: the previous run's number of continuing code blocks (page-locked, copied back after every
-  // compacted run; read without waiting -- it only steers whether the first launch stores its extrinsic rows)
-  uint32_t* h_cont = nullptr;   // the last turbo stage wrote the payload bytes itself (packed decoder, PDSCH batch)
+  // the last turbo stage wrote the payload bytes itself (packed decoder, PDSCH batch)
+  // waterfall compaction: the number of continuing code blocks of an earlier run (page-locked, copied back after every
+  // compacted run) steers whether the first launch stores its extrinsic rows.  It is read only once cont_ev (recorded
+  // after the copy) has completed -- never while the copy may be in flight -- and otherwise the last value read
+  // (cont_last) is used: only the schedule depends on it, both forms are exact
+  uint32_t* h_cont = nullptr;
+  hipEvent_t cont_ev = nullptr;
+  bool cont_pending = false;
+  uint32_t cont_last = 0;
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,

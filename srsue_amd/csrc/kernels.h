@@ -54,7 +54,7 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
 // waterfall compaction after iteration 0 of launch_tdec_p2 (one K, early stop; tdec_p2_body.h P2ContSrc):
 // gather the CRC-failing code blocks into dense continuation pairs (cscr: max_pairs x pair_u32 words, cdec:
 // max_pairs x K x 64 bytes, cont: 1 + lanes words) and decode iterations 1 .. max_its - 1 there
-void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
+bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
                       uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                       const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
                       uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,

@@ -63,11 +63,8 @@ template <> __device__ __forceinline__ void dft<8>(float2 (&v)[8]) {
 // both sides keep immediate offsets: 8 j + r -> (8 j + j / 4) + r, and j + r NB -> (j + j / 32) + r (NB + NB / 32)
 // since every NB here is a multiple of 32 -- no address registers are added (an XOR swizzle, 640 cycles,
 // needed one per access and spilled).
-#ifndef MI_OFDM_PAD
-#define MI_OFDM_PAD 1
-#endif
 constexpr int OFDM_PAD_SH = 5;
-__device__ __forceinline__ int lpad(int a) { return MI_OFDM_PAD ? a + (a >> OFDM_PAD_SH) : a; }
+__device__ __forceinline__ int lpad(int a) { return a + (a >> OFDM_PAD_SH); }
 
 // One Stockham stage (decimation in time): butterfly j reads x[j + r N/R], twiddles by
 // W_{Ns R}^{(j mod Ns) r}, writes y[(j / Ns) Ns R + j mod Ns + r Ns].
@@ -194,15 +191,13 @@ __device__ __forceinline__ void fft_rest(float2* buf, const float2* tw) {
 // subframe, twiddles staged once for 14 FFTs -- batches) or 1 (a workgroup per symbol -- small batches,
 // the per-TTI latency path)
 // 6 waves per SIMD: the VGPR budget (<= 80) that matches the 6 workgroups per CU the LDS now allows
-#ifndef MI_OFDM_WAVES
-#define MI_OFDM_WAVES 6
-#endif
+constexpr int OFDM_WAVES = 6;
 template <int N, typename IQ>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI_OFDM_WAVES))) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_WAVES))) void ofdm_rx_kernel(const IQ* __restrict__ iq, float2* __restrict__ grid,
                                                       const MiSfDesc* __restrict__ sfs,
                                                       const uint32_t* __restrict__ list,
                                                       const float2* __restrict__ twg, uint32_t W, int per) {
-  __shared__ float2 buf[N + (MI_OFDM_PAD ? N >> OFDM_PAD_SH : 0)];
+  __shared__ float2 buf[N + (N >> OFDM_PAD_SH)];
   __shared__ float2 tw[N / 2];   // half-wave table (tw_at)
   const MiSfDesc d = sfs[list[blockIdx.x]];
   for (int t = threadIdx.x; t < N / 2; t += 256) tw[t] = twg[t];

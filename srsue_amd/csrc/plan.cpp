@@ -396,13 +396,12 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
   }
   PLAN_T("rank");
   // direct groups (rm.hip): every valid lane new, one rank table, one k0 rank, one unit kind, whole units, E <= N_v;
-  // their rank -> row tables (row = ipos[p] under MI_SB_NAT) into kdata.  MI_RM_DIRECT=0 in the environment
-  // sends every group through the general combine (A/B and parity tests).
+  // their rank -> row tables (row = ipos[p], decoder-input order) into kdata.  rm_direct_on = false (MI_RM_DIRECT=0 at
+  // engine creation) sends every group through the general combine (A/B and parity tests).
   std::vector<uint8_t> direct(groups.size(), 0);
   std::vector<uint32_t> direct_rrow(groups.size(), 0);
   {
-    const char* env = getenv("MI_RM_DIRECT");
-    const bool off = env && !atoi(env);
+    const bool off = !rm_direct_on;
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> rrow_off;
     for (size_t gi = 0; gi < groups.size() && !off; gi++) {
       const MiGroupDesc& g = groups[gi];
@@ -427,7 +426,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
         const auto& rk = rank_cache[key].first;
         std::vector<uint32_t> rrow(l0.Nv, 0u);
         for (uint32_t p = 0; p < (uint32_t)rk.size(); p++)
-          if (rk[p] >= 0) rrow[(uint32_t)rk[p]] = MI_SB_NAT ? kdata[ktabs[g.ktab].ipos_off + p] : p;
+          if (rk[p] >= 0) rrow[(uint32_t)rk[p]] = kdata[ktabs[g.ktab].ipos_off + p];
         ro = rrow_off.emplace(key, (uint32_t)kdata.size()).first;
         kdata.insert(kdata.end(), rrow.begin(), rrow.end());
       }
@@ -509,11 +508,7 @@ int Plan::build(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch) {
       for (size_t i = 0; i < len; i++)
         for (size_t k = 0; k < 8; k++) its[8 * i + k] = i < q[k].size() ? q[k][i] : ((q[k].empty() ? 0u : q[k][0] >> 9) << 9) | 511u;
     };
-    static const bool xcdq = [] {
-      const char* env = getenv("MI_RM_XCDQ");   // A/B: 0 = launch order
-      return !env || atoi(env) != 0;
-    }();
-    if (xcdq) {
+    if (xcd_queues) {   // A/B: false = launch order
       xcd_order(rm_items);
       xcd_order(gbusy);
     }

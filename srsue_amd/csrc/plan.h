@@ -34,7 +34,7 @@ struct PlanData {
   uint32_t rm_busy = 0;
   uint32_t rm_dbusy = 0;                  // the leading busy items that belong to direct groups (rm_direct)
   // per busy item, its folded record (rm.hip): lane0, Ncb | chunk << 16, softbuffer float offset / 64, the
-  // K table's ipos offset (dl_common.h MI_SB_NAT)
+  // K table's ipos offset (rows in decoder-input order, dl_common.h)
   std::vector<uint32_t> rm_recs;
   // direct groups (rm.hip, Plan::build): every valid lane a new TB with the same rank table, the same k0 rank
   // and E <= N_v -- each received position gets exactly one LLR.  Their busy chunks are in rm_items (record
@@ -86,6 +86,9 @@ struct ReKeyHash {
 static_assert(sizeof(ReKey) == 20 + ((NRB_MAX + 3) & ~3), "ReKey must be padding-free (memcmp / hash over its bytes)");
 
 struct Plan : PlanData {
+  // A/B switches, set once at engine creation (Engine::Engine: MI_RM_DIRECT, MI_RM_XCDQ): direct rate de-matching
+  // groups, and the rate de-matching work list dealt to 8 XCD queues (plan.cpp xcd_order)
+  bool rm_direct_on = true, xcd_queues = true;
   void build_pairs();
   // cached per-key tables (kept across rebuilds)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::vector<float>> crs_cache;

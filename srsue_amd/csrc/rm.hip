@@ -20,37 +20,13 @@
 #include "kernels.h"
 #include "rm_body.h"
 
-#ifndef MI_RM_NT
-#define MI_RM_NT 0   // non-temporal softbuffer stores (A/B switch)
-#endif
-#ifndef MI_RM_IDLE_OFF
-#define MI_RM_IDLE_OFF 0
-#endif
-#ifndef MI_RM_RECS
-#define MI_RM_RECS 1   // one folded work-item record per workgroup (A/B switch: 0 = item -> group descriptor)
-#endif
-#ifndef MI_RM_DIRECT_FORM
-#define MI_RM_DIRECT_FORM 1   // rank-driven stores for Plan::rm_direct groups (0: their records run the general combine)
-#endif
-#ifndef MI_RM_DIRECT_WPE
-#define MI_RM_DIRECT_WPE 8   // 8-wavefront direct workgroups: waves per SIMD the registers must allow (8: 4 per CU)
-#endif
-#ifndef MI_RM_GENERAL_NW
-#define MI_RM_GENERAL_NW 8   // wavefronts per workgroup of the general (non-direct) chunks
-#endif
-#ifndef MI_RM_GENERAL_WPE
-#define MI_RM_GENERAL_WPE 6   // with 8 wavefronts: waves per SIMD its registers must allow (80 VGPRs, 3 groups per CU)
-#endif
-// same box, configs[4] mix on one stream (profiles/r3/ab_rm_split/ab_g8*): general chunks 977 us with 4-wavefront
-// groups (122 VGPRs, 4 waves per SIMD), 918 us with 8 at 6 waves per SIMD, 1,121 us at 8 (45 VGPRs spilled)
-#ifndef MI_RM_DIRECT_PIPE1
-#define MI_RM_DIRECT_PIPE1 1   // direct workgroups stage unit after unit (0: the 3-stage pipeline; same-box 2.34-2.40 vs 2.44-2.49 ms)
-#endif
-#ifndef MI_RM_DENSE
-#define MI_RM_DENSE 0   // A/B switch: write and materialise every row (the pre-sparse behaviour)
-#endif
-
 namespace mi {
+
+// wavefronts per workgroup of the general (non-direct) chunks and the waves per SIMD their registers must allow (80
+// VGPRs, 3 groups per CU); direct chunks run 8-wavefront workgroups at 8 waves per SIMD (4 per CU).  Same box, configs[4]
+// mix on one stream (profiles/r3/ab_rm_split/ab_g8*): general chunks 977 us with 4-wavefront groups (122 VGPRs, 4 waves
+// per SIMD), 918 us with 8 at 6 waves per SIMD, 1,121 us at 8 (45 VGPRs spilled)
+constexpr int RM_GENERAL_NW = 8, RM_GENERAL_WPE = 6, RM_DIRECT_WPE = 8;
 
 // workgroup shape: RM_NW wavefronts per chunk, each owning RM_CHUNK / RM_NW = 32 consecutive positions
 // in the combine and 64 / RM_NW code-block rows (2 row-segments each) in the staging
@@ -193,11 +169,11 @@ __device__ __forceinline__ float fused_llr(const RmFuse& f, const MiLaneSrc& src
 }
 
 // FQ / FT: the batch's common modulation order and transmission mode (FQ = 0: mixed, per-unit switch).
-// NW / DIR: wavefronts per workgroup; DIR = every item is a direct group's chunk (MI_RM_DIRECT_SPLIT: those run
+// NW / DIR: wavefronts per workgroup; DIR = every item is a direct group's chunk (those run
 // as 8-wavefront workgroups -- the same tile, each wavefront staging 8 rows and storing 16 ranks -- in a
 // launch of their own, whose instantiation carries none of the general combine's registers)
 template <bool FUSED, int FQ = 0, bool FT = false, int NW = RM_NW, bool DIR = false>
-__global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_GENERAL_WPE : 1)) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
+__global__ __launch_bounds__(64 * NW, DIR ? RM_DIRECT_WPE : (NW == 8 ? RM_GENERAL_WPE : 1)) void rm_combine_kernel(const float* __restrict__ e, float* __restrict__ sb,
                                                         const MiGroupDesc* __restrict__ groups,
                                                         const MiLaneDesc* __restrict__ lanes,
                                                         const uint32_t* __restrict__ kdata, RmFuse fz,
@@ -220,11 +196,11 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
   uint32_t lane0, Ncb, ci, ipos_off;
   uint64_t sb_off;
   bool direct = DIR;   // a Plan::rm_direct group: r.w is its rank -> row table
-  if (MI_RM_RECS && recs) {
+  if (recs) {
     const uint4 r = recs[blockIdx.x];
     lane0 = r.x;
     Ncb = r.y & 0x7FFFu;
-    direct = DIR || (MI_RM_DIRECT_FORM && ((r.y >> 15) & 1u));
+    direct = DIR || ((r.y >> 15) & 1u);
     ci = r.y >> 16;
     sb_off = (uint64_t)r.z * LANES;
     ipos_off = r.w;
@@ -273,18 +249,11 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
       s_dra = ra;
       s_dnr = nr;
     }
-    if (ci == 0) {   // the group's zero row, and its mirror's
-      sbg[(size_t)Ncb * LANES + tid] = 0.0f;
-      sb_q16_put(sbg, Ncb, (size_t)Ncb * LANES + tid, 0);
-    }
+    if (ci == 0) sbg[(size_t)Ncb * LANES + tid] = 0.0f;   // the group's zero row
   }
   if (tid < RM_CHUNK / 4 && !direct) busy |= reinterpret_cast<const uint32_t*>(map)[tid] != 0;
   // nothing received and nothing materialised: the chunk stays all-zero, no HBM traffic
   if (!__syncthreads_or(busy)) return;
-#if MI_RM_DIAG_PROLOGUE   // timing diagnostic only: the descriptor chain alone (wrong results)
-  if (s_j0[tid & 63] == 0xFFFFFFFFu) sbg[tid] = 1.f;
-  return;
-#endif
   // stage: tile[l][t] = e_l[(j0 + t) mod Nv] (0 beyond E), t < nr; a wavefront per code-block row,
   // all of a wavefront's loads issued before its LDS writes
   constexpr int ROWS = LANES / NW, PER = RM_CHUNK / 64;
@@ -335,8 +304,9 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
       }
       return lo;
     };
-    if constexpr (FQ != 0 && DIR && MI_RM_DIRECT_PIPE1) {
-      // direct 8-wavefront form (A/B): ~3 units per thread, one unit after the other; occupancy hides latency
+    if constexpr (FQ != 0 && DIR) {
+      // direct 8-wavefront form: ~3 units per thread, one unit after the other; occupancy hides latency (the
+      // three-stage pipeline below measured 2.44-2.49 ms against 2.34-2.40 here, same box)
       for (uint32_t fi = q; fi < total; fi += 64) {
         const uint32_t lo = locate(fi), l = w + NW * (lo >> 1);
         fused_unit<FQ, FT>(fz, s_src[l], rs_u0[w][lo] + (fi - rs_pre[w][lo]), rs_ga[w][lo], rs_gb[w][lo], rs_ta[w][lo],
@@ -368,9 +338,7 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
             uC = rs_u0[w][loC] + (fi + 128 - rs_pre[w][loC]);
             iC = fused_idx<FQ, FT>(fz, s_src[w + NW * (loC >> 1)], uC);
           }
-#if !MI_RM_SKIP_UNITS   // diagnostic A/B only: staging without the demap arithmetic (wrong LLRs)
           fused_compute<FQ, FT>(fz, dA, uA, rs_ga[w][loA], rs_gb[w][loA], rs_ta[w][loA], tile[w + NW * (loA >> 1)]);
-#endif
           if (!hasB) break;
           loA = loB; uA = uB; dA = dB;
           loB = loC; uB = uC; iB = iC;
@@ -407,10 +375,6 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
   }
   }
   __syncthreads();
-#if MI_RM_DIAG_NOCOMBINE   // timing diagnostic only: staging without the combine (wrong results)
-  if (tile[threadIdx.x & 63][threadIdx.x >> 6] == 12345.f) sbg[threadIdx.x] = 1.f;
-  return;
-#endif
   // combine: wavefront w owns the NP consecutive positions pw .. pw+NP-1, one row (64 lanes) each
   constexpr int NP = RM_CHUNK / NW;
   const int lane = (int)(tid & 63), wave = (int)(tid >> 6);
@@ -423,11 +387,7 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
 #pragma unroll
     for (int i = 0; i < NP; i++) {
       const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)rowv, i);
-      if ((uint32_t)i < nt && lvalid) {
-        const float v = 0.0f + tile[lane][t0 + i];
-        sbg[(size_t)row * LANES + lane] = v;
-        sb_q16_put(sbg, Ncb, (size_t)row * LANES + lane, q16s(v));
-      }
+      if ((uint32_t)i < nt && lvalid) sbg[(size_t)row * LANES + lane] = 0.0f + tile[lane][t0 + i];
     }
     return;
   }
@@ -440,11 +400,11 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
   const bool rep = E > nv, comb = s_comb, fresh = s_new;
   // materialised-before bits of the wave's rows (wave-uniform)
   const uint32_t was_m = (uint32_t)__ballot(lane < NP && (uint32_t)lane < np && map[NP * wave + lane] != 0);
-  // the softbuffer rows of the wave's positions (dl_common.h MI_SB_NAT): lane i < NP holds ipos[pw + i], read
+  // the softbuffer rows of the wave's positions (decoder-input order, dl_common.h): lane i < NP holds ipos[pw + i], read
   // back wave-uniform per position (dummy positions are never written)
-  const uint32_t rowv = MI_SB_NAT && (uint32_t)lane < np ? kdata[ipos_off + pw + lane] : pw + (uint32_t)lane;
+  const uint32_t rowv = (uint32_t)lane < np ? kdata[ipos_off + pw + lane] : pw + (uint32_t)lane;
   auto row_of = [&](int i) -> size_t {
-    return MI_SB_NAT ? (size_t)(uint32_t)__builtin_amdgcn_readlane((int)rowv, i) : (size_t)(pw + i);
+    return (size_t)(uint32_t)__builtin_amdgcn_readlane((int)rowv, i);
   };
   int32_t rk[NP];
   float old[NP];
@@ -474,15 +434,8 @@ __global__ __launch_bounds__(64 * NW, DIR ? MI_RM_DIRECT_WPE : (NW == 8 ? MI_RM_
       }
     }
     const bool any = __ballot(c) != 0, was = (was_m >> i) & 1u;
-    const bool mat = MI_RM_DENSE || any || (was && comb);   // row holds data after this launch
-    if (mat && (MI_RM_DENSE || any || !was || fresh) && ld.valid) {
-#if MI_RM_NT
-      __builtin_nontemporal_store(v, &sbg[row_of(i) * LANES + lane]);
-#else
-      sbg[row_of(i) * LANES + lane] = v;
-#endif
-      sb_q16_put(sbg, Ncb, row_of(i) * LANES + lane, q16s(v));   // the int16 mirror (dl_common.h)
-    }
+    const bool mat = any || (was && comb);   // row holds data after this launch
+    if (mat && (any || !was || fresh) && ld.valid) sbg[row_of(i) * LANES + lane] = v;
     mat_m |= (uint32_t)mat << i;
   }
   if ((uint32_t)lane < np) map[NP * wave + lane] = (uint8_t)((mat_m >> lane) & 1u);
@@ -524,12 +477,9 @@ __global__ __launch_bounds__(256) void rm_idle_kernel(float* __restrict__ sb, co
   for (uint32_t p = 0; p < np; p++) {
     if (!map[p]) continue;
     if (!comb) { map[p] = 0; continue; }
-    const size_t row = MI_SB_NAT ? kdata[ktabs[g.ktab].ipos_off + pa + p] : pa + p;   // dl_common.h MI_SB_NAT
+    const size_t row = kdata[ktabs[g.ktab].ipos_off + pa + p];   // rows in decoder-input order (dl_common.h)
     for (int l = 0; l < LANES; l++)
-      if ((fresh >> l) & 1u) {
-        sbg[row * LANES + l] = 0.0f;
-        sb_q16_put(sbg, g.Ncb, row * LANES + l, 0);
-      }
+      if ((fresh >> l) & 1u) sbg[row * LANES + l] = 0.0f;
   }
 }
 
@@ -551,10 +501,7 @@ __global__ __launch_bounds__(256) void rm_direct_map_kernel(float* __restrict__ 
   const MiRmDirect d = dgs[blockIdx.x / RM_DIRECT_MAPB];
   const uint32_t part = blockIdx.x % RM_DIRECT_MAPB;
   float* sbg = sb + (size_t)d.sb64 * LANES;
-  if (part == 0 && threadIdx.x < LANES) {   // the zero row, and its mirror's
-    sbg[(size_t)d.Ncb * LANES + threadIdx.x] = 0.0f;
-    sb_q16_put(sbg, d.Ncb, (size_t)d.Ncb * LANES + threadIdx.x, 0);
-  }
+  if (part == 0 && threadIdx.x < LANES) sbg[(size_t)d.Ncb * LANES + threadIdx.x] = 0.0f;   // the zero row
   uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(d.Ncb));
   const int32_t* rank = reinterpret_cast<const int32_t*>(kdata + d.rank_off);
   const uint32_t emax = d.emax_kind & 0xFFFFFFu;
@@ -578,19 +525,13 @@ static dim3 rm_grid(const uint32_t* items, uint32_t n_busy, uint32_t n_groups, u
 }
 static void rm_idle(float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes, const uint32_t* items,
                     uint32_t n_busy, uint32_t n_items, const MiKTab* ktabs, const uint32_t* kdata, hipStream_t st) {
-#if MI_RM_IDLE_OFF   // A/B only: skip the idle chunks entirely
-  return;
-#endif
   if (items && n_items > n_busy)
     hipLaunchKernelGGL(rm_idle_kernel, dim3((n_items - n_busy + 255) / 256), dim3(256), 0, st, sb, groups, lanes,
                        items + n_busy, n_items - n_busy, ktabs, kdata);
 }
 
-// the direct groups' chunks lead the busy items (Plan::rm_dbusy): with MI_RM_DIRECT_SPLIT they run in their own
-// 8-wavefront launch, the general chunks after them
-#ifndef MI_RM_DIRECT_SPLIT
-#define MI_RM_DIRECT_SPLIT 1
-#endif
+// the direct groups' chunks lead the busy items (Plan::rm_dbusy): they run in their own 8-wavefront launch, the
+// general chunks after them
 void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                        const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_ncb,
                        const uint32_t* items, const uint4* recs, uint32_t n_busy, uint32_t n_dbusy, uint32_t n_items,
@@ -599,14 +540,14 @@ void launch_rm_combine(const float* e, float* sb, const MiGroupDesc* groups, con
   if (items && !n_busy) items = nullptr;
   rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
   uint32_t skip = 0;
-  if (MI_RM_DIRECT_SPLIT && items && n_dbusy) {
+  if (items && n_dbusy) {
     hipLaunchKernelGGL((rm_combine_kernel<false, 0, false, 8, true>), dim3(n_dbusy), dim3(512), 0, st, e, sb, groups,
                        lanes, ktab_data, RmFuse{}, items, recs, ktabs);
     skip = n_dbusy;
     if (skip == n_busy) return;
   }
-  hipLaunchKernelGGL((rm_combine_kernel<false, 0, false, MI_RM_GENERAL_NW>), rm_grid(items, n_busy - skip, n_groups, max_ncb),
-                     dim3(64 * MI_RM_GENERAL_NW), 0, st, e,
+  hipLaunchKernelGGL((rm_combine_kernel<false, 0, false, RM_GENERAL_NW>), rm_grid(items, n_busy - skip, n_groups, max_ncb),
+                     dim3(64 * RM_GENERAL_NW), 0, st, e,
                      sb, groups, lanes, ktab_data, RmFuse{}, items ? items + skip : nullptr,
                      items ? recs + skip : nullptr, ktabs);
 }
@@ -621,7 +562,7 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
   rm_idle(sb, groups, lanes, items, n_busy, n_items, ktabs, ktab_data, st);
   const RmFuse fz{grid, ce, lane_src, re_tab, scr_tab, noise, (uint32_t)compact_ce};
   uint32_t skip = 0;
-  if (MI_RM_DIRECT_SPLIT && items && n_dbusy) {
+  if (items && n_dbusy) {
 #define MI_RM_LAUNCH(...) \
   hipLaunchKernelGGL((__VA_ARGS__), dim3(n_dbusy), dim3(512), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, items, \
                      recs, ktabs)
@@ -642,9 +583,9 @@ void launch_rm_fused(const float2* grid, const float2* ce, const MiLaneSrc* lane
   const uint32_t* it = items ? items + skip : nullptr;
   const uint4* rc = items ? recs + skip : nullptr;
 #define MI_RM_LAUNCH(...) \
-  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(64 * MI_RM_GENERAL_NW), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, \
+  hipLaunchKernelGGL((__VA_ARGS__), g, dim3(64 * RM_GENERAL_NW), 0, st, nullptr, sb, groups, lanes, ktab_data, fz, \
                      it, rc, ktabs)
-  constexpr int GNW = MI_RM_GENERAL_NW;
+  constexpr int GNW = RM_GENERAL_NW;
   switch (unit_kind) {   // Qm + 8 * (TM2)
     case 2: MI_RM_LAUNCH(rm_combine_kernel<true, 2, false, GNW>); break;
     case 4: MI_RM_LAUNCH(rm_combine_kernel<true, 4, false, GNW>); break;

@@ -35,7 +35,7 @@ MI_HD inline float rm_value(const MiLaneDesc& ld, const int32_t* rank, const flo
 MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, const float* e, float* sbg, uint32_t Ncb,
                                  uint32_t p, const uint32_t* ipos) {
   uint8_t* map = reinterpret_cast<uint8_t*>(sbg + sb_map_off(Ncb));
-  const size_t row = MI_SB_NAT ? ipos[p] : p;   // dl_common.h MI_SB_NAT
+  const size_t row = ipos[p];   // rows in decoder-input order (dl_common.h)
   bool comb = false, any = false;
   for (int l = 0; l < LANES; l++) comb |= lds[l].valid && !lds[l].new_tb;
   const bool was = map[p] != 0;
@@ -54,7 +54,6 @@ MI_HD inline void rm_combine_row(const MiLaneDesc* lds, const uint32_t* kdata, c
     for (int l = 0; l < LANES; l++)
       if (lds[l].valid) {
         sbg[row * LANES + l] = v[l];
-        sb_q16_put(sbg, Ncb, row * LANES + l, q16s(v[l]));   // the int16 mirror (dl_common.h)
       }
   map[p] = mat ? 1 : 0;
 }

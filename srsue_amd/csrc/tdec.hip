@@ -121,12 +121,9 @@ __global__ __launch_bounds__(64) void tdec_kernel_gen(const float* __restrict__ 
                                                      uint32_t max_its, uint32_t early_stop) {
   tdec_group<false, false>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
-// int16 decoder: held to MI_TDEC_I16_WAVES waves per SIMD (3: <= 168 VGPRs), enough to keep every
-// group of a 12,500-subframe batch resident (2,540 waves on 1,024 SIMDs)
-#ifndef MI_TDEC_I16_WAVES
-#define MI_TDEC_I16_WAVES 3
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_TDEC_I16_WAVES)))
+// int16 decoder: held to 3 waves per SIMD (<= 168 VGPRs), enough to keep every group of a 12,500-subframe batch
+// resident (2,540 waves on 1,024 SIMDs)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void tdec_kernel_i16(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch, uint8_t* __restrict__ dec, TdecOut out,
                      const MiGroupDesc* __restrict__ groups, const MiLaneDesc* __restrict__ lanes,
                      const MiKTab* __restrict__ ktabs, const uint32_t* __restrict__ kdata, uint32_t max_its,
@@ -143,10 +140,7 @@ __global__ __launch_bounds__(128) void tdec_kernel_genx(const float* __restrict_
                                                        uint32_t early_stop) {
   tdec_group<false, true>(sb, wm, scratch, dec, out, groups, lanes, ktabs, kdata, max_its, early_stop);
 }
-#ifndef MI_TDEC_X_WAVES
-#define MI_TDEC_X_WAVES 4
-#endif
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_X_WAVES)))
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
 void tdec_kernel_i16x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                       uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
                       const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
@@ -170,41 +164,34 @@ struct TdecP2ExecGpu {
   int wave;
   uint32_t* xs;   // LDS [64]: wave F's per-lane code-block CRC verdicts
   template <class F, class B>
-  __device__ void run(F f, B b) {
+  __device__ __forceinline__ void run(F f, B b) {
     if (wave == 0) f(); else b();
     __syncthreads();
   }
   // wave F's value of this lane, on both waves
-  __device__ uint32_t share(uint32_t v, int lane) {
+  __device__ __forceinline__ uint32_t share(uint32_t v, int lane) {
     if (wave == 0) xs[lane] = v;
     __syncthreads();
     const uint32_t r = xs[lane];
     __syncthreads();   // xs is reused by the next exchange
     return r;
   }
-  // wave B's N values of this lane, on both waves (xs holds N x 64 words)
-  template <int N>
-  __device__ void share_from_b(uint32_t (&v)[N], int lane) {
-    if (wave == 1)
-      for (int i = 0; i < N; i++) xs[i * LANES + lane] = v[i];
-    __syncthreads();
-    for (int i = 0; i < N; i++) v[i] = xs[i * LANES + lane];
-    __syncthreads();
-  }
   __device__ bool pack_wave() const { return wave == 0; }
 };
 
-#ifndef MI_TDEC_P2_WAVES
-#define MI_TDEC_P2_WAVES 3
-#endif
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2_WAVES)))
+// 3 waves per SIMD (<= 168 VGPRs): the headline's 1,270 pairs (2,540 wavefronts) resident in one round
+constexpr int P2_WAVES = 3;
+// LDS rows of a wavefront's 16-step stash (tdec_p2_body.h P2_STASH_ROWS; one row when the spacing does not use it)
+constexpr uint32_t P2_STASH_LDS = P2_CKS == 16 ? P2_STASH_ROWS : 1;
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
                      const uint32_t* __restrict__ kdata, const uint32_t* __restrict__ pairs, uint32_t max_its,
                      uint32_t early_stop, uint32_t no_w) {
   __shared__ uint32_t crc8[256], crc8b[256];
-  __shared__ uint32_t xs[4 * LANES];
+  __shared__ uint32_t xs[LANES];
+  __shared__ uint32_t stash[2][P2_STASH_LDS * LANES];
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
     crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
     crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
@@ -223,8 +210,6 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   if (!a.live) return;   // the same on both wavefronts: no barrier is left waiting
   a.sb[0] = sb + gA.sb_off;
   a.sb[1] = sb + gB.sb_off;
-  a.sbq[0] = sb_q16(a.sb[0], gA.Ncb);
-  a.sbq[1] = sb_q16(a.sb[1], gB.Ncb);
   a.wm[0] = wm + (size_t)ga * WM_STRIDE;
   a.wm[1] = wm + (size_t)gb * WM_STRIDE;
   a.zrow[0] = gA.Ncb;
@@ -249,6 +234,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.cont_w = 0;
   a.no_w = no_w;   // a one-iteration first launch whose continuation re-forms the w rows (launch_tdec_p2)
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
+  a.stash = stash[ex.wave];
   const TdecP2Result r = tdec_p2_lane(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
@@ -267,13 +253,7 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
                     hipStream_t st) {
   if (!n_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
-  // MI_TDEC_P2_LDS (A/B knob, bytes): unused dynamic LDS per workgroup, capping the workgroups one CU holds
-  // (e.g. 29,000 B: 5 of 160 KB) so the dispatcher spreads the pairs evenly over the CUs
-  static const size_t dyn_lds = [] {
-    const char* e = getenv("MI_TDEC_P2_LDS");
-    return e ? (size_t)atol(e) : (size_t)0;
-  }();
-  hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), dyn_lds, st, sb, wm, scratch, dec, out, groups, lanes,
+  hipLaunchKernelGGL(tdec_kernel_p2x, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups, lanes,
                      ktabs, ktab_data, pairs, max_its, early_stop, (uint32_t)(no_w && max_its == 1));
 }
 
@@ -343,7 +323,6 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
       const uint32_t li = cont[1 + d], g = li / LANES;   // plan.cpp: group g = lanes 64 g .. 64 g + 63
       live |= 1u << h;
       s[h].sb = sb + groups[g].sb_off;
-      s[h].sbq = sb_q16(s[h].sb, groups[g].Ncb);
       s[h].wm = wm + (size_t)g * WM_STRIDE;
       s[h].scr = reinterpret_cast<const uint32_t*>(scratch + groups[g & ~1u].scratch_off);   // pairs (2j, 2j + 1)
       s[h].ls = li % LANES;
@@ -403,24 +382,17 @@ __global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* 
 }
 
 // 3. iterations it0 .. it_end - 1 of the continuing code blocks, dense pairs (pair stride pair_u32, decision rows
-// dec_stride bytes apart).  Its register budget is a parameter of its own (MI_TDEC_P2C_WAVES): the continuation
-// holds well under one wavefront per SIMD, so a larger budget costs it no occupancy
-#ifndef MI_TDEC_P2C_WAVES
-#define MI_TDEC_P2C_WAVES MI_TDEC_P2_WAVES
-#endif
-// MI_TDEC_P2C_CK_LATE: the re-compaction rounds after the first (few pairs, far below the HBM rate) take 4-step
-// checkpoints -- a shorter lone chain for twice the checkpoint bytes (MI_TDEC_P2C_CK8 above)
-#ifndef MI_TDEC_P2C_CK_LATE
-#define MI_TDEC_P2C_CK_LATE 1
-#endif
-template <bool CK8>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MI_TDEC_P2C_WAVES)))
+// dec_stride bytes apart), checkpoints every CKS steps (tdec_p2_body.h P2C_CKS, P2C_CKS_LATE).  (A 2-waves-per-SIMD
+// register budget of its own, with q-row loads 2-3 windows ahead, measured neutral on 4 streams: profiles/r4/ab_cont_pf)
+template <int CKS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
                      uint32_t w_stored, uint32_t it0, uint32_t it_end) {
+  static_assert(CKS != 16, "the continuation has no LDS stash");
   __shared__ uint32_t crc8[256], crc8b[256];
-  __shared__ uint32_t xs[4 * LANES];
+  __shared__ uint32_t xs[LANES];
   const uint32_t n = cont[0], p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
@@ -454,7 +426,7 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.it0 = it0;
   a.it_end = it_end;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
-  const TdecP2Result r = tdec_p2_lane<true, CK8>(a, lane, ex);
+  const TdecP2Result r = tdec_p2_lane<true, CKS>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -465,28 +437,28 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   }
 }
 
-void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
+bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
                       uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                       const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
                       uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,
                       uint32_t gather_wgs, uint8_t* payload, bool w_stored, bool rounds, uint32_t* h_count,
                       hipStream_t st) {
-  if (!n_groups || !max_pairs) return;
+  if (!n_groups || !max_pairs) return true;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   const size_t nl = (size_t)n_groups * LANES + 1;   // one list: count + lane indices
   uint32_t* lists[2] = {cont, cont + nl};
   uint32_t* src = cont + 2 * nl;
-  (void)hipMemsetAsync(cont, 0, 4, st);
+  if (hipMemsetAsync(cont, 0, 4, st) != hipSuccess) return false;
   hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
-  if (h_count) (void)hipMemcpyAsync(h_count, cont, 4, hipMemcpyDeviceToHost, st);
+  if (h_count && hipMemcpyAsync(h_count, cont, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
                      ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored);
   const size_t cdec_stride = (size_t)K * LANES;
   if (!rounds) {   // one launch for iterations 1 .. max_its - 1 (each pair until its slowest code block stops)
-    hipLaunchKernelGGL(tdec_kernel_p2c<MI_TDEC_P2C_CK8>, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes,
+    hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS>, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes,
                        ktab_data, kt, cont,
                        pair_u32, cdec_stride, K, max_its, (uint32_t)w_stored, 1u, max_its);
-    return;
+    return true;
   }
   // re-compaction: one iteration per round, the code blocks still failing gathered into fewer dense pairs for the
   // next.  The pair buffers alternate between the continuation scratch and the groups' own scratch (free after the
@@ -498,21 +470,22 @@ void launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
   for (uint32_t it = 1; it < max_its; it++) {
     const int b = (int)((it - 1) & 1u), l = b;
     if (it > 1) {
-      (void)hipMemsetAsync(lists[l], 0, 4, st);
+      if (hipMemsetAsync(lists[l], 0, 4, st) != hipSuccess) return false;
       hipLaunchKernelGGL(tdec_cont_assign2_kernel, dim3(2 * max_pairs), dim3(64), 0, st, lists[l ^ 1], cb_crc, lists[l],
                          src);
       hipLaunchKernelGGL(tdec_cont_gather2_kernel, dim3(gather_wgs), dim3(256), 0, st, bufs[b ^ 1], strides[b ^ 1],
                          lists[l], src, bufs[b], strides[b], K);
     }
-    if (MI_TDEC_P2C_CK_LATE && it > 1)
-      hipLaunchKernelGGL(tdec_kernel_p2c<false>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes,
+    if (it > 1)
+      hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS_LATE>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes,
                          ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, (uint32_t)(w_stored || it > 1),
                          it, it + 1);
     else
-      hipLaunchKernelGGL(tdec_kernel_p2c<MI_TDEC_P2C_CK8>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out,
+      hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out,
                          lanes, ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its,
                          (uint32_t)(w_stored || it > 1), it, it + 1);
   }
+  return true;
 }
 
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc,

@@ -119,9 +119,8 @@ MI_HD inline void beta_step(const T (&bn)[8], T xs, T xp, T (&bk)[8]) {
 // The packed int16 decoder (P2) takes each 8-term maximum of the LLR as two interleaved chains joined at the end
 // (half the dependent depth); an integer maximum is exact in any order.  The float decoders keep their single chains
 // (fmaxf's choice between -0 and +0 could depend on the order).
-#ifndef MI_TDEC_P2_TREE
-#define MI_TDEC_P2_TREE 1   // A/B switch: 0 = single chains in the packed decoder too
-#endif
+template <class T>
+constexpr bool LLR_TREE = std::is_same<T, P2>::value;
 
 // one forward step: llr_k and alpha_{k+1} from alpha_k, beta_{k+1} (NORM: alpha normalised)
 // (max(-inf, t) = t exactly, so the maxima start from the first term)
@@ -137,12 +136,12 @@ MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
       c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
       T t = c[s][u] + bn[tr_next(s, u)];
       t8[u][s] = t;
-      if constexpr (!(MI_TDEC_P2_TREE && std::is_same<T, P2>::value)) {
+      if constexpr (!LLR_TREE<T>) {
         if (u) m1 = s ? fmaxf(m1, t) : t; else m0 = s ? fmaxf(m0, t) : t;
       }
     }
   }
-  if constexpr (MI_TDEC_P2_TREE && std::is_same<T, P2>::value) {   // two interleaved chains per maximum (llr_step)
+  if constexpr (LLR_TREE<T>) {   // two interleaved chains per maximum (llr_step)
     m0 = fmaxf(fmaxf(fmaxf(t8[0][0], t8[0][2]), fmaxf(t8[0][4], t8[0][6])), fmaxf(fmaxf(t8[0][1], t8[0][3]), fmaxf(t8[0][5], t8[0][7])));
     m1 = fmaxf(fmaxf(fmaxf(t8[1][0], t8[1][2]), fmaxf(t8[1][4], t8[1][6])), fmaxf(fmaxf(t8[1][1], t8[1][3]), fmaxf(t8[1][5], t8[1][7])));
   }
@@ -167,17 +166,10 @@ MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
 // and no address registers held across the pipelined windows (plain global pointers compile to
 // one v_lshl_add_u64 + a VGPR pair per load on gfx950).  The host emulation indexes directly.
 // Offsets are 32-bit: every stream is addressed from its group's base (< 6 MB).
-#ifndef MI_ROW_BUFFER
-#define MI_ROW_BUFFER 1
-#endif
-// MI_ROW_CROW_SOFF: the compile-time row delta goes into the wave-uniform soffset instead of the lane
-// offset.  In the VGPR form LICM hoists every distinct (lane + crow * 64) * size out of the window loops
-// -- one loop-invariant VGPR per row delta, live across the whole pass -- instead of leaving the
-// constant in the instruction's immediate offset.
-#ifndef MI_ROW_CROW_SOFF
-#define MI_ROW_CROW_SOFF 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+// The compile-time row delta goes into the wave-uniform soffset, not the lane offset: in the VGPR form LICM hoisted
+// every distinct (lane + crow * 64) * size out of the window loops -- one loop-invariant VGPR per row delta, live
+// across the whole pass -- instead of leaving the constant in the instruction's immediate offset.
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
@@ -185,13 +177,8 @@ __device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
 // immediate offset): consecutive rows of one window share a single soffset SGPR
 template <class T>
 __device__ inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 0) {
-#if MI_ROW_CROW_SOFF
   const uint32_t so = ((uint32_t)row + crow) * (uint32_t)(LANES * sizeof(T));
   const uint32_t vo = (uint32_t)lane * (uint32_t)sizeof(T);
-#else
-  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
-  const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
-#endif
   if constexpr (sizeof(T) == 4)
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), vo, so, 0));
   else if constexpr (sizeof(T) == 2)
@@ -201,13 +188,8 @@ __device__ inline T row_ld(const T* base, size_t row, int lane, uint32_t crow = 
 }
 template <class T>
 __device__ inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) {
-#if MI_ROW_CROW_SOFF
   const uint32_t so = ((uint32_t)row + crow) * (uint32_t)(LANES * sizeof(T));
   const uint32_t vo = (uint32_t)lane * (uint32_t)sizeof(T);
-#else
-  const uint32_t so = (uint32_t)row * (uint32_t)(LANES * sizeof(T));
-  const uint32_t vo = ((uint32_t)lane + crow * LANES) * (uint32_t)sizeof(T);
-#endif
   if constexpr (sizeof(T) == 4)
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), row_rsrc(base), vo, so, 0);
   else if constexpr (sizeof(T) == 2)
@@ -231,22 +213,15 @@ MI_HD inline void row_st(T* base, size_t row, int lane, T v, uint32_t crow = 0) 
 //   SRC_MKQ (DEC1 only) the backward pass reads the softbuffer, quantises all three streams and
 //           writes the q rows; the forward pass reads the q rows
 //   SRC_Q   the int16 q rows [3(K+4)][64] (2-byte rows, natural order, no position table)
-// The q rows are created in iteration MI_TDEC_MKQ_IT (1 = only once a second iteration is needed:
+// The q rows are created in iteration TDEC_MKQ_IT (1 = only once a second iteration is needed:
 // a one-iteration decode never pays for them).
 enum { SRC_SB = 0, SRC_MKQ = 1, SRC_Q = 2 };
-#ifndef MI_TDEC_MKQ_IT
-#define MI_TDEC_MKQ_IT 1
-#endif
+constexpr uint32_t TDEC_MKQ_IT = 1;
 // software-pipelining depth (windows ahead) of a pass, by where it reads its channel inputs: the
 // softbuffer passes 1 (ping-pong), the q-row passes 2 (three buffers).  Same-box A/B (ab_pf,
 // ab_tord): 2 for every pass made the one-iteration headline 3 % slower and the 8-iteration
 // configs[0] 6-10 % faster.
-#ifndef MI_TDEC_PF_SB
-#define MI_TDEC_PF_SB 1
-#endif
-#ifndef MI_TDEC_PF_Q
-#define MI_TDEC_PF_Q 2
-#endif
+constexpr int TDEC_PF_SB = 1, TDEC_PF_Q = 2;
 
 // Raw loaded values of one window of BETA_W steps, kept exactly as loaded (softbuffer floats or
 // int16 words as int) and converted only when the window is computed, so that the loads of the next
@@ -288,31 +263,10 @@ MI_HD inline void scr_st(float* scr, size_t row, int lane, float v, uint32_t cro
   else row_st(scr, row, lane, v, crow);
 }
 
-#if MI_SB_NAT && defined(MI_TDEC_DIAG_NOPI)   // timing diagnostic only: the QPP table replaced by a hash (wrong results)
-#define MI_POS(a, t) ((uint32_t)(t))
-#if MI_TDEC_DIAG_NOPI == 2   // ... by the identity: DEC2's interleaved rows read in sequence
-#define MI_PI(a, k) ((uint32_t)(k))
-#else
-#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
-#endif
-#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
-#elif MI_SB_NAT || defined(MI_TDEC_DIAG_SEQ)   // rows in decoder-input order (dl_common.h MI_SB_NAT)
-#define MI_POS(a, t) ((uint32_t)(t))
+// softbuffer rows in decoder-input order (dl_common.h): decoder input t is row t; the QPP interleaver and the CRC
+// contributions come from the per-K tables
 #define MI_PI(a, k) ((a).pi[k])
 #define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
-#elif defined(MI_TDEC_DIAG_NOPI)   // timing diagnostic only: QPP table lookups replaced by a hash (wrong results)
-#define MI_POS(a, t) ((a).pos[t])
-#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
-#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
-#elif defined(MI_TDEC_DIAG_NOTAB)   // timing diagnostic only: table lookups replaced by hashes (wrong results)
-#define MI_POS(a, t) ((((uint32_t)(t) * 40503u) >> 2) & 16383u)
-#define MI_PI(a, k) ((((uint32_t)(k) * 40503u) >> 3) & 4095u)
-#define MI_CRC(a, pk) 0u
-#else
-#define MI_POS(a, t) ((a).pos[t])
-#define MI_PI(a, k) ((a).pi[k])
-#define MI_CRC(a, pk) ((a).crc24a ? (a).crc_a[pk] : (a).crc_b[pk])
-#endif
 // window mask of decoder inputs 12w .. 12w+11 (tail: w = K/4): bit i = row pos[12w+i] materialised
 MI_HD inline uint32_t tdec_window_mask(const uint8_t* map, const uint32_t* pos, uint32_t w) {
   uint32_t m = 0;
@@ -321,61 +275,22 @@ MI_HD inline uint32_t tdec_window_mask(const uint8_t* map, const uint32_t* pos, 
 }
 // the mask of window w (a scalar load, batched with the window's position-table loads)
 MI_HD inline uint32_t wmask(const TdecArgs& a, uint32_t w) { return a.wm[w]; }
-// softbuffer float of decoder input t0 + dt (t0 = 12 w, m = wmask(w)): materialised rows through the
-// position table; an unmaterialised row is 0 without HBM traffic.  Two ways: read the group's zero
-// row instead (one scalar select; the row stays cache-resident) -- the default for both decoders --
-// or (MI_SB_ZROW_* = 0) a lane offset beyond the descriptor's range (2^31), for which the hardware
-// returns 0 without a memory access.  Same-box A/B (gpurun_out ab_sparse2): int16 tdec 9.60 ms with
-// the zero row, 9.80 ms out of range, 9.83 ms with every row materialised, 10.5 ms before.
-#ifndef MI_SB_ZROW_GEN
-#define MI_SB_ZROW_GEN 1
-#endif
-#ifndef MI_SB_ZROW_I16
-#define MI_SB_ZROW_I16 1
-#endif
-// The 12 position-table entries of window inputs t0 .. t0 + 11 (t0 = 12 w; the tail's 12 inputs start at
-// 3 K = 12 (K / 4)), loaded together as three 128-bit scalar loads (Plan::add_ktab aligns every table to 16
-// B).  Loaded one by one, each entry feeds only a select and the backend turns the select into a scalar
-// branch around a lone scalar load and a full wait -- 12 serialised table loads per window and group.
+// softbuffer float of decoder input t0 + dt (t0 = 12 w, m = wmask(w)): materialised rows are read; an
+// unmaterialised row is 0 without HBM traffic -- the group's zero row is read instead (one scalar select; the row
+// stays cache-resident).  Same-box A/B (gpurun_out ab_sparse2, profiles/r3/ab_oob): reading out of the buffer
+// descriptor's range instead (the hardware returns 0) measured slower for both decoders.
+// The row indices of window inputs t0 .. t0 + 11 (the tail's 12 inputs start at 3 K = 12 (K / 4)).
 struct PosW { uint32_t v[12]; };
-MI_HD inline PosW pos_window(const uint32_t* pos, uint32_t t0) {
+#define MI_POSW(a, t0) pos_window(t0)
+MI_HD inline PosW pos_window(uint32_t t0) {
   PosW P;
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(MI_TDEC_DIAG_NOTAB) && !defined(MI_TDEC_DIAG_SEQ) && !MI_SB_NAT
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  typedef const __attribute__((address_space(4))) u4 cu4;
-  cu4* q = (cu4*)(pos + t0);
 #pragma unroll
-  for (int j = 0; j < 3; j++) {
-    const u4 x = q[j];
-    P.v[4 * j] = x.x; P.v[4 * j + 1] = x.y; P.v[4 * j + 2] = x.z; P.v[4 * j + 3] = x.w;
-  }
-#else
-  for (int j = 0; j < 12; j++) P.v[j] = pos[t0 + j];
-#endif
+  for (int j = 0; j < 12; j++) P.v[j] = t0 + (uint32_t)j;
   return P;
 }
-#if defined(MI_TDEC_DIAG_NOTAB) || defined(MI_TDEC_DIAG_SEQ) || MI_SB_NAT
-#define MI_POSW(a, t0) PosW{{MI_POS(a, t0), MI_POS(a, t0 + 1), MI_POS(a, t0 + 2), MI_POS(a, t0 + 3), MI_POS(a, t0 + 4), \
-                             MI_POS(a, t0 + 5), MI_POS(a, t0 + 6), MI_POS(a, t0 + 7), MI_POS(a, t0 + 8), MI_POS(a, t0 + 9), \
-                             MI_POS(a, t0 + 10), MI_POS(a, t0 + 11)}}
-#else
-#define MI_POSW(a, t0) pos_window((a).pos, t0)
-#endif
 template <bool Q16>
 MI_HD inline float sb_in(const TdecArgs& a, uint32_t m, const PosW& P, uint32_t dt, int lane) {
   const bool on = (m >> dt) & 1u;
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
-  if constexpr (!(Q16 ? MI_SB_ZROW_I16 : MI_SB_ZROW_GEN)) {
-    const uint32_t so = P.v[dt] * (uint32_t)(LANES * sizeof(float));
-    const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb), vo, so, 0));
-  }
-#endif
-#if defined(MI_TDEC_DIAG_Q16SB)   // timing diagnostic only: int16-wide softbuffer reads (wrong values)
-  if constexpr (Q16)
-    return __builtin_bit_cast(float, (uint32_t)(uint16_t)row_ld(reinterpret_cast<const int16_t*>(a.sb),
-                                                                  on ? P.v[dt] : a.zrow, lane));
-#endif
   return row_ld(a.sb, on ? P.v[dt] : a.zrow, lane);
 }
 
@@ -415,7 +330,7 @@ MI_HD inline void tdec_load_window(const TdecArgs& a, int lane, uint32_t base, T
   }
 }
 
-// int16 decoder, q-creating pass (DEC1 backward of iteration MI_TDEC_MKQ_IT): the three softbuffer
+// int16 decoder, q-creating pass (DEC1 backward of iteration TDEC_MKQ_IT): the three softbuffer
 // inputs of each step through the position table (+ w); the window computation quantises them and
 // writes the q rows
 template <bool FIRST, bool Q16>
@@ -465,7 +380,7 @@ MI_HD inline void ck_store(float* scr, size_t ck0, uint32_t c, int lane, const f
     w[7] = 0u;
   }
   const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * ESZ), vo = (uint32_t)lane * 8 * ESZ;
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+#if defined(__HIP_DEVICE_COMPILE__)
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
 #pragma unroll
@@ -487,7 +402,7 @@ MI_HD inline void ck_load_raw(const float* scr, size_t ck0, uint32_t c, int lane
   }
   constexpr uint32_t NW = Q16 ? 4 : 8, ESZ = Q16 ? 2 : 4;
   const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * 8 * LANES) * ESZ), vo = (uint32_t)lane * 8 * ESZ;
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+#if defined(__HIP_DEVICE_COMPILE__)
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
 #pragma unroll
@@ -618,7 +533,7 @@ MI_HD inline void tdec_half(const TdecArgs& a, int lane, TdecCrc& crc) {
   constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;   // backward pass: softbuffer -> q rows
   constexpr bool SQB = Q16 && SRC == SRC_Q;              // backward pass reads q rows
   constexpr bool SQF = Q16 && SRC != SRC_SB;             // forward pass reads q rows
-  constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_PF_Q;
+  constexpr int PF = SRC == SRC_SB ? TDEC_PF_SB : TDEC_PF_Q;
   const uint32_t K = a.K, F = a.F, nw = K / BETA_W;
   const size_t ck = (size_t)2 * K;  // beta checkpoints (row)
   const float NINF = -INFINITY;
@@ -786,7 +701,7 @@ MI_HD inline void alpha_fwd(T (&al)[8], T xs, T xp) {
 // packed int16 decoder's first trellis steps, where "-inf" is a finite stand-in, tdec_p2_body.h)
 template <uint32_t REACH = 0xFFu, class T>
 MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
-  if constexpr (MI_TDEC_P2_TREE && std::is_same<T, P2>::value) {
+  if constexpr (LLR_TREE<T>) {
     // packed int16: the same terms, each maximum as two interleaved chains (states of even / odd rank among the
     // reachable ones) joined at the end: half the dependent depth, two more live accumulators
     const T luz = xs + xp;
@@ -860,9 +775,6 @@ MI_HD inline void tdec_alpha_only_window_mkq(const TdecArgs& a, int lane, const 
 #else
 #define MI_OPAQUE8(v) do { } while (0)
 #endif
-#ifndef MI_TDEC_B2_TWO_LEVEL
-#define MI_TDEC_B2_TWO_LEVEL 1
-#endif
 template <bool DEC2, bool Q16, bool SQ>
 MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecWin<Q16>& w, uint32_t base,
                                         float (&b)[8], TdecCrc& crc) {
@@ -882,41 +794,29 @@ MI_HD inline void tdec_beta_emit_window(const TdecArgs& a, int lane, const TdecW
 #pragma unroll
     for (int s = 0; s < 8; s++) b[s] = nb[s];
   };
-  if constexpr (MI_TDEC_B2_TWO_LEVEL) {
-    // two-level: alpha_{base+2} kept, 4 recursion steps per window
-    float a2[8];
-    ck(a2);
-    alpha_fwd<!Q16>(a2, xs[0], xp[0]);
-    alpha_fwd<!Q16>(a2, xs[1], xp[1]);
-    {
-      float ai[8];
+  // two-level: alpha_{base+2} kept, 4 recursion steps per window (every step's alpha from the checkpoint: 6)
+  float a2[8];
+  ck(a2);
+  alpha_fwd<!Q16>(a2, xs[0], xp[0]);
+  alpha_fwd<!Q16>(a2, xs[1], xp[1]);
+  {
+    float ai[8];
 #pragma unroll
-      for (int s = 0; s < 8; s++) ai[s] = a2[s];
-      alpha_fwd<!Q16>(ai, xs[2], xp[2]);
-      emit_back(ai, 3);
-    }
-    emit_back(a2, 2);
-    {
-      float ai[8];
-      ck(ai);
-      alpha_fwd<!Q16>(ai, xs[0], xp[0]);
-      emit_back(ai, 1);
-    }
-    {
-      float ai[8];
-      ck(ai);
-      emit_back(ai, 0);
-    }
-  } else {
-    // every step's alpha from the checkpoint: 6 recursion steps per window, no alpha vector kept
-#pragma unroll
-    for (int i = BETA_W - 1; i >= 0; i--) {
-      float ai[8];
-      ck(ai);
-#pragma unroll
-      for (int j = 0; j < i; j++) alpha_fwd<!Q16>(ai, xs[j], xp[j]);
-      emit_back(ai, i);
-    }
+    for (int s = 0; s < 8; s++) ai[s] = a2[s];
+    alpha_fwd<!Q16>(ai, xs[2], xp[2]);
+    emit_back(ai, 3);
+  }
+  emit_back(a2, 2);
+  {
+    float ai[8];
+    ck(ai);
+    alpha_fwd<!Q16>(ai, xs[0], xp[0]);
+    emit_back(ai, 1);
+  }
+  {
+    float ai[8];
+    ck(ai);
+    emit_back(ai, 0);
   }
   norm8<Q16>(b);
 }
@@ -1053,16 +953,14 @@ MI_HD inline void pipe_windows(int n, Idx widx, Load load, Run run) {
 
 // pipelining depth of the crossed schedule's q-row passes (twice the waves hide more latency, and the
 // three-buffer rotation spills at the 128-VGPR budget of 4 waves per SIMD)
-#ifndef MI_TDEC_XPF_Q
-#define MI_TDEC_XPF_Q 1
-#endif
+constexpr int TDEC_XPF_Q = 1;
 // the four phase bodies of one constituent decoder (same source modes as tdec_half)
 template <bool DEC2, bool FIRST, bool Q16, int SRC, bool RC>
 struct TdecX {
   static constexpr bool MKQ = Q16 && !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = Q16 && SRC == SRC_Q;
   static constexpr bool SQF = Q16 && SRC != SRC_SB;
-  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_PF_SB : MI_TDEC_XPF_Q;
+  static constexpr int PF = SRC == SRC_SB ? TDEC_PF_SB : TDEC_XPF_Q;
   using Win = TdecWin<Q16>;
 
   MI_HD static void load1(const TdecArgs& a, int lane, uint32_t w, Win& r) {
@@ -1184,7 +1082,7 @@ MI_HD inline TdecLaneResult tdec_lane_x(const TdecArgs& a, int lane, Exec& ex) {
   TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
     TdecCrc cF{0}, cB{0};
-    constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;
+    constexpr uint32_t MK = Q16 ? TDEC_MKQ_IT : 0xffffffffu;
     if (it == 0) {
       if (MK == 0) {
         tdec_xhalf<false, true, Q16, SRC_MKQ, RC>(a, lane, ex, cF, cB);
@@ -1238,7 +1136,7 @@ MI_HD inline TdecLaneResult tdec_lane(const TdecArgs& a, int lane) {
   TdecLaneResult r{0, 0, 0};
   for (uint32_t it = 0; it < a.max_its; it++) {
     TdecCrc crc{0};
-    constexpr uint32_t MK = Q16 ? MI_TDEC_MKQ_IT : 0xffffffffu;   // iteration creating the q rows
+    constexpr uint32_t MK = Q16 ? TDEC_MKQ_IT : 0xffffffffu;   // iteration creating the q rows
     if (it == 0) {
       if (MK == 0) {
         tdec_half<false, true, Q16, SRC_MKQ>(a, lane, crc);

@@ -35,9 +35,12 @@
 
 namespace mi {
 
+// the packed decoder's phase bodies are large enough for the inliner to outline them as calls (register saves through
+// scratch at every call): force them inline
+#define MI_P2_INL MI_HD __attribute__((always_inline)) inline
+
 struct TdecArgsP2 {
   const float* sb[2];     // the two groups' softbuffers (dl_common.h sb_group_floats layout)
-  const int16_t* sbq[2];  // their int16 mirrors (dl_common.h sb_q16): what MI_TDEC_P2_QSB reads
   const uint32_t* wm[2];  // their window masks (rowmask_kernel)
   uint32_t zrow[2];       // their all-zero rows
   uint32_t* q;            // packed q rows [3 (K + 4)][64] (lo = group A, hi = group B)
@@ -60,6 +63,7 @@ struct TdecArgsP2 {
   uint32_t cont_w;        // continuation only: iteration 0's w rows were gathered (no DEC2 re-run)
   uint32_t it0, it_end;   // continuation only: this launch runs iterations it0 .. it_end - 1 (a round of the
                           // re-compacted waterfall: one iteration; the one-shot continuation: 1 .. max_its - 1)
+  uint32_t* stash;        // this wave's P2_STASH_ROWS x 64 words of LDS (16-step checkpoints, TdecP2X; host: a buffer)
 };
 struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 // the offset of half h's byte j = 0 from out_bytes: byte j of its run is out_bytes[p2_run_off(a, h) + j].  Signed and
@@ -68,27 +72,6 @@ struct TdecP2Result { uint32_t its[2], crc_ok[2], tb_part[2]; };
 MI_HD inline int64_t p2_run_off(const TdecArgsP2& a, int h) {
   return (int64_t)a.cb_off[h] - (int64_t)(a.to_payload ? a.F[h] / 8 : 0u);
 }
-
-// timing diagnostics only (wrong results): 1 = phase 1 alone, 2 = phase 2 alone, 3 = no check pass (no CRC verdicts,
-// no payload), 4 = no check pass and no decision stores (tdec_p2_xhalf, tdec_p2_lane, p2_emit), 5 = the check pass
-// without its payload byte stores
-#ifndef MI_TDEC_P2_DIAG
-#define MI_TDEC_P2_DIAG 0
-#endif
-// MI_TDEC_P2_QSB (= MI_SB_Q16, off by default, dl_common.h): the channel inputs come from the softbuffer's int16 mirror (dl_common.h sb_q16_off:
-// q(x) written by rate de-matching beside every fp32 row): 2-byte loads from 128-B rows, and the pair is packed with
-// one v_lshl_or instead of quantised (2 fma + 2 med3 + perm).  Every pass reads the mirror -- later iterations too,
-// so the int16 q rows are never created (MI_TDEC_MKQ_IT does not apply); the compaction continuation still gathers
-// dense q rows (from the mirror).  The raw slot of a loaded input holds the zero-extended 16 bits.
-#ifndef MI_TDEC_P2_QSB
-#define MI_TDEC_P2_QSB MI_SB_Q16
-#endif
-// the raw slot of one loaded softbuffer input: the mirror's 16 bits zero-extended (QSB), or the fp32 value
-#if MI_TDEC_P2_QSB
-typedef uint32_t SbRaw;
-#else
-typedef float SbRaw;
-#endif
 
 // decoder-input quantiser q(x) = clamp(rint(32 x), +-511) of two floats, packed.  Device: fma(x, 32,
 // 1.5 * 2^23) rounds 32 x to the nearest (even) integer in the low mantissa bits (|32 x| < 2^22; beyond,
@@ -106,71 +89,28 @@ MI_HD inline P2 q16_pair(float a, float b) {
 #endif
 }
 
-// the packed decoder input of two loaded softbuffer values (p2_sb_in): the mirror's two int16 words, or the two fp32
-// values quantised
-MI_HD inline P2 p2_qpair(SbRaw a, SbRaw b) {
-#if MI_TDEC_P2_QSB
-  return p2_from_bits(a | (b << 16));
-#else
-  return q16_pair(a, b);
-#endif
-}
-
 // DEC2's systematic input x2(k) = clamp(llr1(k) - w(k)) (tdec_body.h) is formed by DEC1 when it emits
 // step k -- w(k) is the a-priori row DEC1 has just read in natural order, and it is still the value DEC2
 // would read at row pi(k): DEC2 rewrites that row only after reading it -- and stored in the llr1 rows, so
-// DEC2 loads one interleaved row per step instead of two (MI_TDEC_P2_X2; identical integers)
-#ifndef MI_TDEC_P2_X2
-#define MI_TDEC_P2_X2 1
-#endif
+// DEC2 loads one interleaved row per step instead of two (identical integers)
 // raw loads of one window (BETA_W steps), converted only at use (software pipelining, tdec_body.h):
 //   q-row passes: s0 / s1 = packed q rows;  softbuffer passes: a0/b0, a1/b1 = groups A / B floats
-//   DEC1: s0 = systematic, s1 = parity 1, r0 = w;   DEC2: s0 = parity 2, r0 = llr1[pi], r1 = w[pi]
+//   DEC1: s0 = systematic, s1 = parity 1, r0 = w;   DEC2: s0 = parity 2, r0 = x2 = llr1[pi] (the x2 rows)
 //   MKQ (DEC1, the q-creating pass): a0..a2 / b0..b2 = the three streams of both groups
 struct TdecWinP2 {
   uint32_t s0[BETA_W], s1[BETA_W];
-  SbRaw a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
-  uint32_t r0[BETA_W], r1[BETA_W];
+  float a0[BETA_W], b0[BETA_W], a1[BETA_W], b1[BETA_W], a2[BETA_W], b2[BETA_W];
+  uint32_t r0[BETA_W];
   uint32_t pk[BETA_W];   // DEC2: pi(k) of the window's steps (wave-uniform: scalar registers)
   uint32_t ck[7];
 };
 
-#ifndef MI_TDEC_P2_OOB
-// 1: unmaterialised rows read out of range (0) instead of from the zero row.  Fewer SGPR spills (249 vs 334)
-// but slower: same-box A/B profiles/r3/ab_oob, tdec_kernel_p2x 6.61/6.74 ms vs 6.54/6.56 ms with the zero row.
-#define MI_TDEC_P2_OOB 0
-#endif
 MI_HD inline uint32_t p2_wmask(const TdecArgsP2& a, int h, uint32_t w) { return a.wm[h][w]; }
-MI_HD inline SbRaw p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
-  const bool on = (m >> dt) & 1u;
-#if MI_TDEC_P2_QSB
-  return (uint16_t)row_ld(a.sbq[h], on ? P.v[dt] : a.zrow[h], lane);
-#elif MI_SB_NAT && MI_TDEC_P2_OOB && defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
-  // rows in decoder-input order (dl_common.h MI_SB_NAT): row P.v[0] + dt; an unmaterialised row reads as 0
-  // through an out-of-range VGPR offset (the range check covers the VGPR offset, not soffset: tdec_body.h
-  // sb_in) -- no zero-row select, no per-input row register
-  const uint32_t so = (P.v[0] + dt) * (uint32_t)(LANES * sizeof(float));
-  const uint32_t vo = ((uint32_t)lane * 4u) | (on ? 0u : 0x80000000u);
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(a.sb[h]), vo, so, 0));
-#else
-  return row_ld(a.sb[h], on ? P.v[dt] : a.zrow[h], lane);   // tdec_body.h sb_in
-#endif
+// softbuffer row of decoder input 12 w + dt of half h (tdec_body.h sb_in: unmaterialised rows from the zero row)
+MI_HD inline float p2_sb_in(const TdecArgsP2& a, int h, uint32_t m, const PosW& P, uint32_t dt, int lane) {
+  return row_ld(a.sb[h], ((m >> dt) & 1u) ? P.v[dt] : a.zrow[h], lane);
 }
-
-#if defined(MI_TDEC_P2_DIAG_W2) && defined(__HIP_DEVICE_COMPILE__)
-// timing diagnostic only (wrong results): both halves' inputs of a row from ONE 8-B-per-lane load of group A's rows
-// r, r + 1 (512 B per instruction) -- the access pattern of a pair-interleaved softbuffer ([row][lane][half])
-MI_HD inline void p2_sb_in2(const TdecArgsP2& a, uint32_t m, const PosW& P, uint32_t dt, int lane, SbRaw& x, SbRaw& y) {
-  const uint32_t row = ((m >> dt) & 1u) ? P.v[dt] : a.zrow[0];
-  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  const u2 v = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(a.sb[0]), (uint32_t)lane * 8u, row * 256u, 0);
-  x = __builtin_bit_cast(float, v.x);
-  y = __builtin_bit_cast(float, v.y);
-}
-#define MI_P2_SB_PAIR(A, B, M, DT) p2_sb_in2(a, M, P, DT, lane, A, B)
-#else
 #define MI_P2_SB_PAIR(A, B, M, DT) (A = p2_sb_in(a, 0, ma, P, DT, lane), B = p2_sb_in(a, 1, mb, P, DT, lane))
-#endif
 template <bool DEC2, bool FIRST, bool SQ>
 MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, TdecWinP2& r) {
   const uint32_t* llr1 = a.scr + (size_t)a.K * LANES;
@@ -198,7 +138,6 @@ MI_HD inline void p2_load_window(const TdecArgsP2& a, int lane, uint32_t base, T
         MI_P2_SB_PAIR(r.a0[i], r.b0[i], ma, 3 * i + 2);
       }
       r.r0[i] = row_ld(llr1, pk, lane);
-      if constexpr (!MI_TDEC_P2_X2) r.r1[i] = FIRST ? 0u : row_ld(a.scr, pk, lane);
     }
   }
 }
@@ -227,7 +166,7 @@ MI_HD inline void p2_ck_store(uint32_t* scr, size_t ck0, uint32_t c, int lane, c
 #pragma unroll
   for (int k = 0; k < 7; k++) w[k] = p2_bits(b[k + 1]);
   const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * P2_CKW * LANES) * 4), vo = (uint32_t)lane * (4 * P2_CKW);
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+#if defined(__HIP_DEVICE_COMPILE__)
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u3 __attribute__((ext_vector_type(3)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
@@ -239,7 +178,7 @@ MI_HD inline void p2_ck_store(uint32_t* scr, size_t ck0, uint32_t c, int lane, c
 }
 MI_HD inline void p2_ck_load_to(const uint32_t* scr, size_t ck0, uint32_t c, int lane, uint32_t (&ck)[P2_CKW]) {
   const uint32_t so = (uint32_t)((ck0 * LANES + (size_t)c * P2_CKW * LANES) * 4), vo = (uint32_t)lane * (4 * P2_CKW);
-#if defined(__HIP_DEVICE_COMPILE__) && MI_ROW_BUFFER
+#if defined(__HIP_DEVICE_COMPILE__)
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u3 __attribute__((ext_vector_type(3)));
   const __amdgpu_buffer_rsrc_t rs = row_rsrc(scr);
@@ -264,9 +203,9 @@ MI_HD inline void p2_ck_vec(const TdecWinP2& r, P2 (&v)[8]) { p2_ck_vec(r.ck, v)
 // decoder inputs (xs, xp) of step base + i; filler bits (k < F, known zeros; F < 64) of each half get
 // q(FILLER_LLR) = -511 in the systematic and parity-1 inputs
 template <bool SQ>
-MI_HD inline P2 p2_chan0(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s0[i]) : p2_qpair(r.a0[i], r.b0[i]); }
+MI_HD inline P2 p2_chan0(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s0[i]) : q16_pair(r.a0[i], r.b0[i]); }
 template <bool SQ>
-MI_HD inline P2 p2_chan1(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s1[i]) : p2_qpair(r.a1[i], r.b1[i]); }
+MI_HD inline P2 p2_chan1(const TdecWinP2& r, int i) { return SQ ? p2_from_bits(r.s1[i]) : q16_pair(r.a1[i], r.b1[i]); }
 MI_HD inline P2 p2_fill(P2 x, uint32_t k, const TdecArgsP2& a) {
   const int FILL = -(int)I16_CI;
   return p2_make(k < a.F[0] ? FILL : p2_lo(x), k < a.F[1] ? FILL : p2_hi(x));
@@ -282,27 +221,25 @@ MI_HD inline void p2_xs_xp(const TdecArgsP2& a, const TdecWinP2& r, int i, uint3
     xs = c0 + p2_from_bits(r.r0[i]);
     xp = c1;
   } else {
-    if constexpr (MI_TDEC_P2_X2) xs = p2_from_bits(r.r0[i]);
-    else xs = p2_clamp(p2_from_bits(r.r0[i]) - p2_from_bits(r.r1[i]), (int)I16_CX);
+    xs = p2_from_bits(r.r0[i]);
     xp = p2_chan0<SQ>(r, i);
   }
 }
 
-// per-step outputs (tdec_body.h tdec_emit): DEC1 stores llr1 (MI_TDEC_P2_X2: x2 = clamp(llr1 - w), xs =
-// the step's a-priori w); DEC2 updates w at row pi(k) (pk, carried from the window's loads) and stores
+// per-step outputs (tdec_body.h tdec_emit): DEC1 stores x2 = clamp(llr1 - w) in the llr1 rows (xs = the step's
+// a-priori w); DEC2 updates w at row pi(k) (pk, carried from the window's loads) and stores
 // the two decision bits there (the code-block CRCs are taken from the decision rows after the iteration:
 // tdec_p2_check)
 template <bool DEC2>
 MI_HD inline void p2_emit(const TdecArgsP2& a, int lane, uint32_t base, int i, uint32_t pk, P2 llr, P2 xs) {
   if (!DEC2) {
-    const P2 v = MI_TDEC_P2_X2 ? p2_clamp(llr - xs, (int)I16_CX) : llr;
-    row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(v), i);
+    row_st(a.scr + (size_t)a.K * LANES, base, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CX)), i);
   } else {
     if (!a.no_w) row_st(a.scr, pk, lane, p2_bits(p2_clamp(llr - xs, (int)I16_CW)));
     const uint32_t ng = p2_bits(Metric<P2>::zero() - llr);   // sign bits 15 / 31: llr > 0 per half
     // decision byte: half 0's bit at bit 0, half 1's at bit 4 (the check pass packs 4 rows with 3 shift-ors)
     const uint32_t b0 = (ng >> 15) & 1u, b1 = ng >> 31;
-    if (MI_TDEC_P2_DIAG != 4) row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 4)));
+    row_st(a.dec, pk, lane, (uint8_t)(b0 | (b1 << 4)));
   }
 }
 
@@ -321,9 +258,9 @@ MI_HD inline void p2_alpha_only_window(const TdecArgsP2& a, const TdecWinP2& w, 
 // the q-creating first pass (DEC1): quantise the window's three streams of both groups, store the packed
 // q rows, then the steps
 MI_HD inline void p2_store_q(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, int i, P2& q0, P2& q1) {
-  q0 = p2_qpair(w.a0[i], w.b0[i]);
-  q1 = p2_qpair(w.a1[i], w.b1[i]);
-  const P2 q2 = p2_qpair(w.a2[i], w.b2[i]);
+  q0 = q16_pair(w.a0[i], w.b0[i]);
+  q1 = q16_pair(w.a1[i], w.b1[i]);
+  const P2 q2 = q16_pair(w.a2[i], w.b2[i]);
   row_st(a.q, 3 * base, lane, p2_bits(q0), 3 * i);
   row_st(a.q, 3 * base, lane, p2_bits(q1), 3 * i + 1);
   row_st(a.q, 3 * base, lane, p2_bits(q2), 3 * i + 2);
@@ -376,7 +313,7 @@ MI_HD inline void p2_beta_window_mkq(const TdecArgsP2& a, int lane, const TdecWi
 // the emit's last operand: DEC2 its systematic input xs, DEC1 (x2 form) the step's a-priori w
 template <bool DEC2>
 MI_HD inline P2 p2_emit_x(const TdecWinP2& w, const P2 (&xs)[BETA_W], int i) {
-  if constexpr (DEC2 || !MI_TDEC_P2_X2) return xs[i];
+  if constexpr (DEC2) return xs[i];
   else return p2_from_bits(w.r0[i]);
 }
 // wave F, phase 2: beta_{base+1..base+4} recomputed from the closing checkpoint, then alpha + LLRs
@@ -432,7 +369,7 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
   norm8<true>(b);
 }
 
-// ---- 8-step checkpoint spacing (MI_TDEC_P2_CK8, default) -------------------------------------------
+// ---- 8-step checkpoint spacing -------------------------------------------------------------------
 // The phase-1 passes store a checkpoint every second window (8 steps) and the phase-2 passes walk PAIRS
 // of windows between them: half the checkpoint stores and loads (8 of the ~35 B per code block and
 // step), and each pair's loads are issued once the previous pair's inputs are converted, so they are in
@@ -442,9 +379,6 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
 // form.  Every LLR still takes its alpha and beta at most 3 unnormalised steps from a normalised vector
 // and the running metrics are normalised after every 4 steps exactly as before, so the int16 bounds
 // (p2.h) and every output are unchanged; only the traversal of the recomputation differs.
-#ifndef MI_TDEC_P2_CK8
-#define MI_TDEC_P2_CK8 1
-#endif
 // scheduling fences keep the pair's recomputation in program order (left alone, the scheduler interleaves
 // the independent metric chains and the next pair's loads, and the live vectors exceed the register budget)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -474,7 +408,7 @@ MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t bas
       x.pk[i] = r.lo.pk[i];
       x.pk[BETA_W + i] = r.hi.pk[i];
     }
-  } else if constexpr (MI_TDEC_P2_X2) {
+  } else {
 #pragma unroll
     for (int i = 0; i < BETA_W; i++) {
       x.w[i] = p2_from_bits(r.lo.r0[i]);
@@ -484,9 +418,15 @@ MI_HD inline void p2_cvt8(const TdecArgsP2& a, const TdecWin8P2& r, uint32_t bas
 }
 template <bool DEC2>
 MI_HD inline P2 p2_emit_x8(const TdecX8P2& x, int i) {
-  if constexpr (DEC2 || !MI_TDEC_P2_X2) return x.xs[i];
+  if constexpr (DEC2) return x.xs[i];
   else return x.w[i];
 }
+// the default argument of a window body's precomputed vector (unused unless HAVE4)
+MI_HD inline const P2 (&p2_no_vec())[8] {
+  static constexpr P2 v[8] = {};
+  return v;
+}
+#define P2_NO_VEC p2_no_vec()
 MI_HD inline void p2_cp8(P2 (&d)[8], const P2 (&s)[8]) {
 #pragma unroll
   for (int k = 0; k < 8; k++) d[k] = s[k];
@@ -517,16 +457,21 @@ MI_HD inline void p2_alpha_run(P2 (&v)[8], const TdecX8P2& x) {
 #pragma unroll
   for (int i = LO; i <= HI; i++) alpha_fwd<false>(v, x.xs[i], x.xp[i]);
 }
-// wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1)
-template <bool DEC2>
+// wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1).
+// HAVE4: B(4) was computed on the way (a 16-step span's upper pair, TdecP2X::f2) and comes in B4in
+template <bool DEC2, bool HAVE4 = false>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
-                                   P2 (&al)[8]) {
+                                   P2 (&al)[8], const P2 (&B4in)[8] = P2_NO_VEC) {
   P2 B4[8], Bm[8], Bt[8];
 #define emit(I, BN) \
   p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
-  p2_cp8_opaque(B4, B8);
-  p2_beta_run<7, 4>(B4, x);
-  norm8<true>(B4);
+  if constexpr (HAVE4) {
+    p2_cp8_opaque(B4, B4in);
+  } else {
+    p2_cp8_opaque(B4, B8);
+    p2_beta_run<7, 4>(B4, x);
+    norm8<true>(B4);
+  }
   p2_cp8_opaque(Bm, B4);
   p2_beta_run<3, 2>(Bm, x);   // B(2)
   p2_cp8_opaque(Bt, Bm);
@@ -575,15 +520,20 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
   p2_cp8(b, nb);
 }
 // wave B, phase 2, one pair: A(j) = alpha_{base + j}, A(0) = the checkpoint (pair 0: the start state);
-// LLR i from A(i) and beta_{base + i + 1} (the running b)
-template <bool DEC2, bool FIRST_WIN>
+// LLR i from A(i) and beta_{base + i + 1} (the running b).  HAVE4: A(4) was computed on the way (a 16-step span's lower
+// pair, TdecP2X::b2) and comes in A4in
+template <bool DEC2, bool FIRST_WIN, bool HAVE4 = false>
 MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
-                                       uint32_t base, P2 (&b)[8]) {
+                                       uint32_t base, P2 (&b)[8], const P2 (&A4in)[8] = P2_NO_VEC) {
   P2 A4[8], Am[8], At[8];
 #define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b)
-  p2_cp8_opaque(A4, A0);
-  p2_alpha_run<0, 3>(A4, x);
-  norm8<true>(A4);
+  if constexpr (HAVE4) {
+    p2_cp8_opaque(A4, A4in);
+  } else {
+    p2_cp8_opaque(A4, A0);
+    p2_alpha_run<0, 3>(A4, x);
+    norm8<true>(A4);
+  }
   p2_cp8_opaque(Am, A4);
   p2_alpha_run<4, 5>(Am, x);   // A(6)
   p2_cp8_opaque(At, Am);
@@ -617,76 +567,199 @@ MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const Tdec
 #undef emit
 }
 
-#ifndef MI_TDEC_P2_PF_Q
-#define MI_TDEC_P2_PF_Q 1
+// ---- pipelining depths and checkpoint spacings -----------------------------------------------------
+// q-row passes keep one window of loads in flight (two: 17 VGPRs spilled at the 3-waves-per-SIMD budget); the
+// softbuffer passes follow tdec_body.h.  The check pass keeps two decision-row chunks in flight (three: 38 VGPRs
+// spilled).
+constexpr int P2_PF_Q = 1, P2_PF_SB = TDEC_PF_SB, P2_PF_CHK = 2;
+// Checkpoint spacing (steps) of the first launch, tdec_kernel_p2x: 16 (spans with the LDS stash below), 8 or 4.
+#ifndef MI_TDEC_P2_CKS
+#define MI_TDEC_P2_CKS 8
 #endif
-// the waterfall continuation (tdec_kernel_p2c) runs few wavefronts (0.74 per SIMD at the 21.5 dB bench point), each a
-// lone chain.  Its checkpoint spacing is a parameter of its own: 4-step checkpoints (6 recursion steps per 8 instead of
-// 12) shorten a lone chain (one stream, same box: waterfall tdec 21.95 -> 21.25 ms) but move twice the checkpoint bytes,
-// and beside the other streams' batches that costs more than it saves (4 streams: waterfall 56.7-57.2 Gbps with 8-step
-// checkpoints, 53.0-53.8 with 4-step ones; profiles/r4/ab_cont_ck): 8-step by default.  Its q-row loads stay one
-// window ahead (two: 17 VGPRs spilled at the 3-waves-per-SIMD budget)
-#ifndef MI_TDEC_P2C_CK8
-#define MI_TDEC_P2C_CK8 1
+constexpr int P2_CKS = MI_TDEC_P2_CKS;
+static_assert(P2_CKS == 4 || P2_CKS == 8 || P2_CKS == 16, "checkpoint spacing: 4, 8 or 16 steps");
+// The waterfall continuation (tdec_kernel_p2c) runs few wavefronts (0.74 per SIMD at the 21.5 dB bench point), each a
+// lone chain, so its spacing is a parameter of its own.  Its first round keeps 8-step checkpoints: 4-step ones (6
+// recursion steps per 8 instead of 12) shorten a lone chain (one stream, same box: waterfall tdec 21.95 -> 21.25 ms)
+// but move twice the checkpoint bytes, and beside the other streams' batches that costs more than it saves (4
+// streams: 56.7-57.2 Gbps with 8-step checkpoints, 53.0-53.8 with 4-step ones; profiles/r4/ab_cont_ck).  The later
+// re-compaction rounds hold a few dozen pairs, far below the HBM rate, and take 4-step checkpoints
+// (profiles/r4/ab_ck_late: one stream waterfall tdec 18.58-18.61 -> 18.32 ms, headline unchanged).
+constexpr int P2C_CKS = 8, P2C_CKS_LATE = 4;
+
+// ---- 16-step checkpoint spacing (P2_CKS = 16) ------------------------------------------------------
+// Phase 1 stores a checkpoint every fourth window and phase 2 walks SPANS of four windows (two pairs) between them:
+// half the checkpoint bytes of the 8-step form (20 of the ~141 KB per code block and iteration at the headline).  A
+// span's midpoint vector -- the checkpoint the 8-step form would have loaded -- is recomputed on the way:
+//   wave F (forward, closing checkpoint B16): the upper pair's inputs arrive first; B8 = 8 backward steps from B16,
+//     normalised after each window exactly as phase 1 normalises before it stores a checkpoint; then the lower pair
+//     runs against B8 and the upper pair against B16;
+//   wave B (backward, opening checkpoint A0): the lower pair's inputs arrive first; A8 = 8 forward steps from A0,
+//     normalised per window; then the upper pair runs against A8 and the lower pair against A0.
+// The pair processed last needs inputs that were converted two pair-steps earlier: they wait in this wave's LDS stash
+// (xs, xp, the DEC1 a-priori w: 24 rows of 64 words, + the span's checkpoint vector: 7 rows), not in registers (the
+// 8-step form already uses the 168-VGPR budget of 3 waves per SIMD) and not re-read from HBM.  B8 / A8 are exactly
+// the vectors phase 1 would have stored (the same deterministic recursion from the same normalised vector over the
+// same inputs), and every pair then runs p2_alpha_window8 / p2_beta_emit_window8 as in the 8-step form, so every
+// output is unchanged.  The quarter-point vector (B12 / A4) is normalised on the way to the midpoint and is the first
+// vector the pair processed last recomputes: it is stashed too (7 more rows), so the extra cost is 4 recursion steps
+// per 16 in phase 2 (28 + 16 instead of 24 + 16).
+constexpr uint32_t P2_STASH_X = 3 * 2 * BETA_W, P2_STASH_ROWS = P2_STASH_X + 2 * P2_CKW;
+MI_HD inline void p2_stash_st(uint32_t* st, uint32_t row, int lane, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  ((__attribute__((address_space(3))) uint32_t*)st)[row * LANES + (uint32_t)lane] = v;   // ds_write_b32: LDS
+#else
+  st[row * LANES + (uint32_t)lane] = v;
 #endif
-#ifndef MI_TDEC_P2C_PF_Q
-#define MI_TDEC_P2C_PF_Q 1
+}
+MI_HD inline uint32_t p2_stash_ld(const uint32_t* st, uint32_t row, int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ((const __attribute__((address_space(3))) uint32_t*)st)[row * LANES + (uint32_t)lane];
+#else
+  return st[row * LANES + (uint32_t)lane];
 #endif
-#ifndef MI_TDEC_P2_PF_SB
-#define MI_TDEC_P2_PF_SB MI_TDEC_PF_SB
-#endif
+}
+// park a pair's converted inputs and two normalised vectors (state 0 is 0): the span's checkpoint and the vector 4
+// steps into the pair
+template <bool DEC2, bool FIRST>
+MI_HD inline void p2_stash_put(uint32_t* st, int lane, const TdecX8P2& x, const P2 (&v)[8], const P2 (&v4)[8]) {
+#pragma unroll
+  for (int i = 0; i < 2 * BETA_W; i++) {
+    p2_stash_st(st, i, lane, p2_bits(x.xs[i]));
+    p2_stash_st(st, 2 * BETA_W + i, lane, p2_bits(x.xp[i]));
+    if constexpr (!DEC2 && !FIRST) p2_stash_st(st, 4 * BETA_W + i, lane, p2_bits(x.w[i]));
+  }
+#pragma unroll
+  for (int s = 1; s < 8; s++) {
+    p2_stash_st(st, P2_STASH_X + s - 1, lane, p2_bits(v[s]));
+    p2_stash_st(st, P2_STASH_X + P2_CKW + s - 1, lane, p2_bits(v4[s]));
+  }
+}
+// ... and take them back: DEC2's interleaver indices pi(k) (wave-uniform) come from the table again
+template <bool DEC2, bool FIRST>
+MI_HD inline void p2_stash_get(const TdecArgsP2& a, const uint32_t* st, int lane, uint32_t base, TdecX8P2& x,
+                               P2 (&v)[8], P2 (&v4)[8]) {
+#pragma unroll
+  for (int i = 0; i < 2 * BETA_W; i++) {
+    x.xs[i] = p2_from_bits(p2_stash_ld(st, i, lane));
+    x.xp[i] = p2_from_bits(p2_stash_ld(st, 2 * BETA_W + i, lane));
+    if constexpr (DEC2) x.pk[i] = MI_PI(a, base + i);
+    else x.w[i] = FIRST ? Metric<P2>::zero() : p2_from_bits(p2_stash_ld(st, 4 * BETA_W + i, lane));
+  }
+  v[0] = v4[0] = Metric<P2>::zero();
+#pragma unroll
+  for (int s = 1; s < 8; s++) {
+    v[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_X + s - 1, lane));
+    v4[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_X + P2_CKW + s - 1, lane));
+  }
+}
+MI_HD inline void p2_start(P2 (&v)[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; s++) v[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+}
+
 // the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
-// CK8: 8-step checkpoints (MI_TDEC_P2_CK8) or 4-step ones; PFQ: windows of q-row loads in flight (MI_TDEC_P2_PF_Q).
-// The first launch takes the defaults; the waterfall continuation its own (tdec_p2_lane)
-template <bool DEC2, bool FIRST, int SRC, bool CK8 = MI_TDEC_P2_CK8, int PFQ = MI_TDEC_P2_PF_Q>
+// CKS: checkpoint spacing in steps (4, 8 or 16); PFQ: windows of q-row loads in flight.  The first launch takes
+// P2_CKS / P2_PF_Q, the waterfall continuation its own (tdec_p2_lane)
+template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q>
 struct TdecP2X {
   static constexpr bool MKQ = !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = SRC == SRC_Q;    // backward-side passes read q rows
   static constexpr bool SQF = SRC != SRC_SB;   // forward-side passes read q rows
-  static constexpr int PF = SRC == SRC_SB ? MI_TDEC_P2_PF_SB : PFQ;
+  static constexpr int PF = SRC == SRC_SB ? P2_PF_SB : PFQ;
   using Win = TdecWinP2;
+
+  // Phase 2's traversal: wave F walks windows h .. nw - 1 upwards as 16-step spans (CKS = 16), then 8-step pairs,
+  // then a lone last window; wave B walks windows h - 1 .. 0 downwards the same way (a lone window 0 last).  The
+  // checkpoints phase 1 stores are exactly the ones these read: beta at every span / pair / window end above h (and
+  // at nw, from the tail), alpha at every span / pair start below h except window 0 (the start state).
+  MI_HD static uint32_t spans(uint32_t n) { return CKS == 16 ? n / 4 : 0u; }
+  MI_HD static bool beta_ck(uint32_t w, uint32_t h, uint32_t nw) {   // h < w < nw
+    if constexpr (CKS == 4) return true;
+    const uint32_t w1 = h + 4 * spans(nw - h);
+    return w <= w1 ? ((w - h) & 3u) == 0 : ((w - w1) & 1u) == 0;
+  }
+  MI_HD static bool alpha_ck(uint32_t w, uint32_t h) {   // 0 < w < h
+    if constexpr (CKS == 4) return true;
+    const uint32_t wlo = h - 4 * spans(h);
+    return w >= wlo ? ((h - w) & 3u) == 0 : ((wlo - w) & 1u) == 0;
+  }
+  // a pair's loads: windows w0, w0 + 1 and (CK) the checkpoint in slot c
+  MI_HD static void load8(const TdecArgsP2& a, int lane, uint32_t w0, uint32_t c, bool with_ck, TdecWin8P2& r) {
+    p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
+    p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
+    if (with_ck) p2_ck_load_to(a.scr, (size_t)2 * a.K, c, lane, r.ck);
+  }
 
   MI_HD static void load1(const TdecArgsP2& a, int lane, uint32_t w, Win& r) {
     if constexpr (MKQ) p2_load_window_mkq<FIRST>(a, lane, w * BETA_W, r);
     else p2_load_window<DEC2, FIRST, SQB>(a, lane, w * BETA_W, r);
   }
-  // wave F, phase 1: alpha_0 .. alpha_{K/2}, alpha checkpoints 1 .. h - 1
-  MI_HD static void f1(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
+  // wave F, phase 1: alpha_0 .. alpha_{K/2}, the alpha checkpoints phase 2 of wave B reads
+  MI_P2_INL static void f1(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
-#pragma unroll
-    for (int s = 0; s < 8; s++) al[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    p2_start(al);
     pipe_windows<PF, Win>(
         (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
-          if (w && (!CK8 || !((h - w) & 1u))) p2_ck_store(a.scr, ck, w, lane, al);
+          if (w && alpha_ck(w, h)) p2_ck_store(a.scr, ck, w, lane, al);
           if constexpr (MKQ) p2_alpha_only_window_mkq(a, lane, r, w * BETA_W, al);
           else p2_alpha_only_window<DEC2, SQB>(a, r, w * BETA_W, al);
         });
   }
   // wave F, phase 2: windows h .. nw - 1, LLRs of steps K/2 .. K - 1
-  MI_HD static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
+  MI_P2_INL static void f2(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
     const uint32_t nw = a.K / BETA_W, h = nw / 2;
     const size_t ck = (size_t)2 * a.K;
-    if constexpr (CK8) {
-      // pairs (h + 2j, h + 2j + 1), beta checkpoint h + 2j + 2; an odd count leaves window nw - 1 alone
-      const uint32_t n = nw - h, np = n / 2;
-      auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
-        p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
-        p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
-        p2_ck_load_to(a.scr, ck, w0 + 2, lane, r.ck);
-      };
+    if constexpr (CKS >= 8) {
+      const uint32_t ns = spans(nw - h), w1 = h + 4 * ns;
+      if (ns) {
+        // span j: windows w0 .. w0 + 3 (w0 = h + 4 j), closing checkpoint w0 + 4.  The upper pair (and the checkpoint)
+        // is loaded first; the loads of the next span's upper pair are in flight through this span's two pairs
+        TdecWin8P2 r;
+        load8(a, lane, h + 2, h + 4, true, r);
+        for (uint32_t j = 0; j < ns; j++) {
+          const uint32_t w0 = h + 4 * j;
+          TdecX8P2 x;
+          P2 B16[8], B8[8];
+          p2_cvt8<DEC2, SQF>(a, r, (w0 + 2) * BETA_W, x);
+          p2_ck_vec(r.ck, B16);
+          MI_SCHED_FENCE();
+          load8(a, lane, w0, 0, false, r);   // the lower pair
+          MI_SCHED_FENCE();
+          p2_cp8_opaque(B8, B16);
+          p2_beta_run<7, 4>(B8, x);
+          norm8<true>(B8);   // B12: the upper pair's "B(4)", stashed with its inputs
+          p2_stash_put<DEC2, FIRST>(a.stash, lane, x, B16, B8);
+          p2_beta_run<3, 0>(B8, x);
+          norm8<true>(B8);
+          MI_SCHED_FENCE();
+          p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+          MI_SCHED_FENCE();
+          const uint32_t wn = j + 1 < ns ? w0 + 6 : w0 + 2;   // the last span reloads its upper pair (unused)
+          load8(a, lane, wn, wn + 2, true, r);
+          MI_SCHED_FENCE();
+          p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
+          MI_SCHED_FENCE();
+          p2_stash_get<DEC2, FIRST>(a, a.stash, lane, (w0 + 2) * BETA_W, x, B16, B8);
+          p2_alpha_window8<DEC2, true>(a, lane, x, B16, (w0 + 2) * BETA_W, al, B8);
+        }
+      }
+      // pairs (w1 + 2j, w1 + 2j + 1), beta checkpoint w1 + 2j + 2; an odd count leaves window nw - 1 alone
+      const uint32_t n = nw - w1, np = n / 2;
       if (np) {
         TdecWin8P2 r;
-        load8(h, r);
+        load8(a, lane, w1, w1 + 2, true, r);
         for (uint32_t j = 0; j < np; j++) {
-          const uint32_t w0 = h + 2 * j;
+          const uint32_t w0 = w1 + 2 * j;
           TdecX8P2 x;
           P2 B8[8];
           p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
           p2_ck_vec(r.ck, B8);
           MI_SCHED_FENCE();
-          load8(j + 1 < np ? w0 + 2 : w0, r);   // the last pair reloads itself (unused)
+          const uint32_t wn = j + 1 < np ? w0 + 2 : w0;   // the last pair reloads itself (unused)
+          load8(a, lane, wn, wn + 2, true, r);
           MI_SCHED_FENCE();
           p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
         }
@@ -707,12 +780,11 @@ struct TdecP2X {
           [&](const Win& r, uint32_t w) { p2_alpha_window<DEC2, SQF>(a, lane, r, w * BETA_W, al); });
     }
   }
-  // wave B, phase 1: tail, then beta_K .. beta_{K/2}, beta checkpoints h + 1 .. nw
-  MI_HD static void b1(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
+  // wave B, phase 1: tail, then beta_K .. beta_{K/2}, the beta checkpoints phase 2 of wave F reads
+  MI_P2_INL static void b1(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
     const uint32_t K = a.K, nw = K / BETA_W, h = nw / 2;
     const size_t ck = (size_t)2 * K;
-#pragma unroll
-    for (int s = 0; s < 8; s++) b[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    p2_start(b);
     {
       const uint32_t t0 = 3 * K + (DEC2 ? 6 : 0);
       P2 tx[3], tp[3];
@@ -722,7 +794,7 @@ struct TdecP2X {
         const PosW PT = MI_POSW(a, 3 * K);
 #pragma unroll
         for (int j = 0; j < 12; j++) {
-          const P2 q = p2_qpair(p2_sb_in(a, 0, ma, PT, j, lane), p2_sb_in(a, 1, mb, PT, j, lane));
+          const P2 q = q16_pair(p2_sb_in(a, 0, ma, PT, j, lane), p2_sb_in(a, 1, mb, PT, j, lane));
           row_st(a.q, 3 * K, lane, p2_bits(q), j);
           if (j < 6) { if (j & 1) tp[j / 2] = q; else tx[j / 2] = q; }
         }
@@ -732,8 +804,8 @@ struct TdecP2X {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
           const uint32_t d = t0 - 3 * K + 2 * j;
-          tx[j] = p2_qpair(p2_sb_in(a, 0, ma, PT, d, lane), p2_sb_in(a, 1, mb, PT, d, lane));
-          tp[j] = p2_qpair(p2_sb_in(a, 0, ma, PT, d + 1, lane), p2_sb_in(a, 1, mb, PT, d + 1, lane));
+          tx[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d, lane), p2_sb_in(a, 1, mb, PT, d, lane));
+          tp[j] = q16_pair(p2_sb_in(a, 0, ma, PT, d + 1, lane), p2_sb_in(a, 1, mb, PT, d + 1, lane));
         }
       } else {
 #pragma unroll
@@ -757,44 +829,71 @@ struct TdecP2X {
         [&](const Win& r, uint32_t w) {
           if constexpr (MKQ) p2_beta_window_mkq(a, lane, r, w * BETA_W, b);
           else p2_beta_window<DEC2, SQB>(a, r, w * BETA_W, b);
-          if (w > h && (!CK8 || !((w - h) & 1u))) p2_ck_store(a.scr, ck, w, lane, b);
+          if (w > h && beta_ck(w, h, nw)) p2_ck_store(a.scr, ck, w, lane, b);
         });
   }
   // wave B, phase 2: windows h - 1 .. 0 backward, LLRs of steps 0 .. K/2 - 1
-  MI_HD static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
+  MI_P2_INL static void b2(const TdecArgsP2& a, int lane, P2 (&b)[8]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
-    if constexpr (CK8) {
-      // pairs (h - 2j - 2, h - 2j - 1), alpha checkpoint h - 2j - 2 (pair 0: the start state); an odd h
-      // leaves window 0 alone
-      const uint32_t np = h / 2;
-      auto load8 = [&](uint32_t w0, TdecWin8P2& r) {
-        p2_load_window<DEC2, FIRST, SQF>(a, lane, w0 * BETA_W, r.lo);
-        p2_load_window<DEC2, FIRST, SQF>(a, lane, (w0 + 1) * BETA_W, r.hi);
-        p2_ck_load_to(a.scr, ck, w0, lane, r.ck);   // w0 = 0: slot 0 is loaded but not used
-      };
+    if constexpr (CKS >= 8) {
+      const uint32_t ns = spans(h), wlo = h - 4 * ns;
+      if (ns) {
+        // span j: windows w0 .. w0 + 3 (w0 = h - 4 j - 4), opening checkpoint w0 (w0 = 0: the start state).  The lower
+        // pair (and the checkpoint) is loaded first
+        TdecWin8P2 r;
+        load8(a, lane, h - 4, h - 4, true, r);   // w0 = 0: slot 0 is loaded but not used
+        for (uint32_t j = 0; j < ns; j++) {
+          const uint32_t w0 = h - 4 * j - 4;
+          TdecX8P2 x;
+          P2 A0[8], A8[8];
+          p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
+          if (w0) p2_ck_vec(r.ck, A0);
+          else p2_start(A0);
+          MI_SCHED_FENCE();
+          load8(a, lane, w0 + 2, 0, false, r);   // the upper pair
+          MI_SCHED_FENCE();
+          p2_cp8_opaque(A8, A0);
+          p2_alpha_run<0, 3>(A8, x);
+          norm8<true>(A8);   // A4: the lower pair's "A(4)", stashed with its inputs
+          p2_stash_put<DEC2, FIRST>(a.stash, lane, x, A0, A8);
+          p2_alpha_run<4, 7>(A8, x);
+          norm8<true>(A8);
+          MI_SCHED_FENCE();
+          p2_cvt8<DEC2, SQF>(a, r, (w0 + 2) * BETA_W, x);
+          MI_SCHED_FENCE();
+          const uint32_t wn = j + 1 < ns ? w0 - 4 : w0;   // the last span reloads its lower pair (unused)
+          load8(a, lane, wn, wn, true, r);
+          MI_SCHED_FENCE();
+          p2_beta_emit_window8<DEC2, false>(a, lane, x, A8, (w0 + 2) * BETA_W, b);
+          MI_SCHED_FENCE();
+          p2_stash_get<DEC2, FIRST>(a, a.stash, lane, w0 * BETA_W, x, A0, A8);
+          if (w0) p2_beta_emit_window8<DEC2, false, true>(a, lane, x, A0, w0 * BETA_W, b, A8);
+          else p2_beta_emit_window8<DEC2, true, true>(a, lane, x, A0, 0, b, A8);
+        }
+      }
+      // pairs (wlo - 2j - 2, wlo - 2j - 1), alpha checkpoint wlo - 2j - 2 (0: the start state); an odd wlo leaves
+      // window 0 alone
+      const uint32_t np = wlo / 2;
       if (np) {
         TdecWin8P2 r;
-        load8(h - 2, r);
+        load8(a, lane, wlo - 2, wlo - 2, true, r);   // w0 = 0: slot 0 is loaded but not used
         for (uint32_t j = 0; j < np; j++) {
-          const uint32_t w0 = h - 2 * j - 2;
+          const uint32_t w0 = wlo - 2 * j - 2;
           TdecX8P2 x;
           P2 A0[8];
           p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
-          if (w0) {
-            p2_ck_vec(r.ck, A0);
-          } else {
-  #pragma unroll
-            for (int s = 0; s < 8; s++) A0[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
-          }
+          if (w0) p2_ck_vec(r.ck, A0);
+          else p2_start(A0);
           MI_SCHED_FENCE();
-          load8(j + 1 < np ? w0 - 2 : w0, r);   // the last pair reloads itself (unused)
+          const uint32_t wn = j + 1 < np ? w0 - 2 : w0;   // the last pair reloads itself (unused)
+          load8(a, lane, wn, wn, true, r);
           MI_SCHED_FENCE();
           if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b);
           else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b);
         }
       }
-      if (h & 1u) {
+      if (wlo & 1u) {
         Win r;
         p2_load_window<DEC2, FIRST, SQF>(a, lane, 0, r);
         p2_beta_emit_window<DEC2, SQF, true>(a, lane, r, 0, b);
@@ -814,17 +913,13 @@ struct TdecP2X {
   }
 };
 
-template <bool DEC2, bool FIRST, int SRC, bool CK8 = MI_TDEC_P2_CK8, int PFQ = MI_TDEC_P2_PF_Q, class Exec>
-MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
-  using X = TdecP2X<DEC2, FIRST, SRC, CK8, PFQ>;
+template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q, class Exec>
+MI_P2_INL void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
+  using X = TdecP2X<DEC2, FIRST, SRC, CKS, PFQ>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
-#if MI_TDEC_P2_DIAG != 2   // timing diagnostics (MI_TDEC_P2_DIAG, above)
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
-#endif
-#if MI_TDEC_P2_DIAG != 1
   ex.run([&] { X::f2(a, lane, mF); }, [&] { X::b2(a, lane, mB); });
-#endif
 }
 
 // The pass after an iteration (wave F; tdec_body.h tdec_pack is the one-code-block form): for every half in
@@ -834,20 +929,13 @@ MI_HD inline void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
 // partial TB CRC24A of its payload bytes F/8 .. K/8 - (CB CRC ? 3 : 0) that tb_kernel combines.  Returns
 // bit h = half h's code-block CRC passed.  (The byte-wise register of a K-bit block equals the XOR of the
 // per-bit contributions crc_a / crc_b[k] the one-code-block kernels accumulate: CRC is linear.)
-// payload bytes of the check pass as aligned dword stores: 0 = one byte store per byte and half (each store
-// instruction touches 64 code blocks' lines for one byte: 0.5 ms of a 6.6 ms launch, diagnostic 5); 1 = dword stores
-// in every launch; 2 = in the first launch only (the continuation keeps byte stores)
-#ifndef MI_TDEC_P2_PAY32
-#define MI_TDEC_P2_PAY32 1
-#endif
-#ifndef MI_TDEC_P2_PF_CHK
-#define MI_TDEC_P2_PF_CHK 2   // decision-row chunks in flight in the check pass (1 = the round-3 form; 3: 38 VGPRs spilled)
-#endif
-// the code-block and TB CRC registers of both halves over the decision-row chunks [c0, c1) (4 bytes each), from 0;
-// the chunks' payload bytes of the halves in `act` are written
+// The payload bytes go out as aligned dword stores (a byte store per payload byte and half put 64 code blocks' lines
+// under every store instruction for one byte each: 0.5 ms of a 6.6 ms launch, profiles/r4/diag_pay).
+// Measured and not kept: the pass split over both waves (wave B waits at the barrier otherwise; the registers combine
+// by linearity, R(A || B) = R(A) x^(8 |B|) ^ R(B)): more scalar spills, one stream 6.47-6.51 -> 6.50-6.65 ms, four
+// streams 112.3-113.0 -> 110.5-110.9 Gbps (profiles/r4/ab_split_chk), although the pass alone costs 0.45 ms.
 struct P2CrcRegs { uint32_t cb[2], tb[2]; };
-template <bool PAY32>
-MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32_t act, uint32_t c0, uint32_t c1) {
+MI_P2_INL uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2]) {
   uint32_t bl[2], bh[2];
   P2CrcRegs g{{0u, 0u}, {0u, 0u}};
   const uint32_t* ct[2];
@@ -857,10 +945,11 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
     bh[h] = a.K / 8 - ((a.crc24a[h] & 1u) ? 0 : 3);
     ct[h] = (a.crc24a[h] & 1u) ? a.crc8 : a.crc8b;
   }
-  const uint32_t nb = a.K / 8;
-  // the decision rows of 4 bytes (32 rows) per chunk, MI_TDEC_P2_PF_CHK chunks' loads in flight ahead of the chunk
-  // whose bits are used (the trellis registers are dead here); rows past K are clamped to row K - 1 and their bytes
-  // never used
+  const uint32_t nb = a.K / 8, c1 = (nb + 3) / 4;
+  constexpr uint32_t c0 = 0;
+  // the decision rows of 4 bytes (32 rows) per chunk, P2_PF_CHK chunks' loads in flight ahead of the chunk whose
+  // bits are used (the trellis registers are dead here); rows past K are clamped to row K - 1 and their bytes never
+  // used
   struct Chunk { uint32_t d[32]; };
   auto load = [&](uint32_t c, Chunk& dd) {
 #pragma unroll
@@ -901,89 +990,40 @@ MI_HD inline P2CrcRegs tdec_p2_check_range(const TdecArgsP2& a, int lane, uint32
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      if (MI_TDEC_P2_DIAG == 5 || !((act >> h) & 1u)) continue;
+      if (!((act >> h) & 1u)) continue;
       const int64_t off = p2_run_off(a, h);   // byte j at out_bytes[off + j], j in the run
-      if constexpr (PAY32) {
-        // aligned dword stores: the chunk's bytes sit at 4c + m .. 4c + m + 3 (mod 4); it completes the dword at 4c - m
-        // (the previous chunk's last m bytes and its first 4 - m), written whole when it lies inside the run and the
-        // previous chunk is in this range; the bytes of a dword that is not (the run's and the range's edges) go one
-        // by one.  Every byte is written exactly once, only inside the run (the neighbouring code blocks' bytes are
-        // untouched).
-        const uint32_t m = rng[h] & 3u, lo = (rng[h] >> 4) & 0xFFFu, hi = rng[h] >> 16;
-        // the dword at byte 4c - m, i.e. at 4c .. 4c + 3 in the shifted index
-        const bool full0 = c > c0 && 4 * c >= lo && 4 * c + 4 <= hi;
-        const bool full1 = c + 1 < c1 && 4 * c + 4 >= lo && 4 * c + 8 <= hi;   // the next chunk writes it
-        if (full0) {
+      // aligned dword stores: the chunk's bytes sit at 4c + m .. 4c + m + 3 (mod 4); it completes the dword at 4c - m
+      // (the previous chunk's last m bytes and its first 4 - m), written whole when it lies inside the run and the
+      // previous chunk is in this range; the bytes of a dword that is not (the run's and the range's edges) go one
+      // by one.  Every byte is written exactly once, only inside the run (the neighbouring code blocks' bytes are
+      // untouched).
+      const uint32_t m = rng[h] & 3u, lo = (rng[h] >> 4) & 0xFFFu, hi = rng[h] >> 16;
+      // the dword at byte 4c - m, i.e. at 4c .. 4c + 3 in the shifted index
+      const bool full0 = c > c0 && 4 * c >= lo && 4 * c + 4 <= hi;
+      const bool full1 = c + 1 < c1 && 4 * c + 4 >= lo && 4 * c + 8 <= hi;   // the next chunk writes it
+      if (full0) {
 #if defined(__HIP_DEVICE_COMPILE__)
-          const uint32_t v = m ? __builtin_amdgcn_alignbyte(w[h], wprev[h], 4 - m) : w[h];
+        const uint32_t v = m ? __builtin_amdgcn_alignbyte(w[h], wprev[h], 4 - m) : w[h];
 #else
-          const uint32_t v = m ? (uint32_t)((((uint64_t)w[h] << 32) | wprev[h]) >> (8 * (4 - m))) : w[h];
+        const uint32_t v = m ? (uint32_t)((((uint64_t)w[h] << 32) | wprev[h]) >> (8 * (4 - m))) : w[h];
 #endif
-          *reinterpret_cast<uint32_t*>(a.out_bytes + (off + (int64_t)(4 * c) - (int64_t)m)) = v;
-        }
-        // uncovered bytes lie in the range's first 3 chunks (jlo + m < 11) and its last 5 (hi >= nb - 6), a
-        // wave-uniform test
-        if (c < c0 + 3 || c + 5 >= c1) {
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const uint32_t j = 4 * c + (uint32_t)b;
-            const bool covered = (uint32_t)b < 4 - m ? full0 : full1;
-            if (j + m >= lo && j + m < hi && !covered) a.out_bytes[off + (int64_t)j] = (uint8_t)(w[h] >> (8 * b));
-          }
-        }
-        wprev[h] = w[h];
-      } else {
+        *reinterpret_cast<uint32_t*>(a.out_bytes + (off + (int64_t)(4 * c) - (int64_t)m)) = v;
+      }
+      // uncovered bytes lie in the range's first 3 chunks (jlo + m < 11) and its last 5 (hi >= nb - 6), a
+      // wave-uniform test
+      if (c < c0 + 3 || c + 5 >= c1) {
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const uint32_t j = 4 * c + (uint32_t)b;
-          const uint32_t m = rng[h] & 3u;
-          if (j + m >= ((rng[h] >> 4) & 0xFFFu) && j + m < (rng[h] >> 16))
-            a.out_bytes[off + (int64_t)j] = (uint8_t)(w[h] >> (8 * b));
+          const bool covered = (uint32_t)b < 4 - m ? full0 : full1;
+          if (j + m >= lo && j + m < hi && !covered) a.out_bytes[off + (int64_t)j] = (uint8_t)(w[h] >> (8 * b));
         }
       }
+      wprev[h] = w[h];
     }
   };
   if (c1 > c0)
-    pipe_windows<MI_TDEC_P2_PF_CHK, Chunk>(
-        (int)(c1 - c0), [c0](int i) { return c0 + (uint32_t)i; }, load, run);
-  return g;
-}
-// a register shifted past L zero bytes: r x^(8 L) mod g (the byte-wise CRC is linear: R(A || B) = R(A) x^(8 |B|) ^ R(B))
-MI_HD inline uint32_t crc24_shift(uint32_t r, uint32_t L, const uint32_t* tab) {
-  for (uint32_t i = 0; i < L; i++) r = ((r << 8) & 0xFFFFFFu) ^ tab[(r >> 16) & 0xFFu];
-  return r;
-}
-// The check pass over both waves (MI_TDEC_P2_SPLIT_CHK=1, measured and not kept): wave F takes the first half of the
-// chunks, wave B the second (it waits at the barrier otherwise), each from a zero register; wave F then shifts its
-// registers past the bytes of B's half and XORs B's in -- identical registers, verdicts and payload bytes, but the
-// kernel spills more scalar registers and the step got slower (one stream 6.47-6.51 -> 6.50-6.65 ms, four streams
-// 112.3-113.0 -> 110.5-110.9 Gbps; profiles/r4/ab_split_chk), although the pass alone costs 0.45 ms of the launch
-// (a diagnostic build without it: 6.62 -> 6.14 ms at one iteration, profiles/r4/diag_chk)
-#ifndef MI_TDEC_P2_SPLIT_CHK
-#define MI_TDEC_P2_SPLIT_CHK 0
-#endif
-template <bool PAY32, class Exec>
-MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, uint32_t (&tbp)[2], Exec& ex) {
-  const uint32_t nb = a.K / 8, nc = (nb + 3) / 4;
-  P2CrcRegs g;
-  if constexpr (MI_TDEC_P2_SPLIT_CHK) {
-    const uint32_t ncf = (nc + 1) / 2, jb = 4 * ncf;   // wave B: bytes jb .. nb - 1
-    P2CrcRegs gf{{0u, 0u}, {0u, 0u}}, gb{{0u, 0u}, {0u, 0u}};
-    ex.run([&] { gf = tdec_p2_check_range<PAY32>(a, lane, act, 0, ncf); }, [&] { gb = tdec_p2_check_range<PAY32>(a, lane, act, ncf, nc); });
-    uint32_t v[4] = {gb.cb[0], gb.cb[1], gb.tb[0], gb.tb[1]};
-    ex.share_from_b(v, lane);
-    const uint32_t lcb = nb > jb ? nb - jb : 0u;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint32_t bl = a.F[h] / 8, bh = a.K / 8 - ((a.crc24a[h] & 1u) ? 0 : 3), s = jb > bl ? jb : bl;
-      const uint32_t ltb = bh > s ? bh - s : 0u;   // TB-CRC bytes in B's half
-      const uint32_t* ct = (a.crc24a[h] & 1u) ? a.crc8 : a.crc8b;
-      g.cb[h] = crc24_shift(gf.cb[h], lcb, ct) ^ v[h];
-      g.tb[h] = crc24_shift(gf.tb[h], ltb, a.crc8) ^ v[2 + h];
-    }
-  } else {
-    g = tdec_p2_check_range<PAY32>(a, lane, act, 0, nc);
-  }
+    pipe_windows<P2_PF_CHK, Chunk>((int)c1, [](int i) { return (uint32_t)i; }, load, run);
   if (act & 1u) tbp[0] = g.tb[0];
   if (act & 2u) tbp[1] = g.tb[1];
   return (g.cb[0] == 0u ? 1u : 0u) | (g.cb[1] == 0u ? 2u : 0u);
@@ -995,22 +1035,20 @@ MI_HD inline uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act,
 // iteration count) only the last iteration's pass runs.
 // CONT (waterfall compaction, tdec.hip): the code blocks continue from iteration 1 in a dense continuation
 // pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
-template <bool CONT = false, bool CKC = MI_TDEC_P2C_CK8, class Exec>
-MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
+template <bool CONT = false, int CKC = P2C_CKS, class Exec>
+MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
   // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
-  constexpr bool CK = CONT ? CKC : MI_TDEC_P2_CK8;   // CKC: the continuation's spacing (tdec.hip tdec_kernel_p2c)
-  constexpr int PQ = CONT ? MI_TDEC_P2C_PF_Q : MI_TDEC_P2_PF_Q;
-  constexpr bool PAY = MI_TDEC_P2_PAY32 == 1 || (MI_TDEC_P2_PAY32 == 2 && !CONT);
+  constexpr int CK = CONT ? CKC : P2_CKS;   // CKC: the continuation's spacing (tdec.hip tdec_kernel_p2c)
   if constexpr (CONT)
-    if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
+    if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CK>(a, lane, ex);
   for (uint32_t it = CONT ? a.it0 : 0u; it < (CONT ? a.it_end : a.max_its) && active; it++) {
-    constexpr uint32_t MK = MI_TDEC_P2_QSB ? 0xFFFFFFFFu : MI_TDEC_MKQ_IT;   // QSB: every pass reads the mirror
+    constexpr uint32_t MK = TDEC_MKQ_IT;
     if constexpr (CONT) {
-      tdec_p2_xhalf<false, false, SRC_Q, CK, PQ>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q, CK, PQ>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_Q, CK>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CK>(a, lane, ex);
     } else if (it == 0) {
       if (MK == 0) {
         tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex);
@@ -1032,11 +1070,7 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
     const bool last = it + 1 == a.max_its;
     uint32_t ok = 0u;
     if (a.early_stop || last) {   // wave-uniform
-      if constexpr (MI_TDEC_P2_SPLIT_CHK) {   // both waves run the pass; wave F's verdicts go to both
-        if (MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check<PAY>(a, lane, active, r.tb_part, ex);
-      } else {
-        if (ex.pack_wave() && MI_TDEC_P2_DIAG < 3) ok = tdec_p2_check<PAY>(a, lane, active, r.tb_part, ex);
-      }
+      if (ex.pack_wave()) ok = tdec_p2_check(a, lane, active, r.tb_part);
       ok = ex.share(ok, lane);
     }
     uint32_t stop = 0u;
@@ -1067,7 +1101,6 @@ MI_HD inline TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) 
 // goes by q window (12 rows: one window-mask word per source) and by w row.
 struct P2ContSrc {
   const float* sb;      // the code block's group softbuffer
-  const int16_t* sbq;   // its int16 mirror (MI_TDEC_P2_QSB)
   const uint32_t* wm;   // the group's window masks
   const uint32_t* scr;  // the scratch of the group's pair (w rows: packed, this code block = half hs)
   uint32_t ls, hs;      // lane in the group, half in the pair
@@ -1079,27 +1112,15 @@ MI_HD inline void p2_cont_qwin(const P2ContSrc (&s)[2], uint32_t live, const uin
   uint32_t m[2];
 #pragma unroll
   for (int h = 0; h < 2; h++) m[h] = ((live >> h) & 1u) ? s[h].wm[w] : 0u;
-#if MI_TDEC_P2_QSB
-  uint32_t v[3 * BETA_W][2];
-#pragma unroll
-  for (int i = 0; i < 3 * BETA_W; i++) {
-    const size_t row = MI_SB_NAT ? 3 * BETA_W * w + i : pos[3 * BETA_W * w + i];
-#pragma unroll
-    for (int h = 0; h < 2; h++) v[i][h] = ((m[h] >> i) & 1u) ? (uint16_t)s[h].sbq[row * LANES + s[h].ls] : 0u;
-  }
-#pragma unroll
-  for (int i = 0; i < 3 * BETA_W; i++) q[i] = v[i][0] | (v[i][1] << 16);
-#else
   float v[3 * BETA_W][2];
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) {
-    const size_t row = MI_SB_NAT ? 3 * BETA_W * w + i : pos[3 * BETA_W * w + i];
+    const size_t row = 3 * BETA_W * w + i;   // rows in decoder-input order
 #pragma unroll
     for (int h = 0; h < 2; h++) v[i][h] = ((m[h] >> i) & 1u) ? s[h].sb[row * LANES + s[h].ls] : 0.0f;
   }
 #pragma unroll
   for (int i = 0; i < 3 * BETA_W; i++) q[i] = p2_bits(q16_pair(v[i][0], v[i][1]));
-#endif
 }
 // packed row `row` of one continuation lane from its sources' packed rows (each half's 16 bits from its source pair's
 // row, half hs): the w rows (at 0) after a first launch that stored them, and every row of a re-compaction round
@@ -1126,8 +1147,6 @@ struct TdecP2ExecHost {
   template <class F, class B>
   void run(F f, B b) { f(); b(); }
   uint32_t share(uint32_t v, int) { return v; }
-  template <int N>
-  void share_from_b(uint32_t (&)[N], int) {}   // both waves' values are this thread's
   bool pack_wave() const { return true; }
 };
 

@@ -5,10 +5,6 @@
 #include "kernels.h"
 #include "tdec_win_body.h"
 
-#ifndef MI_WIN_DIAG_STOP
-#define MI_WIN_DIAG_STOP 0
-#endif
-
 namespace mi {
 
 struct TdecWinOut {
@@ -90,25 +86,15 @@ __global__ __launch_bounds__(P) void tdec_win_kernel(const float* __restrict__ s
   for (uint32_t b = t; b < 256; b += P) crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
   win_load_map(c, t, P, sb + g.sb_off, g.Ncb);
   __syncthreads();
-  win_load(c, t, P, sb + g.sb_off, g.Ncb, kdata + (MI_SB_NAT ? kt.pos_off : kt.ipos_off), kdata + kt.pi_off, li % LANES,
-           ld.F);
+  win_load(c, t, P, sb + g.sb_off, kdata + kt.pos_off, kdata + kt.pi_off, li % LANES, ld.F);
   __syncthreads();
-#if MI_WIN_DIAG_STOP == 1   // timing diagnostics only (phase cut-offs, wrong outputs)
-  return;
-#endif
   const uint32_t* tab = kdata + (ld.crc24a ? kt.crca_off : kt.crcb_off);
   uint32_t its = 0, ok = 0;
   for (uint32_t it = 0; it < max_its; it++) {
     win_half<false>(c, t);
     __syncthreads();
-#if MI_WIN_DIAG_STOP == 2
-    return;
-#endif
     win_half<true>(c, t);
     __syncthreads();
-#if MI_WIN_DIAG_STOP == 3
-    return;
-#endif
     ok = block_xor<P>(win_crc_part(c, t, P, tab), red) == 0;
     its = it + 1;
     if (early_stop && ok) break;

@@ -261,15 +261,11 @@ MI_HD inline void win_load_map(const WinCb& c, uint32_t t, uint32_t P, const flo
 // position-table and softbuffer loads of a batch are independent (one round trip per batch of B per
 // thread) and consecutive threads read consecutive rows.  (Gathering in decoder order -- position,
 // then map, then value: three dependent loads, B = 8 -- was 53 us of a 174 us single-subframe decode.)
-// tab = the position table pos (rows in decoder-input order, MI_SB_NAT: row t is read whatever its state and
-// kept when its position pos[t] is materialised -- the row and table loads stay independent) or ipos
-MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, uint32_t Ncb,
-                           const uint32_t* tab, const uint32_t* pi32, uint32_t lane, uint32_t F) {
-#ifndef MI_WIN_LOAD_B
-#define MI_WIN_LOAD_B 24
-#endif
-  constexpr uint32_t B = MI_WIN_LOAD_B;
-#if MI_SB_NAT
+// tab = the position table pos (rows in decoder-input order: row t is read whatever its state and kept when its
+// position pos[t] is materialised -- the row and table loads stay independent)
+MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* sbg, const uint32_t* tab,
+                           const uint32_t* pi32, uint32_t lane, uint32_t F) {
+  constexpr uint32_t B = 24;   // independent loads per thread and round (72 measured the same)
   const uint32_t T = 3 * (c.K + 4);
   for (uint32_t t0 = t; t0 < T; t0 += B * P) {
     uint32_t pp[B];
@@ -289,27 +285,6 @@ MI_HD inline void win_load(const WinCb& c, uint32_t t, uint32_t P, const float* 
       c.q[i] = (int16_t)x;
     }
   }
-#else
-  const uint32_t* ipos = tab;
-  for (uint32_t p0 = t; p0 < Ncb; p0 += B * P) {
-    uint32_t ii[B];
-    float xx[B];
-#pragma unroll
-    for (uint32_t b = 0; b < B; b++) {
-      const uint32_t p = p0 + b * P;
-      ii[b] = p < Ncb ? ipos[p] : 0xFFFFFFFFu;
-      xx[b] = (p < Ncb && c.lmap[p]) ? sbg[(size_t)p * LANES + lane] : 0.0f;
-    }
-#pragma unroll
-    for (uint32_t b = 0; b < B; b++) {
-      const uint32_t i = ii[b];
-      if (i == 0xFFFFFFFFu) continue;
-      float x = q16f(xx[b]);
-      if (i < 3 * F && i % 3 != 2) x = -I16_CI;
-      c.q[i] = (int16_t)x;
-    }
-  }
-#endif
   for (uint32_t k = t; k < c.K; k += P) {
     c.pi[k] = (uint16_t)pi32[k];
     c.w[k] = 0;

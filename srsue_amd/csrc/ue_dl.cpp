@@ -200,7 +200,8 @@ void srslte_softbuffer_rx_free(srslte_softbuffer_rx_t* q) {
   if (q) memset(q, 0, sizeof(*q));
 }
 void srslte_softbuffer_rx_reset(srslte_softbuffer_rx_t* q) {
-  if (q && q->dev) (void)hipMemset(q->dev, 0, q->dev_bytes);   // == RX_NULL everywhere
+  // == RX_NULL everywhere (srsLTE's reset returns nothing: a failure is left in mi_last_error)
+  if (q && q->dev) (void)mi::hip_ok(hipMemset(q->dev, 0, q->dev_bytes), "softbuffer reset");
 }
 void srslte_softbuffer_rx_reset_tbs(srslte_softbuffer_rx_t* q, uint32_t /*tbs*/) {
   // srsLTE resets the rows of the TB's code blocks; the arena only ever holds one TB

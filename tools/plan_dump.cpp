@@ -115,6 +115,8 @@ static void digest(const Plan& P) {
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 12500;
   Plan P;
+  // MI_RM_XCDQ=0: the work list in launch order (the engine reads this at creation, engine.cpp Engine::Engine)
+  if (const char* e = getenv("MI_RM_XCDQ")) P.xcd_queues = atoi(e) != 0;
   for (int k = 0; k < 4; k++) {
     const auto cfgs = scenario(k, n);
     double best = 1e30;
