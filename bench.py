@@ -23,14 +23,29 @@ import time
 
 import numpy as np
 
+
+def hw_queues_arg(argv):
+    """--hw-queues N / --hw-queues=N (default 8; 0 keeps the environment's value), checked to 0..32."""
+    v = "8"
+    for i, a in enumerate(argv):
+        if a == "--hw-queues" and i + 1 < len(argv):
+            v = argv[i + 1]
+        elif a.startswith("--hw-queues="):
+            v = a.split("=", 1)[1]
+    if not v.isdigit() or not 0 <= int(v) <= 32:
+        raise SystemExit(f"bench.py: --hw-queues must be an integer in 0..32, got {v!r}")
+    return v
+
+
 # HIP hardware queues per process (--hw-queues, default 8; 0 keeps the environment's value): the bench keeps 4
 # batches in flight on as many HIP streams, and with HIP's default of 4 queues per process the streams' kernels
 # share them with the runtime's own copies; 8 queues measured +0.7 % at the headline, 16 no better
-# (profiles/r4/ab_queues).  Set here, before torch and the HIP runtime start (the runtime reads it once); the ranks
-# bench.py spawns inherit it.
-HW_QUEUES = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--hw-queues"), "8")
-if HW_QUEUES != "0":
-    os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
+# (profiles/r4/ab_queues).  Set only when bench.py runs as the program (not when tests import it), before torch and
+# the HIP runtime start (the runtime reads it once); the ranks bench.py spawns inherit it.
+if __name__ == "__main__":
+    HW_QUEUES = hw_queues_arg(sys.argv[1:])
+    if HW_QUEUES != "0":
+        os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -541,11 +556,14 @@ def bench_sync(args, batch, dev):
                     f"correction of all {B} subframes into the batch IQ buffer, per step"}
 
 
-def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
+def bench_h2d(args, cfgs, pool_iq, batch, bits_ok, iq=None, steps=None):
     """IQ resident in page-locked host memory, each step copied H2D and decoded through the
-    double-buffered pipeline (copy of step i+1 overlaps the decode of step i)."""
+    double-buffered pipeline (copy of step i+1 overlaps the decode of step i): the deployable (PCIe-inclusive)
+    rate, reported beside value and never as value."""
     B = len(cfgs)
-    sc16 = args.iq == "sc16"
+    iq_fmt = iq or args.iq
+    steps = steps or args.steps
+    sc16 = iq_fmt == "sc16"
     pipe = abi.Pipe(cfgs, max_its=args.max_its, tdec_i16=args.tdec == "i16", iq_sc16=sc16)
     nfl = 2 * batch.iq_samples
     esz = 2 if sc16 else 4
@@ -558,16 +576,17 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok):
     for _ in range(max(2, args.warmup)):
         pipe.wait(pipe.submit(hb.ptr))
     t0 = time.perf_counter()
-    last = [pipe.submit(hb.ptr) for _ in range(args.steps)]
+    last = [pipe.submit(hb.ptr) for _ in range(steps)]
     pipe.wait(last[-1] ^ 1)
     pipe.wait(last[-1])
     dt = time.perf_counter() - t0
     ok = pipe.batch(last[-1]).download(abi.BUF_TB_CRC, np.uint32)[:B]
     pipe.close()
     hb.close()
-    return {"value": round(bits_ok * args.steps / dt / 1e6, 2), "unit": "Mbps", "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "pcie_GBps": round(nfl * esz * args.steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
-            "what": f"IQ ({args.iq}, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy "
+    return {"value": round(bits_ok * steps / dt / 1e6, 2), "unit": "Mbps", "ms_per_step": round(dt / steps * 1e3, 3),
+            "steps": steps, "iq_bytes_per_subframe": round(nfl * esz / B),
+            "pcie_GBps": round(nfl * esz * steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
+            "what": f"IQ ({iq_fmt}, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy "
                     "stream overlapped with the previous batch's decode"}
 
 
@@ -665,6 +684,8 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     S = max(1, args.streams)
     J = len(lists)
     # one workspace per stream; static mode needs S a multiple of J so that each stream always runs one list
+    if not replan and S % J:
+        raise ValueError(f"replan_steps: static mode needs the streams ({S}) to be a multiple of the lists ({J})")
     batches = [abi.Batch(lists[k % J], max_its=args.max_its, profile=False, tdec_i16=args.tdec == "i16",
                          sched=args.sched, compact_ce=True) for k in range(S)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
@@ -717,16 +738,34 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     bits = [0.0] * J
     bad = 0
     seen = set()
-    for k, b in enumerate(batches):
-        j = last_list[k]
-        if j is None or j in seen:
-            continue
-        seen.add(j)
+
+    def check(b, j):
+        nonlocal bad
         crc = b.download(abi.BUF_TB_CRC, np.uint32)[:len(b.cfgs)]
         bits[j] = float(sum(b.cfgs[i].tbs for i in range(len(crc)) if crc[i]))
         pay = b.download(abi.BUF_PAYLOAD, np.uint8)
         bad += sum(int(not np.array_equal(b.payload(i, pay), args._pool_tb[j][i % len(args._pool_tb[j])]))
                    for i in range(len(crc)) if crc[i])
+    for k, b in enumerate(batches):
+        j = last_list[k]
+        if j is None or j in seen:
+            continue
+        seen.add(j)
+        check(b, j)
+    # a list no workspace ran last (fewer streams than lists, re-planned): one more run of it after the timed region,
+    # so every list's CRC-OK bits and payloads come from a run of that list
+    for j in range(J):
+        if j in seen:
+            continue
+        p = abi.Plan()
+        p.build(lists[j])
+        batches[0].replan(p, sptr[0])
+        batches[0].run(iqs[j].data_ptr(), sptr[0])
+        torch.cuda.synchronize(dev)
+        p.close()
+        check(batches[0], j)
+    if not all(bits):
+        raise RuntimeError(f"replan_steps: a list decoded no CRC-OK TB ({bits})")
     for b in batches:
         b.close()
     for p in plans:
@@ -943,7 +982,7 @@ def main():
                     help="--streams of the waterfall block; 0 = auto (= --streams: its continuation holds 0.74 "
                          "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
                          "profiles/r3/ab_streams*)")
-    ap.add_argument("--hw-queues", type=int, default=8,
+    ap.add_argument("--hw-queues", type=int, default=8, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process and its ranks (set before the HIP runtime starts, see "
                          "HW_QUEUES above); 0 = keep the environment's value")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -960,6 +999,8 @@ def main():
                     help="BASELINE.json configs[n-1]; 4 (default) = 20 MHz TM1 MCS-28 shard per GPU")
     ap.add_argument("--cb-per-gpu", type=int, default=65536, help="config 1: code blocks per GPU per step")
     ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
+    ap.add_argument("--h2d-steps", type=int, default=20,
+                    help="steps of the PCIe-inclusive (h2d) block of the default line (0 = off)")
     ap.add_argument("--h2d", action="store_true",
                     help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
                          "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
@@ -1102,6 +1143,11 @@ def main():
         }
         if args.h2d:
             out["h2d"] = bench_h2d(args, cfgs, pool_iq, batch, bits_ok)
+        elif args.config == 4 and args.h2d_steps > 0 and world == 1:
+            # the deployable rate of this build: UHD's sc16 wire format and srsLTE's fc32, IQ
+            # from page-locked host memory, beside value
+            out["h2d"] = {f: bench_h2d(args, cfgs, pool_iq, batch, bits_ok, iq=f, steps=args.h2d_steps)
+                          for f in ("sc16", "fc32")}
         if itr:
             out["iterating"] = itr
         if args.config == 4 and args.plan_steps > 0 and world == 1:

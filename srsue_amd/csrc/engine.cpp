@@ -62,11 +62,13 @@ Engine::~Engine() {
     (void)hipEventSynchronize(cont_ev);
     (void)hipEventDestroy(cont_ev);
   }
-  if (stage_done) {
-    (void)hipEventSynchronize(stage_done);
-    (void)hipEventDestroy(stage_done);
+  for (int k = 0; k < NSTAGE; k++) {
+    if (stage_done[k]) {
+      (void)hipEventSynchronize(stage_done[k]);
+      (void)hipEventDestroy(stage_done[k]);
+    }
+    if (h_stage[k]) (void)hipHostFree(h_stage[k]);
   }
-  if (h_stage) (void)hipHostFree(h_stage);
   if (h_cont) (void)hipHostFree(h_cont);
   for (auto& set : ev_sets)
     for (auto& e : set) (void)hipEventDestroy(e);
@@ -98,14 +100,16 @@ int Engine::stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t s
   MI_ENGINE_TABS(P);
   size_t total = 0;
   for (const Tab& t : tabs) total += tab_span(t.bytes);
-  // the previous DMA out of the staging buffer must be done before it is rewritten
-  if (stage_done && !hip_ok(hipEventSynchronize(stage_done), "stage wait")) return -1;
-  if (total > h_stage_bytes) {
-    if (h_stage) (void)hipHostFree(h_stage);
-    h_stage = nullptr;
-    h_stage_bytes = 0;
-    if (!hip_ok(hipHostMalloc(&h_stage, total, hipHostMallocDefault), "hipHostMalloc tables")) return -1;
-    h_stage_bytes = total;
+  // this staging buffer's previous DMA must be done before it is rewritten
+  const int k = stage_next;
+  stage_next = (stage_next + 1) % NSTAGE;
+  if (stage_done[k] && !hip_ok(hipEventSynchronize(stage_done[k]), "stage wait")) return -1;
+  if (total > h_stage_bytes[k]) {
+    if (h_stage[k]) (void)hipHostFree(h_stage[k]);
+    h_stage[k] = nullptr;
+    h_stage_bytes[k] = 0;
+    if (!hip_ok(hipHostMalloc(&h_stage[k], total, hipHostMallocDefault), "hipHostMalloc tables")) return -1;
+    h_stage_bytes[k] = total;
   }
   if (total > arena.bytes || arena.view) {
     if (&arena == &d_tables)
@@ -115,13 +119,13 @@ int Engine::stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t s
   offs.clear();
   size_t off = 0;
   for (const Tab& t : tabs) {
-    if (t.bytes) memcpy(static_cast<char*>(h_stage) + off, t.src, t.bytes);
+    if (t.bytes) memcpy(static_cast<char*>(h_stage[k]) + off, t.src, t.bytes);
     offs.push_back(off);
     off += tab_span(t.bytes);
   }
-  if (!stage_done && !hip_ok(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "event")) return -1;
-  return hip_ok(hipMemcpyAsync(arena.p, h_stage, total, hipMemcpyHostToDevice, st), "upload tables") &&
-                 hip_ok(hipEventRecord(stage_done, st), "event")
+  if (!stage_done[k] && !hip_ok(hipEventCreateWithFlags(&stage_done[k], hipEventDisableTiming), "event")) return -1;
+  return hip_ok(hipMemcpyAsync(arena.p, h_stage[k], total, hipMemcpyHostToDevice, st), "upload tables") &&
+                 hip_ok(hipEventRecord(stage_done[k], st), "event")
              ? 0
              : -1;
 }

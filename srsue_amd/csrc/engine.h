@@ -81,9 +81,14 @@ struct Engine {
   DevBuf d_rmdir;               // Plan::rm_direct
   const uint32_t* rm_items() const { return plan.rm_items.empty() ? nullptr : d_rmitems.as<uint32_t>(); }
   const uint4* rm_recs() const { return plan.rm_recs.empty() ? nullptr : d_rmrecs.as<uint4>(); }
-  void* h_stage = nullptr;
-  size_t h_stage_bytes = 0;
-  hipEvent_t stage_done = nullptr;   // the last DMA out of h_stage (waited for before h_stage is rewritten)
+  // two page-locked staging buffers used in turn, each with the event of its last DMA (waited for before it is
+  // rewritten): a re-plan does not wait for the previous one's table upload, which another stream may still have
+  // queued behind its kernels (the main thread blocked 7-26 ms per pipelined re-plan)
+  static constexpr int NSTAGE = 2;
+  void* h_stage[NSTAGE] = {nullptr, nullptr};
+  size_t h_stage_bytes[NSTAGE] = {0, 0};
+  hipEvent_t stage_done[NSTAGE] = {nullptr, nullptr};
+  int stage_next = 0;
   // Per-TTI plan memo (the srsLTE per-TTI API re-plans every call; srsUE cycles through the same few
   // configurations -- one per subframe index and stage): a configuration planned before is re-activated
   // by swapping its parked plan in and pointing the table views at its own device arena, instead of

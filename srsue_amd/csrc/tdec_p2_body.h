@@ -572,12 +572,14 @@ MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const Tdec
 // softbuffer passes follow tdec_body.h.  The check pass keeps two decision-row chunks in flight (three: 38 VGPRs
 // spilled).
 constexpr int P2_PF_Q = 1, P2_PF_SB = TDEC_PF_SB, P2_PF_CHK = 2;
-// Checkpoint spacing (steps) of the first launch, tdec_kernel_p2x: 16 (spans with the LDS stash below), 8 or 4.
-#ifndef MI_TDEC_P2_CKS
-#define MI_TDEC_P2_CKS 8
-#endif
-constexpr int P2_CKS = MI_TDEC_P2_CKS;
-static_assert(P2_CKS == 4 || P2_CKS == 8 || P2_CKS == 16, "checkpoint spacing: 4, 8 or 16 steps");
+// Checkpoint spacing (steps) of tdec_kernel_p2x, chosen per launch (tdec.hip launch_tdec_p2): 16-step spans (the LDS
+// stash below) when the launch runs several iterations, 8 for the one-iteration first launch of the compacted path.
+// Measured (round 5, profiles/r5/ab_ck16): 16-step spans cut the traffic of a headline launch from 22.8 to 19.5 GB
+// (2.00 -> 1.70 x algorithmic) and its isolated time by 1-2 %, but their 19 KB of LDS per workgroup leave room for
+// one co-resident rate de-matching workgroup per CU instead of three, and the 4-stream headline lost 2 % (rate
+// de-matching overlapped 11.9 -> 18.0 ms); configs[0] (8 iterations, no rate de-matching beside it) gains 9 %:
+// 16.1 -> 17.6 Gbps, one launch 31.3 -> 30.4 ms.  P2_CKS is the spacing of the host emulation (emu.cpp).
+constexpr int P2_CKS = 8, P2_CKS_ITER = 16;
 // The waterfall continuation (tdec_kernel_p2c) runs few wavefronts (0.74 per SIMD at the 21.5 dB bench point), each a
 // lone chain, so its spacing is a parameter of its own.  Its first round keeps 8-step checkpoints: 4-step ones (6
 // recursion steps per 8 instead of 12) shorten a lone chain (one stream, same box: waterfall tdec 21.95 -> 21.25 ms)
@@ -1035,37 +1037,38 @@ MI_P2_INL uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, ui
 // iteration count) only the last iteration's pass runs.
 // CONT (waterfall compaction, tdec.hip): the code blocks continue from iteration 1 in a dense continuation
 // pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
-template <bool CONT = false, int CKC = P2C_CKS, class Exec>
+// CKS: the checkpoint spacing of every pass (the first launch: P2_CKS or P2_CKS_ITER; the continuation: P2C_CKS or
+// P2C_CKS_LATE, tdec.hip tdec_kernel_p2c)
+template <bool CONT = false, int CKS = P2_CKS, class Exec>
 MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
   // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
-  constexpr int CK = CONT ? CKC : P2_CKS;   // CKC: the continuation's spacing (tdec.hip tdec_kernel_p2c)
   if constexpr (CONT)
-    if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CK>(a, lane, ex);
+    if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
   for (uint32_t it = CONT ? a.it0 : 0u; it < (CONT ? a.it_end : a.max_its) && active; it++) {
     constexpr uint32_t MK = TDEC_MKQ_IT;
     if constexpr (CONT) {
-      tdec_p2_xhalf<false, false, SRC_Q, CK>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q, CK>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_Q, CKS>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
     } else if (it == 0) {
       if (MK == 0) {
-        tdec_p2_xhalf<false, true, SRC_MKQ>(a, lane, ex);
-        tdec_p2_xhalf<true, true, SRC_Q>(a, lane, ex);
+        tdec_p2_xhalf<false, true, SRC_MKQ, CKS>(a, lane, ex);
+        tdec_p2_xhalf<true, true, SRC_Q, CKS>(a, lane, ex);
       } else {
-        tdec_p2_xhalf<false, true, SRC_SB>(a, lane, ex);
-        tdec_p2_xhalf<true, true, SRC_SB>(a, lane, ex);
+        tdec_p2_xhalf<false, true, SRC_SB, CKS>(a, lane, ex);
+        tdec_p2_xhalf<true, true, SRC_SB, CKS>(a, lane, ex);
       }
     } else if (it < MK) {
-      tdec_p2_xhalf<false, false, SRC_SB>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_SB>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_SB, CKS>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_SB, CKS>(a, lane, ex);
     } else if (it == MK) {
-      tdec_p2_xhalf<false, false, SRC_MKQ>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_MKQ, CKS>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
     } else {
-      tdec_p2_xhalf<false, false, SRC_Q>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_Q, CKS>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
     }
     const bool last = it + 1 == a.max_its;
     uint32_t ok = 0u;

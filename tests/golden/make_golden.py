@@ -11,8 +11,11 @@ Fixtures
   sf_1p4mhz.npz           1.4 MHz TM1 subframe: IQ (product TX, 20 dB), TB, oracle grid/ce/LLR/payload
   tdec16_K6144.npz        the config-1 LLRs of tdec_K6144_ebno.npz through the int16 ("SSE") decoder:
                           decisions, bit errors, and the decisions after 1 and 2 iterations
+  sf_20mhz_tm1.npz        BASELINE configs[1]: one 20 MHz TM1 MCS-28 subframe (product TX at 21.5 dB, where code
+                          blocks need up to 4 iterations): IQ, TB, oracle grid / ce / metrics / LLR, and the payload and
+                          iteration count of both turbo arithmetics (float srsLTE-gen, int16 SSE design)
 
-`python tests/golden/make_golden.py tdec16` regenerates only the int16 fixture.
+`python tests/golden/make_golden.py tdec16` regenerates only the int16 fixture, `... sf20` only the 20 MHz one.
 """
 import ctypes as C
 import os
@@ -56,9 +59,30 @@ def make_tdec16():
     print("int16 K=6144 bit errors per Eb/N0", dict(zip(g["ebno"].tolist(), errs)))
 
 
+def make_sf20():
+    """configs[1]'s subframe through the oracle chain, both turbo arithmetics (GPU tests compare against the arrays)."""
+    cfg = abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=1, cfi=1, tbs=75376, Qm=6)
+    tb = O.splitmix_bytes(0x5EED0000 + 20, cfg.tbs // 8)
+    iq = abi.tx_subframe(cfg, tb, snr_db=21.5, seed=0xA5A5 + 20)
+    grid, ce, met, llr = oracle_front(cfg, iq)
+    out = {}
+    for name, mode in (("gen", O.TDEC_GEN), ("i16", O.TDEC_I16)):
+        with O.tdec_mode(mode):
+            ok, pay, noi, _ = oracle_dlsch(cfg, llr)
+        assert ok and np.array_equal(pay, tb), name
+        out["payload_" + name], out["noi_" + name] = pay, np.array([noi])
+    np.savez_compressed(os.path.join(HERE, "sf_20mhz_tm1.npz"), iq=iq, tb=tb, grid=grid, ce=ce, metrics=met, llr=llr,
+                        cfg=np.array([cfg.cell_id, cfg.nof_prb, cfg.nof_ports, cfg.sf_idx, cfg.cfi, cfg.tbs, cfg.Qm]),
+                        **out)
+    print("sf_20mhz_tm1: iterations gen", out["noi_gen"][0], "i16", out["noi_i16"][0])
+
+
 def main():
     if sys.argv[1:] == ["tdec16"]:
         make_tdec16()
+        return
+    if sys.argv[1:] == ["sf20"]:
+        make_sf20()
         return
     L = O.lib()
     rng = np.random.default_rng(1)
@@ -107,6 +131,7 @@ def main():
                         payload=pay, noi=np.array([noi]),
                         cfg=np.array([cfg.cell_id, cfg.nof_prb, cfg.nof_ports, cfg.sf_idx, cfg.cfi, cfg.tbs, cfg.Qm]))
     make_tdec16()
+    make_sf20()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

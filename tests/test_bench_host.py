@@ -5,8 +5,10 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
@@ -68,3 +70,21 @@ def test_isolated_stages_only_for_overlapped_steps(monkeypatch):
     assert t["avg_launch_ms"] == 6.4 and t["launches_averaged"] == 10
     assert t["avg_launch_ms_overlapped"] == 19.3 and t["launches_averaged_overlapped"] == 200
     assert bench.roofline_timing({"tdec": 6.5}, 200, None) == {"avg_launch_ms": 6.5, "launches_averaged": 200}
+
+
+def test_hw_queues_argument():
+    """--hw-queues N and --hw-queues=N are both honoured, checked to 0..32 (gpurun refuses more than 32), and
+    importing bench (as the GPU tests do) leaves GPU_MAX_HW_QUEUES alone."""
+    import bench
+    assert bench.hw_queues_arg([]) == "8"
+    assert bench.hw_queues_arg(["--hw-queues", "16"]) == "16"
+    assert bench.hw_queues_arg(["--steps", "3", "--hw-queues=0"]) == "0"
+    for bad in (["--hw-queues", "33"], ["--hw-queues=-1"], ["--hw-queues=x"]):
+        with pytest.raises(SystemExit):
+            bench.hw_queues_arg(bad)
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([sys.executable, "-c", "import os, bench; print(os.environ.get('GPU_MAX_HW_QUEUES'))"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.stdout.strip() == "None", out.stdout + out.stderr

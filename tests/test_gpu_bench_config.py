@@ -195,7 +195,7 @@ def test_configs2_tm2_at_size_vs_oracle():
     CRC, TB and per-code-block iterations, payload; those LLRs are within 1e-4 of the oracle front end's."""
     n, pool = 1000, 40
     H = [0.8 + 0.3j, -0.4 + 0.5j]
-    snrs = [24.0 + 5.0 * j / (pool - 1) for j in range(pool)]   # TM2's waterfall through this channel: 24-28 dB
+    snrs = [24.0 + 5.0 * j / (pool - 1) for j in range(pool)]   # TM2's waterfall through this channel: 24-29 dB
     pcfgs = [abi.sf_cfg(nof_prb=100, nof_ports=2, tm=2, sf_idx=SF_CYCLE[j % 8], tbs=TBS, Qm=6, rnti=0x46)
              for j in range(pool)]
     tbs_pool = [tb_bytes(8000 + j, TBS) for j in range(pool)]

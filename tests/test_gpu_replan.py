@@ -21,7 +21,15 @@ def _gpu(built):
 
 
 def _config(cfgs, snr=30.0):
-    iq, tb = bench.make_pool(cfgs, snr, 8, 0)
+    """cfgs, their IQ laid out for a batch (in HBM) and their TBs; snr: one value, or one per subframe"""
+    if np.ndim(snr):
+        iq, tb = [], []
+        for i, c in enumerate(cfgs):
+            t = bench.tb_payload(i, c.tbs // 8)
+            iq.append(abi.tx_subframe(c, t, snr_db=float(snr[i]), seed=0xA5A5 + i))
+            tb.append(t)
+    else:
+        iq, tb = bench.make_pool(cfgs, snr, 8, 0)
     probe = abi.Batch(cfgs, compact_ce=True)
     flat = np.zeros(2 * probe.iq_samples, np.float32)
     for i, x in enumerate(iq):
@@ -63,4 +71,51 @@ def test_replan_matches_fresh_batches():
                 assert np.array_equal(w.payload(i, pay), tbs[i]), (name, i)
         assert crc.sum() >= len(cfgs) // 2, (name, int(crc.sum()))
     w.close()
+    p.close()
+
+
+def test_retransmission_after_replan():
+    """HARQ continuity across mi_dl_batch_replan (include/mi_dl.h): a retransmission (new_tb = 0, rv 2) combines with
+    the rows of its first transmission only when the softbuffer layout is the same; after a replan to a different
+    layout the softbuffer is cleared, so the retransmission decodes exactly as in a fresh batch (RX_NULL history) --
+    never against another plan's rows."""
+    n = 32
+    first = [abi.sf_cfg(nof_prb=100, sf_idx=bench.SF_CYCLE[i % 8], tbs=75376, Qm=6, rv=0) for i in range(n)]
+    retx = [abi.sf_cfg(nof_prb=100, sf_idx=bench.SF_CYCLE[i % 8], tbs=75376, Qm=6, rv=2, new_tb=0) for i in range(n)]
+    snrs = np.linspace(19.5, 23.0, n)         # through the waterfall: some TBs fail their first transmission
+    X0 = _config(first, snr=snrs)
+    X2 = (retx, _config(retx, snr=snrs)[1], X0[2])
+    Y = _config(bench.config_cfgs(5, 48, 0))  # another layout (mixed cells)
+    st = torch.cuda.current_stream().cuda_stream
+    # reference: the retransmission alone, from a cleared softbuffer
+    f = abi.Batch(retx, compact_ce=True)
+    f.run(X2[1].data_ptr(), st)
+    alone = _results(f)
+    f.close()
+    w = abi.Batch(first, compact_ce=True)
+    p = abi.Plan()
+    w.run(X0[1].data_ptr(), st)
+    crc0 = _results(w)[1]
+    assert 0 < crc0.sum() < n
+    # same layout: rv 0 + rv 2 combine -- at least every TB rv 0 or rv 2 alone decoded
+    p.build(retx)
+    w.replan(p, st)
+    w.run(X2[1].data_ptr(), st)
+    comb = _results(w)
+    assert comb[1].sum() >= max(crc0.sum(), alone[1].sum()) and comb[1].sum() > alone[1].sum()
+    # another layout in between: the retransmission then combines with nothing
+    w2 = abi.Batch(first, compact_ce=True)
+    w2.run(X0[1].data_ptr(), st)
+    for cfgs, d in ((Y[0], Y[1]), (retx, X2[1])):
+        p.build(cfgs)
+        w2.replan(p, st)
+        w2.run(d.data_ptr(), st)
+    got = _results(w2)
+    for a, b in zip(got, alone):
+        assert np.array_equal(a[:len(b)], b)
+    for i in range(n):
+        if got[1][i]:
+            assert np.array_equal(w2.payload(i, got[0]), X0[2][i])
+    for b in (w, w2):
+        b.close()
     p.close()

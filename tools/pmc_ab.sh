@@ -17,11 +17,11 @@ for v in "$@"; do
   mkdir -p $D
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 $R/bench.py $ARGS > $D/trace.log 2>&1 || exit 10
   i=0
-  GROUPS=("FETCH_SIZE" "WRITE_SIZE")
-  [ "${PMC_SET:-all}" = traffic ] || GROUPS+=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU" \
+  PASSES=("FETCH_SIZE" "WRITE_SIZE")
+  [ "${PMC_SET:-all}" = traffic ] || PASSES+=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU" \
              "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" \
              "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE")
-  for grp in "${GROUPS[@]}"; do
+  for grp in "${PASSES[@]}"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $D/pmc$i -o run -- python3 $R/bench.py $ARGS > $D/pmc$i.log 2>&1 || exit 1$i
   done

@@ -50,6 +50,9 @@ def main(root, prefixes):
             continue
         for k, ms, tr, ins, a, s, p, vb, w in build(d, prefixes):
             f = lambda x, n=1: "-" if x is None else f"{x:.{n}f}"   # noqa: E731
+            if w <= 1:   # no SQ pass (PMC_SET=traffic)
+                print(f"| {os.path.basename(d)} | {k} | {f(ms, 3)} | {f(tr and tr / 1e9, 2)} |" + " - |" * 11)
+                continue
             print(f"| {os.path.basename(d)} | {k} | {f(ms, 3)} | {f(tr and tr / 1e9, 2)} | {w:.0f} | {ins['VALU']:.0f} | "
                   f"{ins['SALU']:.0f} | {ins['VMEM_RD']:.0f} | {ins['VMEM_WR']:.0f} | {ins['LDS']:.0f} | {ins['SMEM']:.0f} | "
                   f"{a:.1f} | {s:.1f} | {p:.1f} | {f(vb)} |")
