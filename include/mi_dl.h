@@ -97,6 +97,12 @@ enum { MI_DL_BUF_GRID = 0, MI_DL_BUF_CE, MI_DL_BUF_LLR, MI_DL_BUF_PAYLOAD, MI_DL
  * A run whose stage mask includes DEMAP but not CHEST after a compact estimation fails (returns -1,
  * mi_dl_last_error says why) instead of reading rows that were never written. */
 #define MI_DL_FLAG_CE_COMPACT 1024u
+/* waterfall compaction (packed decoder, CRC early stop): the re-compaction rounds after the first decode each dense
+ * pair with 8 wavefronts, one per trellis segment, made exact by fix-up rounds instead of the crossed
+ * pair of wavefronts: a shorter chain for more wavefronts.  Results identical.  Pays when the batch runs alone (one
+ * stream, waterfall: +6 %); beside other streams' work the extra wavefronts cost more than the shorter chain saves
+ * (4 streams: -2 %), so it is off by default. */
+#define MI_DL_FLAG_TDEC_SEG  2048u
 
 typedef struct mi_dl_batch mi_dl_batch_t;
 

@@ -26,6 +26,7 @@ FLAG_TDEC_X = 128  # lane-per-code-block decoder, crossed schedule (two wavefron
 FLAG_TDEC_XR = 256  # crossed kernel, recompute form (5 waves per SIMD)
 FLAG_TDEC_P2 = 512   # two code blocks per lane (packed int16), crossed
 FLAG_CE_COMPACT = 1024  # compact channel estimates (4 pilot rows per port), interpolated in the fused demap
+FLAG_TDEC_SEG = 2048  # packed turbo waterfall: late rounds as exact 8-step segments (one stream faster, see mi_dl.h)
 SCHED_FLAGS = {None: 0, "auto": 0, "win": FLAG_TDEC_WIN, "lane": FLAG_TDEC_LANE, "lanex": FLAG_TDEC_LANE | FLAG_TDEC_X,
                "lanexr": FLAG_TDEC_LANE | FLAG_TDEC_X | FLAG_TDEC_XR, "p2": FLAG_TDEC_LANE | FLAG_TDEC_P2}
 FLAG_KEEP_LLR = 64  # keep the LLR stream of a full run (else demap is fused into rate de-matching)
@@ -197,12 +198,12 @@ class Batch:
     """Owns one mi_dl_batch_t (planned once; run() only enqueues kernels)."""
 
     def __init__(self, cfgs, max_its=4, profile=False, tdec_i16=True, iq_sc16=False, sched=None, keep_llr=False,
-                 compact_ce=False):
+                 compact_ce=False, seg_rounds=False):
         self.cfgs = list(cfgs)
         self._arr = cfg_array(self.cfgs)
         flags = (FLAG_PROFILE if profile else 0) | (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | \
             (FLAG_IQ_SC16 if iq_sc16 else 0) | SCHED_FLAGS[sched] | (FLAG_KEEP_LLR if keep_llr else 0) | \
-            (FLAG_CE_COMPACT if compact_ce else 0)
+            (FLAG_CE_COMPACT if compact_ce else 0) | (FLAG_TDEC_SEG if seg_rounds else 0)
         self.h = lib().mi_dl_batch_create(C.cast(self._arr, C.c_void_p), len(self.cfgs), max_its, flags)
         if not self.h:
             raise RuntimeError("mi_dl_batch_create: " + last_error())

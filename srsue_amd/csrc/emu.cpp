@@ -33,6 +33,8 @@ static uint64_t g_cont_cbs = 0;
 extern "C" void emu_set_tdec_compact(int on) { g_compact = on; g_cont_cbs = 0; }
 static int g_store_w = 0;   // compaction: the first launch stores its w rows, the continuation gathers them
 extern "C" void emu_set_tdec_store_w(int on) { g_store_w = on; }
+static int g_seg = 0;      // compaction rounds after the first: segmented, g_seg wavefronts per pair (tdec_kernel_p2s)
+extern "C" void emu_set_tdec_seg(int s) { g_seg = s; }
 static int g_rounds = 0;    // compaction: one iteration per round, the failing code blocks re-compacted between rounds
 static uint64_t g_round_cbs = 0;
 extern "C" void emu_set_tdec_rounds(int on) { g_rounds = on; g_round_cbs = 0; }
@@ -243,6 +245,7 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
             }
           }
         // iterations it0 .. it_end - 1 of every dense pair (tdec_kernel_p2c)
+        std::vector<uint32_t> segv((size_t)4 * 64 * mi::P2_CKW * mi::LANES);   // the segmented form's boundary vectors
         auto run_pairs = [&](std::vector<std::vector<uint32_t>>& pb, const std::vector<uint32_t>& list, uint32_t it0,
                              uint32_t it_end) {
           for (size_t p = 0; p < pb.size(); p++) {
@@ -269,9 +272,21 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               a.cont_w = it0 > 1 || g_store_w;
               a.it0 = it0; a.it_end = it_end;
               mi::TdecP2ExecHost ex;
-              // tdec.hip launch_tdec_cont: 4-step checkpoints in the rounds after the first
-              const mi::TdecP2Result r = it0 > 1 ? mi::tdec_p2_lane<true, mi::P2C_CKS_LATE>(a, lane, ex)
-                                                 : mi::tdec_p2_lane<true, mi::P2C_CKS>(a, lane, ex);
+              mi::TdecP2Result r{};
+              if (g_seg && it0 > 1) {
+                // tdec.hip tdec_kernel_p2s: the segments of one lane in turn, fix-up rounds until nothing changes
+                const size_t vw = (size_t)g_seg * mi::P2_CKW * mi::LANES;
+                mi::P2SegVecs V{&segv[0], &segv[vw], &segv[2 * vw], &segv[3 * vw]};
+                mi::p2s_half_host<false>(a, lane, (uint32_t)g_seg, V);
+                mi::p2s_half_host<true>(a, lane, (uint32_t)g_seg, V);
+                uint32_t tbp[2] = {0u, 0u};
+                const uint32_t ok = mi::tdec_p2_check(a, lane, a.live, tbp);
+                for (int h = 0; h < 2; h++) r.its[h] = it0 + 1, r.crc_ok[h] = (ok >> h) & 1u, r.tb_part[h] = tbp[h];
+              } else {
+                // tdec.hip launch_tdec_cont: 4-step checkpoints in the rounds after the first
+                r = it0 > 1 ? mi::tdec_p2_lane<true, mi::P2C_CKS_LATE>(a, lane, ex)
+                            : mi::tdec_p2_lane<true, mi::P2C_CKS>(a, lane, ex);
+              }
               for (int h = 0; h < 2; h++) {
                 if (!((a.live >> h) & 1u)) continue;
                 cits[li[h]] = r.its[h];

@@ -52,6 +52,7 @@ Engine::Engine() {
   opts.compact = env_int("MI_TDEC_COMPACT", -1);
   opts.store_w = env_int("MI_TDEC_STORE_W", -1);
   opts.rounds = env_int("MI_TDEC_ROUNDS", -1);
+  opts.seg = env_int("MI_TDEC_SEG", -1);
   opts.win_threads = (uint32_t)std::max(0, env_int("MI_TDEC_WIN_THREADS", 0));
   plan.rm_direct_on = env_int("MI_RM_DIRECT", 1) != 0;
   plan.xcd_queues = env_int("MI_RM_XCDQ", 1) != 0;
@@ -429,17 +430,18 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
     bool store_w = false;
     if (cont) {
       if (!h_cont) {
-        if (!hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h_cont), 4, hipHostMallocDefault), "pinned") ||
+        static_assert(sizeof(cont_last) / sizeof(cont_last[0]) == CONT_HIST, "one count per recorded round");
+        if (!hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h_cont), 4 * CONT_HIST, hipHostMallocDefault), "pinned") ||
             !hip_ok(hipEventCreateWithFlags(&cont_ev, hipEventDisableTiming), "event"))
           return false;
-        *h_cont = 0;
+        memset(h_cont, 0, 4 * CONT_HIST);
       }
       // the previous run's count, once its copy has landed (an event query, no wait); until then the last one read
       if (cont_pending && hipEventQuery(cont_ev) == hipSuccess) {
-        cont_last = *h_cont;
+        memcpy(cont_last, h_cont, sizeof(cont_last));
         cont_pending = false;
       }
-      store_w = opts.store_w >= 0 ? opts.store_w != 0 : (uint64_t)cont_last * 50 > P.lanes.size();
+      store_w = opts.store_w >= 0 ? opts.store_w != 0 : (uint64_t)cont_last[0] * 50 > P.lanes.size();
     }
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
@@ -459,7 +461,9 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
                        d_lanes.as<MiLaneDesc>(), d_kdata.as<uint32_t>(), P.ktabs[P.groups[0].ktab],
                        (uint32_t)P.groups.size(), d_cont.as<uint32_t>(), d_cscr.as<uint32_t>(), d_cdec.as<uint8_t>(),
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its, 2048,
-                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, cont_pending ? nullptr : h_cont, st))
+                       direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, cont_pending ? nullptr : h_cont,
+                       opts.seg == 4 || opts.seg == 8 ? (uint32_t)opts.seg
+                       : opts.seg < 0 && (flags & MI_DL_FLAG_TDEC_SEG) ? 8u : 0u, st))
         return false;
       // the copy of the count (skipped while an earlier one is still unread) is complete when cont_ev is
       if (!cont_pending) {

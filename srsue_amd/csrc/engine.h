@@ -39,8 +39,10 @@ struct Engine {
   //   MI_TDEC_X        turbo form (0 lane, 1 crossed, 2 crossed recompute, 3 packed pairs)
   //   MI_TDEC_COMPACT  0 = no waterfall compaction;  MI_TDEC_STORE_W / MI_TDEC_ROUNDS  0 / 1 = force
   //   MI_TDEC_WIN_THREADS  latency form: threads per code block;  MI_RM_DIRECT=0 / MI_RM_XCDQ=0 (Plan)
+  //   MI_TDEC_SEG=4/8  the waterfall's late rounds segmented over 4 / 8 wavefronts per pair (tdec_kernel_p2s)
+  //                    instead of the crossed form
   struct Opts {
-    int tdec_x = -1, compact = -1, store_w = -1, rounds = -1;
+    int tdec_x = -1, compact = -1, store_w = -1, rounds = -1, seg = -1;
     uint32_t win_threads = 0;
   } opts;
   Engine();
@@ -62,10 +64,11 @@ struct Engine {
   // compacted run) steers whether the first launch stores its extrinsic rows.  It is read only once cont_ev (recorded
   // after the copy) has completed -- never while the copy may be in flight -- and otherwise the last value read
   // (cont_last) is used: only the schedule depends on it, both forms are exact
+  // h_cont[r]: the code blocks continuation round r + 1 decoded (CONT_HIST words); cont_last: the last counts read
   uint32_t* h_cont = nullptr;
   hipEvent_t cont_ev = nullptr;
   bool cont_pending = false;
-  uint32_t cont_last = 0;
+  uint32_t cont_last[8] = {};
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,

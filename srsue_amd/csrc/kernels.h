@@ -62,8 +62,12 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
                       bool w_stored /* the first launch stored w rows: gather them (no DEC2 re-run) */,
                       bool rounds /* one iteration per launch, the failing code blocks re-compacted between them;
                                      cont holds 3 n_groups * 64 + 2 words, scratch / dec are reused as pair buffers */,
-                      uint32_t* h_count /* page-locked: the number of code blocks continuing after iteration 0 */,
+                      uint32_t* h_count /* page-locked [CONT_HIST]: the code blocks each round decodes (round 1:
+                                           those continuing after iteration 0) */,
+                      uint32_t seg /* 0, or the rounds after the first segmented over 4 / 8 wavefronts per pair
+                                      (tdec_kernel_p2s) */,
                       hipStream_t st);
+constexpr uint32_t CONT_HIST = 8;   // rounds whose counts are recorded (h_count)
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS
 void launch_tdec_win(const float* sb, uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp,

@@ -443,12 +443,104 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   }
 }
 
+// 3'. a re-compaction round after the first, segmented (tdec_p2_body.h p2s_*): one workgroup of S wavefronts per dense
+// pair, wavefront j owning trellis segment j of every pass; the boundaries are made exact by fix-up rounds (a
+// workgroup-wide OR decides whether another round runs).  One iteration (it0), w rows gathered (cont_w).
+// one constituent decoder of a segmented pair: first passes, then fix-up rounds until no boundary changes (every wave
+// joins every barrier; the neighbour's vector is read before the round's barrier, the fix-up writes after it)
+template <bool DEC2>
+__device__ __forceinline__ void p2s_half(const TdecArgsP2& a, int lane, uint32_t wave, const P2Seg& g, const P2SegVecs& V) {
+  const bool mine = wave < g.nseg;
+  if (mine) p2s_bwd_first<DEC2>(a, lane, g, V);
+  __syncthreads();
+  for (;;) {
+    P2 nb[8];
+    const bool act = mine && wave + 1 < g.nseg;
+    if (act) p2s_vld(V.bend, wave + 1, lane, nb);
+    __syncthreads();
+    const bool ch = act ? p2s_bwd_fix<DEC2>(a, lane, g, V, nb) : false;
+    if (!__syncthreads_or(ch)) break;
+  }
+  if (mine) p2s_fwd_first<DEC2>(a, lane, g, V);
+  __syncthreads();
+  for (;;) {
+    P2 na[8];
+    const bool act = mine && wave > 0;
+    if (act) p2s_vld(V.aend, wave - 1, lane, na);
+    __syncthreads();
+    const bool ch = act ? p2s_fwd_fix<DEC2>(a, lane, g, V, na) : false;
+    if (!__syncthreads_or(ch)) break;
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
+void tdec_kernel_p2s(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
+                     const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
+                     const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
+                     uint32_t it0) {
+  __shared__ uint32_t crc8[256], crc8b[256];
+  __shared__ uint32_t vecs[4][S * P2_CKW * LANES];
+  const uint32_t n = cont[0], p = blockIdx.x;
+  if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
+    crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
+    crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x % LANES;
+  const uint32_t wave = threadIdx.x / LANES;
+  const uint32_t d0 = p * 2 * LANES + lane, d1 = d0 + LANES;
+  TdecArgsP2 a{};
+  a.live = (d0 < n ? 1u : 0u) | (d1 < n ? 2u : 0u);   // dead halves decode zeros, consistently (no early exit: barriers)
+  const uint32_t li[2] = {d0 < n ? cont[1 + d0] : cont[1 + p * 2 * LANES],
+                          d1 < n ? cont[1 + d1] : (d0 < n ? cont[1 + d0] : cont[1 + p * 2 * LANES])};
+  const MiLaneDesc l0 = lanes[li[0]], l1 = lanes[li[1]];
+  a.scr = cscr + (size_t)p * pair_u32;
+  a.q = a.scr + (size_t)(4 * K + 8) * LANES;
+  a.pos = kdata + kt.pos_off;
+  a.pi = kdata + kt.pi_off;
+  a.crc8 = crc8;
+  a.crc8b = crc8b;
+  a.dec = cdec + (size_t)p * dec_stride;
+  p2_out(a, 0, out, li[0], l0);
+  p2_out(a, 1, out, li[1], l1);
+  a.to_payload = out.payload != nullptr;
+  a.K = K;
+  a.F[0] = l0.F;
+  a.F[1] = l1.F;
+  a.max_its = max_its;
+  a.early_stop = 1;
+  a.cont_w = 1;
+  a.it0 = it0;
+  a.it_end = it0 + 1;
+  // (built field by field: a const aggregate of LDS addresses becomes a static initializer the backend cannot emit)
+  P2SegVecs V;
+  V.bvec = vecs[0];
+  V.bend = vecs[1];
+  V.avec = vecs[2];
+  V.aend = vecs[3];
+  const P2Seg g = p2s_seg(K, S, wave);
+  p2s_half<false>(a, lane, wave, g, V);
+  p2s_half<true>(a, lane, wave, g, V);
+  if (wave || !a.live) return;   // wave 0: the check pass over the decision rows and the outputs
+  uint32_t tbp[2] = {0u, 0u};
+  const uint32_t ok = tdec_p2_check(a, lane, a.live, tbp);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (!((a.live >> h) & 1u)) continue;
+    out.its[li[h]] = it0 + 1;
+    out.crc_ok[li[h]] = (ok >> h) & 1u;
+    out.tb_part[li[h]] = tbp[h];
+  }
+}
+
 bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_t scr_pair_u32, uint8_t* dec,
                       uint8_t* cb_bytes, uint32_t* cb_its, uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups,
                       const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
                       uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,
                       uint32_t gather_wgs, uint8_t* payload, bool w_stored, bool rounds, uint32_t* h_count,
-                      hipStream_t st) {
+                      uint32_t seg, hipStream_t st) {
   if (!n_groups || !max_pairs) return true;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   const size_t nl = (size_t)n_groups * LANES + 1;   // one list: count + lane indices
@@ -482,10 +574,19 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
       hipLaunchKernelGGL(tdec_cont_gather2_kernel, dim3(gather_wgs), dim3(256), 0, st, bufs[b ^ 1], strides[b ^ 1],
                          lists[l], src, bufs[b], strides[b], K);
     }
-    if (it > 1)
+    // each round's count, for the next run's grids (h_count[it - 1]: the list this round decodes)
+    if (it > 1 && h_count && it <= CONT_HIST &&
+        hipMemcpyAsync(h_count + it - 1, lists[l], 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      return false;
+    if (it > 1 && seg == 8)   // the late rounds segmented: seg wavefronts per pair (tdec_kernel_p2s)
+      hipLaunchKernelGGL(tdec_kernel_p2s<8>, dim3(max_pairs), dim3(512), 0, st, bufs[b], decs[b], out, lanes, ktab_data,
+                         kt, lists[l], strides[b], dstrides[b], K, max_its, it);
+    else if (it > 1 && seg == 4)
+      hipLaunchKernelGGL(tdec_kernel_p2s<4>, dim3(max_pairs), dim3(256), 0, st, bufs[b], decs[b], out, lanes, ktab_data,
+                         kt, lists[l], strides[b], dstrides[b], K, max_its, it);
+    else if (it > 1)
       hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS_LATE>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes,
-                         ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, (uint32_t)(w_stored || it > 1),
-                         it, it + 1);
+                         ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, 1u, it, it + 1);
     else
       hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out,
                          lanes, ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its,

@@ -459,12 +459,25 @@ MI_HD inline void p2_alpha_run(P2 (&v)[8], const TdecX8P2& x) {
 }
 // wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1).
 // HAVE4: B(4) was computed on the way (a 16-step span's upper pair, TdecP2X::f2) and comes in B4in
-template <bool DEC2, bool HAVE4 = false>
+// FIRST_WIN (steps 0..7 from the start state; the segmented continuation, p2s_fwd): the LLRs of steps 0..2 leave the
+// unreachable alpha states out of their maxima (p2_beta_emit_window)
+template <int I, bool FIRST_WIN>
+MI_HD inline P2 p2_alpha_llr(P2 (&al)[8], const P2 (&bn)[8], P2 xs, P2 xp) {
+  if constexpr (FIRST_WIN && I < 3) {
+    constexpr uint32_t REACH = I == 0 ? 0x01u : I == 1 ? 0x11u : 0x55u;
+    const P2 llr = llr_step<REACH>(al, bn, xs, xp);
+    alpha_fwd<false>(al, xs, xp);
+    return llr;
+  } else {
+    return alpha_step<false>(al, bn, xs, xp);
+  }
+}
+template <bool DEC2, bool HAVE4 = false, bool FIRST_WIN = false>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
                                    P2 (&al)[8], const P2 (&B4in)[8] = P2_NO_VEC) {
   P2 B4[8], Bm[8], Bt[8];
 #define emit(I, BN) \
-  p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
+  p2_emit<DEC2>(a, lane, base, I, x.pk[I], p2_alpha_llr<I, FIRST_WIN>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
   if constexpr (HAVE4) {
     p2_cp8_opaque(B4, B4in);
   } else {
@@ -1143,6 +1156,202 @@ MI_HD inline uint32_t p2_cont_xrow(const P2ContSrc (&s)[2], uint32_t live, uint3
   for (int h = 0; h < 2; h++)
     w[h] = ((live >> h) & 1u) ? (s[h].scr[(size_t)(K + k) * LANES + s[h].ls] >> (16 * s[h].hs)) & 0xFFFFu : 0u;
   return w[0] | (w[1] << 16);
+}
+
+// ---- segmented continuation: the late re-compaction rounds of the waterfall (tdec.hip tdec_kernel_p2s) ----------
+// A round after the first holds a few dozen dense pairs (21.5 dB: 84, then 19), far under one wavefront per SIMD, and
+// each pair's iteration is a lone chain of 4 x K/2 dependent trellis steps per wavefront in the crossed schedule
+// (~3 ms whatever the pair count).  Here one dense pair is decoded by S wavefronts, wavefront j owning the trellis
+// segment [a, e) = [j L, min((j + 1) L, K)) (L a multiple of 8 steps) in BOTH recursions of both constituent
+// decoders -- a chain of 4 K / S steps -- and the segments are made exact exactly as the latency form's threads are
+// (tdec_win_body.h): in the int16 design a recursion started from a GUESSED normalised vector reproduces the true one
+// from the first step where the two coincide, so
+//   backward: every segment runs beta from a guess (the last one from the tail) and stores a checkpoint every 8 steps
+//     and its left-end vector; then fix-up rounds: a segment whose right neighbour's left-end vector differs from
+//     the vector it started from restarts from it and re-walks until a recomputed vector EQUALS the stored one (all
+//     lanes: the re-walk is wave-uniform) or its left end changes (the next round re-checks its left neighbour);
+//   forward: the same with alpha (the first segment from the start state), emitting the half-iteration's outputs
+//     (DEC1: x2 rows; DEC2: extrinsic rows and decision bytes) from alpha and the final betas; a fix-up re-emits
+//     exactly the steps whose alpha changed.
+// Rounds end when no boundary changed (a workgroup-wide OR).  Every value that survives is the full-length
+// recursion's, so the outputs equal tdec_p2_lane<true>'s (and the oracle's).  Checkpoints: beta at step 8c in slot c,
+// alpha at step 8c in slot K/8 + 1 + c of the pair's checkpoint region (interior steps of a segment only: both fit its
+// K/4 + 1 slots); the boundary vectors live in LDS (4 x [S][7][64] words): bvec[j] = the beta segment j started
+// from (at e), bend[j] = its beta at a; avec[j] / aend[j] = its alpha at a / at e.
+constexpr uint32_t P2S_SPAN = 2 * BETA_W;   // checkpoint spacing of both directions (steps)
+struct P2Seg { uint32_t j, nseg, a, e; };
+MI_HD inline P2Seg p2s_seg(uint32_t K, uint32_t S, uint32_t j) {
+  const uint32_t L = (K + P2S_SPAN * S - 1) / (P2S_SPAN * S) * P2S_SPAN;
+  P2Seg g;
+  g.j = j;
+  g.nseg = (K + L - 1) / L;
+  g.a = j * L < K ? j * L : K;
+  g.e = g.a + L < K ? g.a + L : K;
+  return g;
+}
+// wave-uniform: every lane's predicate (GPU: all active lanes; host: the one lane emulated)
+MI_HD inline bool p2_all(bool v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ballot_w64(!v) == 0;
+#else
+  return v;
+#endif
+}
+MI_HD inline bool p2_vec_eq(const P2 (&x)[8], const P2 (&y)[8]) {
+  bool eq = true;
+#pragma unroll
+  for (int s = 1; s < 8; s++) eq = eq && p2_bits(x[s]) == p2_bits(y[s]);   // state 0 is 0 in both
+  return eq;
+}
+// boundary vector j of an LDS array [S][7][64] (state 0 is 0)
+MI_HD inline void p2s_vst(uint32_t* v, uint32_t j, int lane, const P2 (&x)[8]) {
+#pragma unroll
+  for (int s = 1; s < 8; s++) p2_stash_st(v, j * P2_CKW + (uint32_t)(s - 1), lane, p2_bits(x[s]));
+}
+MI_HD inline void p2s_vld(const uint32_t* v, uint32_t j, int lane, P2 (&x)[8]) {
+  x[0] = Metric<P2>::zero();
+#pragma unroll
+  for (int s = 1; s < 8; s++) x[s] = p2_from_bits(p2_stash_ld(v, j * P2_CKW + (uint32_t)(s - 1), lane));
+}
+MI_HD inline void p2_zero8(P2 (&x)[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; s++) x[s] = Metric<P2>::zero();
+}
+struct P2SegVecs { uint32_t *bvec, *bend, *avec, *aend; };
+// the 8 steps 8c .. 8c + 7 of a continuation pass (q rows), converted
+template <bool DEC2>
+MI_P2_INL void p2s_load(const TdecArgsP2& a, int lane, uint32_t c, TdecX8P2& x) {
+  TdecWin8P2 r;
+  p2_load_window<DEC2, false, true>(a, lane, c * P2S_SPAN, r.lo);
+  p2_load_window<DEC2, false, true>(a, lane, c * P2S_SPAN + BETA_W, r.hi);
+  p2_cvt8<DEC2, true>(a, r, c * P2S_SPAN, x);
+}
+MI_HD inline void p2s_beta8(P2 (&b)[8], const TdecX8P2& x) {   // beta_{8c} from beta_{8c+8}, normalised per window
+  p2_beta_run<7, 4>(b, x);
+  norm8<true>(b);
+  p2_beta_run<3, 0>(b, x);
+  norm8<true>(b);
+}
+MI_HD inline void p2s_ck_get(const TdecArgsP2& a, uint32_t slot, int lane, P2 (&v)[8]) {
+  uint32_t ck[P2_CKW];
+  p2_ck_load_to(a.scr, (size_t)2 * a.K, slot, lane, ck);
+  p2_ck_vec(ck, v);
+}
+// backward: the first pass of segment g (from the tail or a zero guess)
+template <bool DEC2>
+MI_P2_INL void p2s_bwd_first(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V) {
+  P2 b[8];
+  if (g.j + 1 == g.nseg) {
+    // beta_K from the three tail steps (TdecP2X::b1, q rows)
+    const uint32_t t0 = 3 * a.K + (DEC2 ? 6 : 0);
+    p2_start(b);
+#pragma unroll
+    for (int j = 2; j >= 0; j--) {
+      P2 nb[8];
+      beta_step<false>(b, p2_from_bits(row_ld(a.q, t0, lane, 2 * j)), p2_from_bits(row_ld(a.q, t0, lane, 2 * j + 1)), nb);
+      p2_cp8(b, nb);
+    }
+    norm8<true>(b);
+  } else {
+    p2_zero8(b);
+  }
+  p2s_vst(V.bvec, g.j, lane, b);
+  for (uint32_t c = g.e / P2S_SPAN; c-- > g.a / P2S_SPAN;) {
+    TdecX8P2 x;
+    p2s_load<DEC2>(a, lane, c, x);
+    p2s_beta8(b, x);
+    if (c > g.a / P2S_SPAN) p2_ck_store(a.scr, (size_t)2 * a.K, c, lane, b);
+  }
+  p2s_vst(V.bend, g.j, lane, b);
+}
+// backward fix-up of segment g (g.j + 1 < g.nseg) from its right neighbour's left-end vector nb: true when its own
+// left-end vector changed
+template <bool DEC2>
+MI_P2_INL bool p2s_bwd_fix(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V, const P2 (&nb)[8]) {
+  P2 b[8];
+  p2s_vld(V.bvec, g.j, lane, b);
+  if (p2_all(p2_vec_eq(b, nb))) return false;
+  p2s_vst(V.bvec, g.j, lane, nb);
+  p2_cp8(b, nb);
+  for (uint32_t c = g.e / P2S_SPAN; c-- > g.a / P2S_SPAN;) {
+    TdecX8P2 x;
+    p2s_load<DEC2>(a, lane, c, x);
+    p2s_beta8(b, x);
+    P2 old[8];
+    const bool inner = c > g.a / P2S_SPAN;
+    if (inner) p2s_ck_get(a, c, lane, old);
+    else p2s_vld(V.bend, g.j, lane, old);
+    if (p2_all(p2_vec_eq(old, b))) return false;   // merged: every earlier vector of the segment is already exact
+    if (inner) p2_ck_store(a.scr, (size_t)2 * a.K, c, lane, b);
+    else p2s_vst(V.bend, g.j, lane, b);
+  }
+  return true;
+}
+// forward over the steps 8c .. 8c + 7 with the outputs: the closing beta from the checkpoint or the segment's bvec
+template <bool DEC2>
+MI_P2_INL void p2s_fwd8(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V, uint32_t c, P2 (&al)[8]) {
+  TdecX8P2 x;
+  p2s_load<DEC2>(a, lane, c, x);
+  P2 B8[8];
+  if (c + 1 < g.e / P2S_SPAN) p2s_ck_get(a, c + 1, lane, B8);
+  else p2s_vld(V.bvec, g.j, lane, B8);
+  if (c == 0) p2_alpha_window8<DEC2, false, true>(a, lane, x, B8, 0, al);
+  else p2_alpha_window8<DEC2>(a, lane, x, B8, c * P2S_SPAN, al);
+}
+template <bool DEC2>
+MI_P2_INL void p2s_fwd_first(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V) {
+  P2 al[8];
+  if (g.j == 0) p2_start(al);
+  else p2_zero8(al);
+  p2s_vst(V.avec, g.j, lane, al);
+  const uint32_t K8 = a.K / P2S_SPAN;
+  for (uint32_t c = g.a / P2S_SPAN; c < g.e / P2S_SPAN; c++) {
+    p2s_fwd8<DEC2>(a, lane, g, V, c, al);
+    if (c + 1 < g.e / P2S_SPAN) p2_ck_store(a.scr, (size_t)2 * a.K, K8 + 1 + c + 1, lane, al);
+  }
+  p2s_vst(V.aend, g.j, lane, al);
+}
+// forward fix-up of segment g (g.j > 0) from its left neighbour's right-end vector na: re-emits the steps whose alpha
+// changed; true when its own right-end vector changed
+template <bool DEC2>
+MI_P2_INL bool p2s_fwd_fix(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V, const P2 (&na)[8]) {
+  P2 al[8];
+  p2s_vld(V.avec, g.j, lane, al);
+  if (p2_all(p2_vec_eq(al, na))) return false;
+  p2s_vst(V.avec, g.j, lane, na);
+  p2_cp8(al, na);
+  const uint32_t K8 = a.K / P2S_SPAN;
+  for (uint32_t c = g.a / P2S_SPAN; c < g.e / P2S_SPAN; c++) {
+    p2s_fwd8<DEC2>(a, lane, g, V, c, al);
+    P2 old[8];
+    const bool inner = c + 1 < g.e / P2S_SPAN;
+    if (inner) p2s_ck_get(a, K8 + 1 + c + 1, lane, old);
+    else p2s_vld(V.aend, g.j, lane, old);
+    if (p2_all(p2_vec_eq(old, al))) return false;
+    if (inner) p2_ck_store(a.scr, (size_t)2 * a.K, K8 + 1 + c + 1, lane, al);
+    else p2s_vst(V.aend, g.j, lane, al);
+  }
+  return true;
+}
+// one constituent decoder of one lane on the host: the segments in turn, rounds until no boundary changes -- the
+// GPU kernel's schedule with its barriers (tdec.hip tdec_kernel_p2s), for the test emulation
+template <bool DEC2>
+inline void p2s_half_host(const TdecArgsP2& a, int lane, uint32_t S, const P2SegVecs& V) {
+  const uint32_t nseg = p2s_seg(a.K, S, 0).nseg;
+  for (uint32_t j = 0; j < nseg; j++) p2s_bwd_first<DEC2>(a, lane, p2s_seg(a.K, S, j), V);
+  for (bool ch = true; ch;) {
+    ch = false;
+    P2 nb[64][8];
+    for (uint32_t j = 0; j + 1 < nseg; j++) p2s_vld(V.bend, j + 1, lane, nb[j]);
+    for (uint32_t j = 0; j + 1 < nseg; j++) ch = p2s_bwd_fix<DEC2>(a, lane, p2s_seg(a.K, S, j), V, nb[j]) || ch;
+  }
+  for (uint32_t j = 0; j < nseg; j++) p2s_fwd_first<DEC2>(a, lane, p2s_seg(a.K, S, j), V);
+  for (bool ch = true; ch;) {
+    ch = false;
+    P2 na[64][8];
+    for (uint32_t j = 1; j < nseg; j++) p2s_vld(V.aend, j - 1, lane, na[j]);
+    for (uint32_t j = 1; j < nseg; j++) ch = p2s_fwd_fix<DEC2>(a, lane, p2s_seg(a.K, S, j), V, na[j]) || ch;
+  }
 }
 
 struct TdecP2ExecHost {

@@ -120,7 +120,7 @@ def test_emulated_segment_parallel_turbo_bit_exact(built, nprb, ports, tbs, qm, 
     assert np.array_equal(pe, opay)
 
 
-@pytest.mark.parametrize("compact", [False, True, "store_w", "rounds"])
+@pytest.mark.parametrize("compact", [False, True, "store_w", "rounds", "segments8", "segments3"])
 @pytest.mark.parametrize("snr0", [18.6, 30.0])
 def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     """The packed decoder (two code blocks per lane, tdec_p2_body.h) on a batch whose code blocks fill
@@ -133,7 +133,9 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     "store_w": the same with the first launch storing its extrinsic rows and the continuation gathering them
     instead of re-running iteration 0's DEC2 (engine.cpp: the waterfall's choice); "rounds": that, with one iteration
     per continuation round and the code blocks still failing re-compacted (in reverse slot order, new partners again)
-    between rounds (tdec.hip launch_tdec_cont)."""
+    between rounds (tdec.hip launch_tdec_cont); "segments<S>": those rounds after the first decoded by S trellis
+    segments per pair made exact by fix-up rounds (tdec_p2_body.h p2s_*, tdec.hip tdec_kernel_p2s; 3 segments: the
+    last one shorter)."""
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(11)]
     cfgs.append(abi.sf_cfg(cell_id=301, nof_prb=6, sf_idx=2, tbs=4392, Qm=6))
     snrs = [snr0 + 0.35 * (i % 5) for i in range(len(cfgs))]
@@ -152,7 +154,10 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     E.emu_set_tdec_x(3)
     E.emu_set_tdec_compact(int(bool(compact)))
     E.emu_set_tdec_store_w(int(compact in ("store_w", "rounds")))
-    E.emu_set_tdec_rounds(int(compact == "rounds"))
+    rounds = compact in ("rounds", "segments8", "segments3")
+    E.emu_set_tdec_store_w(int(compact in ("store_w",) or rounds))
+    E.emu_set_tdec_rounds(int(rounds))
+    E.emu_set_tdec_seg(int(compact[8:]) if isinstance(compact, str) and compact.startswith("segments") else 0)
     E.emu_round_codeblocks.restype = C.c_uint64
     E.emu_cont_codeblocks.restype = C.c_uint64
     try:
@@ -166,6 +171,7 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
         E.emu_set_tdec_compact(0)
         E.emu_set_tdec_store_w(0)
         E.emu_set_tdec_rounds(0)
+        E.emu_set_tdec_seg(0)
     assert rc == 0
     # lanes sorted by K (plan.cpp), each K's groups padded to 64 lanes: the 1.4 MHz code block is group 0
     lane = 64
@@ -181,7 +187,7 @@ def test_emulated_packed_pairs_bit_exact_vs_oracle(built, snr0, compact):
     if snr0 < 20:
         assert len(set(cbits[64:64 + 143].tolist())) >= 3   # code blocks of one lane stopped at different its
         assert not compact or n_cont > 20
-        assert compact != "rounds" or n_round > 0   # some code blocks went through a re-compaction
+        assert not rounds or n_round > 0   # some code blocks went through a re-compaction
 
 
 @pytest.mark.parametrize("base", [1, 2, 3])

@@ -45,12 +45,12 @@ def min_subframes_for_p2():
     return -(-simds * 64 // C)
 
 
-def run_bench_config(n, pool_iq, max_its=4):
+def run_bench_config(n, pool_iq, max_its=4, seg_rounds=False):
     """n subframes (subframe i carries pool entry i % pool, sf_idx cycling as the bench does) through the bench's
     batch flags; returns the batch after one run."""
     pool = len(pool_iq)
     cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=SF_CYCLE[i % 8], tbs=TBS, Qm=6, rnti=0x46) for i in range(n)]
-    b = abi.Batch(cfgs, max_its=max_its, tdec_i16=True, compact_ce=True)
+    b = abi.Batch(cfgs, max_its=max_its, tdec_i16=True, compact_ce=True, seg_rounds=seg_rounds)
     L = 2 * abi.lib().mi_sf_len(100)
     assert b.iq_offset(1) * 2 == L and b.iq_samples * 2 == n * L
     d_pool = torch.from_numpy(np.stack(pool_iq)).cuda()
@@ -160,7 +160,9 @@ def test_waterfall_compaction_matches_uncompacted(monkeypatch):
     blocks whose CRC failed gathered into dense continuation pairs for iterations 1..) against the packed
     decoder running every iteration in place (MI_TDEC_COMPACT=0): identical TB CRCs, TB and per-code-block
     iterations and payload on a 16-25 dB mix -- continuation partners differ between runs (slot order is
-    atomic), so this also checks that a lane's two halves never interact."""
+    atomic), so this also checks that a lane's two halves never interact.  The last two runs decode the rounds after
+    the first as exact trellis segments (tdec.hip tdec_kernel_p2s): 8 per pair through the batch flag
+    MI_DL_FLAG_TDEC_SEG, 4 per pair through MI_TDEC_SEG -- bit-identical too."""
     pool = 40
     n = -(-min_subframes_for_p2() // pool) * pool
     pcfgs = [abi.sf_cfg(nof_prb=100, sf_idx=SF_CYCLE[j % 8], tbs=TBS, Qm=6, rnti=0x46) for j in range(pool)]
@@ -170,17 +172,22 @@ def test_waterfall_compaction_matches_uncompacted(monkeypatch):
     # compacted with the first launch's extrinsic rows dropped (re-formed by the continuation), uncompacted,
     # compacted with them stored and gathered, and that with one iteration per round and the failing code blocks
     # re-compacted between rounds (engine.cpp: the waterfall's choice)
-    for compact, store_w, rounds in (("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
+    # re-compacted between rounds (engine.cpp: the waterfall's choice); then segmented late rounds (flag; env)
+    for compact, store_w, rounds, seg in (("1", "0", "0", None), ("0", "0", "0", None), ("1", "1", "0", None),
+                                          ("1", "1", "1", None), ("1", "1", "1", "flag"), ("1", "1", "1", "4")):
         monkeypatch.setenv("MI_TDEC_COMPACT", compact)
         monkeypatch.setenv("MI_TDEC_STORE_W", store_w)
         monkeypatch.setenv("MI_TDEC_ROUNDS", rounds)
-        b, _ = run_bench_config(n, iqs)
+        if seg not in (None, "flag"):
+            monkeypatch.setenv("MI_TDEC_SEG", seg)
+        b, _ = run_bench_config(n, iqs, seg_rounds=seg == "flag")
+        monkeypatch.delenv("MI_TDEC_SEG", raising=False)
         assert b.turbo_sched == "p2", b.turbo_sched
         outs.append([b.download(k, np.uint32 if k != abi.BUF_PAYLOAD else np.uint8)
                      for k in (abi.BUF_TB_CRC, abi.BUF_TB_ITS, abi.BUF_CB_ITS, abi.BUF_PAYLOAD)])
         b.close()
     for k, name in enumerate(("TB CRC", "TB its", "CB its", "payload")):
-        for o in (0, 2, 3):
+        for o in (0, 2, 3, 4, 5):
             assert np.array_equal(outs[o][k], outs[1][k]), (o, name)
     crc, cbits = outs[0][0], outs[0][2][:C * n]
     assert 0 < crc.sum() < n and set(np.unique(cbits).tolist()) >= {1, 2, 3, 4}
