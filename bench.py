@@ -17,6 +17,7 @@ events on the stream the kernels run on, averaged over the timed steps) and the 
 import argparse
 import concurrent.futures as cf
 import json
+import math
 import os
 import sys
 import time
@@ -683,11 +684,11 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     import collections
     S = max(1, args.streams)
     J = len(lists)
-    # one workspace per stream; static mode needs S a multiple of J so that each stream always runs one list
-    if not replan and S % J:
-        raise ValueError(f"replan_steps: static mode needs the streams ({S}) to be a multiple of the lists ({J})")
+    # re-planned: one workspace per stream.  Static: each workspace keeps one list, so there are lcm(S, J) of them,
+    # workspace k on stream k % S (one stream and two lists: two workspaces alternating on the one stream)
+    W = S if replan else S * J // math.gcd(S, J)
     batches = [abi.Batch(lists[k % J], max_its=args.max_its, profile=False, tdec_i16=args.tdec == "i16",
-                         sched=args.sched, compact_ce=True) for k in range(S)]
+                         sched=args.sched, compact_ce=True) for k in range(W)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     sptr = [st.cuda_stream for st in streams]
     D = max(1, threads)
@@ -702,10 +703,10 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
         queue.append((ex.submit(p.build, lists[j]), p, j))
 
     rep_t = [0.0, 0]
-    last_list = [None] * S
+    last_list = [None] * W
 
     def step(i):
-        b = batches[i % S]
+        b = batches[i % W]
         if replan:
             fut, p, j = queue.popleft()
             fut.result()
@@ -715,19 +716,19 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
             rep_t[1] += 1
             submit(p)            # the plan object now holds the previous data: rebuild it for a later step
         else:
-            j = i % S % J
-        b.run(iqs[j].data_ptr(), sptr[i % S])
-        last_list[i % S] = j
+            j = i % W % J
+        b.run(iqs[j].data_ptr(), sptr[i % W % S])
+        last_list[i % W] = j
     try:
         if replan:
             for p in plans:
                 submit(p)
-        for i in range(warmup * S):
+        for i in range(warmup * W):
             step(i)
         torch.cuda.synchronize(dev)
         rep_t[:] = [0.0, 0]
         t0 = time.perf_counter()
-        for i in range(warmup * S, warmup * S + steps):
+        for i in range(warmup * W, warmup * W + steps):
             step(i)
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
@@ -770,7 +771,7 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
         b.close()
     for p in plans:
         p.close()
-    nsteps_per_list = [sum(1 for i in range(warmup * S, warmup * S + steps) if (i % J if replan else i % S % J) == j)
+    nsteps_per_list = [sum(1 for i in range(warmup * W, warmup * W + steps) if (i % J if replan else i % W % J) == j)
                        for j in range(J)]
     total_bits = sum(bits[j] * nsteps_per_list[j] for j in range(J))
     return elapsed, total_bits, (rep_t[0] / max(1, rep_t[1])) * 1e3, bad, bits

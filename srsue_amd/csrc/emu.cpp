@@ -182,9 +182,9 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.cont_w = 0;
         a.no_w = a.max_its == 1 && !g_store_w;   // tdec.hip launch_tdec_p2
         mi::TdecP2ExecHost ex;
-        // the spacing tdec.hip launch_tdec_p2 picks: 16-step spans for a launch of several iterations
-        const mi::TdecP2Result r = a.max_its > 1 ? mi::tdec_p2_lane<false, mi::P2_CKS_ITER>(a, lane, ex)
-                                                 : mi::tdec_p2_lane<false, mi::P2_CKS>(a, lane, ex);
+        // the spacing of tdec.hip tdec_kernel_p2x: 16-step spans
+        const mi::TdecP2Result r = a.max_its == 1 ? mi::tdec_p2_lane<false, mi::P2_CKS, true>(a, lane, ex)
+                                                  : mi::tdec_p2_lane<false, mi::P2_CKS>(a, lane, ex);
         for (int h = 0; h < 2; h++) {
           if (!((a.live >> h) & 1u)) continue;
           cits[li[h]] = r.its[h];

@@ -181,8 +181,9 @@ struct TdecP2ExecGpu {
 
 // 3 waves per SIMD (<= 168 VGPRs): the headline's 1,270 pairs (2,540 wavefronts) resident in one round
 constexpr int P2_WAVES = 3;
-// CKS: checkpoint spacing (tdec_p2_body.h P2_CKS / P2_CKS_ITER); 16-step spans hold a wavefront's stash in LDS
-template <int CKS>
+// 16-step spans (tdec_p2_body.h P2_CKS) hold a wavefront's stash in LDS; ONE: a one-iteration launch, whose passes never
+// stash DEC1's a-priori rows (30 rows per wavefront instead of 38: room for the other streams' rate de-matching)
+template <bool ONE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
@@ -191,7 +192,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
                      uint32_t early_stop, uint32_t no_w) {
   __shared__ uint32_t crc8[256], crc8b[256];
   __shared__ uint32_t xs[LANES];
-  __shared__ uint32_t stash[2][(CKS == 16 ? P2_STASH_ROWS : 1) * LANES];
+  __shared__ uint32_t stash[2][(ONE ? P2_STASH_ROWS_FIRST : P2_STASH_ROWS) * LANES];
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
     crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
     crc8b[b] = crc24_byte_entry(b, CRC24B_POLY);
@@ -235,7 +236,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.no_w = no_w;   // a one-iteration first launch whose continuation re-forms the w rows (launch_tdec_p2)
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   a.stash = stash[ex.wave];
-  const TdecP2Result r = tdec_p2_lane<false, CKS>(a, lane, ex);
+  const TdecP2Result r = tdec_p2_lane<false, P2_CKS, ONE>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -253,13 +254,12 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
                     hipStream_t st) {
   if (!n_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
-  // several iterations per launch: 16-step spans; one (the compacted path's first launch, beside other streams' rate
-  // de-matching): 8-step checkpoints, whose workgroups need almost no LDS (tdec_p2_body.h P2_CKS_ITER)
+  // a one-iteration launch (the compacted path's first, beside other streams' rate de-matching): the smaller stash
   if (max_its > 1)
-    hipLaunchKernelGGL(tdec_kernel_p2x<P2_CKS_ITER>, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups,
+    hipLaunchKernelGGL(tdec_kernel_p2x<false>, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups,
                        lanes, ktabs, ktab_data, pairs, max_its, early_stop, 0u);
   else
-    hipLaunchKernelGGL(tdec_kernel_p2x<P2_CKS>, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups,
+    hipLaunchKernelGGL(tdec_kernel_p2x<true>, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups,
                        lanes, ktabs, ktab_data, pairs, max_its, early_stop, (uint32_t)no_w);
 }
 

@@ -585,14 +585,16 @@ MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const Tdec
 // softbuffer passes follow tdec_body.h.  The check pass keeps two decision-row chunks in flight (three: 38 VGPRs
 // spilled).
 constexpr int P2_PF_Q = 1, P2_PF_SB = TDEC_PF_SB, P2_PF_CHK = 2;
-// Checkpoint spacing (steps) of tdec_kernel_p2x, chosen per launch (tdec.hip launch_tdec_p2): 16-step spans (the LDS
-// stash below) when the launch runs several iterations, 8 for the one-iteration first launch of the compacted path.
-// Measured (round 5, profiles/r5/ab_ck16): 16-step spans cut the traffic of a headline launch from 22.8 to 19.5 GB
-// (2.00 -> 1.70 x algorithmic) and its isolated time by 1-2 %, but their 19 KB of LDS per workgroup leave room for
-// one co-resident rate de-matching workgroup per CU instead of three, and the 4-stream headline lost 2 % (rate
-// de-matching overlapped 11.9 -> 18.0 ms); configs[0] (8 iterations, no rate de-matching beside it) gains 9 %:
-// 16.1 -> 17.6 Gbps, one launch 31.3 -> 30.4 ms.  P2_CKS is the spacing of the host emulation (emu.cpp).
-constexpr int P2_CKS = 8, P2_CKS_ITER = 16;
+// Checkpoint spacing (steps) of tdec_kernel_p2x: 16-step spans (the LDS stash below) in every launch.  Measured (round 5,
+// profiles/r5/ab_ck16): 16-step spans cut the traffic of a headline launch from 22.8 to 19.5 GB (2.00 -> 1.70 x
+// algorithmic) and leave its isolated time as it was (the decoder follows its instruction stream); configs[0] (8
+// iterations) gains 9 %: 16.1 -> 17.6 Gbps.  Beside other streams' rate de-matching the stash's LDS matters: 38 rows per
+// wavefront (19 KB per workgroup) left one co-resident rate de-matching workgroup per CU instead of three (4-stream
+// headline -2 %); a one-iteration launch (the headline, the waterfall's first) never stashes DEC1's a-priori rows, and
+// at 30 rows (15 KB) the 4-stream headline is unchanged (112.6 vs 112.8 Gbps over four interleaved pairs) and the
+// waterfall gains 1 % (65.0 vs 64.4); without the quarter-point vector (23 rows, 12 KB) the 4 recomputed steps per
+// span cost more than the LDS saves (111.3-112.1 Gbps).
+constexpr int P2_CKS = 16;
 // The waterfall continuation (tdec_kernel_p2c) runs few wavefronts (0.74 per SIMD at the 21.5 dB bench point), each a
 // lone chain, so its spacing is a parameter of its own.  Its first round keeps 8-step checkpoints: 4-step ones (6
 // recursion steps per 8 instead of 12) shorten a lone chain (one stream, same box: waterfall tdec 21.95 -> 21.25 ms)
@@ -602,7 +604,7 @@ constexpr int P2_CKS = 8, P2_CKS_ITER = 16;
 // (profiles/r4/ab_ck_late: one stream waterfall tdec 18.58-18.61 -> 18.32 ms, headline unchanged).
 constexpr int P2C_CKS = 8, P2C_CKS_LATE = 4;
 
-// ---- 16-step checkpoint spacing (P2_CKS = 16) ------------------------------------------------------
+// ---- 16-step checkpoint spacing (CKS = 16) ------------------------------------------------------
 // Phase 1 stores a checkpoint every fourth window and phase 2 walks SPANS of four windows (two pairs) between them:
 // half the checkpoint bytes of the 8-step form (20 of the ~141 KB per code block and iteration at the headline).  A
 // span's midpoint vector -- the checkpoint the 8-step form would have loaded -- is recomputed on the way:
@@ -619,7 +621,10 @@ constexpr int P2C_CKS = 8, P2C_CKS_LATE = 4;
 // output is unchanged.  The quarter-point vector (B12 / A4) is normalised on the way to the midpoint and is the first
 // vector the pair processed last recomputes: it is stashed too (7 more rows), so the extra cost is 4 recursion steps
 // per 16 in phase 2 (28 + 16 instead of 24 + 16).
-constexpr uint32_t P2_STASH_X = 3 * 2 * BETA_W, P2_STASH_ROWS = P2_STASH_X + 2 * P2_CKW;
+// Stash rows: xs, xp (2 x 8), the span's checkpoint vector (7), the quarter-point vector (7), DEC1's a-priori w (8;
+// never in a one-iteration launch, whose passes are all FIRST: P2_STASH_ROWS_FIRST)
+constexpr uint32_t P2_STASH_V = 2 * 2 * BETA_W, P2_STASH_V4 = P2_STASH_V + P2_CKW, P2_STASH_W = P2_STASH_V4 + P2_CKW,
+                   P2_STASH_ROWS = P2_STASH_W + 2 * BETA_W, P2_STASH_ROWS_FIRST = P2_STASH_W;
 MI_HD inline void p2_stash_st(uint32_t* st, uint32_t row, int lane, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   ((__attribute__((address_space(3))) uint32_t*)st)[row * LANES + (uint32_t)lane] = v;   // ds_write_b32: LDS
@@ -642,12 +647,12 @@ MI_HD inline void p2_stash_put(uint32_t* st, int lane, const TdecX8P2& x, const 
   for (int i = 0; i < 2 * BETA_W; i++) {
     p2_stash_st(st, i, lane, p2_bits(x.xs[i]));
     p2_stash_st(st, 2 * BETA_W + i, lane, p2_bits(x.xp[i]));
-    if constexpr (!DEC2 && !FIRST) p2_stash_st(st, 4 * BETA_W + i, lane, p2_bits(x.w[i]));
+    if constexpr (!DEC2 && !FIRST) p2_stash_st(st, P2_STASH_W + i, lane, p2_bits(x.w[i]));
   }
 #pragma unroll
   for (int s = 1; s < 8; s++) {
-    p2_stash_st(st, P2_STASH_X + s - 1, lane, p2_bits(v[s]));
-    p2_stash_st(st, P2_STASH_X + P2_CKW + s - 1, lane, p2_bits(v4[s]));
+    p2_stash_st(st, P2_STASH_V + s - 1, lane, p2_bits(v[s]));
+    p2_stash_st(st, P2_STASH_V4 + s - 1, lane, p2_bits(v4[s]));
   }
 }
 // ... and take them back: DEC2's interleaver indices pi(k) (wave-uniform) come from the table again
@@ -659,13 +664,13 @@ MI_HD inline void p2_stash_get(const TdecArgsP2& a, const uint32_t* st, int lane
     x.xs[i] = p2_from_bits(p2_stash_ld(st, i, lane));
     x.xp[i] = p2_from_bits(p2_stash_ld(st, 2 * BETA_W + i, lane));
     if constexpr (DEC2) x.pk[i] = MI_PI(a, base + i);
-    else x.w[i] = FIRST ? Metric<P2>::zero() : p2_from_bits(p2_stash_ld(st, 4 * BETA_W + i, lane));
+    else x.w[i] = FIRST ? Metric<P2>::zero() : p2_from_bits(p2_stash_ld(st, P2_STASH_W + i, lane));
   }
   v[0] = v4[0] = Metric<P2>::zero();
 #pragma unroll
   for (int s = 1; s < 8; s++) {
-    v[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_X + s - 1, lane));
-    v4[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_X + P2_CKW + s - 1, lane));
+    v[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_V + s - 1, lane));
+    v4[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_V4 + s - 1, lane));
   }
 }
 MI_HD inline void p2_start(P2 (&v)[8]) {
@@ -1050,12 +1055,28 @@ MI_P2_INL uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, ui
 // iteration count) only the last iteration's pass runs.
 // CONT (waterfall compaction, tdec.hip): the code blocks continue from iteration 1 in a dense continuation
 // pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
-// CKS: the checkpoint spacing of every pass (the first launch: P2_CKS or P2_CKS_ITER; the continuation: P2C_CKS or
+// CKS: the checkpoint spacing of every pass (the first launch: P2_CKS; the continuation: P2C_CKS or
 // P2C_CKS_LATE, tdec.hip tdec_kernel_p2c)
-template <bool CONT = false, int CKS = P2_CKS, class Exec>
+// ONE: a launch of one iteration (a.max_its == 1; tdec.hip tdec_kernel_p2x<true>): only iteration 0's passes are built
+template <bool CONT = false, int CKS = P2_CKS, bool ONE = false, class Exec>
 MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
+  if constexpr (ONE && !CONT) {
+    static_assert(TDEC_MKQ_IT != 0, "the one-iteration form reads the softbuffer in both passes");
+    tdec_p2_xhalf<false, true, SRC_SB, CKS>(a, lane, ex);
+    tdec_p2_xhalf<true, true, SRC_SB, CKS>(a, lane, ex);
+    uint32_t ok = 0u;
+    if (ex.pack_wave()) ok = tdec_p2_check(a, lane, active, r.tb_part);
+    ok = ex.share(ok, lane);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (!((active >> h) & 1u)) continue;
+      r.its[h] = 1u;
+      r.crc_ok[h] = (ok >> h) & 1u;
+    }
+    return r;
+  }
   // CONT: iteration 0 ran with no_w (no extrinsic rows); its DEC2 pass is re-run here from the gathered q rows
   // and DEC1 outputs (x2 rows) -- the same integers as in iteration 0 -- to form the w rows iteration 1 reads
   if constexpr (CONT)

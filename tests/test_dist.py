@@ -153,3 +153,28 @@ def test_bench_two_ranks_on_one_gpu(built):
     devs = d["rank_devices"]
     assert [x["rank"] for x in devs] == [0, 1] and all(x["pci_bus_id"] and x["device"] for x in devs)
     assert len({x["pci_bus_id"] for x in devs}) == 1       # --share-gpu: one card
+
+
+@pytest.mark.gpu
+def test_bench_one_stream_full_line(built):
+    """`bench.py --streams 1` (serial, the profiling runs' setting) prints the whole line: the planning block's
+    static replay of two grant lists needs one workspace per list even on one stream (bench.py replan_steps), and
+    the PCIe-inclusive h2d block runs beside it.  A small shard keeps it short."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--sf-per-gpu", "256", "--steps", "4",
+                        "--warmup", "1", "--streams", "1", "--no-cpu-baseline", "--iterating-snr", "0",
+                        "--plan-steps", "4", "--h2d-steps", "2"],
+                       cwd=root, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["config"]["streams"] == 1 and d["crc_ok_rate"] == 1.0 and d["payload_mismatches_crc_ok"] == 0
+    pl = d["planning"]
+    for k in ("pipelined_default", "varied_static", "pipelined_varied"):
+        assert pl[k]["payload_mismatches_crc_ok"] == 0 and pl[k]["Mbps"] > 0, k
+    assert all(b > 0 for b in pl["varied_static"]["crc_ok_bits_per_list"])
+    assert set(d["h2d"]) >= {"sc16", "fc32"}
