@@ -180,7 +180,10 @@ int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
 int Engine::upload(hipStream_t st, bool alloc_sb) {
   // a plain plan.build() over an active memo entry overwrote that entry's (swapped-in) plan: drop the entry
   if (memo_active >= 0) {
-    (void)hipStreamSynchronize(st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      set_error("upload: an earlier launch on the stream failed");
+      return -1;
+    }
     memo.erase(memo.begin() + memo_active);
     memo_active = -1;
   }
@@ -213,7 +216,11 @@ int Engine::plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, h
       size_t lru = 0;
       for (size_t i = 1; i < memo.size(); i++)
         if (memo[i]->used < memo[lru]->used) lru = i;
-      (void)hipStreamSynchronize(st);   // its arena may still be read by this stream's kernels
+      // its arena may still be read by this stream's kernels
+      if (hipStreamSynchronize(st) != hipSuccess) {
+        set_error("plan memo: an earlier launch on the stream failed");
+        return -1;
+      }
       memo.erase(memo.begin() + (ptrdiff_t)lru);
     }
     memo.push_back(std::make_unique<PlanMemo>());

@@ -183,8 +183,11 @@ struct TdecP2ExecGpu {
 constexpr int P2_WAVES = 3;
 // 16-step spans (tdec_p2_body.h P2_CKS) hold a wavefront's stash in LDS; ONE: a one-iteration launch, whose passes never
 // stash DEC1's a-priori rows (30 rows per wavefront instead of 38: room for the other streams' rate de-matching)
+#ifndef P2X_ONE_WAVES
+#define P2X_ONE_WAVES P2_WAVES
+#endif
 template <bool ONE>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ONE ? P2X_ONE_WAVES : P2_WAVES)))
 void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,

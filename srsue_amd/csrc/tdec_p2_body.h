@@ -1063,7 +1063,6 @@ MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
   if constexpr (ONE && !CONT) {
-    static_assert(TDEC_MKQ_IT != 0, "the one-iteration form reads the softbuffer in both passes");
     tdec_p2_xhalf<false, true, SRC_SB, CKS>(a, lane, ex);
     tdec_p2_xhalf<true, true, SRC_SB, CKS>(a, lane, ex);
     uint32_t ok = 0u;
