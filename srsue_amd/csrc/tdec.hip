@@ -399,9 +399,9 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
                      uint32_t w_stored, uint32_t it0, uint32_t it_end) {
-  static_assert(CKS != 16, "the continuation has no LDS stash");
   __shared__ uint32_t crc8[256], crc8b[256];
   __shared__ uint32_t xs[LANES];
+  __shared__ uint32_t stash[2][(CKS == 16 ? P2_STASH_ROWS : 1) * LANES];   // 16-step spans (tdec_p2_body.h)
   const uint32_t n = cont[0], p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
@@ -435,6 +435,7 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.it0 = it0;
   a.it_end = it_end;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
+  a.stash = stash[ex.wave];
   const TdecP2Result r = tdec_p2_lane<true, CKS>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
