@@ -246,7 +246,6 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
           }
         // iterations it0 .. it_end - 1 of every dense pair (tdec_kernel_p2c)
         std::vector<uint32_t> segv((size_t)4 * 64 * mi::P2_CKW * mi::LANES);   // the segmented form's boundary vectors
-        std::vector<uint32_t> cstash((size_t)mi::P2_STASH_ROWS * mi::LANES);   // 16-step spans (tdec_kernel_p2c's LDS)
         auto run_pairs = [&](std::vector<std::vector<uint32_t>>& pb, const std::vector<uint32_t>& list, uint32_t it0,
                              uint32_t it_end) {
           for (size_t p = 0; p < pb.size(); p++) {
@@ -272,7 +271,6 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
               a.K = K; a.max_its = max_its; a.early_stop = 1;
               a.cont_w = it0 > 1 || g_store_w;
               a.it0 = it0; a.it_end = it_end;
-              a.stash = cstash.data();
               mi::TdecP2ExecHost ex;
               mi::TdecP2Result r{};
               if (g_seg && it0 > 1) {

@@ -183,11 +183,8 @@ struct TdecP2ExecGpu {
 constexpr int P2_WAVES = 3;
 // 16-step spans (tdec_p2_body.h P2_CKS) hold a wavefront's stash in LDS; ONE: a one-iteration launch, whose passes never
 // stash DEC1's a-priori rows (30 rows per wavefront instead of 38: room for the other streams' rate de-matching)
-#ifndef P2X_ONE_WAVES
-#define P2X_ONE_WAVES P2_WAVES
-#endif
 template <bool ONE>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ONE ? P2X_ONE_WAVES : P2_WAVES)))
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
                      const MiLaneDesc* __restrict__ lanes, const MiKTab* __restrict__ ktabs,
@@ -400,8 +397,8 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
                      uint32_t w_stored, uint32_t it0, uint32_t it_end) {
   __shared__ uint32_t crc8[256], crc8b[256];
+  static_assert(CKS != 16, "the continuation has no LDS stash (16-step spans measured slower here: profiles/r5/ab_misc)");
   __shared__ uint32_t xs[LANES];
-  __shared__ uint32_t stash[2][(CKS == 16 ? P2_STASH_ROWS : 1) * LANES];   // 16-step spans (tdec_p2_body.h)
   const uint32_t n = cont[0], p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
@@ -435,7 +432,6 @@ void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, Td
   a.it0 = it0;
   a.it_end = it_end;
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
-  a.stash = stash[ex.wave];
   const TdecP2Result r = tdec_p2_lane<true, CKS>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll

@@ -584,10 +584,7 @@ MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const Tdec
 // q-row passes keep one window of loads in flight (two: 17 VGPRs spilled at the 3-waves-per-SIMD budget); the
 // softbuffer passes follow tdec_body.h.  The check pass keeps two decision-row chunks in flight (three: 38 VGPRs
 // spilled).
-#ifndef P2_PF_SB_V
-#define P2_PF_SB_V TDEC_PF_SB
-#endif
-constexpr int P2_PF_Q = 1, P2_PF_SB = P2_PF_SB_V, P2_PF_CHK = 2;
+constexpr int P2_PF_Q = 1, P2_PF_SB = TDEC_PF_SB, P2_PF_CHK = 2;
 // Checkpoint spacing (steps) of tdec_kernel_p2x: 16-step spans (the LDS stash below) in every launch.  Measured (round 5,
 // profiles/r5/ab_ck16): 16-step spans cut the traffic of a headline launch from 22.8 to 19.5 GB (2.00 -> 1.70 x
 // algorithmic) and leave its isolated time as it was (the decoder follows its instruction stream); configs[0] (8
@@ -605,10 +602,7 @@ constexpr int P2_CKS = 16;
 // streams: 56.7-57.2 Gbps with 8-step checkpoints, 53.0-53.8 with 4-step ones; profiles/r4/ab_cont_ck).  The later
 // re-compaction rounds hold a few dozen pairs, far below the HBM rate, and take 4-step checkpoints
 // (profiles/r4/ab_ck_late: one stream waterfall tdec 18.58-18.61 -> 18.32 ms, headline unchanged).
-#ifndef P2C_CKS_V
-#define P2C_CKS_V 8
-#endif
-constexpr int P2C_CKS = P2C_CKS_V, P2C_CKS_LATE = 4;
+constexpr int P2C_CKS = 8, P2C_CKS_LATE = 4;
 
 // ---- 16-step checkpoint spacing (CKS = 16) ------------------------------------------------------
 // Phase 1 stores a checkpoint every fourth window and phase 2 walks SPANS of four windows (two pairs) between them:
