@@ -80,3 +80,26 @@ def test_latency_form_thread_counts(built, threads, monkeypatch):
         dec, oits, ook = td.decode_cb(llr[i], K, max_its=6, early_stop=True)
         assert its[i] == oits and bool(ok[i]) == bool(ook), f"cb {i}"
         assert np.array_equal(got[i], dec), f"cb {i}"
+
+
+@pytest.mark.parametrize("n", [70, 150])
+@pytest.mark.parametrize("K,ebno", [(6144, 0.8), (512, 1.5)])
+def test_packed_one_iteration_launch(built, n, K, ebno):
+    """The one-iteration packed launch (tdec.hip tdec_kernel_p2x<true>: iteration 0 only, the 30-row LDS stash of the
+    16-step spans) is what the headline and the waterfall's first launch run; here on its own through the raw
+    code-block contract (max_its 1): decisions, CRC verdicts and iteration counts equal the oracle's int16 decoder
+    for a partial second group (70 code blocks: one pair) and an unpaired third group (150: two pairs, the second
+    with no high half)."""
+    rng = np.random.default_rng(K + n)
+    bits = rng.integers(0, 2, (n, K)).astype(np.uint8)
+    llr = np.stack([llr_bpsk(abi.turbo_encode(b, K), K, ebno, rng) for b in bits])
+    llr *= np.float32(rng.uniform(0.5, 8.0))
+    tb = abi.TdecBatch(K, n, max_its=1, early_stop=True, tdec_i16=True, sched="p2")
+    d = torch.from_numpy(llr).cuda()
+    tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got, its, ok = tb.results()
+    td = O.Tdec(O.TDEC_I16)
+    for i in range(n):
+        dec, oits, ook = td.decode_cb(llr[i], K, max_its=1, early_stop=True)
+        assert its[i] == oits == 1 and bool(ok[i]) == bool(ook), f"cb {i}"
+        assert np.array_equal(got[i], dec), f"cb {i}"
