@@ -457,6 +457,43 @@ MI_HD inline void p2_alpha_run(P2 (&v)[8], const TdecX8P2& x) {
 #pragma unroll
   for (int i = LO; i <= HI; i++) alpha_fwd<false>(v, x.xs[i], x.xp[i]);
 }
+MI_HD inline void p2_opaque8(P2 (&d)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+  for (int k = 0; k < 8; k++) asm volatile("" : "+v"(d[k].v));
+#endif
+}
+// a recomputation chain that starts from vector s.  DIRECT: its first step reads s itself (no copy) and an empty asm on
+// that step's result keeps GVN from merging the rest of the chain with another one -- at most one chain per source
+// vector starts this way (the others from an opaque copy), so no two chains compute the same first step; 8 v_mov less
+// per chain, but the copies also anchor the scheduler, and without them the kernels whose registers are full spill
+// (the one-iteration kernel takes DIRECT: -64 v_mov per 16-step span, 149 -> 168 VGPRs, no spill in its loops;
+// same box: its launch 6.13 -> 6.01 ms, 4-stream headline +1.7 %, profiles/r5/ab_direct)
+template <int HI, int LO, bool DIRECT>
+MI_HD inline void p2_beta_run_from(P2 (&v)[8], const P2 (&s)[8], const TdecX8P2& x) {
+  if constexpr (DIRECT) {
+    P2 nb[8];
+    beta_step<false>(s, x.xs[HI], x.xp[HI], nb);
+    p2_cp8(v, nb);
+    p2_opaque8(v);
+    if constexpr (HI > LO) p2_beta_run<HI - 1, LO>(v, x);
+  } else {
+    p2_cp8_opaque(v, s);
+    p2_beta_run<HI, LO>(v, x);
+  }
+}
+template <int LO, int HI, bool DIRECT>
+MI_HD inline void p2_alpha_run_from(P2 (&v)[8], const P2 (&s)[8], const TdecX8P2& x) {
+  if constexpr (DIRECT) {
+    p2_cp8(v, s);
+    alpha_fwd<false>(v, x.xs[LO], x.xp[LO]);
+    p2_opaque8(v);
+    if constexpr (HI > LO) p2_alpha_run<LO + 1, HI>(v, x);
+  } else {
+    p2_cp8_opaque(v, s);
+    p2_alpha_run<LO, HI>(v, x);
+  }
+}
 // wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1).
 // HAVE4: B(4) was computed on the way (a 16-step span's upper pair, TdecP2X::f2) and comes in B4in
 // FIRST_WIN (steps 0..7 from the start state; the segmented continuation, p2s_fwd): the LLRs of steps 0..2 leave the
@@ -472,38 +509,40 @@ MI_HD inline P2 p2_alpha_llr(P2 (&al)[8], const P2 (&bn)[8], P2 xs, P2 xp) {
     return alpha_step<false>(al, bn, xs, xp);
   }
 }
-template <bool DEC2, bool HAVE4 = false, bool FIRST_WIN = false>
+template <bool DEC2, bool HAVE4 = false, bool FIRST_WIN = false, bool DIRECT = false>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
                                    P2 (&al)[8], const P2 (&B4in)[8] = P2_NO_VEC) {
   P2 B4[8], Bm[8], Bt[8];
 #define emit(I, BN) \
   p2_emit<DEC2>(a, lane, base, I, x.pk[I], p2_alpha_llr<I, FIRST_WIN>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
+  // chains from B8: B(4) (without HAVE4) directly, B(6) and B(7) from copies; from B(4): B(3) directly, B(2) from a
+  // copy; B(1) and B(5) directly from B(2) and B(6)
   if constexpr (HAVE4) {
-    p2_cp8_opaque(B4, B4in);
+    p2_cp8_opaque(B4, B4in);   // (opaque: also anchors the scheduler -- a plain copy costs 5 VGPRs here)
   } else {
-    p2_cp8_opaque(B4, B8);
-    p2_beta_run<7, 4>(B4, x);
+    p2_beta_run_from<7, 4, DIRECT>(B4, B8, x);
     norm8<true>(B4);
   }
   p2_cp8_opaque(Bm, B4);
   p2_beta_run<3, 2>(Bm, x);   // B(2)
-  p2_cp8_opaque(Bt, Bm);
-  p2_beta_run<1, 1>(Bt, x);   // B(1)
+  p2_beta_run_from<1, 1, DIRECT>(Bt, Bm, x);   // B(1)
   MI_SCHED_FENCE();
   emit(0, Bt);
   MI_SCHED_FENCE();
   emit(1, Bm);
-  p2_cp8_opaque(Bt, B4);
-  p2_beta_run<3, 3>(Bt, x);   // B(3)
+  p2_beta_run_from<3, 3, DIRECT>(Bt, B4, x);   // B(3)
   MI_SCHED_FENCE();
   emit(2, Bt);
   MI_SCHED_FENCE();
   emit(3, B4);
   norm8<true>(al);
-  p2_cp8_opaque(Bm, B8);
-  p2_beta_run<7, 6>(Bm, x);   // B(6)
-  p2_cp8_opaque(Bt, Bm);
-  p2_beta_run<5, 5>(Bt, x);   // B(5)
+  if constexpr (HAVE4) {
+    p2_beta_run_from<7, 6, DIRECT>(Bm, B8, x);   // B(6): B8's only direct chain here
+  } else {
+    p2_cp8_opaque(Bm, B8);
+    p2_beta_run<7, 6>(Bm, x);   // B(6)
+  }
+  p2_beta_run_from<5, 5, DIRECT>(Bt, Bm, x);   // B(5)
   MI_SCHED_FENCE();
   emit(4, Bt);
   MI_SCHED_FENCE();
@@ -535,37 +574,39 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
 // wave B, phase 2, one pair: A(j) = alpha_{base + j}, A(0) = the checkpoint (pair 0: the start state);
 // LLR i from A(i) and beta_{base + i + 1} (the running b).  HAVE4: A(4) was computed on the way (a 16-step span's lower
 // pair, TdecP2X::b2) and comes in A4in
-template <bool DEC2, bool FIRST_WIN, bool HAVE4 = false>
+template <bool DEC2, bool FIRST_WIN, bool HAVE4 = false, bool DIRECT = false>
 MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
                                        uint32_t base, P2 (&b)[8], const P2 (&A4in)[8] = P2_NO_VEC) {
   P2 A4[8], Am[8], At[8];
 #define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b)
+  // the mirror of p2_alpha_window8: from A0, A(4) (without HAVE4) directly, A(2) and A(1) from copies; from A(4), A(5)
+  // directly, A(6) from a copy; A(7) and A(3) directly from A(6) and A(2)
   if constexpr (HAVE4) {
-    p2_cp8_opaque(A4, A4in);
+    p2_cp8_opaque(A4, A4in);   // (opaque: also anchors the scheduler -- a plain copy costs 5 VGPRs here)
   } else {
-    p2_cp8_opaque(A4, A0);
-    p2_alpha_run<0, 3>(A4, x);
+    p2_alpha_run_from<0, 3, DIRECT>(A4, A0, x);
     norm8<true>(A4);
   }
   p2_cp8_opaque(Am, A4);
   p2_alpha_run<4, 5>(Am, x);   // A(6)
-  p2_cp8_opaque(At, Am);
-  p2_alpha_run<6, 6>(At, x);   // A(7)
+  p2_alpha_run_from<6, 6, DIRECT>(At, Am, x);   // A(7)
   MI_SCHED_FENCE();
   emit(7, At);
   MI_SCHED_FENCE();
   emit(6, Am);
-  p2_cp8_opaque(At, A4);
-  p2_alpha_run<4, 4>(At, x);   // A(5)
+  p2_alpha_run_from<4, 4, DIRECT>(At, A4, x);   // A(5)
   MI_SCHED_FENCE();
   emit(5, At);
   MI_SCHED_FENCE();
   emit(4, A4);
   norm8<true>(b);
-  p2_cp8_opaque(Am, A0);
-  p2_alpha_run<0, 1>(Am, x);   // A(2)
-  p2_cp8_opaque(At, Am);
-  p2_alpha_run<2, 2>(At, x);   // A(3)
+  if constexpr (HAVE4) {
+    p2_alpha_run_from<0, 1, DIRECT>(Am, A0, x);   // A(2): A0's only direct chain here
+  } else {
+    p2_cp8_opaque(Am, A0);
+    p2_alpha_run<0, 1>(Am, x);   // A(2)
+  }
+  p2_alpha_run_from<2, 2, DIRECT>(At, Am, x);   // A(3)
   MI_SCHED_FENCE();
   emit(3, At);
   MI_SCHED_FENCE();
@@ -681,7 +722,7 @@ MI_HD inline void p2_start(P2 (&v)[8]) {
 // the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
 // CKS: checkpoint spacing in steps (4, 8 or 16); PFQ: windows of q-row loads in flight.  The first launch takes
 // P2_CKS / P2_PF_Q, the waterfall continuation its own (tdec_p2_lane)
-template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q>
+template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q, bool DIRECT = false>
 struct TdecP2X {
   static constexpr bool MKQ = !DEC2 && SRC == SRC_MKQ;
   static constexpr bool SQB = SRC == SRC_Q;    // backward-side passes read q rows
@@ -748,8 +789,7 @@ struct TdecP2X {
           MI_SCHED_FENCE();
           load8(a, lane, w0, 0, false, r);   // the lower pair
           MI_SCHED_FENCE();
-          p2_cp8_opaque(B8, B16);
-          p2_beta_run<7, 4>(B8, x);
+          p2_beta_run_from<7, 4, true>(B8, B16, x);   // B16's only chain in registers (the stash keeps B16)
           norm8<true>(B8);   // B12: the upper pair's "B(4)", stashed with its inputs
           p2_stash_put<DEC2, FIRST>(a.stash, lane, x, B16, B8);
           p2_beta_run<3, 0>(B8, x);
@@ -760,10 +800,10 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < ns ? w0 + 6 : w0 + 2;   // the last span reloads its upper pair (unused)
           load8(a, lane, wn, wn + 2, true, r);
           MI_SCHED_FENCE();
-          p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
+          p2_alpha_window8<DEC2, false, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
           MI_SCHED_FENCE();
           p2_stash_get<DEC2, FIRST>(a, a.stash, lane, (w0 + 2) * BETA_W, x, B16, B8);
-          p2_alpha_window8<DEC2, true>(a, lane, x, B16, (w0 + 2) * BETA_W, al, B8);
+          p2_alpha_window8<DEC2, true, false, DIRECT>(a, lane, x, B16, (w0 + 2) * BETA_W, al, B8);
         }
       }
       // pairs (w1 + 2j, w1 + 2j + 1), beta checkpoint w1 + 2j + 2; an odd count leaves window nw - 1 alone
@@ -781,7 +821,7 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < np ? w0 + 2 : w0;   // the last pair reloads itself (unused)
           load8(a, lane, wn, wn + 2, true, r);
           MI_SCHED_FENCE();
-          p2_alpha_window8<DEC2>(a, lane, x, B8, w0 * BETA_W, al);
+          p2_alpha_window8<DEC2, false, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
         }
       }
       if (n & 1u) {
@@ -873,8 +913,7 @@ struct TdecP2X {
           MI_SCHED_FENCE();
           load8(a, lane, w0 + 2, 0, false, r);   // the upper pair
           MI_SCHED_FENCE();
-          p2_cp8_opaque(A8, A0);
-          p2_alpha_run<0, 3>(A8, x);
+          p2_alpha_run_from<0, 3, true>(A8, A0, x);   // A0's only chain in registers (the stash keeps A0)
           norm8<true>(A8);   // A4: the lower pair's "A(4)", stashed with its inputs
           p2_stash_put<DEC2, FIRST>(a.stash, lane, x, A0, A8);
           p2_alpha_run<4, 7>(A8, x);
@@ -885,11 +924,11 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < ns ? w0 - 4 : w0;   // the last span reloads its lower pair (unused)
           load8(a, lane, wn, wn, true, r);
           MI_SCHED_FENCE();
-          p2_beta_emit_window8<DEC2, false>(a, lane, x, A8, (w0 + 2) * BETA_W, b);
+          p2_beta_emit_window8<DEC2, false, false, DIRECT>(a, lane, x, A8, (w0 + 2) * BETA_W, b);
           MI_SCHED_FENCE();
           p2_stash_get<DEC2, FIRST>(a, a.stash, lane, w0 * BETA_W, x, A0, A8);
-          if (w0) p2_beta_emit_window8<DEC2, false, true>(a, lane, x, A0, w0 * BETA_W, b, A8);
-          else p2_beta_emit_window8<DEC2, true, true>(a, lane, x, A0, 0, b, A8);
+          if (w0) p2_beta_emit_window8<DEC2, false, true, DIRECT>(a, lane, x, A0, w0 * BETA_W, b, A8);
+          else p2_beta_emit_window8<DEC2, true, true, DIRECT>(a, lane, x, A0, 0, b, A8);
         }
       }
       // pairs (wlo - 2j - 2, wlo - 2j - 1), alpha checkpoint wlo - 2j - 2 (0: the start state); an odd wlo leaves
@@ -909,8 +948,8 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < np ? w0 - 2 : w0;   // the last pair reloads itself (unused)
           load8(a, lane, wn, wn, true, r);
           MI_SCHED_FENCE();
-          if (w0) p2_beta_emit_window8<DEC2, false>(a, lane, x, A0, w0 * BETA_W, b);
-          else p2_beta_emit_window8<DEC2, true>(a, lane, x, A0, 0, b);
+          if (w0) p2_beta_emit_window8<DEC2, false, false, DIRECT>(a, lane, x, A0, w0 * BETA_W, b);
+          else p2_beta_emit_window8<DEC2, true, false, DIRECT>(a, lane, x, A0, 0, b);
         }
       }
       if (wlo & 1u) {
@@ -933,9 +972,9 @@ struct TdecP2X {
   }
 };
 
-template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q, class Exec>
+template <bool DEC2, bool FIRST, int SRC, int CKS = P2_CKS, int PFQ = P2_PF_Q, bool DIRECT = false, class Exec>
 MI_P2_INL void tdec_p2_xhalf(const TdecArgsP2& a, int lane, Exec& ex) {
-  using X = TdecP2X<DEC2, FIRST, SRC, CKS, PFQ>;
+  using X = TdecP2X<DEC2, FIRST, SRC, CKS, PFQ, DIRECT>;
   P2 mF[8], mBs[8];
   P2(&mB)[8] = Exec::SHARED ? mF : mBs;   // GPU: each wave holds only its own metric
   ex.run([&] { X::f1(a, lane, mF); }, [&] { X::b1(a, lane, mB); });
@@ -1063,8 +1102,8 @@ MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
   if constexpr (ONE && !CONT) {
-    tdec_p2_xhalf<false, true, SRC_SB, CKS>(a, lane, ex);
-    tdec_p2_xhalf<true, true, SRC_SB, CKS>(a, lane, ex);
+    tdec_p2_xhalf<false, true, SRC_SB, CKS, P2_PF_Q, true>(a, lane, ex);   // direct recomputation chains
+    tdec_p2_xhalf<true, true, SRC_SB, CKS, P2_PF_Q, true>(a, lane, ex);
     uint32_t ok = 0u;
     if (ex.pack_wave()) ok = tdec_p2_check(a, lane, active, r.tb_part);
     ok = ex.share(ok, lane);
