@@ -183,8 +183,9 @@ extern "C" int emu_decode_llr(const mi_dl_sf_cfg_t* cfgs, uint32_t n, const floa
         a.no_w = a.max_its == 1 && !g_store_w;   // tdec.hip launch_tdec_p2
         mi::TdecP2ExecHost ex;
         // the spacing of tdec.hip tdec_kernel_p2x: 16-step spans
-        const mi::TdecP2Result r = a.max_its == 1 ? mi::tdec_p2_lane<false, mi::P2_CKS, true>(a, lane, ex)
-                                                  : mi::tdec_p2_lane<false, mi::P2_CKS>(a, lane, ex);
+        const mi::TdecP2Result r = a.max_its == 1  ? mi::tdec_p2_lane<false, mi::P2_CKS, true>(a, lane, ex)
+                                   : !a.early_stop ? mi::tdec_p2_lane<false, mi::P2_CKS, false, 0u>(a, lane, ex)
+                                                   : mi::tdec_p2_lane<false, mi::P2_CKS>(a, lane, ex);
         for (int h = 0; h < 2; h++) {
           if (!((a.live >> h) & 1u)) continue;
           cits[li[h]] = r.its[h];

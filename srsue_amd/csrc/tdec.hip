@@ -183,7 +183,8 @@ struct TdecP2ExecGpu {
 constexpr int P2_WAVES = 3;
 // 16-step spans (tdec_p2_body.h P2_CKS) hold a wavefront's stash in LDS; ONE: a one-iteration launch, whose passes never
 // stash DEC1's a-priori rows (30 rows per wavefront instead of 38: room for the other streams' rate de-matching)
-template <bool ONE>
+// FIXED: several iterations without early stop (configs[0]): the q rows are created in iteration 0
+template <bool ONE, bool FIXED = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ wm, float* __restrict__ scratch,
                      uint8_t* __restrict__ dec, TdecOut out, const MiGroupDesc* __restrict__ groups,
@@ -236,7 +237,7 @@ void tdec_kernel_p2x(const float* __restrict__ sb, const uint32_t* __restrict__ 
   a.no_w = no_w;   // a one-iteration first launch whose continuation re-forms the w rows (launch_tdec_p2)
   TdecP2ExecGpu ex{(int)(threadIdx.x / LANES), xs};
   a.stash = stash[ex.wave];
-  const TdecP2Result r = tdec_p2_lane<false, P2_CKS, ONE>(a, lane, ex);
+  const TdecP2Result r = tdec_p2_lane<false, P2_CKS, ONE, FIXED ? 0u : TDEC_MKQ_IT>(a, lane, ex);
   if (ex.wave) return;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -255,7 +256,10 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
   if (!n_pairs) return;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   // a one-iteration launch (the compacted path's first, beside other streams' rate de-matching): the smaller stash
-  if (max_its > 1)
+  if (max_its > 1 && !early_stop)
+    hipLaunchKernelGGL((tdec_kernel_p2x<false, true>), dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out,
+                       groups, lanes, ktabs, ktab_data, pairs, max_its, early_stop, 0u);
+  else if (max_its > 1)
     hipLaunchKernelGGL(tdec_kernel_p2x<false>, dim3(n_pairs), dim3(128), 0, st, sb, wm, scratch, dec, out, groups,
                        lanes, ktabs, ktab_data, pairs, max_its, early_stop, 0u);
   else

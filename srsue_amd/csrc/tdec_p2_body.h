@@ -1096,8 +1096,11 @@ MI_P2_INL uint32_t tdec_p2_check(const TdecArgsP2& a, int lane, uint32_t act, ui
 // pair whose q rows and extrinsic rows were gathered after iteration 0 -- every pass reads q rows.
 // CKS: the checkpoint spacing of every pass (the first launch: P2_CKS; the continuation: P2C_CKS or
 // P2C_CKS_LATE, tdec.hip tdec_kernel_p2c)
-// ONE: a launch of one iteration (a.max_its == 1; tdec.hip tdec_kernel_p2x<true>): only iteration 0's passes are built
-template <bool CONT = false, int CKS = P2_CKS, bool ONE = false, class Exec>
+// ONE: a launch of one iteration (a.max_its == 1; tdec.hip tdec_kernel_p2x<true>): only iteration 0's passes are built.
+// MK: the iteration whose DEC1 pass creates the packed q rows (TDEC_MKQ_IT: only once a second iteration runs; 0 for a
+// fixed iteration count without early stop -- configs[0] -- where every later iteration reads them: +2.9 %,
+// profiles/r5/ab_misc)
+template <bool CONT = false, int CKS = P2_CKS, bool ONE = false, uint32_t MK = TDEC_MKQ_IT, class Exec>
 MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   TdecP2Result r{{0u, 0u}, {0u, 0u}, {0u, 0u}};
   uint32_t active = a.live & 3u;
@@ -1120,7 +1123,6 @@ MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
   if constexpr (CONT)
     if (!a.cont_w && a.it0 == 1) tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
   for (uint32_t it = CONT ? a.it0 : 0u; it < (CONT ? a.it_end : a.max_its) && active; it++) {
-    constexpr uint32_t MK = TDEC_MKQ_IT;
     if constexpr (CONT) {
       tdec_p2_xhalf<false, false, SRC_Q, CKS>(a, lane, ex);
       tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
