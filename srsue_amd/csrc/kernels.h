@@ -37,7 +37,7 @@ void launch_rm_direct_maps(float* sb, const uint32_t* ktab_data, const MiRmDirec
 // turbo decoder (srslte_tdec_*): one wavefront per group of 64 code blocks
 // window masks of the sparse softbuffer rows (which decoder inputs have a materialised row)
 void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,
-                    const uint32_t* kdata, uint32_t n_groups, hipStream_t st);
+                    const uint32_t* kdata, uint32_t n_groups, uint32_t* zero, hipStream_t st);
 void launch_tdec(const float* sb, const uint32_t* wm, float* scratch, uint8_t* dec, uint8_t* cb_bytes, uint32_t* cb_its,
                  uint32_t* cb_crc, uint32_t* cb_tbp, const MiGroupDesc* groups, const MiLaneDesc* lanes,
                  const MiKTab* ktabs, const uint32_t* ktab_data, uint32_t n_groups, uint32_t max_its,
@@ -66,7 +66,7 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
                                            those continuing after iteration 0) */,
                       uint32_t seg /* 0, or the rounds after the first segmented over 4 / 8 wavefronts per pair
                                       (tdec_kernel_p2s) */,
-                      hipStream_t st);
+                      bool cont_zeroed /* cont[0] already reset on st (launch_rowmask's zero) */, hipStream_t st);
 constexpr uint32_t CONT_HIST = 8;   // rounds whose counts are recorded (h_count)
 // latency form of the int16 turbo decoder: one workgroup of `threads` (64/128/256) per code block
 // (lane descriptor), exact trellis segments (tdec_win_body.h); max_k sizes the dynamic LDS

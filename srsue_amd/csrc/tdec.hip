@@ -93,11 +93,13 @@ __device__ __forceinline__ void tdec_group(const float* __restrict__ sb, const u
 }
 
 // window masks of the sparse softbuffer rows: one thread per 4-step window (12 decoder inputs) of a
-// group; bit i = row pos[12w + i] is materialised (dl_common.h sb_group_floats)
+// group; bit i = row pos[12w + i] is materialised (dl_common.h sb_group_floats).  zero (if set): the continuation's
+// count, reset here for launch_tdec_cont (one launch fewer on the stream, between the decoder and its assign kernel)
 __global__ __launch_bounds__(256) void rowmask_kernel(const float* __restrict__ sb, uint32_t* __restrict__ wm,
                                                      const MiGroupDesc* __restrict__ groups,
                                                      const MiKTab* __restrict__ ktabs,
-                                                     const uint32_t* __restrict__ kdata) {
+                                                     const uint32_t* __restrict__ kdata, uint32_t* zero) {
+  if (zero && !(blockIdx.x | blockIdx.y | threadIdx.x)) *zero = 0u;
   const MiGroupDesc g = groups[blockIdx.y];
   const uint32_t w = blockIdx.x * 256 + threadIdx.x;
   if (w > g.K / BETA_W) return;
@@ -106,10 +108,10 @@ __global__ __launch_bounds__(256) void rowmask_kernel(const float* __restrict__ 
 }
 
 void launch_rowmask(const float* sb, uint32_t* wm, const MiGroupDesc* groups, const MiKTab* ktabs,
-                    const uint32_t* kdata, uint32_t n_groups, hipStream_t st) {
+                    const uint32_t* kdata, uint32_t n_groups, uint32_t* zero, hipStream_t st) {
   if (!n_groups) return;
   hipLaunchKernelGGL(rowmask_kernel, dim3((WM_STRIDE + 255) / 256, n_groups), dim3(256), 0, st, sb, wm, groups,
-                     ktabs, kdata);
+                     ktabs, kdata, zero);
 }
 
 // float decoder
@@ -544,13 +546,13 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
                       const MiLaneDesc* lanes, const uint32_t* ktab_data, const MiKTab& kt, uint32_t n_groups, uint32_t* cont,
                       uint32_t* cscr, uint8_t* cdec, uint32_t max_pairs, size_t pair_u32, uint32_t K, uint32_t max_its,
                       uint32_t gather_wgs, uint8_t* payload, bool w_stored, bool rounds, uint32_t* h_count,
-                      uint32_t seg, hipStream_t st) {
+                      uint32_t seg, bool cont_zeroed, hipStream_t st) {
   if (!n_groups || !max_pairs) return true;
   const TdecOut out{cb_bytes, cb_its, cb_crc, cb_tbp, payload};
   const size_t nl = (size_t)n_groups * LANES + 1;   // one list: count + lane indices
   uint32_t* lists[2] = {cont, cont + nl};
   uint32_t* src = cont + 2 * nl;
-  if (hipMemsetAsync(cont, 0, 4, st) != hipSuccess) return false;
+  if (!cont_zeroed && hipMemsetAsync(cont, 0, 4, st) != hipSuccess) return false;
   hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
   if (h_count && hipMemcpyAsync(h_count, cont, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
