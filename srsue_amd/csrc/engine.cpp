@@ -16,10 +16,6 @@
 
 #include "kernels.h"
 
-#ifndef MI_LEAN_CONT   // A/B switch (profiles/r5/ab_lean): 0 = a memset launch and a 2048-workgroup gather every run
-#define MI_LEAN_CONT 1
-#endif
-
 namespace mi {
 
 bool hip_ok(hipError_t e, const char* what) {
@@ -430,7 +426,7 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
                     d_cdec.bytes >= (size_t)cont_max_pairs() * P.groups[0].K * LANES;
   // (the row masks' kernel also resets the continuation's count: no memset launch between the decoder and its assign)
   launch_rowmask(sb, d_wm.as<uint32_t>(), d_groups.as<MiGroupDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(),
-                 (uint32_t)P.groups.size(), cont && MI_LEAN_CONT ? d_cont.as<uint32_t>() : nullptr, st);
+                 (uint32_t)P.groups.size(), cont ? d_cont.as<uint32_t>() : nullptr, st);
   if (p2) {
     // PDSCH batches: the decoder writes the payload bytes in place (tb_kernel then only combines the CRCs)
     const bool direct = P.has_pdsch && !P.cb_n;
@@ -476,10 +472,10 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its,
                        // the gather is grid-stride: when the history continued nothing, a small grid (its 2048
                        // early-exiting workgroups otherwise wait ~1 ms for CU slots behind the other streams' decoders)
-                       !MI_LEAN_CONT || cont_last[0] || cont_last[1] ? 2048u : 64u,
+                       cont_last[0] || cont_last[1] ? 2048u : 64u,
                        direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, cont_pending ? nullptr : h_cont,
                        opts.seg == 4 || opts.seg == 8 ? (uint32_t)opts.seg
-                       : opts.seg < 0 && (flags & MI_DL_FLAG_TDEC_SEG) ? 8u : 0u, MI_LEAN_CONT != 0, st))
+                       : opts.seg < 0 && (flags & MI_DL_FLAG_TDEC_SEG) ? 8u : 0u, true, st))
         return false;
       // the copy of the count (skipped while an earlier one is still unread) is complete when cont_ev is
       if (!cont_pending) {
