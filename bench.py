@@ -131,13 +131,43 @@ def shard_range(total, rank, world):
     return start, per + (1 if rank < rem else 0)
 
 
+_LINE_FD = None   # the process's original stdout once native libraries' prints are sent to stderr (keep_stdout_clean)
+
+
+def keep_stdout_clean():
+    """RCCL prints a version banner on stdout when its communicator comes up (seen on the GPU box: 'RCCL version :
+    ...'); the driver reads rank 0's stdout as ONE JSON line.  Before the nccl process group starts, file descriptor
+    1 is pointed at stderr for the rest of the process, and emit() writes the line to the original stdout."""
+    global _LINE_FD
+    if _LINE_FD is None:
+        sys.stdout.flush()
+        _LINE_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(out):
+    """Rank 0's one JSON line, on the process's original stdout."""
+    line = (json.dumps(out) + "\n").encode()
+    if _LINE_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        sys.stdout.flush()
+        os.write(_LINE_FD, line)
+
+
+def dist_on():
+    """A process group is up: N > 1 ranks, or one rank with --pg (the RCCL path rehearsed on a one-GPU box)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def reduce_over_ranks(elapsed, sums, world, device="cpu"):
     """The only cross-rank traffic, after the timed region: every rank's elapsed time (all-gathered: the max is
     the job's time, the list goes into the JSON) and the sums of this rank's end-of-run counters (`sums`: CRC-OK
     bits, code blocks, CRC-OK TBs, iteration sums, payload mismatches ...).  Returns (max elapsed, [sums],
     [elapsed per rank])."""
     sums = [float(x) for x in sums]
-    if world == 1:
+    if not dist_on():
         return elapsed, sums, [elapsed]
     if dist.get_backend() == "gloo":   # CPU rehearsal, or --share-gpu
         device = "cpu"
@@ -160,8 +190,8 @@ def rank_devices(world, dev):
         p = torch.cuda.get_device_properties(dev)
         me = {"device": p.name, "arch": getattr(p, "gcnArchName", ""), "cuda_index": dev.index,
               "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid)}
-    me = {"rank": dist.get_rank() if world > 1 else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **me}
-    if world == 1:
+    me = {"rank": dist.get_rank() if dist_on() else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **me}
+    if not dist_on():
         return [me]
     allr = [None] * world
     dist.all_gather_object(allr, me)
@@ -334,13 +364,13 @@ def bench_codeblocks(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     for t in tbs:
         t.profile_reset()
-    if world > 1:
+    if dist_on():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         tbs[i % S].run(d.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     per = [t.stage_ms() for t in tbs[:min(S, args.steps)]]
@@ -627,14 +657,14 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     torch.cuda.synchronize(dev)
     for b in batches:
         b.profile_reset()
-    if world > 1:
+    if dist_on():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(steps):
         batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # stage times: HIP events on each workspace's stream, averaged over every timed step
@@ -954,7 +984,7 @@ def dry_run(args, world, rank):
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs, iq,
                                                [tb_payload(first + i, c.tbs // 8) for i, c in enumerate(cfgs)],
                                                "6-PRB rehearsal subframes", True)
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 def main():
@@ -1019,6 +1049,9 @@ def main():
                          "one code block per lane, or auto (latency form up to 1024 code blocks)")
     ap.add_argument("--tdec", choices=("gen", "i16"), default="i16",
                     help="turbo arithmetic: gen = srsLTE-gen float, i16 = srsLTE SSE-design int16 (MI_DL_FLAG_TDEC_I16)")
+    ap.add_argument("--pg", action="store_true",
+                    help="one rank: still bring up the nccl (RCCL) process group, so the timing barrier, the reductions "
+                         "and the device gather run over RCCL as in the N-GPU line (launch with WORLD_SIZE=1, MASTER_*)")
     ap.add_argument("--dry-run-llr", default=None, help=argparse.SUPPRESS)   # CPU launch rehearsal (tests only)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1046,7 +1079,8 @@ def main():
         # so the aggregate is not a scaling measurement)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo")
-    elif world > 1:
+    elif world > 1 or args.pg:
+        keep_stdout_clean()
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -1056,8 +1090,8 @@ def main():
     if args.config == 1:
         out = bench_codeblocks(args, world, rank, dev)
         if out:
-            print(json.dumps(out), flush=True)
-        if world > 1:
+            emit(out)
+        if dist_on():
             dist.destroy_process_group()
         return
 
@@ -1125,6 +1159,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": dtype_of(args), "data": "synthetic",
             "config": {"workload": f"{what}: {B} subframes per GPU per step, {args.snr:g} dB AWGN",
                        **({"share_gpu_rehearsal": True} if args.share_gpu and world > 1 else {}),
+                       **({"process_group": dist.get_backend()} if dist_on() else {}),
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
@@ -1162,9 +1197,9 @@ def main():
         if not args.no_cpu_baseline:   # rank 0 at every N, after the reduction (outside the timed region)
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfgs[:len(pool_iq)], pool_iq, pool_tb, what,
                                                args.tdec == "i16")
-        print(json.dumps(out), flush=True)
+        emit(out)
     batch.close()
-    if world > 1:
+    if dist_on():
         dist.destroy_process_group()
 
 

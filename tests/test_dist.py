@@ -156,6 +156,37 @@ def test_bench_two_ranks_on_one_gpu(built):
 
 
 @pytest.mark.gpu
+def test_bench_rccl_process_group_one_rank(built):
+    """The RCCL side of the N-GPU line on a one-GPU box: one rank launched as torch.distributed.run launches each
+    of the driver's ranks (WORLD_SIZE / RANK / LOCAL_RANK / MASTER_* in its environment), `--pg` bringing up the
+    `nccl` process group with device_id; the timing barriers, the float64 all-reduces of elapsed time and counters on
+    the card, and the device gather (all_gather_object) then run over RCCL exactly as at N = 8."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--pg", "--sf-per-gpu", "256", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--iterating-snr", "0", "--plan-steps", "0",
+                        "--h2d-steps", "0"], cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()   # RCCL's version banner goes to stderr (bench.py keep_stdout_clean)
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[:500]
+    d = json.loads(lines[0])
+    assert d["config"]["process_group"] == "nccl" and d["n_gpus"] == 1
+    assert d["crc_ok_rate"] == 1.0 and d["payload_mismatches_crc_ok"] == 0 and d["subframes_all_ranks"] == 256
+    per = d["elapsed_per_rank_s"]
+    assert len(per) == 1 and abs(d["ms_per_step"] - per[0] / 2 * 1e3) < 1e-2
+    devs = d["rank_devices"]
+    assert len(devs) == 1 and devs[0]["rank"] == 0 and devs[0]["pci_bus_id"]
+
+
+@pytest.mark.gpu
 def test_bench_one_stream_full_line(built):
     """`bench.py --streams 1` (serial, the profiling runs' setting) prints the whole line: the planning block's
     static replay of two grant lists needs one workspace per list even on one stream (bench.py replan_steps), and
@@ -178,3 +209,19 @@ def test_bench_one_stream_full_line(built):
         assert pl[k]["payload_mismatches_crc_ok"] == 0 and pl[k]["Mbps"] > 0, k
     assert all(b > 0 for b in pl["varied_static"]["crc_ok_bits_per_list"])
     assert set(d["h2d"]) >= {"sc16", "fc32"}
+
+
+def test_native_stdout_prints_kept_off_the_line():
+    """bench.py keep_stdout_clean / emit: once the nccl process group is about to start, whatever native code
+    writes to file descriptor 1 (RCCL's version banner) lands on stderr, and stdout carries only the JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; print('before'); bench.keep_stdout_clean(); "
+            "os.write(1, b'RCCL version : x\\n'); print('python noise'); bench.emit({'metric': 'm', 'value': 1.5})"
+            % root)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.splitlines() == ["before", json.dumps({"metric": "m", "value": 1.5})]
+    assert "RCCL version" in r.stderr and "python noise" in r.stderr
