@@ -25,9 +25,14 @@ import time
 import numpy as np
 
 
-def hw_queues_arg(argv):
-    """--hw-queues N / --hw-queues=N (default 8; 0 keeps the environment's value), checked to 0..32."""
-    v = "8"
+def hw_queues_arg(argv, env=None):
+    """--hw-queues N / --hw-queues=N (0 keeps the environment's value), checked to 0..32.  Default 8, or 16 when this
+    process brings up the nccl (RCCL) process group (WORLD_SIZE > 1 without --share-gpu, or --pg): RCCL's own
+    streams take hardware queues too, and at 8 the bench's streams then share queues (profiles/r5/rccl_queues: one
+    rank under RCCL, 8 queues -1.7 % headline and -2 % waterfall, 16 queues level with the plain run)."""
+    env = os.environ if env is None else env
+    rccl = "--pg" in argv or (int(env.get("WORLD_SIZE", "1") or 1) > 1 and "--share-gpu" not in argv)
+    v = "16" if rccl else "8"
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):
             v = argv[i + 1]
@@ -38,10 +43,10 @@ def hw_queues_arg(argv):
     return v
 
 
-# HIP hardware queues per process (--hw-queues, default 8; 0 keeps the environment's value): the bench keeps 4
-# batches in flight on as many HIP streams, and with HIP's default of 4 queues per process the streams' kernels
-# share them with the runtime's own copies; 8 queues measured +0.7 % at the headline, 16 no better
-# (profiles/r4/ab_queues).  Set only when bench.py runs as the program (not when tests import it), before torch and
+# HIP hardware queues per process (--hw-queues, default 8, 16 under RCCL; 0 keeps the environment's value): the
+# bench keeps 4 batches in flight on as many HIP streams, and with HIP's default of 4 queues per process the streams'
+# kernels share them with the runtime's own copies; 8 queues measured +0.7 % at the headline, 16 no better
+# (profiles/r4/ab_queues) -- except beside RCCL's streams (hw_queues_arg).  Set only when bench.py runs as the program (not when tests import it), before torch and
 # the HIP runtime start (the runtime reads it once); the ranks bench.py spawns inherit it.
 if __name__ == "__main__":
     HW_QUEUES = hw_queues_arg(sys.argv[1:])
@@ -154,6 +159,19 @@ def emit(out):
     else:
         sys.stdout.flush()
         os.write(_LINE_FD, line)
+
+
+_STREAMS = []
+
+
+def bench_streams(dev, S):
+    """The S streams a block of the line runs its workspaces on: the current stream and S - 1 more, created once
+    and shared by every block (headline, waterfall, h2d, planning).  HIP binds each stream to one of the
+    process's GPU_MAX_HW_QUEUES hardware queues when it is created; fresh streams per block, created after RCCL's own
+    streams under the nccl process group, landed on shared queues and serialised the waterfall block (16 %)."""
+    while len(_STREAMS) < S - 1:
+        _STREAMS.append(torch.cuda.Stream(dev))
+    return [torch.cuda.current_stream(dev)] + _STREAMS[:S - 1]
 
 
 def dist_on():
@@ -356,7 +374,7 @@ def bench_codeblocks(args, world, rank, dev):
            for _ in range(S)]
     tb = tbs[0]
     d = torch.from_numpy(llr).to(dev)[torch.arange(n, device=dev) % pool].contiguous()
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    streams = bench_streams(dev, S)
     sptr = [st.cuda_stream for st in streams]
     torch.cuda.synchronize(dev)
     for w in range(args.warmup * S):
@@ -649,7 +667,7 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
         idx = torch.arange(B, device=dev) % len(pool_iq)
         d_iq.view(B, sfl).copy_(d_pool[idx])
         del d_pool
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    streams = bench_streams(dev, S)
     sptr = [st.cuda_stream for st in streams]
     torch.cuda.synchronize(dev)
     for w in range(warmup * S):
@@ -719,7 +737,7 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     W = S if replan else S * J // math.gcd(S, J)
     batches = [abi.Batch(lists[k % J], max_its=args.max_its, profile=False, tdec_i16=args.tdec == "i16",
                          sched=args.sched, compact_ce=True) for k in range(W)]
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    streams = bench_streams(dev, S)
     sptr = [st.cuda_stream for st in streams]
     D = max(1, threads)
     plans = [abi.Plan() for _ in range(D + 1)]   # D building + one ready ahead of the step that takes it

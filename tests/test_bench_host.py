@@ -76,8 +76,14 @@ def test_hw_queues_argument():
     """--hw-queues N and --hw-queues=N are both honoured, checked to 0..32 (gpurun refuses more than 32), and
     importing bench (as the GPU tests do) leaves GPU_MAX_HW_QUEUES alone."""
     import bench
-    assert bench.hw_queues_arg([]) == "8"
-    assert bench.hw_queues_arg(["--hw-queues", "16"]) == "16"
+    assert bench.hw_queues_arg([], {}) == "8"
+    assert bench.hw_queues_arg(["--hw-queues", "16"], {}) == "16"
+    # 16 by default when the process brings up RCCL (its streams take queues too): N > 1 ranks or --pg, not the
+    # gloo --share-gpu rehearsal or the parent that only spawns the ranks (it never touches the GPU)
+    assert bench.hw_queues_arg(["--gpus", "8"], {"WORLD_SIZE": "8"}) == "16"
+    assert bench.hw_queues_arg(["--pg"], {}) == "16"
+    assert bench.hw_queues_arg(["--gpus", "2", "--share-gpu"], {"WORLD_SIZE": "2"}) == "8"
+    assert bench.hw_queues_arg(["--gpus", "8", "--hw-queues", "8"], {"WORLD_SIZE": "8"}) == "8"
     assert bench.hw_queues_arg(["--steps", "3", "--hw-queues=0"]) == "0"
     for bad in (["--hw-queues", "33"], ["--hw-queues=-1"], ["--hw-queues=x"]):
         with pytest.raises(SystemExit):
