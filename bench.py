@@ -17,7 +17,6 @@ events on the stream the kernels run on, averaged over the timed steps) and the 
 import argparse
 import concurrent.futures as cf
 import json
-import math
 import os
 import sys
 import time
@@ -632,7 +631,10 @@ def bench_h2d(args, cfgs, pool_iq, batch, bits_ok, iq=None, steps=None):
     ok = pipe.batch(last[-1]).download(abi.BUF_TB_CRC, np.uint32)[:B]
     pipe.close()
     hb.close()
-    return {"value": round(bits_ok * steps / dt / 1e6, 2), "unit": "Mbps", "ms_per_step": round(dt / steps * 1e3, 3),
+    # the pipe's own CRC-OK bits (quantised sc16 IQ can fail a TB the device-resident fc32 run decoded: ADVICE r5);
+    # bits_ok (the fc32 run's) is kept beside it for comparison
+    pipe_bits = float(sum(c.tbs for c, o in zip(cfgs, ok) if o))
+    return {"value": round(pipe_bits * steps / dt / 1e6, 2), "resident_bits_ok": bits_ok, "pipe_bits_ok": pipe_bits, "unit": "Mbps", "ms_per_step": round(dt / steps * 1e3, 3),
             "steps": steps, "iq_bytes_per_subframe": round(nfl * esz / B),
             "pcie_GBps": round(nfl * esz * steps / dt / 1e9, 2), "crc_ok_rate": round(float(ok.mean()), 6),
             "what": f"IQ ({iq_fmt}, batch layout) from page-locked host memory via mi_dl_pipe: H2D on a copy "
@@ -722,6 +724,13 @@ def varied_cfgs(P, first):
     return out
 
 
+def static_workspaces(S, J):
+    """Workspaces of the static planning replay over J lists on S streams: each keeps one list (workspace k: list
+    k % J, stream k % S), so the count is a multiple of J -- S rounded up to one (J for S = 1).  Not lcm(S, J): that is
+    2 S for odd S, and a 12,500-subframe workspace holds ~45 GB (S = 5 would need 10 of them)."""
+    return J * -(-max(1, S) // J)
+
+
 def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     """The streaming receiver with the grant re-derived every step: step i decodes list i % J (a 12,500-subframe
     configuration, IQ buffer iqs[i % J] laid out for it).  With replan, every step's plan is BUILT from scratch on a
@@ -732,9 +741,8 @@ def replan_steps(args, lists, iqs, dev, steps, warmup, threads, replan=True):
     import collections
     S = max(1, args.streams)
     J = len(lists)
-    # re-planned: one workspace per stream.  Static: each workspace keeps one list, so there are lcm(S, J) of them,
-    # workspace k on stream k % S (one stream and two lists: two workspaces alternating on the one stream)
-    W = S if replan else S * J // math.gcd(S, J)
+    # re-planned: one workspace per stream.  Static: each workspace keeps one list (static_workspaces)
+    W = S if replan else static_workspaces(S, J)
     batches = [abi.Batch(lists[k % J], max_its=args.max_its, profile=False, tdec_i16=args.tdec == "i16",
                          sched=args.sched, compact_ce=True) for k in range(W)]
     streams = bench_streams(dev, S)

@@ -149,6 +149,15 @@ uint32_t mi_dl_batch_n_groups(const mi_dl_batch_t *b);
  * circular-buffer position.  The environment variable MI_RM_DIRECT=0 (read when the batch is created) disables
  * the direct form for A/B runs; the softbuffer is bit-identical either way. */
 uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
+/* Waterfall compaction's schedule source.  With compaction the first launch chooses between two exact schedules
+ * (store the iteration-0 extrinsic rows and re-compact per iteration, or not; and the size of the gather grid) from
+ * the continuation counts of THIS batch's earlier runs, read back without a wait -- so by default the timing of a run
+ * depends on the batch's history (its results never do).  mode: -1 = from the history (default); 0 = fixed "few
+ * code blocks continue" (the high-SNR schedule); 1 = fixed "waterfall" (the low-SNR schedule).  A fixed mode makes
+ * the schedule of every run a function of the call alone.  mi_dl_batch_reset_history forgets the recorded counts
+ * (the next run of mode -1 schedules as a fresh batch). */
+int    mi_dl_batch_set_tdec_history(mi_dl_batch_t *b, int mode);   /* 0 = ok, -1 = bad mode */
+void   mi_dl_batch_reset_history(mi_dl_batch_t *b);
 
 /* ---- streaming re-planning (srsUE re-derives the grant every TTI: phch_worker.cc:297 -> :337).
  * The planner is split from the device: mi_dl_plan_build runs the whole host planning of a batch (RE lists,
@@ -159,12 +168,14 @@ uint32_t mi_dl_batch_rm_direct_groups(const mi_dl_batch_t *b);
  * words per (RNTI, sf, G), CRS per cell, per-K tables: srslte_ue_dl_set_rnti's pregeneration) across builds,
  * and after a replan it holds the batch's previous plan, ready to be rebuilt.  One plan object per planning
  * thread; a batch's work buffers only grow (a larger plan reallocates them, synchronously).
- * HARQ continuity across a replan: the softbuffer rows of a code block are where the plan puts them, so soft
- * combining (new_tb = 0 lanes) carries over only when the new plan lays the softbuffer out exactly as the old one
- * (same groups, softbuffer offsets and code-block-to-lane assignment -- e.g. the same grants with a new rv).  When
- * the layout differs and the new plan has retransmission lanes, the replan clears the softbuffer (every value
- * RX_NULL, as srslte_softbuffer_rx_reset), so such a lane combines with nothing rather than with another code
- * block's rows.  (New transmissions overwrite their rows; rows another layout left are settled by the kernels.) */
+ * HARQ continuity across a replan, per 64-lane group: the softbuffer rows of a code block are where the plan puts
+ * them, so soft combining (new_tb = 0 lanes) carries over for every group the new plan lays out exactly as the old
+ * one did (same group index, K, N_cb, first lane and softbuffer offset, and the same code-block-to-lane assignment
+ * in its 64 lanes -- e.g. the same grant with a new rv), whatever happens to the other groups.  A group whose layout
+ * differs and that holds a retransmission lane has its softbuffer region cleared (every value RX_NULL, as
+ * srslte_softbuffer_rx_reset), so such a lane combines with nothing rather than with another code block's rows --
+ * srsLTE's softbuffer is per HARQ process, and a change of another subframe's grant does not touch it.  (New
+ * transmissions overwrite their rows; rows another layout left are settled by the kernels.) */
 typedef struct mi_dl_plan mi_dl_plan_t;
 mi_dl_plan_t *mi_dl_plan_create(void);
 void   mi_dl_plan_destroy(mi_dl_plan_t *p);

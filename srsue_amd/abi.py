@@ -92,6 +92,8 @@ def lib():
             "mi_tdec_turbo_win": (C.c_int, [vp]),
             "mi_dl_batch_n_groups": (u32, [vp]),
             "mi_dl_batch_rm_direct_groups": (u32, [vp]),
+            "mi_dl_batch_set_tdec_history": (C.c_int, [vp, C.c_int]),
+            "mi_dl_batch_reset_history": (None, [vp]),
             "mi_dl_plan_create": (vp, []),
             "mi_dl_plan_destroy": (None, [vp]),
             "mi_dl_plan_build": (C.c_int, [vp, vp, u32]),
@@ -307,6 +309,15 @@ class Batch:
     def rm_direct_groups(self):
         """groups rate-de-matched in the direct form (rm.hip rm_direct_kernel; MI_RM_DIRECT=0 disables)"""
         return lib().mi_dl_batch_rm_direct_groups(self.h)
+
+    def set_tdec_history(self, mode):
+        """Waterfall compaction's schedule source (mi_dl_batch_set_tdec_history): -1 = this batch's history of
+        continuation counts (default), 0 = fixed high-SNR schedule, 1 = fixed waterfall schedule (results identical)."""
+        if lib().mi_dl_batch_set_tdec_history(self.h, int(mode)):
+            raise RuntimeError("set_tdec_history: " + last_error())
+
+    def reset_history(self):
+        lib().mi_dl_batch_reset_history(self.h)
 
     def payload(self, sf, all_payload=None):
         p = all_payload if all_payload is not None else self.download(BUF_PAYLOAD, np.uint8)

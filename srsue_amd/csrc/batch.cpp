@@ -151,24 +151,51 @@ int mi_dl_batch_replan(mi_dl_batch_t* b, mi_dl_plan_t* p, void* stream) {
   std::swap(b->cfgs, p->cfgs);
   p->built = false;
   b->eng.last_stream = st;
-  // HARQ continuity only across an identical softbuffer layout (include/mi_dl.h): p->plan now holds the old plan
+  // HARQ continuity per group (include/mi_dl.h): p->plan now holds the old plan
   const mi::PlanData &nw = b->eng.plan, &old = p->plan;
-  bool same = nw.groups.size() == old.groups.size() && nw.lanes.size() == old.lanes.size() && nw.cb_list == old.cb_list &&
-              nw.sb_floats == old.sb_floats;
-  for (size_t g = 0; same && g < nw.groups.size(); g++)
-    same = nw.groups[g].K == old.groups[g].K && nw.groups[g].Ncb == old.groups[g].Ncb &&
-           nw.groups[g].lane0 == old.groups[g].lane0 && nw.groups[g].sb_off == old.groups[g].sb_off;
-  for (size_t l = 0; same && l < nw.lanes.size(); l++)
-    same = nw.lanes[l].valid == old.lanes[l].valid && nw.lanes[l].tb == old.lanes[l].tb &&
-           nw.lanes[l].F == old.lanes[l].F;
-  bool combines = false;   // new transmissions overwrite their rows (stale rows of another layout are settled)
-  for (const MiLaneDesc& ld : nw.lanes) combines |= ld.valid && !ld.new_tb;
+  auto same_group = [&](size_t g) {
+    if (g >= old.groups.size()) return false;
+    const MiGroupDesc &x = nw.groups[g], &y = old.groups[g];
+    if (x.K != y.K || x.Ncb != y.Ncb || x.lane0 != y.lane0 || x.sb_off != y.sb_off) return false;
+    for (uint32_t l = x.lane0; l < x.lane0 + mi::LANES; l++) {
+      const bool a = l < nw.lanes.size(), c = l < old.lanes.size();
+      if (a != c) return false;
+      if (!a) continue;
+      const MiLaneDesc &u = nw.lanes[l], &v = old.lanes[l];
+      if (u.valid != v.valid || (u.valid && (u.tb != v.tb || u.F != v.F))) return false;
+    }
+    return true;
+  };
+  // the regions to clear: groups with a retransmission lane whose layout changed (contiguous regions merged)
+  std::vector<std::pair<size_t, size_t>> clear;
+  for (size_t g = 0; g < nw.groups.size(); g++) {
+    const MiGroupDesc& x = nw.groups[g];
+    bool combines = false;
+    for (uint32_t l = x.lane0; l < x.lane0 + mi::LANES && l < nw.lanes.size(); l++)
+      combines |= nw.lanes[l].valid && !nw.lanes[l].new_tb;
+    if (!combines || same_group(g)) continue;
+    const size_t off = x.sb_off, n = mi::sb_group_floats(x.Ncb);
+    if (!clear.empty() && clear.back().first + clear.back().second == off) clear.back().second += n;
+    else clear.emplace_back(off, n);
+  }
   const size_t had = b->eng.d_sb.bytes;
   if (b->eng.upload(st, true)) return -1;
   // (a reallocated softbuffer was zeroed by upload)
-  if (!same && combines && had && b->eng.d_sb.bytes == had)
-    return mi::hip_ok(hipMemsetAsync(b->eng.d_sb.p, 0, b->eng.d_sb.bytes, st), "replan softbuffer reset") ? 0 : -1;
+  if (!had || b->eng.d_sb.bytes != had) return 0;
+  for (const auto& c : clear)
+    if (!mi::hip_ok(hipMemsetAsync(b->eng.d_sb.as<float>() + c.first, 0, c.second * sizeof(float), st),
+                    "replan softbuffer reset"))
+      return -1;
   return 0;
+}
+
+int mi_dl_batch_set_tdec_history(mi_dl_batch_t* b, int mode) {
+  if (!b || mode < -1 || mode > 1) { mi::set_error("mi_dl_batch_set_tdec_history: mode is -1, 0 or 1"); return -1; }
+  b->eng.cont_mode = mode;
+  return 0;
+}
+void mi_dl_batch_reset_history(mi_dl_batch_t* b) {
+  if (b) b->eng.reset_history();
 }
 
 /* ---- raw code-block decoding (srslte_tdec_* contract) ---------------------------------------- */

@@ -53,9 +53,20 @@ Engine::Engine() {
   opts.store_w = env_int("MI_TDEC_STORE_W", -1);
   opts.rounds = env_int("MI_TDEC_ROUNDS", -1);
   opts.seg = env_int("MI_TDEC_SEG", -1);
+  if (opts.seg != -1 && opts.seg != 0 && opts.seg != 4 && opts.seg != 8) {
+    // an A/B run must measure the schedule it asked for: an unsupported value is reported and ignored
+    fprintf(stderr, "srsue_amd: MI_TDEC_SEG=%d is not 0 (off), 4 or 8: ignored (automatic)\n", opts.seg);
+    opts.seg = -1;
+  }
   opts.win_threads = (uint32_t)std::max(0, env_int("MI_TDEC_WIN_THREADS", 0));
   plan.rm_direct_on = env_int("MI_RM_DIRECT", 1) != 0;
   plan.xcd_queues = env_int("MI_RM_XCDQ", 1) != 0;
+  // the SIMD count the turbo schedule is chosen by, once per engine (on the device current at creation)
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  simds = 4u * (uint32_t)cus;
 }
 
 Engine::~Engine() {
@@ -366,13 +377,6 @@ bool Engine::use_win() const {
 // occupancy its extra VALU makes it slower than the register form).  MI_DL_FLAG_TDEC_LANE alone = one
 // wavefront per group; MI_DL_FLAG_TDEC_X = crossed; Opts::tdec_x (MI_TDEC_X at creation, A/B) forces a form.
 int Engine::tdec_crossed() const {
-  static uint32_t simds = 0;
-  if (!simds) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    simds = 4u * (uint32_t)cus;
-  }
   const uint64_t waves = 2ull * plan.groups.size();
   const int form = (q16() && waves > 4ull * simds && waves <= 5ull * simds) ? 2 : 1;
   if (opts.tdec_x >= 0) return opts.tdec_x;   // A/B
@@ -450,7 +454,9 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
         memcpy(cont_last, h_cont, sizeof(cont_last));
         cont_pending = false;
       }
-      store_w = opts.store_w >= 0 ? opts.store_w != 0 : (uint64_t)cont_last[0] * 50 > P.lanes.size();
+      store_w = opts.store_w >= 0  ? opts.store_w != 0
+                : cont_mode >= 0     ? cont_mode != 0
+                                     : (uint64_t)cont_last[0] * 50 > P.lanes.size();
     }
     launch_tdec_p2(sb, d_wm.as<uint32_t>(), d_scratch.as<float>(), d_dec.as<uint8_t>(), d_cbbytes.as<uint8_t>(),
                    d_cbits.as<uint32_t>(), d_cbcrc.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_groups.as<MiGroupDesc>(),
@@ -472,7 +478,7 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
                        cont_max_pairs(), cont_pair_u32(), P.groups[0].K, max_its,
                        // the gather is grid-stride: when the history continued nothing, a small grid (its 2048
                        // early-exiting workgroups otherwise wait ~1 ms for CU slots behind the other streams' decoders)
-                       cont_last[0] || cont_last[1] ? 2048u : 64u,
+                       (cont_mode >= 0 ? cont_mode != 0 : cont_last[0] || cont_last[1]) ? 2048u : 64u,
                        direct ? d_payload.as<uint8_t>() : nullptr, store_w, rounds, cont_pending ? nullptr : h_cont,
                        opts.seg == 4 || opts.seg == 8 ? (uint32_t)opts.seg
                        : opts.seg < 0 && (flags & MI_DL_FLAG_TDEC_SEG) ? 8u : 0u, true, st))
@@ -490,6 +496,13 @@ bool Engine::launch_turbo(float* sb, hipStream_t st) {
               d_lanes.as<MiLaneDesc>(), d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(),
               max_its, early_stop, q16(), tdec_crossed(), st);
   return true;
+}
+
+void Engine::reset_history() {
+  if (cont_pending && cont_ev) (void)hipEventSynchronize(cont_ev);
+  cont_pending = false;
+  memset(cont_last, 0, sizeof(cont_last));
+  if (h_cont) memset(h_cont, 0, 4 * CONT_HIST);
 }
 
 int Engine::stage_ms(float* ms, uint32_t* nruns) {

@@ -40,12 +40,14 @@ struct Engine {
   //   MI_TDEC_COMPACT  0 = no waterfall compaction;  MI_TDEC_STORE_W / MI_TDEC_ROUNDS  0 / 1 = force
   //   MI_TDEC_WIN_THREADS  latency form: threads per code block;  MI_RM_DIRECT=0 / MI_RM_XCDQ=0 (Plan)
   //   MI_TDEC_SEG=4/8  the waterfall's late rounds segmented over 4 / 8 wavefronts per pair (tdec_kernel_p2s)
-  //                    instead of the crossed form
+  //                    instead of the crossed form; 0 = explicitly off (overrides MI_DL_FLAG_TDEC_SEG); any other
+  //                    value is reported on stderr and ignored
   struct Opts {
     int tdec_x = -1, compact = -1, store_w = -1, rounds = -1, seg = -1;
     uint32_t win_threads = 0;
   } opts;
   Engine();
+  uint32_t simds = 1024;   // SIMDs of the device (4 per CU), read once at construction: no shared mutable state
   bool q16() const { return (flags & MI_DL_FLAG_TDEC_GEN) == 0; }   // int16 turbo arithmetic (default)
   uint32_t win_threads = 0;   // latency-form turbo: threads per code block (0 = by K)
   bool use_win() const;       // latency-form (segment-parallel) turbo decoder for this plan
@@ -69,6 +71,11 @@ struct Engine {
   hipEvent_t cont_ev = nullptr;
   bool cont_pending = false;
   uint32_t cont_last[8] = {};
+  // the schedule's source (mi_dl_batch_set_tdec_history): -1 = the history above, 0 / 1 = fixed (few continue /
+  // waterfall)
+  int cont_mode = -1;
+  // forget the recorded counts (a pending copy is waited for, so it cannot land in cont_last later)
+  void reset_history();
   float noise = 0.01f;   // MMSE regulariser (srsUE passes 0.01: phch_worker.cc:340)
   // descriptor tables
   DevBuf d_cells, d_crs, d_pds, d_re, d_scr, d_sfs, d_lanes, d_lanesrc, d_groups, d_ktabs, d_kdata, d_tbs, d_cblist,

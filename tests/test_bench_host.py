@@ -94,3 +94,14 @@ def test_hw_queues_argument():
     out = subprocess.run([sys.executable, "-c", "import os, bench; print(os.environ.get('GPU_MAX_HW_QUEUES'))"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.stdout.strip() == "None", out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("S,want", [(1, 2), (2, 2), (3, 4), (4, 4), (5, 6), (6, 6)])
+def test_static_workspaces_count(S, want):
+    """The static planning replay keeps one list per workspace on J = 2 lists: S rounded up to a multiple of J, never
+    lcm(S, J) = 2 S for odd S (10 workspaces of ~45 GB at S = 5)."""
+    W = bench.static_workspaces(S, 2)
+    assert W == want
+    # every list is kept by some workspace, and every stream is used
+    assert {k % 2 for k in range(W)} == {0, 1}
+    assert {k % S for k in range(W)} == set(range(S))

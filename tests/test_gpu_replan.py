@@ -119,3 +119,53 @@ def test_retransmission_after_replan():
     for b in (w, w2):
         b.close()
     p.close()
+
+
+def test_retransmission_survives_unrelated_replan():
+    """HARQ continuity is per 64-lane group (include/mi_dl.h): when only another subframe's grant changes
+    -- here the last subframe becomes a new TB of another code-block size (K = 6144, sorted after K = 5,824) -- every
+    group whose layout is unchanged keeps combining its retransmissions, and only the group whose lanes changed is
+    cleared.  Per code block: lanes of the unchanged groups decode exactly as the same-layout retransmission, the
+    changed group's retransmission lanes exactly as from a cleared softbuffer.  (srsLTE keeps one softbuffer per HARQ
+    process: dl_harq.h:88, reset only by its own new grant, dl_harq.cc:232.)"""
+    n = 32
+    first = [abi.sf_cfg(nof_prb=100, sf_idx=bench.SF_CYCLE[i % 8], tbs=75376, Qm=6, rv=0) for i in range(n)]
+    retx = [abi.sf_cfg(nof_prb=100, sf_idx=bench.SF_CYCLE[i % 8], tbs=75376, Qm=6, rv=2, new_tb=0) for i in range(n)]
+    # the unrelated change: subframe n - 1 a new TB of 6 code blocks of K = 6144 (B' = 36,864)
+    mixed = retx[:n - 1] + [abi.sf_cfg(nof_prb=100, sf_idx=bench.SF_CYCLE[(n - 1) % 8], tbs=36696, Qm=6, rv=0)]
+    snrs = np.linspace(19.5, 23.0, n)
+    X0 = _config(first, snr=snrs)
+    X2 = _config(retx, snr=snrs)
+    XM = _config(mixed, snr=snrs)
+    st = torch.cuda.current_stream().cuda_stream
+    f = abi.Batch(retx, compact_ce=True)
+    f.run(X2[1].data_ptr(), st)
+    alone = _results(f)
+    f.close()
+    runs = {}
+    for name, cfgs, d in (("same", retx, X2[1]), ("mixed", mixed, XM[1])):
+        w = abi.Batch(first, compact_ce=True)
+        p = abi.Plan()
+        w.run(X0[1].data_ptr(), st)
+        p.build(cfgs)
+        w.replan(p, st)
+        w.run(d.data_ptr(), st)
+        runs[name] = (_results(w), w.n_groups)
+        if name == "mixed":
+            for i in range(n):
+                if runs[name][0][1][i]:
+                    assert np.array_equal(w.payload(i, runs[name][0][0]), (X0[2] if i < n - 1 else XM[2])[i])
+        w.close()
+        p.close()
+    same, mix = runs["same"][0], runs["mixed"][0]
+    cb_its = lambda r: r[3]
+    kept = 6 * 64                                  # groups 0..5: the lanes of code blocks 0 .. 383, unchanged
+    cleared = (n - 1) * 13 - kept                  # group 6: the remaining K = 5,824 code blocks
+    assert np.array_equal(cb_its(mix)[:kept], cb_its(same)[:kept])
+    assert np.array_equal(cb_its(mix)[kept:kept + cleared], cb_its(alone)[kept:kept + cleared])
+    # combining happened where it was kept: the same-layout run beats the cleared one on those code blocks
+    assert cb_its(same)[:kept].sum() < cb_its(alone)[:kept].sum()
+    # the TBs whose code blocks all lie in the kept groups decode exactly as with the same layout
+    full = kept // 13
+    for k in (1, 2):
+        assert np.array_equal(mix[k][:full], same[k][:full])

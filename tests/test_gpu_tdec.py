@@ -103,3 +103,57 @@ def test_packed_one_iteration_launch(built, n, K, ebno):
         dec, oits, ook = td.decode_cb(llr[i], K, max_its=1, early_stop=True)
         assert its[i] == oits == 1 and bool(ok[i]) == bool(ook), f"cb {i}"
         assert np.array_equal(got[i], dec), f"cb {i}"
+
+
+def crc24a_attach(payload):
+    """payload bits + their CRC24A parity bits (36.212 5.1.1, g = 0x864CFB, MSB first)"""
+    reg = 0
+    for b in payload:
+        fb = ((reg >> 23) & 1) ^ int(b)
+        reg = (reg << 1) & 0xFFFFFF
+        if fb:
+            reg ^= 0x864CFB
+    par = [(reg >> (23 - i)) & 1 for i in range(24)]
+    return np.concatenate([payload, np.array(par, np.uint8)])
+
+
+@pytest.mark.parametrize("seg", ["8", "4"])
+def test_segmented_rounds_short_last_segment(built, seg, monkeypatch):
+    """the waterfall's segmented late rounds (tdec.hip tdec_kernel_p2s) at a K whose segments do not
+    divide evenly -- K = 328: 8 wavefronts get L = 48-step segments, so nseg = 7 (one idle wavefront) and a 40-step last
+    segment; 4 wavefronts: L = 96, a 40-step last segment -- equal the packed decoder running every iteration in place
+    (MI_TDEC_COMPACT=0): decisions, iterations, CRC verdicts.  65,536 code blocks (the compaction needs the packed
+    schedule, i.e. group pairs covering every SIMD) of 128 distinct CRC24A-carrying blocks across 0.5-3.5 dB, early
+    stop on the CRC; a sample is checked against the oracle's int16 decoder too."""
+    K, n, distinct = 328, 65536, 128
+    rng = np.random.default_rng(328)
+    blocks = [crc24a_attach(rng.integers(0, 2, K - 24).astype(np.uint8)) for _ in range(distinct)]
+    ebnos = np.linspace(0.5, 3.5, distinct)
+    llr = np.stack([llr_bpsk(abi.turbo_encode(b, K), K, e, rng) for b, e in zip(blocks, ebnos)])
+    d = torch.from_numpy(llr).cuda()[torch.arange(n, device="cuda") % distinct].contiguous()
+    outs = []
+    for env in ({"MI_TDEC_COMPACT": "0"}, {"MI_TDEC_STORE_W": "1", "MI_TDEC_ROUNDS": "1", "MI_TDEC_SEG": seg}):
+        for k in ("MI_TDEC_COMPACT", "MI_TDEC_STORE_W", "MI_TDEC_ROUNDS", "MI_TDEC_SEG"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tb = abi.TdecBatch(K, n, max_its=6, early_stop=True, crc24a=True, tdec_i16=True)
+        assert lib_sched(tb) == 4, "the packed schedule (compaction needs it)"
+        tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        outs.append(tb.results())
+        tb.close()
+    for a, b, name in zip(outs[0], outs[1], ("decisions", "iterations", "crc")):
+        assert np.array_equal(a, b), name
+    its, ok = outs[0][1], outs[0][2]
+    # the waterfall reaches the late (segmented) rounds: code blocks stopping at iterations 1 .. >= 3
+    assert 0 < ok.mean() < 1 and its.max() >= 3 and (its >= 3).sum() > 0
+    td = O.Tdec(O.TDEC_I16)
+    bits = outs[1][0]
+    for i in range(0, distinct, 9):
+        dec, oits, ook = td.decode_cb(llr[i], K, max_its=6, early_stop=True, crc24a=True)
+        assert outs[1][1][i] == oits and bool(outs[1][2][i]) == bool(ook), f"cb {i}"
+        assert np.array_equal(bits[i], dec), f"cb {i}"
+
+
+def lib_sched(tb):
+    return abi.lib().mi_tdec_turbo_win(tb.h)
