@@ -181,6 +181,12 @@ mi_dl_plan_t *mi_dl_plan_create(void);
 void   mi_dl_plan_destroy(mi_dl_plan_t *p);
 int    mi_dl_plan_build(mi_dl_plan_t *p, const mi_dl_sf_cfg_t *cfgs, uint32_t n_sf);   /* host only; 0 = ok */
 int    mi_dl_batch_replan(mi_dl_batch_t *b, mi_dl_plan_t *p, void *stream);          /* 0 = ok */
+/* HBM a batch holds: its work buffers, softbuffer arena, descriptor tables and twiddles (the LLR stream only once a
+ * run or a buffer access needed it: the default fused demap never does).  mi_dl_plan_device_bytes: the work buffers
+ * and softbuffer a batch of a built plan would allocate with these max_its / flags -- host only, no HIP call that
+ * allocates; a deployer sizes workspaces per GPU with it (4 workspaces of 12,500 subframes). */
+size_t mi_dl_batch_device_bytes(mi_dl_batch_t *b);
+size_t mi_dl_plan_device_bytes(const mi_dl_plan_t *p, uint32_t max_its, uint32_t flags);
 
 /* ---- raw turbo code-block decoding (the srslte_tdec_* contract; BASELINE configs[0] =
  * srsLTE turbodecoder_test).  n_cb code blocks of size K; decoder input per block = 3(K+4) fp32

@@ -98,6 +98,8 @@ def lib():
             "mi_dl_plan_destroy": (None, [vp]),
             "mi_dl_plan_build": (C.c_int, [vp, vp, u32]),
             "mi_dl_batch_replan": (C.c_int, [vp, vp, vp]),
+            "mi_dl_batch_device_bytes": (sz, [vp]),
+            "mi_dl_plan_device_bytes": (sz, [vp, u32, u32]),
             "mi_tx_subframe": (C.c_int, [vp, vp, vp, C.c_float, C.c_uint64, vp]),
             "mi_turbo_encode": (C.c_int, [vp, u32, u32, vp]),
             "mi_tdec_create": (vp, [u32, u32, u32, C.c_int, C.c_int, u32]),
@@ -310,6 +312,11 @@ class Batch:
         """groups rate-de-matched in the direct form (rm.hip rm_direct_kernel; MI_RM_DIRECT=0 disables)"""
         return lib().mi_dl_batch_rm_direct_groups(self.h)
 
+    @property
+    def device_bytes(self):
+        """HBM this batch holds (mi_dl_batch_device_bytes)."""
+        return lib().mi_dl_batch_device_bytes(self.h)
+
     def set_tdec_history(self, mode):
         """Waterfall compaction's schedule source (mi_dl_batch_set_tdec_history): -1 = this batch's history of
         continuation counts (default), 0 = fixed high-SNR schedule, 1 = fixed waterfall schedule (results identical)."""
@@ -340,6 +347,16 @@ class Plan:
         if lib().mi_dl_plan_build(self.h, C.cast(arr, C.c_void_p), len(arr)):
             raise RuntimeError("mi_dl_plan_build: " + last_error())
         return self
+
+    def device_bytes(self, max_its=4, compact_ce=True, keep_llr=False, tdec_i16=True):
+        """HBM a batch of this plan would allocate for its work buffers and softbuffer (mi_dl_plan_device_bytes;
+        host only)."""
+        flags = (FLAG_TDEC_I16 if tdec_i16 else FLAG_TDEC_GEN) | (FLAG_CE_COMPACT if compact_ce else 0) | \
+            (FLAG_KEEP_LLR if keep_llr else 0)
+        n = lib().mi_dl_plan_device_bytes(self.h, max_its, flags)
+        if not n:
+            raise RuntimeError("mi_dl_plan_device_bytes: " + last_error())
+        return n
 
     def close(self):
         if self.h:

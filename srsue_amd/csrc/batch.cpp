@@ -40,7 +40,7 @@ static mi::DevBuf* buf_of(mi_dl_batch_t* b, int which, size_t* bytes) {
   switch (which) {
     case MI_DL_BUF_GRID: *bytes = P.grid_elems * 8; return &b->eng.d_grid;
     case MI_DL_BUF_CE: *bytes = P.ce_elems * 8; return &b->eng.d_ce;
-    case MI_DL_BUF_LLR: *bytes = P.e_floats * 4; return &b->eng.d_e;
+    case MI_DL_BUF_LLR: *bytes = P.e_floats * 4; return b->eng.ensure_llr() ? &b->eng.d_e : nullptr;
     case MI_DL_BUF_PAYLOAD: *bytes = P.payload_bytes; return &b->eng.d_payload;
     case MI_DL_BUF_TB_CRC: *bytes = nsf * 4; return &b->eng.d_tbok;
     case MI_DL_BUF_TB_ITS: *bytes = nsf * 4; return &b->eng.d_tbits;
@@ -133,6 +133,19 @@ struct mi_dl_plan {
 
 mi_dl_plan_t* mi_dl_plan_create(void) { return new mi_dl_plan(); }
 void mi_dl_plan_destroy(mi_dl_plan_t* p) { delete p; }
+
+size_t mi_dl_batch_device_bytes(mi_dl_batch_t* b) {
+  return b ? b->eng.work_bytes(true, b->eng.d_e.bytes != 0) + b->eng.d_tables.bytes + b->eng.d_tw.bytes : 0;
+}
+
+size_t mi_dl_plan_device_bytes(const mi_dl_plan_t* p, uint32_t max_its, uint32_t flags) {
+  if (!p || !p->built) { mi::set_error("mi_dl_plan_device_bytes: no built plan"); return 0; }
+  mi::Engine e;   // host only: the sizes of the buffers a batch of this plan would allocate
+  static_cast<mi::PlanData&>(e.plan) = p->plan;
+  e.max_its = max_its ? max_its : 4;
+  e.flags = flags;
+  return e.work_bytes(true, (flags & MI_DL_FLAG_KEEP_LLR) != 0);
+}
 
 int mi_dl_plan_build(mi_dl_plan_t* p, const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf) {
   if (!p || !cfgs || !n_sf) { mi::set_error("empty batch"); return -1; }

@@ -166,26 +166,48 @@ int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
     }
     if (!up(d_tw, tw, st) || !hip_ok(hipStreamSynchronize(st), "twiddles")) return -1;
   }
-  const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
-  bool ok = d_grid.ensure(P.grid_elems * 8) && d_ce.ensure(P.ce_elems * 8) && d_metrics.ensure(nsf * 5 * 4);
-  if (P.has_pdsch || P.cb_n) {
-    ok = ok && d_e.ensure(P.e_floats * 4) && d_wm.ensure(P.groups.size() * WM_STRIDE * 4) &&
-         d_scratch.ensure(P.scratch_floats * 4) && d_dec.ensure(P.dec_bytes) &&
-         d_cbbytes.ensure((size_t)P.lanes.size() * CB_BYTES_STRIDE) && d_cbits.ensure(P.lanes.size() * 4) &&
-         d_cbcrc.ensure(P.lanes.size() * 4) && d_cbtbp.ensure(P.lanes.size() * 4) && d_payload.ensure(P.payload_bytes) && d_tbok.ensure(nsf * 4) &&
-         d_tbits.ensure(nsf * 4);
-    if (tdec_compact()) {
-      const uint32_t np = cont_max_pairs();
-      ok = ok && d_cont.ensure((3 * P.lanes.size() + 2) * 4) && d_cscr.ensure((size_t)np * cont_pair_u32() * 4) &&
-           d_cdec.ensure((size_t)np * P.groups[0].K * LANES);
-    }
-    if (alloc_sb) {
-      size_t before = d_sb.bytes;
-      ok = ok && d_sb.ensure(P.sb_floats * 4);
-      if (ok && d_sb.bytes != before) ok = hip_ok(hipMemsetAsync(d_sb.p, 0, d_sb.bytes, st), "memset sb");
-    }
+  bool ok = true;
+  for (const auto& w : work_set()) ok = ok && w.first->ensure(w.second);
+  if (ok && (P.has_pdsch || P.cb_n) && alloc_sb) {
+    size_t before = d_sb.bytes;
+    ok = d_sb.ensure(P.sb_floats * 4);
+    if (ok && d_sb.bytes != before) ok = hip_ok(hipMemsetAsync(d_sb.p, 0, d_sb.bytes, st), "memset sb");
   }
   return ok ? 0 : -1;
+}
+
+// the work buffers of the current plan and their sizes (ensure_work allocates them; work_bytes counts them).  The
+// LLR stream (d_e, 360 KB per 20 MHz MCS-28 subframe) is not among them: the default fused demap never writes it, so
+// it is allocated on first use (ensure_llr): 4.5 GB less per 12,500-subframe workspace
+std::vector<std::pair<DevBuf*, size_t>> Engine::work_set() {
+  const Plan& P = plan;
+  const size_t nsf = std::max<size_t>(P.sfs.size(), 1);
+  std::vector<std::pair<DevBuf*, size_t>> w{{&d_grid, P.grid_elems * 8}, {&d_ce, P.ce_elems * 8}, {&d_metrics, nsf * 5 * 4}};
+  if (P.has_pdsch || P.cb_n) {
+    w.insert(w.end(), {{&d_wm, P.groups.size() * WM_STRIDE * 4}, {&d_scratch, P.scratch_floats * 4},
+                       {&d_dec, P.dec_bytes}, {&d_cbbytes, (size_t)P.lanes.size() * CB_BYTES_STRIDE},
+                       {&d_cbits, P.lanes.size() * 4}, {&d_cbcrc, P.lanes.size() * 4}, {&d_cbtbp, P.lanes.size() * 4},
+                       {&d_payload, P.payload_bytes}, {&d_tbok, nsf * 4}, {&d_tbits, nsf * 4}});
+    if (tdec_compact()) {
+      const uint32_t np = cont_max_pairs();
+      w.insert(w.end(), {{&d_cont, (3 * P.lanes.size() + 2) * 4}, {&d_cscr, (size_t)np * cont_pair_u32() * 4},
+                         {&d_cdec, (size_t)np * P.groups[0].K * LANES}});
+    }
+  }
+  return w;
+}
+
+bool Engine::ensure_llr() { return d_e.ensure(plan.e_floats * 4); }
+
+size_t Engine::work_bytes(bool with_sb, bool with_llr) {
+  auto al = [](size_t n) { return std::max<size_t>((n + 255) & ~(size_t)255, 256); };   // DevBuf::ensure
+  size_t t = 0;
+  for (const auto& w : work_set()) t += al(w.second);
+  if (plan.has_pdsch || plan.cb_n) {
+    if (with_sb) t += al(plan.sb_floats * 4);
+    if (with_llr) t += al(plan.e_floats * 4);
+  }
+  return t;
 }
 
 int Engine::upload(hipStream_t st, bool alloc_sb) {
@@ -300,6 +322,7 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     // fused demap -> rate de-matching unless the caller keeps the LLR stream (or supplies it)
     const bool fuse = (mask & (1u << MI_DL_STAGE_DEMAP)) && (mask & (1u << MI_DL_STAGE_RM)) &&
                       !(flags & MI_DL_FLAG_KEEP_LLR);
+    if (!fuse && (mask & ((1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM))) && !ensure_llr()) return -1;
     if ((mask & (1u << MI_DL_STAGE_DEMAP)) && !fuse)
       launch_demap(d_grid.as<float2>(), d_ce.as<float2>(), d_e.as<float>(), d_sfs.as<MiSfDesc>(),
                    d_pds.as<MiPdschDesc>(), d_cells.as<MiCellDesc>(), d_re.as<uint32_t>(), d_scr.as<uint32_t>(), nsf,

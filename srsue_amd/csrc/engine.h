@@ -133,6 +133,10 @@ struct Engine {
   int stage_tables(DevBuf& arena, std::vector<size_t>& offs, hipStream_t st);
   void bind_tables(const DevBuf& arena, const std::vector<size_t>& offs);
   int ensure_work(hipStream_t st, bool alloc_sb);
+  std::vector<std::pair<DevBuf*, size_t>> work_set();   // the plan's work buffers and sizes (no LLR stream, no sb)
+  bool ensure_llr();                                     // the LLR stream d_e, allocated on first use
+  // HBM bytes of this plan's work buffers (+ the softbuffer arena, + the LLR stream), as DevBuf::ensure rounds them
+  size_t work_bytes(bool with_sb, bool with_llr);
   // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.
   int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override);
   // raw code-block decoding: scatter d into the softbuffer layout, then the turbo kernel

@@ -225,3 +225,68 @@ def test_native_stdout_prints_kept_off_the_line():
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.splitlines() == ["before", json.dumps({"metric": "m", "value": 1.5})]
     assert "RCCL version" in r.stderr and "python noise" in r.stderr
+
+
+def _dry_worker(rank, world, port, q):
+    """One rank of the N-GPU line's host side over gloo: its shard of configs[3]'s 100,000
+    subframes, the reduce of its counters, the hardware-queue setting it would run with under RCCL, and its place in
+    the gathered device list."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    first, n = bench.shard_range(100000, rank, world)
+    # counters: the shard's subframes, its CRC-OK bits at MCS 28, code blocks (13 per subframe), a rank tag
+    t, sums, per = bench.reduce_over_ranks(0.25 * (rank + 1), [n, n * 75376, 13 * n, rank + 1], world)
+    env = {"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank)}
+    queues = (bench.hw_queues_arg([], env), bench.hw_queues_arg(["--share-gpu"], env))
+    devs = bench.rank_devices(world, None)
+    q.put((rank, first, n, t, sums, per, queues, [d["rank"] for d in devs]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [4, 8])
+def test_n_rank_dry_run(world):
+    """The host side of `bench.py --gpus N` at the driver's rank counts over gloo (no GPU): contiguous shards of
+    100,000 subframes cover every subframe once; reduce_over_ranks sums every counter and returns the max and every
+    rank's elapsed time; each rank would run 16 HIP hardware queues under RCCL (8 sharing a GPU), within gpurun's
+    32; rank_devices is gathered in rank order."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dry_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    spans = [(r[1], r[2]) for r in res]
+    assert spans[0][0] == 0 and sum(n for _, n in spans) == 100000
+    assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    assert all(n == 100000 // world for _, n in spans)           # 12,500 per GPU at N = 8
+    for r in res:
+        assert r[3] == 0.25 * world                               # max over ranks
+        assert r[4] == [100000.0, 100000.0 * 75376, 1300000.0, world * (world + 1) / 2]
+        assert r[5] == [0.25 * (k + 1) for k in range(world)]     # in rank order
+        assert r[6] == ("16", "8") and int(r[6][0]) <= 32
+        assert r[7] == list(range(world))
+
+
+def test_rank_hbm_budget_configs3():
+    """Each rank's HBM at configs[3]'s per-GPU shard: the bench keeps 4 workspaces of 12,500 subframes
+    (one per stream) plus the IQ buffer; mi_dl_plan_device_bytes (host only) sizes a workspace.  They fit the
+    MI355X's 288 GB with room, and the LLR stream is not allocated on the default fused path."""
+    import bench
+    from srsue_amd import abi
+    first, n = bench.shard_range(100000, 7, 8)
+    p = abi.Plan().build([bench.make_cfg(first + i) for i in range(n)])
+    ws = p.device_bytes()
+    assert p.device_bytes(keep_llr=True) - ws == n * 90000 * 4   # the LLR stream: 360 KB per subframe
+    iq = n * 30720 * 8
+    total = 4 * ws + iq
+    assert total < 0.75 * 288e9, total / 1e9
+    p.close()
