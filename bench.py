@@ -907,6 +907,44 @@ def bench_planning(args, cfgs, pool_iq, pool_tb, dev, threads, value_mbps):
     return out
 
 
+TTI_BUDGET_US = 3000.0   # srsUE: subframe n's DL decode and the UL it acknowledges go out at n + 4 (phch_recv.cc:330-337)
+
+
+def bench_tti(args):
+    """configs[1] as SURVEY 8d defines it: one 20 MHz TM1 MCS-28 subframe per call through the
+    per-TTI srsLTE ABI, as srsUE's phch_worker drives it -- host IQ in -> srslte_ue_dl_decode_fft_estimate (:254) ->
+    srslte_ue_dl_cfg_grant (:337) -> srslte_pdsch_decode_rnti (:347) -> payload out, then the UL PUSCH encode -- with
+    1 and with 4 concurrent worker instances (srsUE runs 1-4 phch_workers, phy.h:118-119), each in its own thread
+    (tests/c/tti_latency, plain C against include/srslte/srslte.h).  Latencies per TTI, pooled over the workers."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "c", "tti_latency")
+    if not os.path.exists(exe):
+        return {"error": "tests/c/tti_latency not built (__graft_entry__.build)"}
+    out = {}
+    for w in (1, 4):
+        r = subprocess.run([exe, "100", str(args.tti_ttis), str(w)], capture_output=True, text=True, timeout=300)
+        if r.returncode:
+            out[f"workers_{w}"] = {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+            continue
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        dl, ul = d["dl_total"], d["ul_pusch_encode"]
+        out[f"workers_{w}"] = {
+            "ttis": d["ttis"], "crc_ok_and_payload_match": d["crc_ok_and_payload_match"],
+            "dl_p50_us": dl["p50_us"], "dl_p99_us": dl["p99_us"], "dl_max_us": dl["max_us"],
+            "decode_fft_estimate_p50_us": d["decode_fft_estimate"]["p50_us"],
+            "pdsch_decode_rnti_p50_us": d["pdsch_decode_rnti"]["p50_us"],
+            "ul_pusch_encode_p50_us": ul["p50_us"], "ul_pusch_encode_p99_us": ul["p99_us"],
+            "dl_plus_ul_p99_us": round(dl["p99_us"] + ul["p99_us"], 1),
+            "within_tti4_budget": dl["p99_us"] + ul["p99_us"] < TTI_BUDGET_US,
+            "subframes_per_s": round(d["ttis"] / (d["wall_us"] * 1e-6), 1)}
+    out["budget_us"] = TTI_BUDGET_US
+    out["what"] = ("configs[1] through the per-TTI srsLTE ABI (tests/c/tti_latency): host IQ (30,720 cf32) -> "
+                   "decode_fft_estimate -> cfg_grant -> pdsch_decode_rnti -> 9,422 payload bytes, then cfg_grant + "
+                   "pusch_encode (UL 16QAM MCS 20) per TTI; p99 of DL + UL against the TTI+4 budget "
+                   "(phch_recv.cc:330-337); 1 and 4 concurrent srsLTE worker instances (phy.h:118-119)")
+    return out
+
+
 def isolated_stages(runner, run_once, dev, S, steps):
     """With --streams S > 1 the timed steps overlap, so the per-stage HIP-event durations of the timed region
     include other streams' kernels sharing the GPU and are not per-kernel figures.  After the
@@ -1058,6 +1096,9 @@ def main():
     ap.add_argument("--ebno", type=float, default=1.5, help="config 1: Eb/N0 in dB")
     ap.add_argument("--h2d-steps", type=int, default=20,
                     help="steps of the PCIe-inclusive (h2d) block of the default line (0 = off)")
+    ap.add_argument("--tti-ttis", type=int, default=200,
+                    help="TTIs per worker of the per-TTI latency block (configs[1] through the srsLTE ABI at 1 and 4 "
+                         "concurrent instances, tests/c/tti_latency); 0 = off")
     ap.add_argument("--h2d", action="store_true",
                     help="also measure the PCIe-inclusive rate: IQ from page-locked host memory through the "
                          "double-buffered mi_dl_pipe (SURVEY 8f-3); reported beside value, never as value")
@@ -1214,6 +1255,8 @@ def main():
             out["iterating"] = itr
         if args.config == 4 and args.plan_steps > 0 and world == 1:
             out["planning"] = bench_planning(args, cfgs, pool_iq, pool_tb, dev, threads, mbps)
+        if args.config == 4 and args.tti_ttis > 0 and world == 1:
+            out["tti"] = bench_tti(args)
         if args.ctrl:
             out["ctrl"] = bench_ctrl(args, batch, dev)
         if args.ul:

@@ -302,6 +302,19 @@ def test_ue_dl_concurrent_worker_instances():
     assert d["crc_ok"] >= 20 and d["crc_failed"] > 0 and d["iterating_ttis"] > 0, d
 
 
+def test_tti_latency_harness_four_workers():
+    """bench.py's `tti` block (configs[1] through the per-TTI ABI): tests/c/tti_latency with 4
+    concurrent worker instances decodes every TTI to its transmitted TB (30 dB) and reports the pooled latencies."""
+    import json
+    exe = os.path.join(os.path.dirname(HARNESS), "tti_latency")
+    r = subprocess.run([exe, "100", "24", "4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["workers"] == 4 and d["ttis"] == 96 and d["crc_ok_and_payload_match"] == 96, d
+    for k in ("decode_fft_estimate", "pdsch_decode_rnti", "dl_total", "ul_pusch_encode"):
+        assert 0 < d[k]["p50_us"] <= d[k]["p99_us"] <= d[k]["max_us"], k
+
+
 def test_ue_dl_plan_memo_eviction_srsue_call_order():
     """The per-TTI plan memos evict least-recently-used entries (Engine::plan_memo: 32 PDSCH / front-end plans;
     ue_dl.cpp ctrl_plan: 64 control plans keyed by (sf_idx, CFI, RNTI, PHICH query)).  120 TTIs cycle 10 subframe

@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1
 shift
 mkdir -p $OUT
-ARGS=${BENCH_ARGS:-"--no-cpu-baseline --iterating-snr 0 --plan-steps 0 --h2d-steps 0"}
+ARGS=${BENCH_ARGS:-"--no-cpu-baseline --iterating-snr 0 --plan-steps 0 --h2d-steps 0 --tti-ttis 0"}
 for rep in 1 2; do
   for e in "$@"; do
     tag=$(echo "$e r$rep" | tr ' =/.-' '_____')

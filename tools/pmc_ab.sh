@@ -10,7 +10,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1
 shift
-ARGS="--no-cpu-baseline --steps 3 --warmup 1 --iterating-snr 0 --plan-steps 0 --h2d-steps 0 --streams 1 ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline --steps 3 --warmup 1 --iterating-snr 0 --plan-steps 0 --h2d-steps 0 --tti-ttis 0 --streams 1 ${BENCH_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp
 for v in "$@"; do
   if [ "$v" = cur ]; then unset SRSUE_AMD_LIB; else export SRSUE_AMD_LIB=$R/srsue_amd/libsrsue_amd_$v.so; fi

@@ -9,7 +9,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1
 shift
-ARGS="--iterating-snr 0 --plan-steps 0 --h2d-steps 0 --steps 20 --streams 1 $@"   # one operating point per profile, every tdec launch alone on the GPU (rocprof durations = per-kernel)
+ARGS="--iterating-snr 0 --plan-steps 0 --h2d-steps 0 --tti-ttis 0 --steps 20 --streams 1 $@"   # one operating point per profile, every tdec launch alone on the GPU (rocprof durations = per-kernel)
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 python3 $R/bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err || exit 11
