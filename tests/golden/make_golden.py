@@ -15,7 +15,18 @@ Fixtures
                           blocks need up to 4 iterations): IQ, TB, oracle grid / ce / metrics / LLR, and the payload and
                           iteration count of both turbo arithmetics (float srsLTE-gen, int16 SSE design)
 
-`python tests/golden/make_golden.py tdec16` regenerates only the int16 fixture, `... sf20` only the 20 MHz one.
+  otx_*.npz               the same kind of chain fixtures with the IQ from the ORACLE's own transmitter
+                          (oracle/o_tx.c or_tx_subframe, independent of the product's csrc/tx.cpp): a change to the
+                          product transmitter alone cannot move them.  Each holds per subframe
+                          the config (OTX_FIELDS + PRB mask), IQ, TB, the oracle's grid / ce / metrics / LLR and the
+                          payload + iteration count of the int16 decoder:
+    otx_1p4mhz.npz        1.4 MHz TM1 16QAM (cell 301, CFI 2), 20 dB
+    otx_20mhz_tm1.npz     configs[1]: 20 MHz TM1 MCS 28, 20.5 dB (code blocks iterating: 4 iterations)
+    otx_20mhz_tm2.npz     configs[2]: 20 MHz TM2 (2-port SFBC) 64QAM MCS 28 through h = (0.8+0.3j, -0.4+0.5j), 25 dB (2 iterations)
+    otx_mixed.npz         configs[4]: one 1.4 / 5 / 10 / 20 MHz subframe each (bench.config_cfgs(5)), 30 dB
+
+`python tests/golden/make_golden.py tdec16` regenerates only the int16 fixture, `... sf20` only the 20 MHz one,
+`... otx` only the oracle-transmitter ones.
 """
 import ctypes as C
 import os
@@ -77,7 +88,54 @@ def make_sf20():
     print("sf_20mhz_tm1: iterations gen", out["noi_gen"][0], "i16", out["noi_i16"][0])
 
 
+OTX_FIELDS = ("cell_id", "nof_prb", "nof_ports", "sf_idx", "cfi", "tbs", "Qm", "tm", "rnti")
+
+
+def otx_cfg_row(c):
+    return [int(getattr(c, f)) for f in OTX_FIELDS] + [int(c.prb_mask[p]) for p in range(110)]
+
+
+def otx_fixture(name, cfgs, snr, h=None, seed0=0x07A0):
+    """cfgs (abi.sf_cfg) through the ORACLE transmitter and the oracle receive chain; the int16 decode must pass."""
+    rows, iqs, tbs, grids, ces, mets, llrs, pays, nois = [], [], [], [], [], [], [], [], []
+    for i, c in enumerate(cfgs):
+        tb = O.splitmix_bytes(0x5EED0000 + seed0 + i, c.tbs // 8)
+        tc = O.tx_cfg(O.make_cell(c.cell_id, c.nof_prb, c.nof_ports), sf_idx=c.sf_idx, cfi=c.cfi, rv=0, rnti=c.rnti,
+                      tm=c.tm, tbs=c.tbs, qm=c.Qm, prb=[c.prb_mask[p] for p in range(c.nof_prb)], snr_db=snr, h=h,
+                      seed=0xA5A5 + seed0 + i)
+        iq, G = O.tx_subframe(tc, tb)
+        grid, ce, met, llr = oracle_front(c, iq)
+        assert len(llr) == G, (name, i, len(llr), G)
+        ok, pay, noi, _ = oracle_dlsch(c, llr, i16=True)
+        assert ok and np.array_equal(pay, tb), (name, i)
+        rows.append(otx_cfg_row(c)); iqs.append(iq); tbs.append(tb); grids.append(grid); ces.append(ce)
+        mets.append(met); llrs.append(llr); pays.append(pay); nois.append(noi)
+    cat = lambda v: (np.concatenate(v), np.cumsum([0] + [len(x) for x in v]))
+    hh = h if h is not None else [1.0 + 0j, 0.0 + 0j]
+    arrs = {"cfg": np.array(rows, np.int64), "noi_i16": np.array(nois, np.uint32), "metrics": np.stack(mets),
+            "snr_db": np.array([snr]), "seed0": np.array([seed0]),
+            "h": np.array([[x.real, x.imag] for x in hh], np.float64)}
+    for k, v in (("iq", iqs), ("tb", tbs), ("grid", grids), ("ce", ces), ("llr", llrs), ("payload", pays)):
+        arrs[k], arrs[k + "_off"] = cat(v)
+    np.savez_compressed(os.path.join(HERE, name), **arrs)
+    print(name, "int16 iterations", nois, os.path.getsize(os.path.join(HERE, name)), "B")
+
+
+def make_otx():
+    import bench
+    otx_fixture("otx_1p4mhz.npz", [abi.sf_cfg(cell_id=301, nof_prb=6, nof_ports=1, sf_idx=1, cfi=2, tbs=2344, Qm=4)],
+                20.0)
+    otx_fixture("otx_20mhz_tm1.npz", [abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=1, sf_idx=1, cfi=1, tbs=75376,
+                                                 Qm=6)], 20.5)
+    otx_fixture("otx_20mhz_tm2.npz", [abi.sf_cfg(cell_id=1, nof_prb=100, nof_ports=2, sf_idx=2, cfi=1, tm=2,
+                                                 tbs=75376, Qm=6)], 25.0, h=[0.8 + 0.3j, -0.4 + 0.5j])
+    otx_fixture("otx_mixed.npz", bench.config_cfgs(5, 4, 0), 30.0)
+
+
 def main():
+    if sys.argv[1:] == ["otx"]:
+        make_otx()
+        return
     if sys.argv[1:] == ["tdec16"]:
         make_tdec16()
         return
@@ -132,6 +190,7 @@ def main():
                         cfg=np.array([cfg.cell_id, cfg.nof_prb, cfg.nof_ports, cfg.sf_idx, cfg.cfi, cfg.tbs, cfg.Qm]))
     make_tdec16()
     make_sf20()
+    make_otx()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -82,3 +82,20 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     rms = np.sqrt(np.mean(b * b)) + 1e-30
     return float(np.max(np.abs(a - b)) / rms)
+
+
+def otx_fixture(path):
+    """An oracle-transmitter chain fixture (tests/golden/make_golden.py otx_fixture): (arrays, [abi.sf_cfg], accessor)
+    where accessor(key, i) is subframe i's slice of a concatenated array (iq, tb, grid, ce, llr, payload)."""
+    from srsue_amd import abi
+    g = np.load(path)
+    cfgs = []
+    for row in g["cfg"]:
+        cid, nprb, ports, sf, cfi, tbs, qm, tm, rnti = (int(x) for x in row[:9])
+        cfgs.append(abi.sf_cfg(cell_id=cid, nof_prb=nprb, nof_ports=ports, sf_idx=sf, cfi=cfi, tm=tm, rnti=rnti,
+                               tbs=tbs, Qm=qm, prb=[bool(x) for x in row[9:9 + nprb]]))
+
+    def part(key, i):
+        o = g[key + "_off"]
+        return g[key][o[i]:o[i + 1]]
+    return g, cfgs, part
