@@ -274,13 +274,15 @@ def run_for(seconds, nthreads, work):
 
 def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what, i16):
     """The oracle chain (this repo's C restatement) on a bounded sample of the same workload, on one
-    thread and on all host threads; the turbo decoder is the SSE4.1 int16 one (oracle/o_simd.c, the
-    srsLTE SSE design) in int16 mode, the float srsLTE-gen restatement otherwise."""
+    thread and on all host threads; the turbo decoder is the int16 one of the srsLTE SSE design in int16 mode -- AVX2
+    with two code blocks per __m256i (oracle/o_avx2.c) where the host has AVX2, else SSE4.1 (oracle/o_simd.c) -- and
+    the float srsLTE-gen restatement otherwise."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     import oracle_lib as O
     L = O.lib()
-    L.or_set_tdec_mode(O.TDEC_SIMD if i16 else O.TDEC_GEN)
+    avx2 = i16 and L.or_avx2_available() == 1
+    L.or_set_tdec_mode((O.TDEC_AVX2 if avx2 else O.TDEC_SIMD) if i16 else O.TDEC_GEN)
 
     def one(t, i):
         i %= len(pool_iq)
@@ -299,7 +301,8 @@ def cpu_baseline(seconds, pool_cfgs, pool_iq, pool_tb, what, i16):
     (b1, c1, n1), dt1 = run_for(seconds / 3, 1, one)
     (bT, cT, nT), dtT = run_for(2 * seconds / 3, T, one)
     L.or_set_tdec_mode(O.TDEC_GEN)
-    dec = "SSE4.1 int16 turbo (oracle/o_simd.c)" if i16 else "float srsLTE-gen turbo restatement"
+    dec = ("AVX2 int16 turbo, code blocks in pairs (oracle/o_avx2.c)" if avx2 else
+           "SSE4.1 int16 turbo (oracle/o_simd.c)") if i16 else "float srsLTE-gen turbo restatement"
     return {"value": round(bT / dtT / 1e6, 3), "unit": "Mbps", "cores": T, "kind": "port",
             "value_1core": round(b1 / dt1 / 1e6, 3), "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "cores_note": f"all of the job's {HOST_CPU_SHARE}-CPU share of the host (the pool's per-GPU grant; "
@@ -424,16 +427,22 @@ def bench_codeblocks(args, world, rank, dev):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         L, T, i16 = O.lib(), host_threads(), args.tdec == "i16"
-        if i16:
-            # SSE4.1 int16 decoder, one code block per thread, all threads on the same batch call
+        avx2 = i16 and L.or_avx2_available() == 1
+
+        def work_its(its_n, fn):
+            # the int16 decoder (AVX2: two code blocks per __m256i; else SSE4.1), 4 code blocks per call and thread
             def work(t, i):
                 m = 4
                 out_b = np.zeros((m, K), np.uint8)
                 its_ = np.zeros(m, np.uint32)
                 ok_ = np.zeros(m, np.uint8)
                 j = (i * m) % (pool - m + 1)
-                L.or_simd_decode_batch(llr[j:j + m], llr.shape[1], m, K, 8, 0, 0, out_b, its_, ok_, 1)
+                fn(llr[j:j + m], llr.shape[1], m, K, its_n, 0, 0, out_b, its_, ok_, 1)
                 return (m, 0, 0)
+            return work
+        if i16:
+            fn = L.or_avx2_decode_batch if avx2 else L.or_simd_decode_batch
+            work = work_its(8, fn)
         else:
             tds = [O.Tdec() for _ in range(T)]
 
@@ -442,13 +451,25 @@ def bench_codeblocks(args, world, rank, dev):
                 return (1, 0, 0)
         (m1, _, _), dt1 = run_for(args.cpu_seconds / 3, 1, work)
         (mT, _, _), dtT = run_for(2 * args.cpu_seconds / 3, T, work)
-        dec = "SSE4.1 int16 max-log-MAP (oracle/o_simd.c)" if i16 else "float max-log-MAP restatement (oracle/o_fec.c)"
+        dec = ("AVX2 int16 max-log-MAP, two code blocks per __m256i (oracle/o_avx2.c)" if avx2 else
+               "SSE4.1 int16 max-log-MAP (oracle/o_simd.c)") if i16 else "float max-log-MAP restatement (oracle/o_fec.c)"
         out["cpu_baseline"] = {"value": round(mT * K / dtT / 1e6, 4), "unit": "Mbps", "cores": T, "kind": "port",
                                "value_1core": round(m1 * K / dt1 / 1e6, 4),
                                "sample": f"{mT} code blocks K=6144 x 8 iterations through the {dec}, {T} threads "
                                          f"in {dtT:.1f} s; 1 thread: {m1} in {dt1:.1f} s",
                                "codeblocks_per_s": round(mT / dtT, 2), "cpu_model": cpu_model(),
                                "host_cpus_visible": os.cpu_count()}
+        if i16:
+            # per-core figures beside the reference README's "+100 Mbps" SSE decoder (README.md:18, iteration count
+            # unstated): 8 and 4 iterations, the AVX2 and the SSE4.1 decoder, one thread, ~1/6 of the budget each
+            per_core = {}
+            for name, f in (("avx2", L.or_avx2_decode_batch if avx2 else None), ("sse41", L.or_simd_decode_batch)):
+                for its_n in (8, 4):
+                    if f is None:
+                        continue
+                    (mm, _, _), dd = run_for(args.cpu_seconds / 8, 1, work_its(its_n, f))
+                    per_core[f"{name}_{its_n}its_Mbps"] = round(mm * K / dd / 1e6, 3)
+            out["cpu_baseline"]["per_core"] = per_core
     tb.close()
     return out
 

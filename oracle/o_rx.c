@@ -259,26 +259,48 @@ int or_dlsch_decode_cbits(const float *llr, uint32_t G, uint32_t tbs, uint32_t Q
   /* per-call decoder state: or_dlsch_decode / or_decode_subframe are called from several threads
      by the CPU baseline */
   int mode = or_get_tdec_mode();
+  if (mode == OR_TDEC_AVX2 && !or_avx2_available()) mode = OR_TDEC_SIMD;
   void *h = malloc(mode == OR_TDEC_GEN ? sizeof(or_tdec_t)
-                   : mode == OR_TDEC_I16 ? sizeof(or_tdec16_t) : or_simd_tdec_size());
+                   : mode == OR_TDEC_I16 ? sizeof(or_tdec16_t)
+                   : mode == OR_TDEC_AVX2 ? or_avx2_tdec_size() : or_simd_tdec_size());
   if (mode == OR_TDEC_SIMD) or_simd_tdec_init(h);   /* empty QPP-table cache: built once for the TB's K */
-  float *din = (float *)malloc(sizeof(float) * 3 * (OR_TCOD_MAX_K + 4));
-  uint8_t *bits = (uint8_t *)malloc(OR_TCOD_MAX_K), *b = (uint8_t *)malloc(sg.B + 8);
+  if (mode == OR_TDEC_AVX2) or_avx2_tdec_init(h);
+  float *din = (float *)malloc(sizeof(float) * 2 * 3 * (OR_TCOD_MAX_K + 4));
+  float *din2 = din + 3 * (OR_TCOD_MAX_K + 4);
+  uint8_t *bits = (uint8_t *)malloc(2 * OR_TCOD_MAX_K), *b = (uint8_t *)malloc(sg.B + 8);
+  uint8_t *bits2 = bits + OR_TCOD_MAX_K;
   uint32_t pos = 0, pb = 0, noi = 0, ncb_ok = 0;
   for (uint32_t r = 0; r < sg.C; r++) {
     uint32_t K = (r < sg.Cm) ? sg.Km : sg.Kp, F = (r == 0) ? sg.F : 0;
     uint32_t E = (uint32_t)or_rm_E(G, sg.C, Qm, NL, r);
     or_rm_rx(llr + pos, E, K, F, rv, new_tb, sb + (size_t)r * sb_stride, din);
     pos += E;
-    int ok;
-    int its = mode == OR_TDEC_I16    ? or_decode_cb16((or_tdec16_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok)
-              : mode == OR_TDEC_SIMD ? or_simd_decode_cb(h, din, K, max_its, 1, sg.C == 1, bits, &ok)
-                                     : or_decode_cb((or_tdec_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok);
-    if ((uint32_t)its > noi) noi = (uint32_t)its;
-    if (cb_its_out) cb_its_out[r] = (uint32_t)its;
-    ncb_ok += ok ? 1 : 0;
-    uint32_t L = sg.C > 1 ? 24 : 0;
-    for (uint32_t k = F; k < K - L; k++) b[pb++] = bits[k];
+    int ok, ok2 = 0, its, its2 = 0;
+    /* AVX2: code blocks r and r + 1 of equal K decoded together (two per __m256i) */
+    const int pair = mode == OR_TDEC_AVX2 && r + 1 < sg.C && ((r + 1 < sg.Cm) ? sg.Km : sg.Kp) == K;
+    if (pair) {
+      const uint32_t E2 = (uint32_t)or_rm_E(G, sg.C, Qm, NL, r + 1);
+      or_rm_rx(llr + pos, E2, K, 0, rv, new_tb, sb + (size_t)(r + 1) * sb_stride, din2);
+      pos += E2;
+    }
+    if (mode == OR_TDEC_AVX2)
+      or_avx2_decode_pair(h, din, pair ? din2 : NULL, K, max_its, 1, sg.C == 1, bits, pair ? bits2 : NULL, &ok, &ok2,
+                          &its, &its2);
+    else
+      its = mode == OR_TDEC_I16    ? or_decode_cb16((or_tdec16_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok)
+            : mode == OR_TDEC_SIMD ? or_simd_decode_cb(h, din, K, max_its, 1, sg.C == 1, bits, &ok)
+                                   : or_decode_cb((or_tdec_t *)h, din, K, max_its, 1, sg.C == 1, bits, &ok);
+    for (int q = 0; q < 1 + pair; q++) {
+      const uint32_t rr = r + (uint32_t)q, Fq = q ? 0 : F;
+      const int itq = q ? its2 : its, okq = q ? ok2 : ok;
+      const uint8_t *bq = q ? bits2 : bits;
+      if ((uint32_t)itq > noi) noi = (uint32_t)itq;
+      if (cb_its_out) cb_its_out[rr] = (uint32_t)itq;
+      ncb_ok += okq ? 1 : 0;
+      uint32_t L = sg.C > 1 ? 24 : 0;
+      for (uint32_t k = Fq; k < K - L; k++) b[pb++] = bq[k];
+    }
+    r += (uint32_t)pair;
   }
   int tb_ok = (or_crc24a(b, sg.B) == 0);
   memset(payload, 0, (tbs + 7) / 8);

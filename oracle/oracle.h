@@ -121,10 +121,22 @@ int      or_decode_cb16(or_tdec16_t *h, const float *in, uint32_t K, uint32_t ma
 #define OR_TDEC_GEN 0
 #define OR_TDEC_I16 1
 #define OR_TDEC_SIMD 2   /* the SSE4.1 implementation of the int16 decoder (o_simd.c) */
+#define OR_TDEC_AVX2 3   /* the AVX2 implementation, two code blocks per __m256i (o_avx2.c; or_avx2_available()) */
 void     or_set_tdec_mode(int mode);
 int      or_get_tdec_mode(void);
 /* SSE4.1 int16 decoder (CPU baseline), bit-identical to or_decode_cb16.  state: or_simd_tdec_size()
  * bytes (any alignment).  Batch: n code blocks of equal K, input i at in + i*stride floats. */
+/* AVX2 int16 decoder, two equal-K code blocks per call (lane 0 = A, lane 1 = B; inB NULL = A alone), each
+ * bit-identical to or_decode_cb16 (o_avx2.c).  Requires or_avx2_available(). */
+int      or_avx2_available(void);
+size_t   or_avx2_tdec_size(void);
+void     or_avx2_tdec_init(void *state);
+int      or_avx2_decode_pair(void *state, const float *inA, const float *inB, uint32_t K, uint32_t max_its,
+                             int early_stop, int crc_type, uint8_t *bitsA, uint8_t *bitsB, int *okA, int *okB,
+                             int *itsA, int *itsB);
+int      or_avx2_decode_batch(const float *in, uint32_t stride, uint32_t n, uint32_t K, uint32_t max_its,
+                              int early_stop, int crc_type, uint8_t *bits, uint32_t *its, uint8_t *ok,
+                              uint32_t nthreads);
 size_t   or_simd_tdec_size(void);
 void     or_simd_tdec_init(void *state);
 int      or_simd_decode_cb(void *state, const float *in, uint32_t K, uint32_t max_its, int early_stop,

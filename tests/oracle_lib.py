@@ -110,6 +110,13 @@ def lib():
                                             C.POINTER(C.c_int)]),
             "or_simd_decode_batch": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                                C.c_int, u8, u32, u8, C.c_uint32]),
+            "or_avx2_available": (C.c_int, []),
+            "or_avx2_tdec_size": (C.c_size_t, []),
+            "or_avx2_decode_pair": (C.c_int, [C.c_void_p, f32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                              u8, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                              C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+            "or_avx2_decode_batch": (C.c_int, [f32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                               C.c_int, u8, u32, u8, C.c_uint32]),
             "or_set_tdec_mode": (None, [C.c_int]),
             "or_get_tdec_mode": (C.c_int, []),
             "or_phich_ngroups": (C.c_uint32, [C.c_uint32, C.c_uint32]),
@@ -199,7 +206,25 @@ def lib():
 # ------------------------------------------------------------------ convenience wrappers
 TDEC_STATE_BYTES = 4 + 4 * 6144 * 2 + 4 * 6144 * 3 + 4 * 6147 * 2 + 4 * 6148 * 8
 TDEC16_STATE_BYTES = TDEC_STATE_BYTES + 4 * (3 * 6144 + 12)
-TDEC_GEN, TDEC_I16, TDEC_SIMD = 0, 1, 2
+TDEC_GEN, TDEC_I16, TDEC_SIMD, TDEC_AVX2 = 0, 1, 2, 3
+
+
+def avx2_decode_pair(llr_a, llr_b, K, max_its=8, early_stop=True, crc24a=False, state=None):
+    """Two equal-K code blocks through the AVX2 decoder (o_avx2.c; llr_b None: A alone).
+    Returns [(bits, its, ok)] per block."""
+    L = lib()
+    st = state if state is not None else C.create_string_buffer(L.or_avx2_tdec_size() + 64)
+    ba, bb = np.zeros(K, np.uint8), np.zeros(K, np.uint8)
+    oka, okb, ia, ib = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    a = np.ascontiguousarray(llr_a, np.float32)
+    b = None if llr_b is None else np.ascontiguousarray(llr_b, np.float32)
+    assert L.or_avx2_decode_pair(st, a, None if b is None else b.ctypes.data, K, max_its, int(early_stop), int(crc24a),
+                                 ba, None if b is None else bb.ctypes.data, C.byref(oka), C.byref(okb), C.byref(ia),
+                                 C.byref(ib)) == 0
+    out = [(ba, ia.value, bool(oka.value))]
+    if b is not None:
+        out.append((bb, ib.value, bool(okb.value)))
+    return out
 
 
 class Tdec:
