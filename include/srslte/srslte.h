@@ -118,6 +118,8 @@ typedef struct SRSLTE_API {
   float **buffer_f;       /* kept for layout compatibility; NULL (soft bits are device resident) */
   void *dev;              /* device arena: 2 groups x [N_cb][64] floats (K- and K+ code blocks) */
   uint64_t dev_bytes;
+  uint32_t reset_pending; /* reset / reset_tbs since the last decode: the decode clears the arena first, on its own
+                             stream (a reset has no stream of its own to order it with the decoding instance's) */
 } srslte_softbuffer_rx_t;
 
 typedef struct SRSLTE_API {

@@ -193,8 +193,8 @@ int mi_dl_batch_replan(mi_dl_batch_t* b, mi_dl_plan_t* p, void* stream) {
   }
   const size_t had = b->eng.d_sb.bytes;
   if (b->eng.upload(st, true)) return -1;
-  // (a reallocated softbuffer was zeroed by upload)
-  if (!had || b->eng.d_sb.bytes != had) return 0;
+  // (a first softbuffer was zeroed by upload; a grown one keeps its contents and zeroes only its new tail)
+  if (!had) return 0;
   for (const auto& c : clear)
     if (!mi::hip_ok(hipMemsetAsync(b->eng.d_sb.as<float>() + c.first, 0, c.second * sizeof(float), st),
                     "replan softbuffer reset"))

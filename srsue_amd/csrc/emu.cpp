@@ -400,3 +400,73 @@ extern "C" size_t emu_payload_offset(const mi_dl_sf_cfg_t* cfgs, uint32_t n, uin
   if (P.build(cfgs, n, true)) return 0;
   return P.tbs[sf].pay_off;
 }
+
+// The packed decoder's trellis start (tdec_p2_body.h header, p2.h tadd_a): the LLRs of steps 0..2 taken from the start
+// state with the saturating alpha adds and no masking of the unreachable states, against the float recursion with -inf
+// (the oracle's semantics, oracle/o_fec.c), at adversarial magnitudes -- inputs drawn at the quantiser's clamps half of
+// the time and beta vectors from backward recursions over such inputs (the running beta of phase 2: 0..3 unnormalised
+// steps after a window normalisation).  ninf: the start value of the unreachable alpha states (the product's is
+// Metric<P2>::ninf_alpha(), -32768; a weaker one must fail, which shows the draws reach the margin).  Returns the number
+// of (trial, step, half) LLRs -- of llr_step and of alpha_step -- that differ.
+extern "C" uint64_t emu_p2_start_llr_check(uint64_t seed, uint32_t trials, int ninf) {
+  uint64_t st = seed | 1u, bad = 0;
+  auto rnd = [&]() {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint32_t)(st >> 33);
+  };
+  auto pick = [&](int lim) {
+    const uint32_t r = rnd();
+    if (r & 1u) return (r & 2u) ? lim : -lim;
+    return (int)(rnd() % (uint32_t)(2 * lim + 1)) - lim;
+  };
+  const int XS = 1535, XP = (int)mi::I16_CI;   // DEC2's systematic clamp (DEC1: 511 + 1023), the parity quantiser
+  for (uint32_t t = 0; t < trials; t++) {
+    float bf[2][8], xsf[2][3], xpf[2][3];
+    for (int h = 0; h < 2; h++) {
+      for (int s = 0; s < 8; s++) bf[h][s] = 0.f;
+      const int n = 4 + 4 * (int)(rnd() % 4), extra = (int)(rnd() % 4);
+      for (int i = 0; i < n + extra; i++) {
+        float nb[8];
+        mi::beta_step<false>(bf[h], (float)pick(XS), (float)pick(XP), nb);
+        for (int s = 0; s < 8; s++) bf[h][s] = nb[s];
+        if (i < n && (i & 3) == 3) mi::norm8<true>(bf[h]);
+      }
+      for (int k = 0; k < 3; k++) {
+        xsf[h][k] = (float)pick(XS);
+        xpf[h][k] = (float)pick(XP);
+      }
+    }
+    mi::P2 bp[8], ap[8];
+    float af[2][8];
+    for (int s = 0; s < 8; s++) {
+      bp[s] = mi::p2_make((int)bf[0][s], (int)bf[1][s]);
+      ap[s] = s ? mi::p2_make(ninf, ninf) : mi::Metric<mi::P2>::zero();
+      for (int h = 0; h < 2; h++) af[h][s] = s ? -INFINITY : 0.f;
+    }
+    for (int k = 0; k < 3; k++) {
+      const mi::P2 xs = mi::p2_make((int)xsf[0][k], (int)xsf[1][k]), xp = mi::p2_make((int)xpf[0][k], (int)xpf[1][k]);
+      const mi::P2 lp = mi::llr_step(ap, bp, xs, xp);
+      mi::P2 ap2[8];
+      for (int s = 0; s < 8; s++) ap2[s] = ap[s];
+      const mi::P2 lp2 = mi::alpha_step<false>(ap2, bp, xs, xp);
+      for (int h = 0; h < 2; h++) {
+        float a2[8];
+        for (int s = 0; s < 8; s++) a2[s] = af[h][s];
+        const float lf = mi::alpha_step<false>(a2, bf[h], xsf[h][k], xpf[h][k]);
+        const int lo = h ? mi::p2_hi(lp) : mi::p2_lo(lp), lo2 = h ? mi::p2_hi(lp2) : mi::p2_lo(lp2);
+        bad += (float)lo != lf;
+        bad += (float)lo2 != lf;
+      }
+      // both recursions one step on (the next step's alpha), the reachable states checked on the way
+      mi::alpha_fwd<false>(ap, xs, xp);
+      for (int h = 0; h < 2; h++) {
+        mi::alpha_fwd<false>(af[h], xsf[h][k], xpf[h][k]);
+        for (int s = 0; s < 8; s++)
+          if (af[h][s] != -INFINITY) bad += (float)(h ? mi::p2_hi(ap[s]) : mi::p2_lo(ap[s])) != af[h][s];
+      }
+      // and the beta of the next (lower) step from this one's inputs, as phase 2 walks backwards -- kept as drawn: any
+      // vector of bounded spread stands for beta_{k+1}
+    }
+  }
+  return bad;
+}

@@ -169,9 +169,20 @@ int Engine::ensure_work(hipStream_t st, bool alloc_sb) {
   bool ok = true;
   for (const auto& w : work_set()) ok = ok && w.first->ensure(w.second);
   if (ok && (P.has_pdsch || P.cb_n) && alloc_sb) {
-    size_t before = d_sb.bytes;
-    ok = d_sb.ensure(P.sb_floats * 4);
-    if (ok && d_sb.bytes != before) ok = hip_ok(hipMemsetAsync(d_sb.p, 0, d_sb.bytes, st), "memset sb");
+    // the softbuffer arena grows keeping its contents: a re-plan decides per group what is cleared (batch.cpp
+    // mi_dl_batch_replan), so the groups whose layout is unchanged keep combining across the reallocation
+    const size_t before = d_sb.bytes;
+    if (before && P.sb_floats * 4 > before && !d_sb.view) {
+      DevBuf grown;
+      ok = grown.ensure(P.sb_floats * 4) &&
+           hip_ok(hipMemcpyAsync(grown.p, d_sb.p, before, hipMemcpyDeviceToDevice, st), "sb keep") &&
+           hip_ok(hipMemsetAsync(grown.as<char>() + before, 0, grown.bytes - before, st), "memset sb tail") &&
+           hip_ok(hipStreamSynchronize(st), "sb keep");   // the old arena is freed below
+      if (ok) d_sb.swap(grown);
+    } else {
+      ok = d_sb.ensure(P.sb_floats * 4);
+      if (ok && d_sb.bytes != before) ok = hip_ok(hipMemsetAsync(d_sb.p, 0, d_sb.bytes, st), "memset sb");
+    }
   }
   return ok ? 0 : -1;
 }

@@ -42,6 +42,8 @@ __device__ inline P2 operator+(P2 a, P2 b) { return P2{a.v + b.v}; }
 __device__ inline P2 operator-(P2 a, P2 b) { return P2{a.v - b.v}; }
 __device__ inline P2 fmaxf(P2 a, P2 b) { return P2{__builtin_elementwise_max(a.v, b.v)}; }
 __device__ inline P2 p2_min(P2 a, P2 b) { return P2{__builtin_elementwise_min(a.v, b.v)}; }
+// saturating add (v_pk_add_i16 with clamp: the same rate as the wrapping add)
+__device__ inline P2 p2_adds(P2 a, P2 b) { return P2{__builtin_elementwise_add_sat(a.v, b.v)}; }
 #else
 struct P2 {
   int16_t lo, hi;
@@ -56,21 +58,30 @@ inline P2 operator+(P2 a, P2 b) { return P2{(int16_t)(a.lo + b.lo), (int16_t)(a.
 inline P2 operator-(P2 a, P2 b) { return P2{(int16_t)(a.lo - b.lo), (int16_t)(a.hi - b.hi)}; }
 inline P2 fmaxf(P2 a, P2 b) { return P2{a.lo > b.lo ? a.lo : b.lo, a.hi > b.hi ? a.hi : b.hi}; }
 inline P2 p2_min(P2 a, P2 b) { return P2{a.lo < b.lo ? a.lo : b.lo, a.hi < b.hi ? a.hi : b.hi}; }
+inline int16_t p2_sat16(int x) { return (int16_t)(x < -32768 ? -32768 : (x > 32767 ? 32767 : x)); }
+inline P2 p2_adds(P2 a, P2 b) { return P2{p2_sat16(a.lo + b.lo), p2_sat16(a.hi + b.hi)}; }
 #endif
 // clamp both halves to [-c, c]
 MI_P2D inline P2 p2_clamp(P2 a, int c) { return p2_min(fmaxf(a, p2_splat(-c)), p2_splat(c)); }
 
-// the additive identity / "minus infinity" of a metric type: -16384 can never win a maximum against a
-// reachable state (those stay above -6138 - 3 x 2046) and cannot wrap within the three steps after which
-// every state is reachable
+// the additive identity / "minus infinity" of a metric type.  Beta (the tail's start, wrapping adds): -16384 can never
+// win a maximum against a reachable state (those stay above -6138 - 3 x 2046) and cannot wrap within the three steps
+// after which every state is reachable.  Alpha (the trellis start state): -32768 with SATURATING adds on the alpha side
+// (tadd_a below), which also keeps the unreachable states out of the LLR maxima of steps 0..2 (tdec_p2_body.h)
 template <class T> struct Metric;
 template <> struct Metric<float> {
   __host__ __device__ static float zero() { return 0.0f; }
   __host__ __device__ static float ninf() { return -INFINITY; }
+  __host__ __device__ static float ninf_alpha() { return -INFINITY; }
 };
 template <> struct Metric<P2> {
   MI_P2D static P2 zero() { return p2_splat(0); }
   MI_P2D static P2 ninf() { return p2_splat(-16384); }
+  MI_P2D static P2 ninf_alpha() { return p2_splat(-32768); }
 };
+// the adds that take an alpha metric (alpha + gamma, alpha + gamma + beta): plain for the float decoders, saturating
+// for P2.  Every reachable value stays inside +-14R = +-28644 (tdec_p2_body.h), where both adds agree bit for bit.
+MI_P2D inline float tadd_a(float a, float b) { return a + b; }
+MI_P2D inline P2 tadd_a(P2 a, P2 b) { return p2_adds(a, b); }
 
 }  // namespace mi

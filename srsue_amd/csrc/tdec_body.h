@@ -133,8 +133,8 @@ MI_HD inline T alpha_step(T (&al)[8], const T (&bn)[8], T xs, T xp) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const int z = tr_par(s, u);
-      c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
-      T t = c[s][u] + bn[tr_next(s, u)];
+      c[s][u] = (u || z) ? tadd_a(al[s], gam(u, z, xs, xp, luz)) : al[s];
+      T t = tadd_a(c[s][u], bn[tr_next(s, u)]);
       t8[u][s] = t;
       if constexpr (!LLR_TREE<T>) {
         if (u) m1 = s ? fmaxf(m1, t) : t; else m0 = s ? fmaxf(m0, t) : t;
@@ -682,7 +682,7 @@ MI_HD inline void alpha_fwd(T (&al)[8], T xs, T xp) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const int z = tr_par(s, u);
-      c[s][u] = (u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s];
+      c[s][u] = (u || z) ? tadd_a(al[s], gam(u, z, xs, xp, luz)) : al[s];
     }
   T na[8];
 #pragma unroll
@@ -713,7 +713,7 @@ MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int z = tr_par(s, u);
-        const T t = ((u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s]) + bn[tr_next(s, u)];
+        const T t = tadd_a((u || z) ? tadd_a(al[s], gam(u, z, xs, xp, luz)) : al[s], bn[tr_next(s, u)]);
         m[u][n & 1] = n < 2 ? t : fmaxf(m[u][n & 1], t);
       }
       n++;
@@ -730,7 +730,7 @@ MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const int z = tr_par(s, u);
-      const T t = ((u || z) ? al[s] + gam(u, z, xs, xp, luz) : al[s]) + bn[tr_next(s, u)];
+      const T t = tadd_a((u || z) ? tadd_a(al[s], gam(u, z, xs, xp, luz)) : al[s], bn[tr_next(s, u)]);
       if (u) { m1 = f1 ? t : fmaxf(m1, t); f1 = false; }
       else { m0 = f0 ? t : fmaxf(m0, t); f0 = false; }
     }

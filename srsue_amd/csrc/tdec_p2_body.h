@@ -13,10 +13,16 @@
 // oracle/o_fec.c: normalised metrics +-3R, R = 2046; with the once-per-window normalisation of
 // tdec_body.h a candidate alpha + gamma + beta stays inside +-14R = +-28644 and an LLR inside +-13R),
 // so the wrapping packed adds are exact.  The one exception is the "-inf" of the unreachable start
-// states: the packed decoder uses the finite -16384 (p2.h Metric<P2>::ninf), which loses every maximum
-// of the alpha / beta recursions against a reachable state, but could win or wrap in an LLR term whose
-// beta side is large -- so the LLRs of steps 0, 1 and 2 (the only ones with unreachable alpha states)
-// leave those states out of their maxima (llr_step<REACH>), exactly as -inf would.
+// states.  Beta (the tail's start) uses the finite -16384 (p2.h Metric<P2>::ninf), which loses every maximum of
+// the beta recursion against a reachable state.  Alpha (the trellis start) uses -32768 (Metric<P2>::ninf_alpha)
+// and every add that takes an alpha metric saturates (p2.h tadd_a: v_pk_add_i16 with clamp, the same rate), so an
+// unreachable state also drops out of the LLR maxima of steps 0, 1 and 2 (the only ones with unreachable alpha
+// states), exactly as -inf would: at step k <= 2 an unreachable candidate alpha + gamma + beta is at most
+// -32768 + (k + 1) R + beta(s') and a reachable one at least -(k + 1) R + beta(s''), and beta's spread over the states
+// is at most 3R (any state reaches any other in 3 steps, oracle/o_fec.c), so the unreachable one is lower by at
+// least 32768 - (2k + 5) R >= 14,354.  Reachable values never reach the clamp (+-14R), where the saturating and
+// the wrapping add agree.  One code path therefore serves window 0 and every other window (no REACH-masked LLR
+// variants: the specialised copies held the kernel's register peak).
 //
 // Per-code-block early stop: a lane iterates while either of its code blocks is undecided.  After each
 // iteration one pass over the decision rows (tdec_p2_check, on wave F) packs the bytes of every code block
@@ -331,9 +337,9 @@ MI_HD inline void p2_alpha_window(const TdecArgsP2& a, int lane, const TdecWinP2
     p2_emit<DEC2>(a, lane, base, i, w.pk[i], alpha_step<false>(al, bw[i], xs[i], xp[i]), p2_emit_x<DEC2>(w, xs, i));
   norm8<true>(al);
 }
-// wave B, phase 2: alpha of the window recomputed from its opening checkpoint (window 0: the start
-// state), then backward steps emitting the LLRs.  FIRST_WIN (window 0): steps 0..2 have unreachable
-// alpha states, left out of their LLR maxima.
+// wave B, phase 2: alpha of the window recomputed from its opening checkpoint (FIRST_WIN, window 0: the start
+// state), then backward steps emitting the LLRs (the unreachable start states drop out of the maxima by
+// themselves: p2.h tadd_a)
 template <bool DEC2, bool SQ, bool FIRST_WIN>
 MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecWinP2& w, uint32_t base, P2 (&b)[8]) {
   P2 xs[BETA_W], xp[BETA_W];
@@ -342,7 +348,7 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
   P2 aw[BETA_W][8];
   if constexpr (FIRST_WIN) {
 #pragma unroll
-    for (int s = 0; s < 8; s++) aw[0][s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+    for (int s = 0; s < 8; s++) aw[0][s] = s ? Metric<P2>::ninf_alpha() : Metric<P2>::zero();
   } else {
     p2_ck_vec(w, aw[0]);
   }
@@ -354,12 +360,7 @@ MI_HD inline void p2_beta_emit_window(const TdecArgsP2& a, int lane, const TdecW
   }
 #pragma unroll
   for (int i = BETA_W - 1; i >= 0; i--) {
-    P2 llr;
-    // reachable alpha states at steps 0, 1, 2 from state 0 (tr_next: 0 -> {0, 4} -> {0, 2, 4, 6})
-    if (FIRST_WIN && i == 0) llr = llr_step<0x01u>(aw[i], b, xs[i], xp[i]);
-    else if (FIRST_WIN && i == 1) llr = llr_step<0x11u>(aw[i], b, xs[i], xp[i]);
-    else if (FIRST_WIN && i == 2) llr = llr_step<0x55u>(aw[i], b, xs[i], xp[i]);
-    else llr = llr_step(aw[i], b, xs[i], xp[i]);
+    const P2 llr = llr_step(aw[i], b, xs[i], xp[i]);
     p2_emit<DEC2>(a, lane, base, i, w.pk[i], llr, p2_emit_x<DEC2>(w, xs, i));
     P2 nb[8];
     beta_step<false>(b, xs[i], xp[i], nb);
@@ -496,25 +497,12 @@ MI_HD inline void p2_alpha_run_from(P2 (&v)[8], const P2 (&s)[8], const TdecX8P2
 }
 // wave F, phase 2, one pair: B(j) = beta_{base + j}, B(8) = the checkpoint; LLR i from alpha_i and B(i + 1).
 // HAVE4: B(4) was computed on the way (a 16-step span's upper pair, TdecP2X::f2) and comes in B4in
-// FIRST_WIN (steps 0..7 from the start state; the segmented continuation, p2s_fwd): the LLRs of steps 0..2 leave the
-// unreachable alpha states out of their maxima (p2_beta_emit_window)
-template <int I, bool FIRST_WIN>
-MI_HD inline P2 p2_alpha_llr(P2 (&al)[8], const P2 (&bn)[8], P2 xs, P2 xp) {
-  if constexpr (FIRST_WIN && I < 3) {
-    constexpr uint32_t REACH = I == 0 ? 0x01u : I == 1 ? 0x11u : 0x55u;
-    const P2 llr = llr_step<REACH>(al, bn, xs, xp);
-    alpha_fwd<false>(al, xs, xp);
-    return llr;
-  } else {
-    return alpha_step<false>(al, bn, xs, xp);
-  }
-}
-template <bool DEC2, bool HAVE4 = false, bool FIRST_WIN = false, bool DIRECT = false>
+template <bool DEC2, bool HAVE4 = false, bool DIRECT = false>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
                                    P2 (&al)[8], const P2 (&B4in)[8] = P2_NO_VEC) {
   P2 B4[8], Bm[8], Bt[8];
 #define emit(I, BN) \
-  p2_emit<DEC2>(a, lane, base, I, x.pk[I], p2_alpha_llr<I, FIRST_WIN>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
+  p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
   // chains from B8: B(4) (without HAVE4) directly, B(6) and B(7) from copies; from B(4): B(3) directly, B(2) from a
   // copy; B(1) and B(5) directly from B(2) and B(6)
   if constexpr (HAVE4) {
@@ -557,15 +545,10 @@ MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2
 #undef emit
 }
 // LLR of step I from alpha_I (av) and the running beta_{I + 1}, then beta_I
-template <bool DEC2, bool FIRST_WIN, int I>
+template <bool DEC2, int I>
 MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&av)[8], uint32_t base,
                                    P2 (&b)[8]) {
-  P2 llr;
-  // reachable alpha states at steps 0, 1, 2 from state 0 (p2_beta_emit_window)
-  if (FIRST_WIN && I == 0) llr = llr_step<0x01u>(av, b, x.xs[I], x.xp[I]);
-  else if (FIRST_WIN && I == 1) llr = llr_step<0x11u>(av, b, x.xs[I], x.xp[I]);
-  else if (FIRST_WIN && I == 2) llr = llr_step<0x55u>(av, b, x.xs[I], x.xp[I]);
-  else llr = llr_step(av, b, x.xs[I], x.xp[I]);
+  const P2 llr = llr_step(av, b, x.xs[I], x.xp[I]);
   p2_emit<DEC2>(a, lane, base, I, x.pk[I], llr, p2_emit_x8<DEC2>(x, I));
   P2 nb[8];
   beta_step<false>(b, x.xs[I], x.xp[I], nb);
@@ -574,11 +557,11 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
 // wave B, phase 2, one pair: A(j) = alpha_{base + j}, A(0) = the checkpoint (pair 0: the start state);
 // LLR i from A(i) and beta_{base + i + 1} (the running b).  HAVE4: A(4) was computed on the way (a 16-step span's lower
 // pair, TdecP2X::b2) and comes in A4in
-template <bool DEC2, bool FIRST_WIN, bool HAVE4 = false, bool DIRECT = false>
+template <bool DEC2, bool HAVE4 = false, bool DIRECT = false>
 MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
                                        uint32_t base, P2 (&b)[8], const P2 (&A4in)[8] = P2_NO_VEC) {
   P2 A4[8], Am[8], At[8];
-#define emit(I, AV) p2_llr_emit_back<DEC2, FIRST_WIN, I>(a, lane, x, AV, base, b)
+#define emit(I, AV) p2_llr_emit_back<DEC2, I>(a, lane, x, AV, base, b)
   // the mirror of p2_alpha_window8: from A0, A(4) (without HAVE4) directly, A(2) and A(1) from copies; from A(4), A(5)
   // directly, A(6) from a copy; A(7) and A(3) directly from A(6) and A(2)
   if constexpr (HAVE4) {
@@ -714,9 +697,14 @@ MI_HD inline void p2_stash_get(const TdecArgsP2& a, const uint32_t* st, int lane
     v4[s] = p2_from_bits(p2_stash_ld(st, P2_STASH_V4 + s - 1, lane));
   }
 }
+// the tail's start vector (beta, wrapping adds) and the trellis start state (alpha, saturating adds: p2.h)
 MI_HD inline void p2_start(P2 (&v)[8]) {
 #pragma unroll
   for (int s = 0; s < 8; s++) v[s] = s ? Metric<P2>::ninf() : Metric<P2>::zero();
+}
+MI_HD inline void p2_start_alpha(P2 (&v)[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; s++) v[s] = s ? Metric<P2>::ninf_alpha() : Metric<P2>::zero();
 }
 
 // the four phase bodies of one constituent decoder (tdec_body.h TdecX, register form)
@@ -760,7 +748,7 @@ struct TdecP2X {
   MI_P2_INL static void f1(const TdecArgsP2& a, int lane, P2 (&al)[8]) {
     const uint32_t h = a.K / (2 * BETA_W);
     const size_t ck = (size_t)2 * a.K;
-    p2_start(al);
+    p2_start_alpha(al);
     pipe_windows<PF, Win>(
         (int)h, [](int i) { return (uint32_t)i; }, [&](uint32_t w, Win& r) { load1(a, lane, w, r); },
         [&](const Win& r, uint32_t w) {
@@ -800,10 +788,10 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < ns ? w0 + 6 : w0 + 2;   // the last span reloads its upper pair (unused)
           load8(a, lane, wn, wn + 2, true, r);
           MI_SCHED_FENCE();
-          p2_alpha_window8<DEC2, false, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
+          p2_alpha_window8<DEC2, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
           MI_SCHED_FENCE();
           p2_stash_get<DEC2, FIRST>(a, a.stash, lane, (w0 + 2) * BETA_W, x, B16, B8);
-          p2_alpha_window8<DEC2, true, false, DIRECT>(a, lane, x, B16, (w0 + 2) * BETA_W, al, B8);
+          p2_alpha_window8<DEC2, true, DIRECT>(a, lane, x, B16, (w0 + 2) * BETA_W, al, B8);
         }
       }
       // pairs (w1 + 2j, w1 + 2j + 1), beta checkpoint w1 + 2j + 2; an odd count leaves window nw - 1 alone
@@ -821,7 +809,7 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < np ? w0 + 2 : w0;   // the last pair reloads itself (unused)
           load8(a, lane, wn, wn + 2, true, r);
           MI_SCHED_FENCE();
-          p2_alpha_window8<DEC2, false, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
+          p2_alpha_window8<DEC2, false, DIRECT>(a, lane, x, B8, w0 * BETA_W, al);
         }
       }
       if (n & 1u) {
@@ -909,7 +897,7 @@ struct TdecP2X {
           P2 A0[8], A8[8];
           p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
           if (w0) p2_ck_vec(r.ck, A0);
-          else p2_start(A0);
+          else p2_start_alpha(A0);
           MI_SCHED_FENCE();
           load8(a, lane, w0 + 2, 0, false, r);   // the upper pair
           MI_SCHED_FENCE();
@@ -924,11 +912,10 @@ struct TdecP2X {
           const uint32_t wn = j + 1 < ns ? w0 - 4 : w0;   // the last span reloads its lower pair (unused)
           load8(a, lane, wn, wn, true, r);
           MI_SCHED_FENCE();
-          p2_beta_emit_window8<DEC2, false, false, DIRECT>(a, lane, x, A8, (w0 + 2) * BETA_W, b);
+          p2_beta_emit_window8<DEC2, false, DIRECT>(a, lane, x, A8, (w0 + 2) * BETA_W, b);
           MI_SCHED_FENCE();
           p2_stash_get<DEC2, FIRST>(a, a.stash, lane, w0 * BETA_W, x, A0, A8);
-          if (w0) p2_beta_emit_window8<DEC2, false, true, DIRECT>(a, lane, x, A0, w0 * BETA_W, b, A8);
-          else p2_beta_emit_window8<DEC2, true, true, DIRECT>(a, lane, x, A0, 0, b, A8);
+          p2_beta_emit_window8<DEC2, true, DIRECT>(a, lane, x, A0, w0 * BETA_W, b, A8);
         }
       }
       // pairs (wlo - 2j - 2, wlo - 2j - 1), alpha checkpoint wlo - 2j - 2 (0: the start state); an odd wlo leaves
@@ -943,13 +930,12 @@ struct TdecP2X {
           P2 A0[8];
           p2_cvt8<DEC2, SQF>(a, r, w0 * BETA_W, x);
           if (w0) p2_ck_vec(r.ck, A0);
-          else p2_start(A0);
+          else p2_start_alpha(A0);
           MI_SCHED_FENCE();
           const uint32_t wn = j + 1 < np ? w0 - 2 : w0;   // the last pair reloads itself (unused)
           load8(a, lane, wn, wn, true, r);
           MI_SCHED_FENCE();
-          if (w0) p2_beta_emit_window8<DEC2, false, false, DIRECT>(a, lane, x, A0, w0 * BETA_W, b);
-          else p2_beta_emit_window8<DEC2, true, false, DIRECT>(a, lane, x, A0, 0, b);
+          p2_beta_emit_window8<DEC2, false, DIRECT>(a, lane, x, A0, w0 * BETA_W, b);
         }
       }
       if (wlo & 1u) {
@@ -1356,13 +1342,12 @@ MI_P2_INL void p2s_fwd8(const TdecArgsP2& a, int lane, const P2Seg& g, const P2S
   P2 B8[8];
   if (c + 1 < g.e / P2S_SPAN) p2s_ck_get(a, c + 1, lane, B8);
   else p2s_vld(V.bvec, g.j, lane, B8);
-  if (c == 0) p2_alpha_window8<DEC2, false, true>(a, lane, x, B8, 0, al);
-  else p2_alpha_window8<DEC2>(a, lane, x, B8, c * P2S_SPAN, al);
+  p2_alpha_window8<DEC2>(a, lane, x, B8, c * P2S_SPAN, al);
 }
 template <bool DEC2>
 MI_P2_INL void p2s_fwd_first(const TdecArgsP2& a, int lane, const P2Seg& g, const P2SegVecs& V) {
   P2 al[8];
-  if (g.j == 0) p2_start(al);
+  if (g.j == 0) p2_start_alpha(al);
   else p2_zero8(al);
   p2s_vst(V.avec, g.j, lane, al);
   const uint32_t K8 = a.K / P2S_SPAN;

@@ -200,8 +200,11 @@ void srslte_softbuffer_rx_free(srslte_softbuffer_rx_t* q) {
   if (q) memset(q, 0, sizeof(*q));
 }
 void srslte_softbuffer_rx_reset(srslte_softbuffer_rx_t* q) {
-  // == RX_NULL everywhere (srsLTE's reset returns nothing: a failure is left in mi_last_error)
-  if (q && q->dev) (void)mi::hip_ok(hipMemset(q->dev, 0, q->dev_bytes), "softbuffer reset");
+  // == RX_NULL everywhere from the next decode on.  The clear itself runs on the decoding instance's stream, ordered
+  // before that decode (srslte_pdsch_decode_rnti): a memset here would run on the null stream, which the instances'
+  // non-blocking streams do not wait for -- beside other workers' decodes it could still be clearing while the next
+  // decode combined into the arena
+  if (q) q->reset_pending = 1;
 }
 void srslte_softbuffer_rx_reset_tbs(srslte_softbuffer_rx_t* q, uint32_t /*tbs*/) {
   // srsLTE resets the rows of the TB's code blocks; the arena only ever holds one TB
@@ -375,6 +378,11 @@ int srslte_pdsch_decode_rnti(srslte_pdsch_t* q, srslte_pdsch_cfg_t* cfg, srslte_
   if (c->eng.plan.sb_floats * sizeof(float) > softbuffer->dev_bytes) return fail_sync(c);
   bool ok = device_grid(c, cell, sf_symbols, ce);
   if (!ok) return fail_sync(c);
+  if (softbuffer->reset_pending) {   // srslte_softbuffer_rx_reset since the last decode: RX_NULL, ordered on this stream
+    if (!mi::hip_ok(hipMemsetAsync(softbuffer->dev, 0, softbuffer->dev_bytes, c->st), "softbuffer reset"))
+      return fail_sync(c);
+    softbuffer->reset_pending = 0;
+  }
   c->prof.mark(8, c->st);
   const uint32_t stages = (1u << MI_DL_STAGE_DEMAP) | (1u << MI_DL_STAGE_RM) | (1u << MI_DL_STAGE_TDEC) |
                           (1u << MI_DL_STAGE_TB);

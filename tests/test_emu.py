@@ -226,3 +226,56 @@ def test_emulated_packed_payload_at_misaligned_base(built, base):
             ok, opay, onoi, _ = oracle_dlsch(c, llrs[i])
         assert ok and bool(eok[i]), i
         assert np.array_equal(pe[offs[i]:offs[i] + c.tbs // 8], opay), i
+
+
+def test_packed_start_state_llrs_without_masking():
+    """The packed decoder drops the REACH-masked LLR copies of window 0 (tdec_p2_body.h header): the unreachable alpha
+    start states hold -32768 and every add that takes an alpha metric saturates (p2.h tadd_a), so they lose every LLR
+    maximum of steps 0..2 by themselves.  200,000 adversarial draws (inputs at the quantiser clamps half of the time,
+    beta vectors from recursions over such inputs) of llr_step and alpha_step against the float recursion with -inf,
+    both halves: no difference.  A start value of -4096 differs in many draws, so the draws do reach the margin (the
+    bound, -32768 + 9 R with R = 2046, is what makes -32768 safe for every input the decoder can form)."""
+    f = abi.emu().emu_p2_start_llr_check
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint32, C.c_int]
+    assert f(0x5EED, 200000, -32768) == 0
+    assert f(0x5EED, 20000, -4096) > 0
+
+
+def test_emulated_packed_pairs_at_clamp_magnitudes(built):
+    """The packed decoder on channel LLRs scaled so that most quantised inputs sit at the clamp (+-511) -- the largest
+    branch metrics and metric spreads the int16 design admits, where the saturating alpha adds and the unmasked start
+    window would first show a difference -- against the oracle's int16 decoder: payload, CRC, iterations, per code
+    block."""
+    cfgs = [abi.sf_cfg(nof_prb=100, sf_idx=1 + i % 4, tbs=75376, Qm=6, rnti=0x46 + i) for i in range(6)]   # 78 CBs: a pair
+    iqs = [abi.tx_subframe(c, tb_bytes(80 + i, c.tbs), snr_db=17.0 + 0.5 * (i % 4), seed=40 + i)
+           for i, c in enumerate(cfgs)]
+    llrs = [(oracle_front(c, iq)[3] * 60.0).astype(np.float32) for c, iq in zip(cfgs, iqs)]
+    arr = abi.cfg_array(cfgs)
+    n = len(cfgs)
+    offs = [abi.emu().emu_payload_offset(C.cast(arr, C.c_void_p), n, i) for i in range(n)]
+    pe = np.zeros(offs[-1] + cfgs[-1].tbs // 8, np.uint8)
+    eok = np.zeros(n, np.uint32)
+    eits = np.zeros(n, np.uint32)
+    cbits = np.zeros(64 * 2, np.uint32)
+    flat = np.concatenate(llrs)   # held: ctypes.data of a temporary would dangle
+    E = abi.emu()
+    E.emu_set_tdec_i16(1)
+    E.emu_set_tdec_x(3)
+    try:
+        rc = E.emu_decode_llr(C.cast(arr, C.c_void_p), n, flat.ctypes.data, 4, pe.ctypes.data,
+                              eok.ctypes.data, eits.ctypes.data, cbits.ctypes.data)
+    finally:
+        E.emu_set_tdec_i16(0)
+        E.emu_set_tdec_x(0)
+    assert rc == 0
+    lane = 0
+    for i, c in enumerate(cfgs):
+        with O.tdec_mode(O.TDEC_I16):
+            ok, opay, onoi, ocb = oracle_dlsch_cbits(c, llrs[i])
+        assert bool(eok[i]) == ok, i
+        assert eits[i] == onoi, i
+        assert np.array_equal(pe[offs[i]:offs[i] + c.tbs // 8], opay), i
+        assert np.array_equal(cbits[lane:lane + len(ocb)], ocb), i
+        lane += len(ocb)
+    assert len(set(cbits[:78].tolist())) >= 2
