@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""A/B of cross-stream issue orders for the headline (configs[3] shard: 12,500 x 20 MHz TM1 MCS-28, 4 workspaces on
+4 streams).  Each step is split into its front end (OFDM, channel estimation, fused demap + rate de-matching) and its
+back end (turbo decoder + TB CRC) with mi_dl_batch_run_stages, and HIP events between streams impose an order:
+  base       one run per step, streams round-robin (bench.py's form)
+  split      front + back on the step's stream, no cross-stream order (must equal base)
+  ser_back   the back end of step i waits for the back end of step i - 1 (one decoder launch at a time)
+  ser_front  the front end of step i waits for the front end of step i - 1
+  ser_both   both
+Usage: python tools/sched_ab.py [steps] [reps] [schedules...]  -> one line per (schedule, rep): ms/step, Gbps, CRC-OK
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from srsue_amd import abi  # noqa: E402
+
+FRONT = (1 << 0) | (1 << 1) | (1 << 2) | (1 << 3)
+BACK = (1 << 4) | (1 << 5)
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    scheds = sys.argv[3:] or ["base", "split", "ser_back", "ser_front", "ser_both"]
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    B, S = 12500, 4
+    cfgs = bench.config_cfgs(4, B, 0)
+    pool_iq, pool_tb = bench.make_pool(cfgs[:256], 30.0, 16, 0, None)
+    batches = [abi.Batch(cfgs, max_its=4, profile=False, tdec_i16=True, compact_ce=True) for _ in range(S)]
+    d_iq = torch.empty(2 * batches[0].iq_samples, dtype=torch.float32, device=dev)
+    sfl = len(pool_iq[0])
+    d_pool = torch.from_numpy(np.stack(pool_iq)).to(dev)
+    d_iq.view(B, sfl).copy_(d_pool[torch.arange(B, device=dev) % len(pool_iq)])
+    del d_pool
+    streams = bench.bench_streams(dev, S)
+    sp = [s.cuda_stream for s in streams]
+    bits = sum(c.tbs for c in cfgs)
+
+    def run(sched, n):
+        fe = [None] * n   # front-end done events
+        be = [None] * n   # back-end done events
+        for i in range(n):
+            k = i % S
+            b, st = batches[k], streams[k]
+            if sched == "base":
+                b.run(d_iq.data_ptr(), sp[k])
+                continue
+            if sched in ("ser_front", "ser_both") and i:
+                st.wait_event(fe[i - 1])
+            b.run_stages(FRONT, d_iq.data_ptr(), sp[k])
+            fe[i] = torch.cuda.Event()
+            fe[i].record(st)
+            if sched in ("ser_back", "ser_both") and i:
+                st.wait_event(be[i - 1])
+            b.run_stages(BACK, d_iq.data_ptr(), sp[k])
+            be[i] = torch.cuda.Event()
+            be[i].record(st)
+
+    for sched in scheds:
+        run(sched, 2 * S)
+    torch.cuda.synchronize()
+    for r in range(reps):
+        for sched in scheds:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(sched, steps)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            ok = int(sum(int(b.download(abi.BUF_TB_CRC, np.uint32)[:B].sum()) for b in batches)) / S
+            print(f"{sched:10s} rep {r}: {el / steps * 1e3:.3f} ms/step  {bits * steps / el / 1e9:.1f} Gbps  "
+                  f"crc_ok {ok:.0f}/{B}", flush=True)
+    for b in batches:
+        b.close()
+
+
+if __name__ == "__main__":
+    main()
