@@ -7,6 +7,8 @@ back end (turbo decoder + TB CRC) with mi_dl_batch_run_stages, and HIP events be
   ser_back   the back end of step i waits for the back end of step i - 1 (one decoder launch at a time)
   ser_front  the front end of step i waits for the front end of step i - 1
   ser_both   both
+  stagger    the first S steps start staggered (front end of step i after that of step i - 1), then free-running
+  stagger_b  the first S steps' back ends staggered the same way, then free-running
 Usage: python tools/sched_ab.py [steps] [reps] [schedules...]  -> one line per (schedule, rep): ms/step, Gbps, CRC-OK
 """
 import os
@@ -53,12 +55,12 @@ def main():
             if sched == "base":
                 b.run(d_iq.data_ptr(), sp[k])
                 continue
-            if sched in ("ser_front", "ser_both") and i:
+            if (sched in ("ser_front", "ser_both") or (sched == "stagger" and i < S)) and i:
                 st.wait_event(fe[i - 1])
             b.run_stages(FRONT, d_iq.data_ptr(), sp[k])
             fe[i] = torch.cuda.Event()
             fe[i].record(st)
-            if sched in ("ser_back", "ser_both") and i:
+            if (sched in ("ser_back", "ser_both") or (sched == "stagger_b" and i < S)) and i:
                 st.wait_event(be[i - 1])
             b.run_stages(BACK, d_iq.data_ptr(), sp[k])
             be[i] = torch.cuda.Event()
