@@ -713,7 +713,8 @@ MI_HD inline T llr_step(const T (&al)[8], const T (&bn)[8], T xs, T xp) {
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int z = tr_par(s, u);
-        const T t = tadd_a((u || z) ? tadd_a(al[s], gam(u, z, xs, xp, luz)) : al[s], bn[tr_next(s, u)]);
+        // alpha + (gamma + beta): one saturating add per term, the gamma + beta sums free of the alpha chain
+        const T t = tadd_a(al[s], (u || z) ? gam(u, z, xs, xp, luz) + bn[tr_next(s, u)] : bn[tr_next(s, u)]);
         m[u][n & 1] = n < 2 ? t : fmaxf(m[u][n & 1], t);
       }
       n++;
