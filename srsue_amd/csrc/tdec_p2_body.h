@@ -17,12 +17,14 @@
 // the beta recursion against a reachable state.  Alpha (the trellis start) uses -32768 (Metric<P2>::ninf_alpha)
 // and every add that takes an alpha metric saturates (p2.h tadd_a: v_pk_add_i16 with clamp, the same rate), so an
 // unreachable state also drops out of the LLR maxima of steps 0, 1 and 2 (the only ones with unreachable alpha
-// states), exactly as -inf would: at step k <= 2 an unreachable candidate alpha + gamma + beta is at most
-// -32768 + (k + 1) R + beta(s') and a reachable one at least -(k + 1) R + beta(s''), and beta's spread over the states
-// is at most 3R (any state reaches any other in 3 steps, oracle/o_fec.c), so the unreachable one is lower by at
-// least 32768 - (2k + 5) R >= 14,354.  Reachable values never reach the clamp (+-14R), where the saturating and
-// the wrapping add agree.  One code path therefore serves window 0 and every other window (no REACH-masked LLR
-// variants: the specialised copies held the kernel's register peak).
+// states), exactly as -inf would.  The forward terms are (alpha + gamma) + beta, both adds saturating: at step k <= 2 an
+// unreachable candidate is at most -32768 + (k + 1) R + beta(s') and a reachable one at least -(k + 1) R + beta(s''),
+// and beta's spread over the states is at most 3R (any state reaches any other in 3 steps, oracle/o_fec.c), so the
+// unreachable one is lower by at least 32768 - (2k + 5) R >= 14,354.  The backward terms (llr_step) are
+// alpha + (gamma + beta), one saturating add (the gamma + beta sums stay off the alpha chain): there the spread of
+// gamma + beta is at most 4R and the margin 32768 - (2k + 4) R >= 16,400.  Reachable values never reach the clamp
+// (+-14R), where the saturating and the wrapping add agree.  One code path therefore serves window 0 and every other
+// window (no REACH-masked LLR variants: the specialised copies held the kernel's register peak).
 //
 // Per-code-block early stop: a lane iterates while either of its code blocks is undecided.  After each
 // iteration one pass over the decision rows (tdec_p2_check, on wave F) packs the bytes of every code block
