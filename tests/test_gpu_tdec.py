@@ -157,3 +157,28 @@ def test_segmented_rounds_short_last_segment(built, seg, monkeypatch):
 
 def lib_sched(tb):
     return abi.lib().mi_tdec_turbo_win(tb.h)
+
+
+@pytest.mark.parametrize("max_its", [1, 8])
+@pytest.mark.parametrize("K", [6144, 40])
+def test_packed_at_clamp_magnitudes(built, K, max_its):
+    """The packed decoder's trellis start without masked copies (tdec_p2_body.h header: unreachable alpha states at
+    -32768, saturating alpha adds) on the GPU at the inputs that stress it most: channel LLRs far beyond the quantiser
+    clamp (+-511 after q), a third of them with the wrong sign, so every branch metric and metric spread sits at its
+    int16 design bound -- decisions, iterations and CRC verdicts equal the oracle's int16 decoder.  K = 40: window 0
+    is a fifth of the trellis."""
+    rng = np.random.default_rng(K + max_its)
+    n = 70
+    bits = rng.integers(0, 2, (n, K)).astype(np.uint8)
+    x = np.stack([1.0 - 2.0 * abi.turbo_encode(b, K) for b in bits])
+    flip = rng.random(x.shape) < 0.33
+    llr = (np.where(flip, x, -x) * rng.uniform(20.0, 200.0, x.shape)).astype(np.float32)
+    tb = abi.TdecBatch(K, n, max_its=max_its, early_stop=max_its == 1, tdec_i16=True, sched="p2")
+    d = torch.from_numpy(np.ascontiguousarray(llr)).cuda()
+    tb.run(d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got, its, ok = tb.results()
+    td = O.Tdec(O.TDEC_I16)
+    for i in range(n):
+        dec, oits, ook = td.decode_cb(llr[i], K, max_its=max_its, early_stop=max_its == 1)
+        assert its[i] == oits and bool(ok[i]) == bool(ook), f"cb {i}"
+        assert np.array_equal(got[i], dec), f"cb {i}"
