@@ -502,9 +502,54 @@ MI_HD inline void p2_alpha_run_from(P2 (&v)[8], const P2 (&s)[8], const TdecX8P2
 template <bool DEC2, bool HAVE4 = false, bool DIRECT = false>
 MI_HD inline void p2_alpha_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&B8)[8], uint32_t base,
                                    P2 (&al)[8], const P2 (&B4in)[8] = P2_NO_VEC) {
-  P2 B4[8], Bm[8], Bt[8];
 #define emit(I, BN) \
   p2_emit<DEC2>(a, lane, base, I, x.pk[I], alpha_step<false>(al, BN, x.xs[I], x.xp[I]), p2_emit_x8<DEC2>(x, I))
+  if constexpr (DIRECT) {
+    // sequential chains, every recomputed vector kept until its LLR (round 6): B(4) from B8 (or B4in), then B(3), B(2),
+    // B(1) one step each from the last; after the first four LLRs B(7), B(6), B(5) the same way from B8 -- 10 recursion
+    // steps per pair (6 with HAVE4) instead of 12 (8), one metric vector more live (5 instead of 4).  The chain to B(4)
+    // and the one to B(7) start with the same step from B8, so the second starts from an opaque copy (GVN would
+    // otherwise keep the first chain's B(7), B(6), B(5) live through the first four LLRs)
+    P2 V4[8], V3[8], V2[8], V1[8];
+    if constexpr (HAVE4) {
+      p2_cp8_opaque(V4, B4in);
+    } else {
+      p2_beta_run_from<7, 4, true>(V4, B8, x);
+      norm8<true>(V4);
+    }
+    p2_beta_run_from<3, 3, true>(V3, V4, x);
+    p2_beta_run_from<2, 2, true>(V2, V3, x);
+    p2_beta_run_from<1, 1, true>(V1, V2, x);
+    MI_SCHED_FENCE();
+    emit(0, V1);
+    MI_SCHED_FENCE();
+    emit(1, V2);
+    MI_SCHED_FENCE();
+    emit(2, V3);
+    MI_SCHED_FENCE();
+    emit(3, V4);
+    norm8<true>(al);
+    P2 V7[8], V6[8], V5[8];
+    if constexpr (HAVE4) {
+      p2_beta_run_from<7, 7, true>(V7, B8, x);
+    } else {
+      p2_cp8_opaque(V7, B8);
+      p2_beta_run<7, 7>(V7, x);
+    }
+    p2_beta_run_from<6, 6, true>(V6, V7, x);
+    p2_beta_run_from<5, 5, true>(V5, V6, x);
+    MI_SCHED_FENCE();
+    emit(4, V5);
+    MI_SCHED_FENCE();
+    emit(5, V6);
+    MI_SCHED_FENCE();
+    emit(6, V7);
+    MI_SCHED_FENCE();
+    emit(7, B8);
+    norm8<true>(al);
+    return;
+  }
+  P2 B4[8], Bm[8], Bt[8];
   // chains from B8: B(4) (without HAVE4) directly, B(6) and B(7) from copies; from B(4): B(3) directly, B(2) from a
   // copy; B(1) and B(5) directly from B(2) and B(6)
   if constexpr (HAVE4) {
@@ -562,8 +607,50 @@ MI_HD inline void p2_llr_emit_back(const TdecArgsP2& a, int lane, const TdecX8P2
 template <bool DEC2, bool HAVE4 = false, bool DIRECT = false>
 MI_HD inline void p2_beta_emit_window8(const TdecArgsP2& a, int lane, const TdecX8P2& x, const P2 (&A0)[8],
                                        uint32_t base, P2 (&b)[8], const P2 (&A4in)[8] = P2_NO_VEC) {
-  P2 A4[8], Am[8], At[8];
 #define emit(I, AV) p2_llr_emit_back<DEC2, I>(a, lane, x, AV, base, b)
+  if constexpr (DIRECT) {
+    // the mirror of p2_alpha_window8's sequential chains: A(4) from A0 (or A4in), A(5), A(6), A(7) one step each; after
+    // the LLRs of steps 7..4, A(1), A(2), A(3) from A0 (an opaque copy when the chain to A(4) started from A0 too)
+    P2 V4[8], V5[8], V6[8], V7[8];
+    if constexpr (HAVE4) {
+      p2_cp8_opaque(V4, A4in);
+    } else {
+      p2_alpha_run_from<0, 3, true>(V4, A0, x);
+      norm8<true>(V4);
+    }
+    p2_alpha_run_from<4, 4, true>(V5, V4, x);
+    p2_alpha_run_from<5, 5, true>(V6, V5, x);
+    p2_alpha_run_from<6, 6, true>(V7, V6, x);
+    MI_SCHED_FENCE();
+    emit(7, V7);
+    MI_SCHED_FENCE();
+    emit(6, V6);
+    MI_SCHED_FENCE();
+    emit(5, V5);
+    MI_SCHED_FENCE();
+    emit(4, V4);
+    norm8<true>(b);
+    P2 V1[8], V2[8], V3[8];
+    if constexpr (HAVE4) {
+      p2_alpha_run_from<0, 0, true>(V1, A0, x);
+    } else {
+      p2_cp8_opaque(V1, A0);
+      p2_alpha_run<0, 0>(V1, x);
+    }
+    p2_alpha_run_from<1, 1, true>(V2, V1, x);
+    p2_alpha_run_from<2, 2, true>(V3, V2, x);
+    MI_SCHED_FENCE();
+    emit(3, V3);
+    MI_SCHED_FENCE();
+    emit(2, V2);
+    MI_SCHED_FENCE();
+    emit(1, V1);
+    MI_SCHED_FENCE();
+    emit(0, A0);
+    norm8<true>(b);
+    return;
+  }
+  P2 A4[8], Am[8], At[8];
   // the mirror of p2_alpha_window8: from A0, A(4) (without HAVE4) directly, A(2) and A(1) from copies; from A(4), A(5)
   // directly, A(6) from a copy; A(7) and A(3) directly from A(6) and A(2)
   if constexpr (HAVE4) {
