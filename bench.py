@@ -31,7 +31,11 @@ def hw_queues_arg(argv, env=None):
     rank under RCCL, 8 queues -1.7 % headline and -2 % waterfall, 16 queues level with the plain run)."""
     env = os.environ if env is None else env
     rccl = "--pg" in argv or (int(env.get("WORLD_SIZE", "1") or 1) > 1 and "--share-gpu" not in argv)
-    v = "16" if rccl else "8"
+    # the low-occupancy configs (1: configs[0], 3: configs[2], 5: configs[4]) keep 8-16 batches in flight (main(): their
+    # default streams), each on its own queue
+    cfg = next((argv[i + 1] for i, a in enumerate(argv[:-1]) if a == "--config"), None)
+    cfg = cfg or next((a.split("=", 1)[1] for a in argv if a.startswith("--config=")), "4")
+    v = "16" if rccl or cfg in ("1", "3", "5") else "8"
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):
             v = argv[i + 1]
@@ -1092,8 +1096,8 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="workspaces / HIP streams the steps rotate over (consecutive batches overlap); 1 = serial; "
                          "0 = auto: 4 for the headline shard (+13-15 %%: one batch's front end and rate de-matching run "
-                         "beside the previous batch's turbo decoder; profiles/r3/ab_streams*) and for the low-occupancy "
-                         "configs[2] / configs[4] batches (2.7x / 1.7x), 3 for configs[0] (1.27x; profiles/r2/streams)")
+                         "beside the previous batch's turbo decoder; profiles/r3/ab_streams*), 16 for the low-occupancy "
+                         "configs[2] / configs[4] batches and 8 for configs[0], at 16 hardware queues (profiles/r6/lowocc)")
     ap.add_argument("--iterating-streams", type=int, default=0,
                     help="--streams of the waterfall block; 0 = auto (= --streams: its continuation holds 0.74 "
                          "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
@@ -1145,7 +1149,15 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))                     # before anything touches the GPU
     if args.streams <= 0:
-        args.streams = 4 if args.config in (3, 4, 5) else 3 if args.config == 1 else 1
+        # one batch of the low-occupancy configs holds well under one turbo wavefront per SIMD (configs[2]: 1,000
+        # subframes), so more batches in flight fill the GPU: configs[2] 39 Gbps on 4 streams -> 84 on 16 (with the
+        # packed decoder), configs[4] 27 -> 32, configs[0] 20 -> 21 on 8 (profiles/r6/lowocc); the headline keeps 4 (5
+        # measured slower, and 6 workspaces of its 12,500-subframe shard do not fit in HBM)
+        args.streams = {1: 8, 3: 16, 4: 4, 5: 16}.get(args.config, 1)
+    if args.config == 3 and args.sched == "auto" and args.streams >= 8:
+        # with 8+ batches in flight the streams, not one batch's pairs, fill the SIMDs: the packed decoder's half VALU per
+        # code block wins although one batch alone would pick the crossed lanes (16 streams: 84 vs 65 Gbps)
+        args.sched = "p2"
     if args.config == 2:
         args.sf_per_gpu = 1
     elif args.config == 3 and args.sf_per_gpu == 12500:

@@ -1203,8 +1203,10 @@ MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
       tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
     } else if (it == 0) {
       if (MK == 0) {
-        tdec_p2_xhalf<false, true, SRC_MKQ, CKS>(a, lane, ex);
-        tdec_p2_xhalf<true, true, SRC_Q, CKS>(a, lane, ex);
+        // fixed iteration count (configs[0]): direct recomputation chains in every pass -- 20 VGPRs spill, but only
+        // around the iteration loop; span loops -7.5 % VALU, one launch 29.8-29.9 -> 27.9 ms (profiles/r6/ab_fixed)
+        tdec_p2_xhalf<false, true, SRC_MKQ, CKS, P2_PF_Q, true>(a, lane, ex);
+        tdec_p2_xhalf<true, true, SRC_Q, CKS, P2_PF_Q, true>(a, lane, ex);
       } else {
         tdec_p2_xhalf<false, true, SRC_SB, CKS>(a, lane, ex);
         tdec_p2_xhalf<true, true, SRC_SB, CKS>(a, lane, ex);
@@ -1216,8 +1218,8 @@ MI_P2_INL TdecP2Result tdec_p2_lane(const TdecArgsP2& a, int lane, Exec& ex) {
       tdec_p2_xhalf<false, false, SRC_MKQ, CKS>(a, lane, ex);
       tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
     } else {
-      tdec_p2_xhalf<false, false, SRC_Q, CKS>(a, lane, ex);
-      tdec_p2_xhalf<true, false, SRC_Q, CKS>(a, lane, ex);
+      tdec_p2_xhalf<false, false, SRC_Q, CKS, P2_PF_Q, MK == 0>(a, lane, ex);
+      tdec_p2_xhalf<true, false, SRC_Q, CKS, P2_PF_Q, MK == 0>(a, lane, ex);
     }
     const bool last = it + 1 == a.max_its;
     uint32_t ok = 0u;
