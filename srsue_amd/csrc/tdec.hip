@@ -271,11 +271,16 @@ void launch_tdec_p2(const float* sb, const uint32_t* wm, float* scratch, uint8_t
 
 // ---- waterfall compaction (tdec_p2_body.h P2ContSrc): one K, early stop, iteration 0 done by
 // tdec_kernel_p2x (max_its 1).  cont[0] = number of continuing code blocks, cont[1 ..] = their lane indices;
-// continuation pair p holds cont[1 + 128 p + 64 h + lane] in half h of lane `lane`.
+// continuation pair p holds cont[1 + 128 p + 64 h + lane] in half h of lane `lane`.  cap = the capacity of a list
+// (n_groups x 64 entries): one run never claims more (each valid lane continues at most once), and every kernel below
+// clamps a count it reads from memory to it and writes no slot beyond it, so two runs of one workspace racing on two
+// unordered streams (a caller error: a batch runs on one stream at a time) cannot take a kernel out of its buffers
+__device__ __forceinline__ uint32_t cont_count(const uint32_t* list, uint32_t cap) { return min(list[0], cap); }
 // 1. one wavefront per group: the lanes whose code block failed its CRC claim consecutive slots
 __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc* __restrict__ groups,
                                                               const MiLaneDesc* __restrict__ lanes,
-                                                              const uint32_t* __restrict__ cb_crc, uint32_t* cont) {
+                                                              const uint32_t* __restrict__ cb_crc, uint32_t* cont,
+                                                              uint32_t cap) {
   const uint32_t lane = threadIdx.x, li = groups[blockIdx.x].lane0 + lane;
   const bool act = lanes[li].valid && !cb_crc[li];
   const uint64_t m = __ballot(act);
@@ -284,7 +289,8 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
   uint32_t base = 0;
   if ((int)lane == lead) base = atomicAdd(cont, (uint32_t)__popcll(m));
   base = __shfl(base, lead);
-  if (act) cont[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = li;
+  const uint32_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
+  if (act && slot < cap) cont[1 + slot] = li;
 }
 
 // 1'. a re-compaction round (waterfall, tdec_p2_body.h): one wavefront per 64 slots of the previous round's list; its
@@ -292,8 +298,8 @@ __global__ __launch_bounds__(64) void tdec_cont_assign_kernel(const MiGroupDesc*
 // its previous slot (src: where the gather finds its state)
 __global__ __launch_bounds__(64) void tdec_cont_assign2_kernel(const uint32_t* __restrict__ prev,
                                                                const uint32_t* __restrict__ cb_crc, uint32_t* next,
-                                                               uint32_t* __restrict__ src) {
-  const uint32_t lane = threadIdx.x, d = blockIdx.x * LANES + lane, n = prev[0];
+                                                               uint32_t* __restrict__ src, uint32_t cap) {
+  const uint32_t lane = threadIdx.x, d = blockIdx.x * LANES + lane, n = cont_count(prev, cap);
   if (blockIdx.x * LANES >= n) return;   // the whole wavefront
   const uint32_t li = d < n ? prev[1 + d] : 0u;
   const bool act = d < n && !cb_crc[li];
@@ -303,8 +309,8 @@ __global__ __launch_bounds__(64) void tdec_cont_assign2_kernel(const uint32_t* _
   uint32_t base = 0;
   if ((int)lane == lead) base = atomicAdd(next, (uint32_t)__popcll(m));
   base = __shfl(base, lead);
-  if (act) {
-    const uint32_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
+  const uint32_t slot = base + __popcll(m & ((1ull << lane) - 1ull));
+  if (act && slot < cap) {
     next[1 + slot] = li;
     src[slot] = d;
   }
@@ -321,8 +327,8 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
                                                                const uint32_t* __restrict__ pos,
                                                                const uint32_t* __restrict__ cont,
                                                                uint32_t* __restrict__ cscr, size_t pair_u32, uint32_t K,
-                                                               uint32_t w_stored) {
-  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
+                                                               uint32_t w_stored, uint32_t cap) {
+  const uint32_t n = cont_count(cont, cap), np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
   const uint32_t nqw = p2_cont_qwins(K), nqt = (nqw + CONT_QW - 1) / CONT_QW, per = nqt + (K + CONT_WR - 1) / CONT_WR;
   for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * per; u += gridDim.x * 4) {
     const uint32_t p = u / per, c = u % per;
@@ -367,8 +373,9 @@ __global__ __launch_bounds__(256) void tdec_cont_gather_kernel(const float* __re
 __global__ __launch_bounds__(256) void tdec_cont_gather2_kernel(const uint32_t* __restrict__ prev, size_t prev_u32,
                                                                 const uint32_t* __restrict__ cont,
                                                                 const uint32_t* __restrict__ src,
-                                                                uint32_t* __restrict__ dst, size_t dst_u32, uint32_t K) {
-  const uint32_t n = cont[0], np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
+                                                                uint32_t* __restrict__ dst, size_t dst_u32, uint32_t K,
+                                                                uint32_t cap) {
+  const uint32_t n = cont_count(cont, cap), np = (n + 2 * LANES - 1) / (2 * LANES), lane = threadIdx.x % LANES;
   const uint32_t nq = 3 * (K + 4), per = (K + CONT_WR - 1) / CONT_WR + (nq + CONT_WR - 1) / CONT_WR;
   for (uint32_t u = blockIdx.x * 4 + threadIdx.x / LANES; u < np * per; u += gridDim.x * 4) {
     const uint32_t p = u / per, c = u % per, nwc = (K + CONT_WR - 1) / CONT_WR;
@@ -401,11 +408,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(P2_WAVES)))
 void tdec_kernel_p2c(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
-                     uint32_t w_stored, uint32_t it0, uint32_t it_end) {
+                     uint32_t w_stored, uint32_t it0, uint32_t it_end, uint32_t cap) {
   __shared__ uint32_t crc8[256], crc8b[256];
   static_assert(CKS != 16, "the continuation has no LDS stash (16-step spans measured slower here: profiles/r5/ab_misc)");
   __shared__ uint32_t xs[LANES];
-  const uint32_t n = cont[0], p = blockIdx.x;
+  const uint32_t n = cont_count(cont, cap), p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
     crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
@@ -484,10 +491,10 @@ __global__ __launch_bounds__(64 * S) __attribute__((amdgpu_waves_per_eu(P2_WAVES
 void tdec_kernel_p2s(uint32_t* __restrict__ cscr, uint8_t* __restrict__ cdec, TdecOut out,
                      const MiLaneDesc* __restrict__ lanes, const uint32_t* __restrict__ kdata, MiKTab kt,
                      const uint32_t* __restrict__ cont, size_t pair_u32, size_t dec_stride, uint32_t K, uint32_t max_its,
-                     uint32_t it0) {
+                     uint32_t it0, uint32_t cap) {
   __shared__ uint32_t crc8[256], crc8b[256];
   __shared__ uint32_t vecs[4][S * P2_CKW * LANES];
-  const uint32_t n = cont[0], p = blockIdx.x;
+  const uint32_t n = cont_count(cont, cap), p = blockIdx.x;
   if ((size_t)p * 2 * LANES >= n) return;   // the whole workgroup
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
     crc8[b] = crc24_byte_entry(b, CRC24A_POLY);
@@ -553,15 +560,16 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
   uint32_t* lists[2] = {cont, cont + nl};
   uint32_t* src = cont + 2 * nl;
   if (!cont_zeroed && hipMemsetAsync(cont, 0, 4, st) != hipSuccess) return false;
-  hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont);
+  const uint32_t cap = n_groups * LANES;
+  hipLaunchKernelGGL(tdec_cont_assign_kernel, dim3(n_groups), dim3(64), 0, st, groups, lanes, cb_crc, cont, cap);
   if (h_count && hipMemcpyAsync(h_count, cont, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
   hipLaunchKernelGGL(tdec_cont_gather_kernel, dim3(gather_wgs), dim3(256), 0, st, sb, wm, scratch, groups,
-                     ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored);
+                     ktab_data + kt.pos_off, cont, cscr, pair_u32, K, (uint32_t)w_stored, cap);
   const size_t cdec_stride = (size_t)K * LANES;
   if (!rounds) {   // one launch for iterations 1 .. max_its - 1 (each pair until its slowest code block stops)
     hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS>, dim3(max_pairs), dim3(128), 0, st, cscr, cdec, out, lanes,
                        ktab_data, kt, cont,
-                       pair_u32, cdec_stride, K, max_its, (uint32_t)w_stored, 1u, max_its);
+                       pair_u32, cdec_stride, K, max_its, (uint32_t)w_stored, 1u, max_its, cap);
     return true;
   }
   // re-compaction: one iteration per round, the code blocks still failing gathered into fewer dense pairs for the
@@ -576,9 +584,9 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
     if (it > 1) {
       if (hipMemsetAsync(lists[l], 0, 4, st) != hipSuccess) return false;
       hipLaunchKernelGGL(tdec_cont_assign2_kernel, dim3(2 * max_pairs), dim3(64), 0, st, lists[l ^ 1], cb_crc, lists[l],
-                         src);
+                         src, cap);
       hipLaunchKernelGGL(tdec_cont_gather2_kernel, dim3(gather_wgs), dim3(256), 0, st, bufs[b ^ 1], strides[b ^ 1],
-                         lists[l], src, bufs[b], strides[b], K);
+                         lists[l], src, bufs[b], strides[b], K, cap);
     }
     // each round's count, for the next run's grids (h_count[it - 1]: the list this round decodes)
     if (it > 1 && h_count && it <= CONT_HIST &&
@@ -586,17 +594,17 @@ bool launch_tdec_cont(const float* sb, const uint32_t* wm, float* scratch, size_
       return false;
     if (it > 1 && seg == 8)   // the late rounds segmented: seg wavefronts per pair (tdec_kernel_p2s)
       hipLaunchKernelGGL(tdec_kernel_p2s<8>, dim3(max_pairs), dim3(512), 0, st, bufs[b], decs[b], out, lanes, ktab_data,
-                         kt, lists[l], strides[b], dstrides[b], K, max_its, it);
+                         kt, lists[l], strides[b], dstrides[b], K, max_its, it, cap);
     else if (it > 1 && seg == 4)
       hipLaunchKernelGGL(tdec_kernel_p2s<4>, dim3(max_pairs), dim3(256), 0, st, bufs[b], decs[b], out, lanes, ktab_data,
-                         kt, lists[l], strides[b], dstrides[b], K, max_its, it);
+                         kt, lists[l], strides[b], dstrides[b], K, max_its, it, cap);
     else if (it > 1)
       hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS_LATE>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out, lanes,
-                         ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, 1u, it, it + 1);
+                         ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its, 1u, it, it + 1, cap);
     else
       hipLaunchKernelGGL(tdec_kernel_p2c<P2C_CKS>, dim3(max_pairs), dim3(128), 0, st, bufs[b], decs[b], out,
                          lanes, ktab_data, kt, lists[l], strides[b], dstrides[b], K, max_its,
-                         (uint32_t)(w_stored || it > 1), it, it + 1);
+                         (uint32_t)(w_stored || it > 1), it, it + 1, cap);
   }
   return true;
 }

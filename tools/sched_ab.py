@@ -9,6 +9,10 @@ back end (turbo decoder + TB CRC) with mi_dl_batch_run_stages, and HIP events be
   ser_both   both
   stagger    the first S steps start staggered (front end of step i after that of step i - 1), then free-running
   stagger_b  the first S steps' back ends staggered the same way, then free-running
+  two        front ends and back ends on separate streams per workspace (2 S streams): the back end of step i waits for
+             its front end, the front end of step i + S for the back end of step i (the workspace is reused)
+  prio_f     the same with the front-end streams at high priority
+  prio_b     the same with the back-end streams at high priority
 Usage: python tools/sched_ab.py [steps] [reps] [schedules...]  -> one line per (schedule, rep): ms/step, Gbps, CRC-OK
 """
 import os
@@ -46,9 +50,29 @@ def main():
     sp = [s.cuda_stream for s in streams]
     bits = sum(c.tbs for c in cfgs)
 
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    two = {"two": ([torch.cuda.Stream(dev) for _ in range(S)], [torch.cuda.Stream(dev) for _ in range(S)]),
+           "prio_f": ([torch.cuda.Stream(dev, priority=hi) for _ in range(S)], [torch.cuda.Stream(dev) for _ in range(S)]),
+           "prio_b": ([torch.cuda.Stream(dev) for _ in range(S)], [torch.cuda.Stream(dev, priority=hi) for _ in range(S)])}
+
     def run(sched, n):
         fe = [None] * n   # front-end done events
         be = [None] * n   # back-end done events
+        if sched in two:
+            fs, bs = two[sched]
+            for i in range(n):
+                k = i % S
+                b = batches[k]
+                if i >= S:
+                    fs[k].wait_event(be[i - S])
+                b.run_stages(FRONT, d_iq.data_ptr(), fs[k].cuda_stream)
+                fe[i] = torch.cuda.Event()
+                fe[i].record(fs[k])
+                bs[k].wait_event(fe[i])
+                b.run_stages(BACK, d_iq.data_ptr(), bs[k].cuda_stream)
+                be[i] = torch.cuda.Event()
+                be[i].record(bs[k])
+            return
         for i in range(n):
             k = i % S
             b, st = batches[k], streams[k]
@@ -66,9 +90,12 @@ def main():
             be[i] = torch.cuda.Event()
             be[i].record(st)
 
+    # each schedule's warmup runs alone: the schedules use different streams for the same workspaces, and two of them
+    # in flight at once would run two steps of one workspace concurrently (an earlier version of this script did, and
+    # the continuation lists of the concurrent steps overran their buffers)
     for sched in scheds:
         run(sched, 2 * S)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     for r in range(reps):
         for sched in scheds:
             torch.cuda.synchronize()
