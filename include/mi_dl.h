@@ -175,7 +175,9 @@ void   mi_dl_batch_reset_history(mi_dl_batch_t *b);
  * differs and that holds a retransmission lane has its softbuffer region cleared (every value RX_NULL, as
  * srslte_softbuffer_rx_reset), so such a lane combines with nothing rather than with another code block's rows --
  * srsLTE's softbuffer is per HARQ process, and a change of another subframe's grant does not touch it.  (New
- * transmissions overwrite their rows; rows another layout left are settled by the kernels.) */
+ * transmissions overwrite their rows; rows another layout left are settled by the kernels.)  When the new plan needs a
+ * larger softbuffer arena, the arena grows keeping its contents (a device copy; the new tail is RX_NULL), so the
+ * unchanged groups keep combining across the growth too. */
 typedef struct mi_dl_plan mi_dl_plan_t;
 mi_dl_plan_t *mi_dl_plan_create(void);
 void   mi_dl_plan_destroy(mi_dl_plan_t *p);
