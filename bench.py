@@ -177,6 +177,28 @@ def bench_streams(dev, S):
     return [torch.cuda.current_stream(dev)] + _STREAMS[:S - 1]
 
 
+_SPLIT = {}
+
+
+def split_share(args, S):
+    """Eighths of the CUs the front end of a split run gets (0 = whole runs on one stream per workspace): --split (off by
+    default: level with whole runs on the median box, -1 %, but 4-5 % ahead where whole runs co-schedule rate
+    de-matching beside the decoder; profiles/r6/cumask)."""
+    if S < 2 or args.split < 0:
+        return 0
+    return args.split
+
+
+def split_streams(S, F):
+    """S front-end streams on the CUs i mod 8 < F and S back-end streams on the others (mi_stream_create_cu_share),
+    created once per share and kept for the process (like bench_streams)."""
+    have = _SPLIT.setdefault(F, ([], []))
+    while len(have[0]) < S:
+        have[0].append(abi.stream_cu_share(0, F))
+        have[1].append(abi.stream_cu_share(F, 8 - F))
+    return have[0][:S], have[1][:S]
+
+
 def dist_on():
     """A process group is up: N > 1 ranks, or one rank with --pg (the RCCL path rehearsed on a one-GPU box)."""
     return dist.is_available() and dist.is_initialized()
@@ -696,9 +718,20 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
         del d_pool
     streams = bench_streams(dev, S)
     sptr = [st.cuda_stream for st in streams]
+    F = split_share(args, S)
+    if F:
+        # split runs (mi_dl_batch_run_split): each workspace's front end on a stream of the CUs i mod 8 < F, its turbo
+        # decoder + TB CRC on a stream of the others
+        fr, bk = split_streams(S, F)
+
+        def step(i):
+            batches[i % S].run_split(d_iq.data_ptr(), fr[i % S], bk[i % S])
+    else:
+        def step(i):
+            batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
     for w in range(warmup * S):
-        batches[w % S].run(d_iq.data_ptr(), sptr[w % S])
+        step(w)
     torch.cuda.synchronize(dev)
     for b in batches:
         b.profile_reset()
@@ -707,7 +740,7 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(steps):
-        batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
+        step(i)
     torch.cuda.synchronize(dev)
     if dist_on():
         dist.barrier()
@@ -1102,6 +1135,14 @@ def main():
                     help="--streams of the waterfall block; 0 = auto (= --streams: its continuation holds 0.74 "
                          "wavefronts per SIMD, so the next batches' iteration 0 fills the rest: 35 -> 56 Gbps with 4; "
                          "profiles/r3/ab_streams*)")
+    ap.add_argument("--split", type=int, default=-1, choices=range(-1, 8), metavar="-1..7",
+                    help="split runs (mi_dl_batch_run_split): each step's front end (OFDM, channel estimation, demap + "
+                         "rate de-matching) on a stream of the CUs whose index mod 8 is < SPLIT, its turbo decoder and "
+                         "TB CRC on a stream of the other CUs, so rate de-matching never shares a CU with the decoder; "
+                         "0 or -1 (default) = whole runs on one stream per workspace.  Headline shard, 4 streams, "
+                         "--split 2: 7.96-8.08 ms per step on every box sampled, against 7.86-8.14 for whole runs on "
+                         "most boxes and 8.2-8.35 on the boxes where whole runs co-schedule rate de-matching beside "
+                         "the decoder (profiles/r6/cumask)")
     ap.add_argument("--hw-queues", type=int, default=8, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process and its ranks (set before the HIP runtime starts, see "
                          "HW_QUEUES above); 0 = keep the environment's value")
@@ -1263,6 +1304,7 @@ def main():
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
+                       "split_front_cu_eighths": split_share(args, max(1, args.streams)),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "channel_estimates": "full" if (args.ce == "full" or args.ctrl or args.llr_stream) else "compact",
                        **({"llr_stream": True} if args.llr_stream else {}),

@@ -81,6 +81,7 @@ def lib():
             "mi_dl_batch_run": (C.c_int, [vp, vp, vp]),
             "mi_dl_batch_download": (C.c_int, [vp, C.c_int, vp, sz]),
             "mi_dl_batch_run_stages": (C.c_int, [vp, vp, vp, u32]),
+            "mi_dl_batch_run_split": (C.c_int, [vp, vp, vp, vp]),
             "mi_dl_batch_upload": (C.c_int, [vp, C.c_int, vp, sz]),
             "mi_dl_batch_device_ptr": (vp, [vp, C.c_int]),
             "mi_dl_batch_stage_ms": (C.c_int, [vp, vp, vp]),
@@ -139,6 +140,8 @@ def lib():
             "mi_device_count": (C.c_int, []),
             "mi_set_device": (C.c_int, [C.c_int]),
             "mi_last_error": (C.c_char_p, []),
+            "mi_stream_create_cu_share": (C.c_int, [u32, u32, vp]),
+            "mi_stream_destroy": (C.c_int, [vp]),
             "mi_ul_batch_create": (vp, [vp, u32, u32]),
             "mi_ul_batch_destroy": (None, [vp]),
             "mi_ul_batch_payload_offset": (sz, [vp, u32]),
@@ -179,6 +182,20 @@ def emu():
 
 def last_error():
     return lib().mi_last_error().decode()
+
+
+def stream_cu_share(first, count):
+    """A HIP stream (handle as int) on the CUs whose index mod 8 lies in [first, first + count) (mi_stream_create_cu_share);
+    release with stream_destroy."""
+    h = C.c_void_p()
+    if lib().mi_stream_create_cu_share(first, count, C.byref(h)):
+        raise RuntimeError("mi_stream_create_cu_share: " + last_error())
+    return h.value
+
+
+def stream_destroy(h):
+    if lib().mi_stream_destroy(C.c_void_p(h)):
+        raise RuntimeError("mi_stream_destroy: " + last_error())
 
 
 def tx_subframe(cfg, tb_bytes, h=None, snr_db=30.0, seed=0xA5A5):
@@ -249,6 +266,13 @@ class Batch:
         if lib().mi_dl_batch_replan(self.h, plan.h, C.c_void_p(stream_ptr or 0)):
             raise RuntimeError("mi_dl_batch_replan: " + last_error())
         plan.cfgs, self.cfgs = self.cfgs, cfgs
+
+    def run_split(self, d_iq_ptr, front_ptr, back_ptr):
+        """mi_dl_batch_run_split: front end on front_ptr, turbo decoder + TB CRC on back_ptr (complete with it)."""
+        rc = lib().mi_dl_batch_run_split(self.h, C.c_void_p(d_iq_ptr), C.c_void_p(front_ptr or 0),
+                                         C.c_void_p(back_ptr or 0))
+        if rc:
+            raise RuntimeError("mi_dl_batch_run_split: " + last_error())
 
     def run_stages(self, mask, d_iq_ptr=None, stream_ptr=None):
         rc = lib().mi_dl_batch_run_stages(self.h, C.c_void_p(d_iq_ptr or 0), C.c_void_p(stream_ptr or 0), mask)

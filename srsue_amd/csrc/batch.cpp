@@ -82,6 +82,13 @@ int mi_dl_batch_run_stages(mi_dl_batch_t* b, const void* d_iq, void* stream, uin
   return b->eng.run(d_iq, reinterpret_cast<hipStream_t>(stream), mask, nullptr);
 }
 
+int mi_dl_batch_run_split(mi_dl_batch_t* b, const void* d_iq, void* front_stream, void* back_stream) {
+  if (!b || !d_iq) { mi::set_error("null argument"); return -1; }
+  if (front_stream == back_stream) return mi_dl_batch_run(b, d_iq, front_stream);
+  const hipStream_t back = reinterpret_cast<hipStream_t>(back_stream);
+  return b->eng.run(d_iq, reinterpret_cast<hipStream_t>(front_stream), 0xFFFFFFFFu, nullptr, &back);
+}
+
 int mi_dl_batch_upload(mi_dl_batch_t* b, int which, const void* host, size_t bytes) {
   size_t n = 0;
   mi::DevBuf* d = buf_of(b, which, &n);
@@ -341,6 +348,34 @@ int mi_device_count(void) {
   return n;
 }
 int mi_set_device(int dev) { return mi::hip_ok(hipSetDevice(dev), "hipSetDevice") ? 0 : -1; }
+
+int mi_stream_create_cu_share(uint32_t first, uint32_t count, void** stream) {
+  if (!stream || !count || first >= 8 || first + count > 8) {
+    mi::set_error("mi_stream_create_cu_share: eighths [first, first + count) must lie in [0, 8)");
+    return -1;
+  }
+  hipStream_t s = nullptr;
+  if (count == 8) {
+    if (!mi::hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream")) return -1;
+  } else {
+    int dev = 0, n_cu = 0;
+    if (!mi::hip_ok(hipGetDevice(&dev), "device") ||
+        !mi::hip_ok(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev), "CU count"))
+      return -1;
+    // CU i is in the share when i mod 8 lies in [first, first + count): every eighth CU index, so that the share
+    // spans the device's XCDs and shader engines evenly
+    std::vector<uint32_t> mask(((size_t)n_cu + 31) / 32, 0u);
+    for (int i = 0; i < n_cu; i++)
+      if ((uint32_t)(i % 8) - first < count) mask[i / 32] |= 1u << (i % 32);
+    if (!mi::hip_ok(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "CU-masked stream"))
+      return -1;
+  }
+  *stream = s;
+  return 0;
+}
+int mi_stream_destroy(void* stream) {
+  return mi::hip_ok(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)), "stream destroy") ? 0 : -1;
+}
 const char* mi_last_error(void) { return mi::last_error(); }
 
 }  // extern "C"

@@ -84,6 +84,11 @@ Engine::~Engine() {
   if (h_cont) (void)hipHostFree(h_cont);
   for (auto& set : ev_sets)
     for (auto& e : set) (void)hipEventDestroy(e);
+  if (back_ev) {
+    (void)hipEventSynchronize(back_ev);
+    (void)hipEventDestroy(back_ev);
+  }
+  if (split_ev) (void)hipEventDestroy(split_ev);
 }
 
 template <class T>
@@ -282,9 +287,18 @@ int Engine::plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, h
   return ensure_work(st, false);
 }
 
-int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_override) {
+int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_override, const hipStream_t* back) {
   const Plan& P = plan;
-  last_stream = st;
+  if (back) {
+    // split run: the front end waits for the previous split run's back end (it rewrites what that one reads)
+    if ((!split_ev && !hip_ok(hipEventCreateWithFlags(&split_ev, hipEventDisableTiming), "event")) ||
+        (!back_ev && !hip_ok(hipEventCreateWithFlags(&back_ev, hipEventDisableTiming), "event")))
+      return -1;
+    if (back_pending && !hip_ok(hipStreamWaitEvent(st, back_ev, 0), "wait")) return -1;
+  }
+  last_stream = back ? *back : st;
+  // the stream the next launches go to: st, then (split run) the back-end stream from the hand-off on
+  hipStream_t cur = st;
   const bool prof = flags & MI_DL_FLAG_PROFILE;
   hipEvent_t* ev = nullptr;
   if (prof) {
@@ -298,7 +312,13 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
   }
   bool ok = true;
   auto mark = [&](int i) {
-    if (prof) ok = hip_ok(hipEventRecord(ev[i], st), "event") && ok;
+    if (prof) ok = hip_ok(hipEventRecord(ev[i], cur), "event") && ok;
+  };
+  // split run: the back-end stream waits for the front end, and the launches from here on go to it
+  auto handoff = [&]() {
+    if (!back) return;
+    ok = hip_ok(hipEventRecord(split_ev, st), "record") && hip_ok(hipStreamWaitEvent(*back, split_ev, 0), "wait") && ok;
+    cur = *back;
   };
   const uint32_t nsf = (uint32_t)P.sfs.size();
   // compact channel estimates (MI_DL_FLAG_CE_COMPACT): only when this run both writes and consumes them
@@ -355,15 +375,22 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
                         d_ktabs.as<MiKTab>(), d_kdata.as<uint32_t>(), (uint32_t)P.groups.size(), P.max_ncb,
                         rm_items(), rm_recs(), P.rm_busy, P.rm_dbusy, (uint32_t)P.rm_items.size(), st);
     mark(4);
-    if (mask & (1u << MI_DL_STAGE_TDEC)) ok = launch_turbo(sb, st) && ok;
+    handoff();
+    if (mask & (1u << MI_DL_STAGE_TDEC)) ok = launch_turbo(sb, cur) && ok;
     mark(5);
     if (mask & (1u << MI_DL_STAGE_TB))
       launch_tb(d_cbbytes.as<uint8_t>(), d_payload.as<uint8_t>(), d_tbok.as<uint32_t>(), d_tbits.as<uint32_t>(),
                 d_cbits.as<uint32_t>(), d_cbtbp.as<uint32_t>(), d_tbs.as<MiTbDesc>(), (uint32_t)P.tbs.size(),
-                d_cblist.as<uint32_t>(), d_kdata.as<uint32_t>(), !tb_copied, st);
+                d_cblist.as<uint32_t>(), d_kdata.as<uint32_t>(), !tb_copied, cur);
     mark(6);
   } else {
-    for (int i = 3; i <= 6; i++) mark(i);
+    for (int i = 3; i <= 4; i++) mark(i);
+    handoff();
+    for (int i = 5; i <= 6; i++) mark(i);
+  }
+  if (back) {
+    ok = hip_ok(hipEventRecord(back_ev, cur), "record") && ok;
+    back_pending = ok;
   }
   return hip_ok(hipGetLastError(), "launch") && ok ? 0 : -1;
 }

@@ -137,8 +137,13 @@ struct Engine {
   bool ensure_llr();                                     // the LLR stream d_e, allocated on first use
   // HBM bytes of this plan's work buffers (+ the softbuffer arena, + the LLR stream), as DevBuf::ensure rounds them
   size_t work_bytes(bool with_sb, bool with_llr);
-  // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.
-  int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override);
+  // split runs (mi_dl_batch_run_split): the front end's hand-off to the back-end stream, and the back end's completion,
+  // which the next split run's front end waits for (the workspace is reused)
+  hipEvent_t split_ev = nullptr, back_ev = nullptr;
+  bool back_pending = false;
+  // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.  back: the stream of the
+  // TDEC and TB stages (split run), nullptr = all on st
+  int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override, const hipStream_t* back = nullptr);
   // raw code-block decoding: scatter d into the softbuffer layout, then the turbo kernel
   int run_codeblocks(const float* d_in, hipStream_t st);
   int stage_ms(float* ms, uint32_t* nruns);   // average over the runs since profile_reset()

@@ -72,6 +72,18 @@ def test_isolated_stages_only_for_overlapped_steps(monkeypatch):
     assert bench.roofline_timing({"tdec": 6.5}, 200, None) == {"avg_launch_ms": 6.5, "launches_averaged": 200}
 
 
+def test_split_share():
+    """--split F: the front end's CU eighths of a split run (mi_dl_batch_run_split), off by default and with one stream
+    (a single workspace's front end waits for its own back end: nothing to overlap)."""
+    import argparse
+    import bench
+    ns = lambda f, c=4: argparse.Namespace(split=f, config=c)   # noqa: E731
+    assert bench.split_share(ns(-1), 4) == 0
+    assert bench.split_share(ns(0), 4) == 0
+    assert bench.split_share(ns(2), 4) == 2 and bench.split_share(ns(3, 5), 16) == 3
+    assert bench.split_share(ns(2), 1) == 0
+
+
 def test_hw_queues_argument():
     """--hw-queues N and --hw-queues=N are both honoured, checked to 0..32 (gpurun refuses more than 32), and
     importing bench (as the GPU tests do) leaves GPU_MAX_HW_QUEUES alone."""
