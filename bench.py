@@ -180,13 +180,47 @@ def bench_streams(dev, S):
 _SPLIT = {}
 
 
+AUTO_SPLIT = 2          # the front end's CU eighths of an auto-tuned split (profiles/r6/cumask: 1-3 measured alike)
+SPLIT_MARGIN = 0.015    # auto: split runs are kept only when faster than whole runs by more than this
+
+
 def split_share(args, S):
-    """Eighths of the CUs the front end of a split run gets (0 = whole runs on one stream per workspace): --split (off by
-    default: level with whole runs on the median box, -1 %, but 4-5 % ahead where whole runs co-schedule rate
-    de-matching beside the decoder; profiles/r6/cumask)."""
-    if S < 2 or args.split < 0:
+    """Eighths of the CUs the front end of a split run gets; 0 = whole runs on one stream per workspace; -1 = decide on
+    the box (tune_split): --split F, or by default -1 for the headline shard on several streams (split runs are level
+    with whole runs on the median box, -1 %, but 4-5 % ahead where whole runs co-schedule rate de-matching beside the
+    decoder; profiles/r6/cumask) and 0 otherwise.  One stream: 0 (a lone workspace's front end waits for its own back
+    end, nothing overlaps)."""
+    if S < 2:
         return 0
-    return args.split
+    if args.split >= 0:
+        return args.split
+    return -1 if args.config == 4 else 0
+
+
+def tune_split(whole, split, S, dev, reps=2):
+    """The stream layout for this box, chosen after the warmup and before the timed region (untimed): `reps` rounds of
+    3 S steps of whole runs and of split runs (each bracketed by device synchronisation, so the two layouts never
+    overlap on a workspace), best ms per step of each; split runs are kept when faster by more than SPLIT_MARGIN.
+    Returns (front-end eighths or 0, the record reported in the line)."""
+    n = 3 * S
+
+    def per_step(fn):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(n):
+            fn(i)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / n * 1e3
+
+    tw, ts = [], []
+    for _ in range(reps):
+        tw.append(per_step(whole))
+        ts.append(per_step(split))
+    F = AUTO_SPLIT if min(ts) < min(tw) * (1 - SPLIT_MARGIN) else 0
+    return F, {"whole_ms_per_step": [round(x, 3) for x in tw], "split_ms_per_step": [round(x, 3) for x in ts],
+               "steps_each": n, "split_front_cu_eighths": AUTO_SPLIT, "chosen": "split" if F else "whole",
+               "rule": f"split runs when faster than whole runs by more than {SPLIT_MARGIN:.1%} (untimed, after the "
+                       "warmup)"}
 
 
 def split_streams(S, F):
@@ -718,21 +752,24 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
         del d_pool
     streams = bench_streams(dev, S)
     sptr = [st.cuda_stream for st in streams]
-    F = split_share(args, S)
-    if F:
+
+    def whole(i):
+        batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
+
+    def split_runs(F):
         # split runs (mi_dl_batch_run_split): each workspace's front end on a stream of the CUs i mod 8 < F, its turbo
         # decoder + TB CRC on a stream of the others
         fr, bk = split_streams(S, F)
+        return lambda i: batches[i % S].run_split(d_iq.data_ptr(), fr[i % S], bk[i % S])
 
-        def step(i):
-            batches[i % S].run_split(d_iq.data_ptr(), fr[i % S], bk[i % S])
-    else:
-        def step(i):
-            batches[i % S].run(d_iq.data_ptr(), sptr[i % S])
     torch.cuda.synchronize(dev)
     for w in range(warmup * S):
-        step(w)
+        whole(w)
     torch.cuda.synchronize(dev)
+    F, tune = split_share(args, S), None
+    if F < 0:
+        F, tune = tune_split(whole, split_runs(AUTO_SPLIT), S, dev)
+    step = split_runs(F) if F else whole
     for b in batches:
         b.profile_reset()
     if dist_on():
@@ -764,7 +801,7 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     for b in batches[1:]:
         b.close()
     return {"batch": batch, "stage": stage, "nprof": nprof, "elapsed": elapsed, "n_ok": n_ok, "its": its,
-            "bad": bad, "bits_ok": bits_ok, "cb_its": cb_its, "iso": iso}
+            "bad": bad, "bits_ok": bits_ok, "cb_its": cb_its, "iso": iso, "split": F, "split_tune": tune}
 
 
 def varied_cfgs(P, first):
@@ -1139,10 +1176,11 @@ def main():
                     help="split runs (mi_dl_batch_run_split): each step's front end (OFDM, channel estimation, demap + "
                          "rate de-matching) on a stream of the CUs whose index mod 8 is < SPLIT, its turbo decoder and "
                          "TB CRC on a stream of the other CUs, so rate de-matching never shares a CU with the decoder; "
-                         "0 or -1 (default) = whole runs on one stream per workspace.  Headline shard, 4 streams, "
-                         "--split 2: 7.96-8.08 ms per step on every box sampled, against 7.86-8.14 for whole runs on "
-                         "most boxes and 8.2-8.35 on the boxes where whole runs co-schedule rate de-matching beside "
-                         "the decoder (profiles/r6/cumask)")
+                         "0 = whole runs on one stream per workspace; -1 (default) = the headline shard on several "
+                         "streams times both layouts after the warmup and keeps split runs (--split 2) only when they "
+                         "are >1.5 %% faster, other configs whole runs.  Headline, 4 streams, --split 2: 7.96-8.08 ms "
+                         "per step on every box sampled, whole runs 7.86-8.14 on most boxes and 8.2-8.35 on the boxes "
+                         "where they co-schedule rate de-matching beside the decoder (profiles/r6/cumask)")
     ap.add_argument("--hw-queues", type=int, default=8, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process and its ranks (set before the HIP runtime starts, see "
                          "HW_QUEUES above); 0 = keep the environment's value")
@@ -1267,7 +1305,10 @@ def main():
             ib = im["batch"]
             ims = im["iso"][0]["tdec"] if im["iso"] else im["stage"]["tdec"]
             iach = ib.algo_bytes(4) / (ims * 1e-3) / 1e9
-            itr = {"snr_db": args.iterating_snr, "steps": isteps, "streams": iargs.streams, "ms_per_step": round(iel / isteps * 1e3, 3),
+            itr = {"snr_db": args.iterating_snr, "steps": isteps, "streams": iargs.streams,
+                   "split_front_cu_eighths": im["split"],
+                   **({"stream_layout_autotune": im["split_tune"]} if im["split_tune"] else {}),
+                   "ms_per_step": round(iel / isteps * 1e3, 3),
                    "Mbps": round(ibits * isteps / iel / 1e6, 2),
                    "turbo_codeblocks_per_s": round(incb * isteps / iel, 1),
                    "crc_ok_rate": round(iok / itb, 6), "mean_turbo_iterations": round(iits / itb, 4),
@@ -1304,7 +1345,8 @@ def main():
                        "baseline_config": args.config, "subframes_per_gpu": B, "turbo_arithmetic": args.tdec,
                        "max_its": args.max_its, "turbo_schedule": SCHED_DESC[batch.turbo_sched],
                        "streams": max(1, args.streams),
-                       "split_front_cu_eighths": split_share(args, max(1, args.streams)),
+                       "split_front_cu_eighths": m["split"],
+                       **({"stream_layout_autotune": m["split_tune"]} if m["split_tune"] else {}),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "channel_estimates": "full" if (args.ce == "full" or args.ctrl or args.llr_stream) else "compact",
                        **({"llr_stream": True} if args.llr_stream else {}),

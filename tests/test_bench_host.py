@@ -73,15 +73,17 @@ def test_isolated_stages_only_for_overlapped_steps(monkeypatch):
 
 
 def test_split_share():
-    """--split F: the front end's CU eighths of a split run (mi_dl_batch_run_split), off by default and with one stream
-    (a single workspace's front end waits for its own back end: nothing to overlap)."""
+    """--split F: the front end's CU eighths of a split run (mi_dl_batch_run_split); by default tuned on the box for the
+    headline shard and off elsewhere, and off with one stream (a lone workspace's front end waits for its own back
+    end: nothing to overlap)."""
     import argparse
     import bench
     ns = lambda f, c=4: argparse.Namespace(split=f, config=c)   # noqa: E731
-    assert bench.split_share(ns(-1), 4) == 0
+    assert bench.split_share(ns(-1), 4) == -1                        # headline: tuned on the box (tune_split)
+    assert bench.split_share(ns(-1, 5), 16) == 0 and bench.split_share(ns(-1, 3), 16) == 0
     assert bench.split_share(ns(0), 4) == 0
     assert bench.split_share(ns(2), 4) == 2 and bench.split_share(ns(3, 5), 16) == 3
-    assert bench.split_share(ns(2), 1) == 0
+    assert bench.split_share(ns(2), 1) == 0 and bench.split_share(ns(-1), 1) == 0
 
 
 def test_hw_queues_argument():
