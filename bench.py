@@ -233,6 +233,16 @@ def split_streams(S, F):
     return have[0][:S], have[1][:S]
 
 
+def release_split_streams(F):
+    """Destroy the split streams of share F (after the device is idle): each CU-masked stream holds a hardware queue of
+    its own."""
+    have = _SPLIT.pop(F, None)
+    if have:
+        torch.cuda.synchronize()
+        for h in have[0] + have[1]:
+            abi.stream_destroy(h)
+
+
 def dist_on():
     """A process group is up: N > 1 ranks, or one rank with --pg (the RCCL path rehearsed on a one-GPU box)."""
     return dist.is_available() and dist.is_initialized()
@@ -768,7 +778,11 @@ def measure(args, cfgs, pool_iq, pool_tb, world, dev, steps, warmup):
     torch.cuda.synchronize(dev)
     F, tune = split_share(args, S), None
     if F < 0:
-        F, tune = tune_split(whole, split_runs(AUTO_SPLIT), S, dev)
+        # tuned on one-process runs only: beside RCCL's streams (N ranks, --pg) the masked streams' extra hardware queues
+        # are not worth the risk of oversubscribing the queue slots, and whole runs are the measured default there
+        F, tune = (0, None) if dist_on() else tune_split(whole, split_runs(AUTO_SPLIT), S, dev)
+        if not F:
+            release_split_streams(AUTO_SPLIT)   # whole runs: the timed region sees the queue set it always had
     step = split_runs(F) if F else whole
     for b in batches:
         b.profile_reset()
