@@ -86,6 +86,28 @@ def test_split_share():
     assert bench.split_share(ns(2), 1) == 0 and bench.split_share(ns(-1), 1) == 0
 
 
+def test_tune_split_rule(monkeypatch):
+    """tune_split keeps split runs only when their best ms per step beats whole runs' by more than SPLIT_MARGIN, timing
+    3 S steps of each layout per round (a fake clock advanced by the fake runs)."""
+    clock = [0.0]
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda dev=None: None)
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: clock[0])
+
+    def runner(ms):
+        def run(i):
+            clock[0] += ms[0] * 1e-3
+        return run
+
+    for whole_ms, split_ms, want in ((8.30, 7.95, bench.AUTO_SPLIT), (7.90, 8.02, 0), (8.00, 7.90, 0)):
+        calls = []
+        w, s = [whole_ms], [split_ms]
+        F, rec = bench.tune_split(lambda i: (calls.append("w"), runner(w)(i)), lambda i: (calls.append("s"), runner(s)(i)),
+                                  4, "cpu")
+        assert F == want, (whole_ms, split_ms)
+        assert calls.count("w") == calls.count("s") == 2 * 12 and rec["steps_each"] == 12
+        assert abs(min(rec["whole_ms_per_step"]) - whole_ms) < 1e-6 and rec["chosen"] == ("split" if F else "whole")
+
+
 def test_hw_queues_argument():
     """--hw-queues N and --hw-queues=N are both honoured, checked to 0..32 (gpurun refuses more than 32), and
     importing bench (as the GPU tests do) leaves GPU_MAX_HW_QUEUES alone."""
