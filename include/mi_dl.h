@@ -124,8 +124,8 @@ int    mi_dl_batch_run(mi_dl_batch_t *b, const void *d_iq, void *stream);
 int    mi_dl_batch_run_stages(mi_dl_batch_t *b, const void *d_iq, void *stream, uint32_t stage_mask);
 /* The whole chain with its front end (OFDM, channel estimation, demap + rate de-matching) on front_stream and its
  * back end (turbo decoding, TB CRC) on back_stream, ordered by events the batch owns: the back end waits for this
- * run's front end, and the front end for the batch's previous split run's back end (the workspace is reused).  The
- * run is complete when back_stream is; downloads synchronise it.  With the two streams on complementary CU shares
+ * run's front end, and the batch's next run or re-plan (split or not, on any stream) waits for this back end (the
+ * workspace is reused).  The run is complete when back_stream is; downloads synchronise it.  With the two streams on complementary CU shares
  * (mi_stream_create_cu_share) and several batches in flight, rate de-matching never shares a CU with the turbo
  * decoder: the headline step is 7.96-8.08 ms on every MI355X sampled, where whole runs on plain streams vary from
  * 7.86 to 8.35 ms by box.  front_stream == back_stream is mi_dl_batch_run.  Results are those of

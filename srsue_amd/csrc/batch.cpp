@@ -166,6 +166,8 @@ int mi_dl_plan_build(mi_dl_plan_t* p, const mi_dl_sf_cfg_t* cfgs, uint32_t n_sf)
 int mi_dl_batch_replan(mi_dl_batch_t* b, mi_dl_plan_t* p, void* stream) {
   if (!b || !p || !p->built) { mi::set_error("mi_dl_batch_replan: no built plan"); return -1; }
   const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the table upload rewrites what a pending split run's back end reads
+  if (!b->eng.order_after_split(st)) return -1;
   // the active plan data and the built one trade places (the planner's caches stay with each object)
   std::swap(static_cast<mi::PlanData&>(b->eng.plan), static_cast<mi::PlanData&>(p->plan));
   std::swap(b->cfgs, p->cfgs);

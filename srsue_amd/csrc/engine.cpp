@@ -289,13 +289,12 @@ int Engine::plan_memo(const mi_dl_sf_cfg_t* cfgs, uint32_t n, bool with_pdsch, h
 
 int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_override, const hipStream_t* back) {
   const Plan& P = plan;
-  if (back) {
-    // split run: the front end waits for the previous split run's back end (it rewrites what that one reads)
-    if ((!split_ev && !hip_ok(hipEventCreateWithFlags(&split_ev, hipEventDisableTiming), "event")) ||
-        (!back_ev && !hip_ok(hipEventCreateWithFlags(&back_ev, hipEventDisableTiming), "event")))
-      return -1;
-    if (back_pending && !hip_ok(hipStreamWaitEvent(st, back_ev, 0), "wait")) return -1;
-  }
+  // after a split run, any run of this batch (split or not, on any stream) waits for that run's back end: it rewrites
+  // what the back end reads
+  if (!order_after_split(st)) return -1;
+  if (back && ((!split_ev && !hip_ok(hipEventCreateWithFlags(&split_ev, hipEventDisableTiming), "event")) ||
+               (!back_ev && !hip_ok(hipEventCreateWithFlags(&back_ev, hipEventDisableTiming), "event"))))
+    return -1;
   last_stream = back ? *back : st;
   // the stream the next launches go to: st, then (split run) the back-end stream from the hand-off on
   hipStream_t cur = st;
@@ -389,8 +388,8 @@ int Engine::run(const void* d_iq, hipStream_t st, uint32_t mask, float* sb_overr
     for (int i = 5; i <= 6; i++) mark(i);
   }
   if (back) {
-    ok = hip_ok(hipEventRecord(back_ev, cur), "record") && ok;
-    back_pending = ok;
+    back_pending = hip_ok(hipEventRecord(back_ev, cur), "record");
+    ok = back_pending && ok;
   }
   return hip_ok(hipGetLastError(), "launch") && ok ? 0 : -1;
 }

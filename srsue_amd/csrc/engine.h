@@ -138,9 +138,15 @@ struct Engine {
   // HBM bytes of this plan's work buffers (+ the softbuffer arena, + the LLR stream), as DevBuf::ensure rounds them
   size_t work_bytes(bool with_sb, bool with_llr);
   // split runs (mi_dl_batch_run_split): the front end's hand-off to the back-end stream, and the back end's completion,
-  // which the next split run's front end waits for (the workspace is reused)
+  // which the batch's next run or re-plan waits for (the workspace is reused)
   hipEvent_t split_ev = nullptr, back_ev = nullptr;
   bool back_pending = false;
+  // enqueue on st a wait for the last split run's back end, if one is pending; false on a HIP error
+  bool order_after_split(hipStream_t st) {
+    if (!back_pending) return true;
+    back_pending = false;
+    return hip_ok(hipStreamWaitEvent(st, back_ev, 0), "wait");
+  }
   // stage mask bit i = stage i (MI_DL_STAGE_*).  sb_override: external softbuffer arena.  back: the stream of the
   // TDEC and TB stages (split run), nullptr = all on st
   int run(const void* d_iq, hipStream_t st, uint32_t stage_mask, float* sb_override, const hipStream_t* back = nullptr);

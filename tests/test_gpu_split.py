@@ -6,7 +6,9 @@ whole run (mi_dl_batch_run) of the same IQ: TB CRC, TB and per-code-block iterat
 Two workspaces run three steps each, issued round-robin with no host synchronisation, on two alternating IQ sets, in
 the turbo waterfall (16-25 dB: continuation rounds run): each run's outputs are copied to host memory on its back-end
 stream right behind it, so a run whose back end overlapped the next front end of its workspace (the ordering the batch's
-events impose) would show as a mismatch in that run's copy, not just in the last one.
+events impose) would show as a mismatch in that run's copy, not just in the last one.  Then each workspace's next front
+end runs on a third stream without synchronisation (mi_dl_batch_run_stages): it must wait for the last split back end
+too, and its back end must complete the step like a whole run.
 
 Anchor: srsUE's srslte_pdsch_decode_rnti (reference ue/src/phy/phch_worker.cc:347-348) per subframe, as every batch run.
 """
@@ -23,6 +25,8 @@ pytestmark = pytest.mark.gpu
 
 SF_CYCLE = (1, 2, 3, 4, 6, 7, 8, 9)
 TBS, NCB = 75376, 13
+FRONT = (1 << 0) | (1 << 1) | (1 << 2) | (1 << 3)   # OFDM, CHEST, DEMAP, RM (MI_DL_STAGE_*)
+BACK = (1 << 4) | (1 << 5)                          # TDEC, TB
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -96,10 +100,24 @@ def test_split_runs_match_whole_runs():
                 cap.append(np.ctypeslib.as_array((C.c_uint8 * nb).from_address(h)).view(t))
             caps.append(cap)
             sets.append(s)
+        # then, without synchronisation, the front end of another step of each workspace on a third stream: it rewrites
+        # the softbuffer its last split run's back end reads, so it must wait for that back end (the batch orders every
+        # run after a pending split back end) -- or the captures of runs steps - S .. steps - 1 would not match
+        other = abi.stream_cu_share(0, 8)
+        fr.append(other)
+        nxt = [1 - sets[steps - S + k] for k in range(S)]
+        for k in range(S):
+            ws[k].run_stages(FRONT, d_iq[nxt[k]].data_ptr(), other)
         assert hip.hipDeviceSynchronize() == 0
         for j in range(steps):
             for (w, _), got, exp in zip(bufs, caps[j], ref[sets[j]]):
                 assert np.array_equal(got, exp), f"split run {j} (workspace {j % S}, IQ set {sets[j]}): buffer {w}"
+        # and its back end completes that step like a whole run
+        for k in range(S):
+            ws[k].run_stages(BACK, None, other)
+            for w, t in bufs:
+                assert np.array_equal(ws[k].download(w, t), ref[nxt[k]][[x for x, _ in bufs].index(w)]), \
+                    f"workspace {k}: the step after the split runs, buffer {w}"
     finally:
         hip.hipDeviceSynchronize()
         for h in pinned:
